@@ -1,0 +1,343 @@
+#!/usr/bin/env python3
+"""EC encode+decode GiB/s with device-resident stripes (BASELINE.json metric).
+
+Step (configs[1] of BASELINE.json, per GPU): EC_4P2, 1 MiB cells, 1024
+stripes --
+  * encode: client write layout, data [S][k][C] -> parity [p][S][C]
+    (obj_ec_recx_encode's loop, ref:src/object/cli_ec.c:593-663), and
+  * degraded decode: recovery layout [S][k+p][C], cells {d0,d1} lost,
+    regenerated in place from the first k survivors
+    (obj_ec_recov_data, ref:src/object/cli_ec.c:2814-2885).
+value = user bytes through the codec (k*C*S per encode + k*C*S per decode,
+summed over ranks) / wall time of K steps, GiB/s.
+
+Stripes are independent: each rank owns its own batch (weak scaling), no
+data-path collective.  torch.distributed (gloo) only provides the barrier and
+the max-over-ranks of the elapsed time.
+
+roofline: the dominant kernel (ecg_mm_kernel<4,2>, which serves both the
+encode and the 2-erasure decode) -- algorithmic bytes per launch
+(k+rows)*C*S / mean launch duration from HIP events on its stream, against
+the 8 TB/s HBM spec peak; `traffic` from the committed rocprofv3 PMC pass
+(profiles/<round>/pmc_traffic.json) when present.
+cpu_baseline: the oracle's SIMD ISA-L-equivalent restatement (AVX2/GFNI +
+OpenMP) on a bounded sample, rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+GIB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0          # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
+ROUND = "r01"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--k", type=int, default=4)
+    ap.add_argument("--p", type=int, default=2)
+    ap.add_argument("--cell", type=int, default=1 << 20)
+    ap.add_argument("--stripes", type=int, default=1024, help="stripes per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
+    ap.add_argument("--no-detail", action="store_true", help="skip the extra per-config rows")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--profile-only", action="store_true", help="just the timed loop (for rocprofv3)")
+    return ap.parse_args()
+
+
+def dist_init():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def max_over_ranks(world, x: float) -> float:
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def fill_device(ctx, buf, nbytes, config_id, chunk=256 << 20):
+    """Seeded random bytes; one generated chunk tiled over the buffer (the
+    codec's cost does not depend on cross-chunk uniqueness)."""
+    from tools.datagen import stripe_bytes
+
+    blk = stripe_bytes(min(chunk, nbytes), config_id)
+    off = 0
+    while off < nbytes:
+        n = min(blk.size, nbytes - off)
+        buf.upload(blk[:n], offset=off)
+        off += n
+
+
+class Workload:
+    """One rank's EC batch: encode (client layout) + decode (recovery layout)."""
+
+    def __init__(self, ctx, k, p, C, S, err=(0, 1), config_id=2):
+        self.ctx, self.k, self.p, self.C, self.S, self.err = ctx, k, p, C, S, list(err)
+        self.data = ctx.alloc(S * k * C)
+        self.parity = ctx.alloc(p * S * C)
+        self.stripes = ctx.alloc(S * (k + p) * C)
+        fill_device(ctx, self.data, S * k * C, config_id)
+        # recovery buffer: a consistent [S][k+p][C] image (encode in place)
+        fill_device(ctx, self.stripes, S * (k + p) * C, config_id + 1)
+        st = (k + p) * C
+        ctx.encode(k, p, C, S, self.stripes.ptr, st, self.stripes.ptr + k * C, C, st)
+        ctx.sync()
+        self.events = []        # per timed step: 4 events bracketing the two launches
+
+    def step(self, timed=False):
+        c, k, p, C, S = self.ctx, self.k, self.p, self.C, self.S
+        ev = [c.event() for _ in range(4)] if timed else None
+        if timed:
+            c.record(ev[0])
+        c.encode(k, p, C, S, self.data.ptr, k * C, self.parity.ptr, S * C, C)
+        if timed:
+            c.record(ev[1])
+            c.record(ev[2])
+        c.recover(k, p, C, S, self.stripes.ptr, (k + p) * C, self.err)
+        if timed:
+            c.record(ev[3])
+            self.events.append(ev)
+
+    def kernel_ms(self):
+        """(encode_ms, decode_ms) per timed step, read after the timed region."""
+        out = []
+        for ev in self.events:
+            out.append((self.ctx.elapsed_ms(ev[0], ev[1]), self.ctx.elapsed_ms(ev[2], ev[3])))
+            for e in ev:
+                self.ctx.destroy_event(e)
+        self.events = []
+        return out
+
+    def user_bytes_per_step(self):
+        return 2 * self.k * self.C * self.S
+
+    def alg_bytes_per_launch(self):
+        # encode: read k, write p cells; decode: read k survivors, write nerrs
+        return (self.k + self.p) * self.C * self.S, (self.k + len(self.err)) * self.C * self.S
+
+    def free(self):
+        for b in (self.data, self.parity, self.stripes):
+            b.free()
+
+
+def time_kernel(ctx, fn, iters):
+    a, b = ctx.event(), ctx.event()
+    fn()
+    ctx.sync()
+    ms = []
+    for _ in range(iters):
+        ctx.record(a)
+        fn()
+        ctx.record(b)
+        ms.append(ctx.elapsed_ms(a, b))
+    ctx.destroy_event(a)
+    ctx.destroy_event(b)
+    ms.sort()
+    return ms[len(ms) // 2]
+
+
+def detail_rows(ctx, iters=5):
+    """Extra device-resident rows (per GPU): the north-star EC_8P2 encode,
+    EC_8P2 2-erasure decode, EC_16P2 128 KiB encode, and this box's measured
+    HBM copy rate.  Median kernel time over `iters` launches."""
+    from daos_amd import ecg
+
+    rows = {}
+    # HBM copy ceiling (2 GiB read + 2 GiB write)
+    n = 2 << 30
+    a, b = ctx.alloc(n), ctx.alloc(n)
+    ms = time_kernel(ctx, lambda: ctx.copy_kernel(b.ptr, a.ptr, n), iters)
+    rows["hbm_copy"] = {"GBps": round(2 * n / ms / 1e6, 1), "frac_of_spec": round(2 * n / ms / 1e6 / HBM_PEAK_GBS, 4)}
+    a.free()
+    b.free()
+    for name, k, p, C, S, mode in (("EC_8P2_1MiB_encode", 8, 2, 1 << 20, 512, "enc"),
+                                   ("EC_8P2_1MiB_decode_d0d1", 8, 2, 1 << 20, 512, "dec"),
+                                   ("EC_16P2_128KiB_encode", 16, 2, 128 << 10, 1024, "enc"),
+                                   ("EC_2P1_128KiB_encode", 2, 1, 128 << 10, 1024, "enc")):
+        st = (k + p) * C
+        buf = ctx.alloc(S * st)
+        fill_device(ctx, buf, S * st, 7)
+        if mode == "enc":
+            fn = (lambda buf=buf, k=k, p=p, C=C, S=S, st=st:
+                  ctx.encode(k, p, C, S, buf.ptr, st, buf.ptr + k * C, C, st))
+            alg = (k + p) * C * S
+        else:
+            ctx.encode(k, p, C, S, buf.ptr, st, buf.ptr + k * C, C, st)
+            fn = (lambda buf=buf, k=k, p=p, C=C, S=S, st=st:
+                  ctx.recover(k, p, C, S, buf.ptr, st, [0, 1]))
+            alg = (k + 2) * C * S
+        ms = time_kernel(ctx, fn, iters)
+        gbs = alg / ms / 1e6
+        rows[name] = {"GiBps_user": round(k * C * S / ms / 1e3 / GIB * 1e6, 1), "alg_GBps": round(gbs, 1),
+                      "roofline_frac": round(gbs / HBM_PEAK_GBS, 4),
+                      "frac_of_measured_copy": round(gbs / rows["hbm_copy"]["GBps"], 4),
+                      "kernel": ecg.last_kernel(), "ms": round(ms, 3)}
+        buf.free()
+    return rows
+
+
+def cpu_baseline(k, p, C, budget_s):
+    """Oracle SIMD restatement (ISA-L-equivalent), OpenMP over stripes, on a
+    bounded sample: 32 stripes of the same workload, encode + {d0,d1} decode,
+    repeated until ~budget_s of CPU time."""
+    import numpy as np
+
+    from oracle import ref
+    from tools.datagen import stripe_bytes
+
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))      # the GPU box's CPU share is 16
+    S = 32
+    data = stripe_bytes(S * k * C, 2)
+    stripes = np.zeros(S * (k + p) * C, dtype=np.uint8)
+    sv = stripes.reshape(S, k + p, C)
+    sv[:, :k] = data.reshape(S, k, C)
+    par = ref.encode_batch(k, p, C, S, data, nthreads=cores, simd=True).reshape(p, S, C)
+    sv[:, k:] = par.transpose(1, 0, 2)
+    rc, de, dec, el, gt, reused = ref.recov_codec(k, p, [0, 1])
+    assert rc == 0
+    user = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        ref.encode_batch(k, p, C, S, data, nthreads=cores, simd=True)
+        ref.recov_batch(k, 2, gt, dec, el, C, (k + p) * C, S, stripes, nthreads=cores, simd=True)
+        user += 2 * k * C * S
+    dt = time.perf_counter() - t0
+    variant = {0: "scalar", 1: "avx2-vpshufb", 2: "gfni-avx512"}[ref.simd_variant()]
+    return {"value": round(user / dt / GIB, 3), "unit": "GiB/s", "cores": cores, "kind": "port",
+            "sample": f"EC_{k}P{p} {C >> 10} KiB cells, {S} stripes, encode + d0,d1 decode, repeated "
+                      f"{dt:.1f} s; ISA-L-equivalent restatement ({variant}, OpenMP)"}
+
+
+def pmc_traffic():
+    path = os.path.join(ROOT, "profiles", ROUND, "pmc_traffic.json")
+    if os.path.exists(path):
+        try:
+            return json.load(open(path))
+        except (OSError, ValueError):
+            return None
+    return None
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_init()
+    import torch  # noqa: F401  (shares libamdhip64 with libecg; sync per contract)
+
+    from daos_amd import ecg
+
+    torch.cuda.set_device(local)
+    ctx = ecg.Context(local)
+    k, p, C, S = args.k, args.p, args.cell, args.stripes
+    wl = Workload(ctx, k, p, C, S)
+
+    for _ in range(args.warmup):
+        wl.step()
+    ctx.sync()
+
+    barrier(world)
+    torch.cuda.synchronize()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        wl.step(timed=True)
+    ctx.sync()
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(world, elapsed)
+
+    if args.profile_only:
+        wl.free()
+        ctx.close()
+        return
+
+    user = wl.user_bytes_per_step() * args.steps * world
+    value = user / elapsed / GIB
+    kms = wl.kernel_ms()
+    enc_ms = sorted(m[0] for m in kms)
+    dec_ms = sorted(m[1] for m in kms)
+    enc_alg, dec_alg = wl.alg_bytes_per_launch()
+    mean_launch_ms = (sum(enc_ms) + sum(dec_ms)) / (2 * len(enc_ms))
+    alg_per_launch = (enc_alg + dec_alg) / 2
+    achieved = alg_per_launch / (mean_launch_ms / 1e3) / 1e9
+    kernel_name = f"ecg_mm_kernel<{k},{p},0,0>"
+    traffic = None
+    pmc = pmc_traffic()
+    if pmc and pmc.get("kernel", "").startswith(f"ecg_mm_kernel<{k},{p}"):
+        traffic = pmc.get("hbm_bytes_per_launch")
+
+    out = {
+        "metric": "EC encode+decode GiB/s (device-resident stripes)",
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: xoshiro256** stripes seeded 0xDA05EC00+id (BASELINE.md §3), device-resident",
+        "config": {"workload": f"EC_{k}P{p} {C >> 10} KiB cells x {S} stripes per GPU: encode (data [S][k][C] -> "
+                               f"parity [p][S][C]) + degraded decode of cells d0,d1 in [S][k+p][C]",
+                   "k": k, "p": p, "cell_bytes": C, "stripes_per_gpu": S, "erasures": wl.err,
+                   "parallelism": f"stripe-sharded x{world}, no collective"},
+        "roofline": {"bound": "hbm", "kernel": kernel_name, "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "alg_bytes_per_launch": int(alg_per_launch),
+                     "mean_launch_ms": round(mean_launch_ms, 4),
+                     "encode_ms_median": round(enc_ms[len(enc_ms) // 2], 4),
+                     "decode_ms_median": round(dec_ms[len(dec_ms) // 2], 4)},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_detail:
+        out["detail"] = detail_rows(ctx)
+    wl.free()
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(k, p, C, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

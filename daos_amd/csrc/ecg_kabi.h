@@ -1,0 +1,81 @@
+/*
+ * ecg_kabi.h -- the private ABI between the C host layer (daos_amd/csrc/host)
+ * and the HIP kernels (daos_amd/csrc/kernels).  Plain C, no HIP types.
+ *
+ * One launch = one batched GF(2^8) "matrix x cells" product over S stripes:
+ *
+ *     dst[s][r][i] (^)= XOR_{j<k} coef[r][j] * src[s][j][i]      i in [0, C)
+ *
+ * which is ISA-L ec_encode_data (ref:src/object/cli_ec.c:540) when coef are
+ * the Cauchy parity rows, DAOS recovery (ref:src/object/cli_ec.c:2641) when
+ * coef are the decode rows, and ec_encode_data_update / agg_update_parity
+ * (ref:src/object/srv_ec_aggregate.c:1089-1101) with `accumulate` and
+ * `diff` set (src = old ^ new).
+ *
+ * Cell j of stripe s lives at  src + s*src_stripe_stride + src_cell_off[j];
+ * that covers the DAOS layouts: client data [S][k][C], parity [p][S][C]
+ * (ref:src/object/cli_ec.c:75-97,638-640), recovery [S][k+p][C]
+ * (ref:src/object/cli_ec.c:2449-2464, 2626-2643), aggregation [k][C]/[p][C]
+ * (ref:src/object/srv_ec_aggregate.c:686-691).
+ *
+ * GF multiply tables ("perm tables"): a byte x splits into bit groups
+ * x = (x & 0x07) ^ (x & 0x38) ^ (x & 0xC0) and, GF multiplication being
+ * linear over GF(2),  c*x = T0[x & 7] ^ T1[(x >> 3) & 7] ^ T2[x >> 6]  with
+ * T0[i] = c*i, T1[i] = c*(i<<3), T2[i] = c*(i<<6).  Each table has <= 8 byte
+ * entries, i.e. exactly what one v_perm_b32 can index.  Packed little-endian:
+ * t0lo = T0[0..3], t0hi = T0[4..7], t1lo/t1hi likewise, t2 = T2[0..3].
+ */
+#ifndef ECG_KABI_H
+#define ECG_KABI_H
+
+#include <stdint.h>
+
+#define ECG_KMAX_K 16	/* data cells per launch; host splits larger k */
+#define ECG_KMAX_R 8	/* output rows per launch */
+
+typedef struct ecg_ptbl {
+	uint32_t t0lo, t0hi, t1lo, t1hi, t2;
+} ecg_ptbl_t;
+
+typedef struct ecg_mm_params {
+	const uint8_t *src;		/* cell bases (stripe 0) */
+	const uint8_t *src2;		/* diff mode: second source, same layout */
+	uint8_t *dst;
+	int64_t src_stripe_stride;
+	int64_t src2_stripe_stride;
+	int64_t dst_stripe_stride;
+	int64_t src_cell_off[ECG_KMAX_K];
+	int64_t src2_cell_off[ECG_KMAX_K];
+	int64_t dst_cell_off[ECG_KMAX_R];
+	uint64_t cell_bytes;
+	uint32_t nstripes;
+	uint32_t k;
+	uint32_t rows;
+	uint32_t accumulate;		/* dst ^= product instead of dst = product */
+	uint32_t diff;			/* source cell j = src[j] ^ src2[j] */
+	uint32_t pad;
+	ecg_ptbl_t tbl[ECG_KMAX_R][ECG_KMAX_K];
+} ecg_mm_params_t;
+
+/* launch tuning (host fills; 0 = kernel default) */
+typedef struct ecg_launch_cfg {
+	uint32_t grid_x;	/* chunks per stripe handled in parallel */
+	uint32_t grid_y;	/* stripes handled in parallel */
+	uint32_t variant;	/* 0 auto, 1 force generic, 2 force byte kernel */
+	uint32_t pad;
+} ecg_launch_cfg_t;
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* Implemented in kernels/ecg_kernels.hip.  Returns a hipError_t value. */
+int ecg_k_launch_matmul(const ecg_mm_params_t *p, const ecg_launch_cfg_t *cfg,
+			void *stream, uint32_t *kernel_id);
+/* Device copy kernel used only to measure the box's achievable HBM rate. */
+int ecg_k_launch_copy(const void *src, void *dst, uint64_t bytes, void *stream);
+const char *ecg_k_kernel_name(uint32_t kernel_id);
+#ifdef __cplusplus
+}
+#endif
+
+#endif

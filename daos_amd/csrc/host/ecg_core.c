@@ -1,0 +1,732 @@
+/*
+ * ecg_core.c -- context, batched codec entry points and the host-staging
+ * (PCIe) pipeline of the MI355X EC engine.  See include/ecg.h.
+ *
+ * Reference loops these entry points replace (one ISA-L call per stripe on
+ * the CPU today):
+ *   client encode     obj_ec_recx_encode   ref:src/object/cli_ec.c:593-663
+ *   degraded read     obj_ec_recov_data    ref:src/object/cli_ec.c:2814-2885
+ *   rebuild parity    migrate_update_parity ref:src/object/srv_obj_migrate.c:1096-1181
+ *   aggregation       agg_encode_full_stripe_ult / agg_update_parity
+ *                     ref:src/object/srv_ec_aggregate.c:671-697, 1062-1105
+ */
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "ecg_internal.h"
+
+static __thread char t_err[512];
+static __thread const char *t_last_kernel = "";
+
+int ecg_fail(int rc, const char *fmt, ...)
+{
+	va_list ap;
+
+	va_start(ap, fmt);
+	vsnprintf(t_err, sizeof(t_err), fmt, ap);
+	va_end(ap);
+	return rc;
+}
+
+int ecg_hip_fail(hipError_t e, const char *what)
+{
+	return ecg_fail(-ECG_DER_IO, "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+}
+
+const char *ecg_strerror(void)
+{
+	return t_err;
+}
+
+void ecg_set_last_kernel(const char *name)
+{
+	t_last_kernel = name;
+}
+
+const char *ecg_last_kernel(void)
+{
+	return t_last_kernel;
+}
+
+#define HIPCHK(call)                                                   \
+	do {                                                           \
+		hipError_t e__ = (call);                               \
+		if (e__ != hipSuccess)                                 \
+			return ecg_hip_fail(e__, #call);               \
+	} while (0)
+
+/* ------------------------------------------------------------------------ */
+/* devices / contexts                                                        */
+/* ------------------------------------------------------------------------ */
+static int is_gfx950(int dev)
+{
+	hipDeviceProp_t prop;
+
+	if (hipGetDeviceProperties(&prop, dev) != hipSuccess)
+		return 0;
+	return strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+}
+
+int ecg_device_count(void)
+{
+	int n = 0, i, good = 0;
+
+	if (hipGetDeviceCount(&n) != hipSuccess)
+		return 0;
+	for (i = 0; i < n; i++)
+		good += is_gfx950(i);
+	return good;
+}
+
+int ecg_ctx_create(int device, ecg_ctx_t **out)
+{
+	ecg_ctx_t *ctx;
+	hipError_t e;
+	int n = 0;
+
+	if (out == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "ctx_create: NULL out");
+	*out = NULL;
+	e = hipGetDeviceCount(&n);
+	if (e != hipSuccess || n == 0)
+		return ecg_fail(-ECG_DER_NOSYS, "ctx_create: no HIP device (%s)",
+				hipGetErrorString(e));
+	if (device < 0 || device >= n)
+		return ecg_fail(-ECG_DER_INVAL, "ctx_create: device %d of %d", device, n);
+	if (!is_gfx950(device))
+		return ecg_fail(-ECG_DER_NOSYS, "ctx_create: device %d is not gfx950", device);
+	ctx = calloc(1, sizeof(*ctx));
+	if (ctx == NULL)
+		return ecg_fail(-ECG_DER_NOMEM, "ctx_create: calloc");
+	ctx->device = device;
+	pthread_mutex_init(&ctx->lock, NULL);
+	ecg_gf_init();
+	e = hipSetDevice(device);
+	if (e == hipSuccess)
+		e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+	if (e != hipSuccess) {
+		free(ctx);
+		return ecg_hip_fail(e, "ctx_create");
+	}
+	*out = ctx;
+	return 0;
+}
+
+static void stage_free(ecg_ctx_t *ctx)
+{
+	int i;
+
+	for (i = 0; i < ECG_NSLOT; i++) {
+		if (ctx->stage.dev[i])
+			(void)hipFree(ctx->stage.dev[i]);
+		if (ctx->stage.st[i])
+			(void)hipStreamDestroy(ctx->stage.st[i]);
+		if (ctx->stage.done[i])
+			(void)hipEventDestroy(ctx->stage.done[i]);
+	}
+	memset(&ctx->stage, 0, sizeof(ctx->stage));
+}
+
+void ecg_ctx_destroy(ecg_ctx_t *ctx)
+{
+	if (ctx == NULL)
+		return;
+	(void)hipSetDevice(ctx->device);
+	(void)hipStreamSynchronize(ctx->stream);
+	stage_free(ctx);
+	(void)hipStreamDestroy(ctx->stream);
+	pthread_mutex_destroy(&ctx->lock);
+	free(ctx);
+}
+
+int ecg_ctx_device(const ecg_ctx_t *ctx)
+{
+	return ctx ? ctx->device : -1;
+}
+
+void *ecg_ctx_stream(ecg_ctx_t *ctx)
+{
+	return ctx ? (void *)ctx->stream : NULL;
+}
+
+int ecg_ctx_enter(ecg_ctx_t *ctx)
+{
+	hipError_t e;
+
+	if (ctx == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "NULL context");
+	e = hipSetDevice(ctx->device);
+	if (e != hipSuccess)
+		return ecg_hip_fail(e, "hipSetDevice");
+	return 0;
+}
+
+hipStream_t ecg_pick_stream(ecg_ctx_t *ctx, void *stream)
+{
+	return stream ? (hipStream_t)stream : ctx->stream;
+}
+
+int ecg_set_launch(ecg_ctx_t *ctx, uint32_t grid_x, uint32_t grid_y, uint32_t variant)
+{
+	if (ctx == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "NULL context");
+	ctx->cfg.grid_x = grid_x;
+	ctx->cfg.grid_y = grid_y;
+	ctx->cfg.variant = variant;
+	return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* batched GF matrix x cells                                                 */
+/* ------------------------------------------------------------------------ */
+static int launch(ecg_ctx_t *ctx, const ecg_mm_params_t *prm, hipStream_t st)
+{
+	uint32_t kid = 0;
+	int e = ecg_k_launch_matmul(prm, &ctx->cfg, (void *)st, &kid);
+
+	if (e != 0)
+		return ecg_hip_fail((hipError_t)e, "kernel launch");
+	ecg_set_last_kernel(ecg_k_kernel_name(kid));
+	return 0;
+}
+
+/*
+ * Core product with optional second source (diff mode).  Splits k into
+ * groups of ECG_KMAX_K (later groups accumulate) and rows into groups of
+ * ECG_KMAX_R.
+ */
+static int matmul2(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef,
+		   uint64_t C, uint32_t S,
+		   const void *src, const int64_t *soff, int64_t sstride,
+		   const void *src2, const int64_t *soff2, int64_t sstride2,
+		   void *dst, const int64_t *doff, int64_t dstride,
+		   unsigned flags, void *stream)
+{
+	ecg_mm_params_t *prm;
+	hipStream_t st;
+	int r0, j0, rc;
+
+	if (k < 1 || k > ECG_MAX_K || rows < 1 || rows > 256)
+		return ecg_fail(-ECG_DER_INVAL, "matmul: bad k=%d rows=%d", k, rows);
+	if (coef == NULL || soff == NULL || doff == NULL || src == NULL || dst == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "matmul: NULL argument");
+	if (C == 0 || S == 0)
+		return 0;
+	rc = ecg_ctx_enter(ctx);
+	if (rc)
+		return rc;
+	ecg_gf_init();
+	st = ecg_pick_stream(ctx, stream);
+	prm = calloc(1, sizeof(*prm));
+	if (prm == NULL)
+		return ecg_fail(-ECG_DER_NOMEM, "matmul: calloc");
+
+	for (r0 = 0; r0 < rows; r0 += ECG_KMAX_R) {
+		int rr = rows - r0 < ECG_KMAX_R ? rows - r0 : ECG_KMAX_R;
+
+		for (j0 = 0; j0 < k; j0 += ECG_KMAX_K) {
+			int kk = k - j0 < ECG_KMAX_K ? k - j0 : ECG_KMAX_K;
+			int r, j;
+
+			memset(prm, 0, sizeof(*prm));
+			prm->src = src;
+			prm->src2 = src2;
+			prm->dst = dst;
+			prm->src_stripe_stride = sstride;
+			prm->src2_stripe_stride = sstride2;
+			prm->dst_stripe_stride = dstride;
+			prm->cell_bytes = C;
+			prm->nstripes = S;
+			prm->k = (uint32_t)kk;
+			prm->rows = (uint32_t)rr;
+			prm->accumulate = (flags & ECG_F_ACCUMULATE) || j0 > 0;
+			prm->diff = src2 != NULL;
+			for (j = 0; j < kk; j++) {
+				prm->src_cell_off[j] = soff[j0 + j];
+				if (src2)
+					prm->src2_cell_off[j] = soff2[j0 + j];
+			}
+			for (r = 0; r < rr; r++) {
+				prm->dst_cell_off[r] = doff[r0 + r];
+				for (j = 0; j < kk; j++)
+					ecg_build_ptbl(coef[(size_t)(r0 + r) * k + j0 + j],
+						       &prm->tbl[r][j]);
+			}
+			rc = launch(ctx, prm, st);
+			if (rc) {
+				free(prm);
+				return rc;
+			}
+		}
+	}
+	free(prm);
+	return 0;
+}
+
+int ecg_matmul(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef,
+	       uint64_t cell_bytes, uint32_t nstripes,
+	       const void *src, const int64_t *src_cell_off, int64_t src_stripe_stride,
+	       void *dst, const int64_t *dst_cell_off, int64_t dst_stripe_stride,
+	       unsigned flags, void *stream)
+{
+	return matmul2(ctx, k, rows, coef, cell_bytes, nstripes, src, src_cell_off,
+		       src_stripe_stride, NULL, NULL, 0, dst, dst_cell_off, dst_stripe_stride,
+		       flags, stream);
+}
+
+static int check_kp(int k, int p)
+{
+	/* DAOS class limits, ref:src/object/obj_class.c:587-601 */
+	if (k < 1 || k > ECG_MAX_K || p < 1 || p > ECG_MAX_P)
+		return ecg_fail(-ECG_DER_INVAL, "bad k=%d p=%d", k, p);
+	return 0;
+}
+
+int ecg_encode(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
+	       const void *data, int64_t data_stripe_stride,
+	       void *parity, int64_t parity_cell_stride, int64_t parity_stripe_stride,
+	       void *stream)
+{
+	unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
+	int64_t soff[ECG_MAX_K], doff[ECG_MAX_P];
+	int i, rc;
+
+	rc = check_kp(k, p);
+	if (rc)
+		return rc;
+	ecg_gen_cauchy1(k, p, en);
+	for (i = 0; i < k; i++)
+		soff[i] = (int64_t)i * (int64_t)C;
+	for (i = 0; i < p; i++)
+		doff[i] = (int64_t)i * parity_cell_stride;
+	return ecg_matmul(ctx, k, p, &en[k * k], C, S, data, soff, data_stripe_stride,
+			  parity, doff, parity_stripe_stride, 0, stream);
+}
+
+/* Recovery rows through the per-context cache (the reference caches its
+ * recovery codec while the error list is unchanged, ref:src/object/cli_ec.c:
+ * 2183-2185). */
+static int recov_lookup(ecg_ctx_t *ctx, int k, int p, const uint32_t *err_list, int nerrs,
+			struct ecg_rcache_ent *out)
+{
+	unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
+	struct ecg_rcache_ent *victim = NULL;
+	int i, rc, reused;
+
+	pthread_mutex_lock(&ctx->lock);
+	for (i = 0; i < ECG_RCACHE; i++) {
+		struct ecg_rcache_ent *e = &ctx->rcache[i];
+
+		if (e->valid && e->k == k && e->p == p && e->nerrs == nerrs &&
+		    memcmp(e->err_list, err_list, sizeof(uint32_t) * nerrs) == 0) {
+			e->stamp = ++ctx->rstamp;
+			*out = *e;
+			pthread_mutex_unlock(&ctx->lock);
+			return 0;
+		}
+		if (victim == NULL || !e->valid || (victim->valid && e->stamp < victim->stamp))
+			victim = e;
+	}
+	pthread_mutex_unlock(&ctx->lock);
+
+	memset(out, 0, sizeof(*out));
+	ecg_gen_cauchy1(k, p, en);
+	rc = ecg_recov_rows(k, p, en, err_list, nerrs, out->rows, out->out_idx, out->dec_idx,
+			    &reused);
+	if (rc)
+		return rc;
+	out->valid = 1;
+	out->k = k;
+	out->p = p;
+	out->nerrs = nerrs;
+	memcpy(out->err_list, err_list, sizeof(uint32_t) * nerrs);
+
+	pthread_mutex_lock(&ctx->lock);
+	out->stamp = ++ctx->rstamp;
+	*victim = *out;
+	pthread_mutex_unlock(&ctx->lock);
+	return 0;
+}
+
+static int recover_with(ecg_ctx_t *ctx, const struct ecg_rcache_ent *ent, uint64_t C,
+			uint32_t S, void *stripes, int64_t stripe_stride, void *stream)
+{
+	int64_t soff[ECG_MAX_K], doff[ECG_MAX_P];
+	int i;
+
+	for (i = 0; i < ent->k; i++)
+		soff[i] = (int64_t)ent->dec_idx[i] * (int64_t)C;
+	for (i = 0; i < ent->nerrs; i++)
+		doff[i] = (int64_t)ent->out_idx[i] * (int64_t)C;
+	return ecg_matmul(ctx, ent->k, ent->nerrs, ent->rows, C, S, stripes, soff,
+			  stripe_stride, stripes, doff, stripe_stride, 0, stream);
+}
+
+int ecg_recover(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
+		void *stripes, int64_t stripe_stride,
+		const uint32_t *err_list, int nerrs, void *stream)
+{
+	struct ecg_rcache_ent ent;
+	int rc;
+
+	rc = check_kp(k, p);
+	if (rc)
+		return rc;
+	if (err_list == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "recover: NULL err_list");
+	if (nerrs > p)
+		return ecg_fail(-ECG_DER_DATA_LOSS, "recover: %d erasures > p=%d", nerrs, p);
+	if (nerrs <= 0)
+		return 0;
+	rc = recov_lookup(ctx, k, p, err_list, nerrs, &ent);
+	if (rc)
+		return rc;
+	return recover_with(ctx, &ent, C, S, stripes, stripe_stride, stream);
+}
+
+int ecg_update(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
+	       int nupd, const uint32_t *cell_idx,
+	       const void *old_cells, const void *new_cells, int64_t upd_stripe_stride,
+	       void *parity, int64_t parity_cell_stride, int64_t parity_stripe_stride,
+	       void *stream)
+{
+	unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
+	unsigned char coef[ECG_MAX_P * ECG_MAX_K];
+	int64_t soff[ECG_MAX_K], doff[ECG_MAX_P];
+	int u, r, rc;
+
+	rc = check_kp(k, p);
+	if (rc)
+		return rc;
+	if (nupd < 1 || nupd > k || cell_idx == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "update: bad nupd=%d", nupd);
+	ecg_gen_cauchy1(k, p, en);
+	for (u = 0; u < nupd; u++) {
+		if (cell_idx[u] >= (uint32_t)k)
+			return ecg_fail(-ECG_DER_INVAL, "update: cell %u >= k", cell_idx[u]);
+		soff[u] = (int64_t)u * (int64_t)C;
+		for (r = 0; r < p; r++)
+			coef[r * nupd + u] = en[(k + r) * k + cell_idx[u]];
+	}
+	for (r = 0; r < p; r++)
+		doff[r] = (int64_t)r * parity_cell_stride;
+	return matmul2(ctx, nupd, p, coef, C, S, old_cells, soff, upd_stripe_stride,
+		       new_cells, soff, upd_stripe_stride, parity, doff, parity_stripe_stride,
+		       ECG_F_ACCUMULATE, stream);
+}
+
+/* ------------------------------------------------------------------------ */
+/* host-staging pipeline                                                     */
+/* ------------------------------------------------------------------------ */
+static int stage_reserve(ecg_ctx_t *ctx, size_t bytes)
+{
+	int i;
+
+	if (ctx->stage.dev_bytes >= bytes)
+		return 0;
+	stage_free(ctx);
+	for (i = 0; i < ECG_NSLOT; i++) {
+		HIPCHK(hipMalloc(&ctx->stage.dev[i], bytes));
+		HIPCHK(hipStreamCreateWithFlags(&ctx->stage.st[i], hipStreamNonBlocking));
+		HIPCHK(hipEventCreateWithFlags(&ctx->stage.done[i], hipEventDisableTiming));
+	}
+	ctx->stage.dev_bytes = bytes;
+	return 0;
+}
+
+int ecg_encode_host(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
+		    const void *data, void *parity, uint32_t chunk)
+{
+	const unsigned char *hd = data;
+	unsigned char *hp = parity;
+	uint32_t s0, slot = 0;
+	int rc, r;
+
+	rc = check_kp(k, p);
+	if (rc)
+		return rc;
+	rc = ecg_ctx_enter(ctx);
+	if (rc)
+		return rc;
+	if (S == 0 || C == 0)
+		return 0;
+	if (chunk == 0)
+		chunk = 64;
+	if (chunk > S)
+		chunk = S;
+	pthread_mutex_lock(&ctx->lock);
+	rc = stage_reserve(ctx, (size_t)chunk * (k + p) * C);
+	for (s0 = 0; rc == 0 && s0 < S; s0 += chunk, slot = (slot + 1) % ECG_NSLOT) {
+		uint32_t cs = S - s0 < chunk ? S - s0 : chunk;
+		unsigned char *dd = ctx->stage.dev[slot];
+		unsigned char *dp = dd + (size_t)cs * k * C;
+		hipStream_t st = ctx->stage.st[slot];
+		hipError_t e;
+
+		e = hipEventSynchronize(ctx->stage.done[slot]);
+		if (e == hipSuccess)
+			e = hipMemcpyAsync(dd, hd + (size_t)s0 * k * C, (size_t)cs * k * C,
+					   hipMemcpyHostToDevice, st);
+		if (e != hipSuccess) {
+			rc = ecg_hip_fail(e, "encode_host H2D");
+			break;
+		}
+		rc = ecg_encode(ctx, k, p, C, cs, dd, (int64_t)k * C, dp, (int64_t)cs * C,
+				(int64_t)C, st);
+		for (r = 0; rc == 0 && r < p; r++) {
+			e = hipMemcpyAsync(hp + ((size_t)r * S + s0) * C, dp + (size_t)r * cs * C,
+					   (size_t)cs * C, hipMemcpyDeviceToHost, st);
+			if (e != hipSuccess)
+				rc = ecg_hip_fail(e, "encode_host D2H");
+		}
+		if (rc == 0) {
+			e = hipEventRecord(ctx->stage.done[slot], st);
+			if (e != hipSuccess)
+				rc = ecg_hip_fail(e, "encode_host event");
+		}
+	}
+	for (r = 0; r < ECG_NSLOT; r++)
+		if (ctx->stage.st[r])
+			(void)hipStreamSynchronize(ctx->stage.st[r]);
+	pthread_mutex_unlock(&ctx->lock);
+	return rc;
+}
+
+int ecg_recover_host(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
+		     void *stripes, const uint32_t *err_list, int nerrs, uint32_t chunk)
+{
+	struct ecg_rcache_ent ent;
+	unsigned char *hs = stripes;
+	const size_t sstride = (size_t)(k + p) * C;
+	uint32_t s0, slot = 0;
+	int rc, i;
+
+	rc = check_kp(k, p);
+	if (rc)
+		return rc;
+	if (nerrs > p)
+		return ecg_fail(-ECG_DER_DATA_LOSS, "recover_host: %d erasures > p=%d", nerrs, p);
+	if (nerrs <= 0 || S == 0 || C == 0)
+		return 0;
+	rc = ecg_ctx_enter(ctx);
+	if (rc)
+		return rc;
+	rc = recov_lookup(ctx, k, p, err_list, nerrs, &ent);
+	if (rc)
+		return rc;
+	if (chunk == 0)
+		chunk = 64;
+	if (chunk > S)
+		chunk = S;
+	pthread_mutex_lock(&ctx->lock);
+	rc = stage_reserve(ctx, (size_t)chunk * sstride);
+	for (s0 = 0; rc == 0 && s0 < S; s0 += chunk, slot = (slot + 1) % ECG_NSLOT) {
+		uint32_t cs = S - s0 < chunk ? S - s0 : chunk;
+		unsigned char *dd = ctx->stage.dev[slot];
+		hipStream_t st = ctx->stage.st[slot];
+		hipError_t e = hipEventSynchronize(ctx->stage.done[slot]);
+
+		/* survivors the decode reads: k strided cells per stripe */
+		for (i = 0; e == hipSuccess && i < k; i++)
+			e = hipMemcpy2DAsync(dd + (size_t)ent.dec_idx[i] * C, sstride,
+					     hs + (size_t)s0 * sstride + (size_t)ent.dec_idx[i] * C,
+					     sstride, C, cs, hipMemcpyHostToDevice, st);
+		if (e != hipSuccess) {
+			rc = ecg_hip_fail(e, "recover_host H2D");
+			break;
+		}
+		rc = recover_with(ctx, &ent, C, cs, dd, (int64_t)sstride, st);
+		for (i = 0; rc == 0 && i < nerrs; i++) {
+			e = hipMemcpy2DAsync(hs + (size_t)s0 * sstride + (size_t)err_list[i] * C,
+					     sstride, dd + (size_t)err_list[i] * C, sstride, C, cs,
+					     hipMemcpyDeviceToHost, st);
+			if (e != hipSuccess)
+				rc = ecg_hip_fail(e, "recover_host D2H");
+		}
+		if (rc == 0) {
+			e = hipEventRecord(ctx->stage.done[slot], st);
+			if (e != hipSuccess)
+				rc = ecg_hip_fail(e, "recover_host event");
+		}
+	}
+	for (i = 0; i < ECG_NSLOT; i++)
+		if (ctx->stage.st[i])
+			(void)hipStreamSynchronize(ctx->stage.st[i]);
+	pthread_mutex_unlock(&ctx->lock);
+	return rc;
+}
+
+/* ------------------------------------------------------------------------ */
+/* plumbing                                                                  */
+/* ------------------------------------------------------------------------ */
+int ecg_dev_alloc(ecg_ctx_t *ctx, size_t bytes, void **ptr)
+{
+	int rc = ecg_ctx_enter(ctx);
+
+	if (rc)
+		return rc;
+	if (ptr == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "dev_alloc: NULL ptr");
+	{
+		hipError_t e = hipMalloc(ptr, bytes ? bytes : 1);
+
+		if (e == hipErrorOutOfMemory)
+			return ecg_fail(-ECG_DER_NOMEM, "dev_alloc: %zu bytes", bytes);
+		if (e != hipSuccess)
+			return ecg_hip_fail(e, "hipMalloc");
+	}
+	return 0;
+}
+
+int ecg_dev_free(ecg_ctx_t *ctx, void *ptr)
+{
+	int rc = ecg_ctx_enter(ctx);
+
+	if (rc)
+		return rc;
+	HIPCHK(hipFree(ptr));
+	return 0;
+}
+
+int ecg_host_alloc(ecg_ctx_t *ctx, size_t bytes, void **ptr)
+{
+	int rc = ecg_ctx_enter(ctx);
+
+	if (rc)
+		return rc;
+	if (ptr == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "host_alloc: NULL ptr");
+	HIPCHK(hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocDefault));
+	return 0;
+}
+
+int ecg_host_free(ecg_ctx_t *ctx, void *ptr)
+{
+	int rc = ecg_ctx_enter(ctx);
+
+	if (rc)
+		return rc;
+	HIPCHK(hipHostFree(ptr));
+	return 0;
+}
+
+int ecg_memcpy(ecg_ctx_t *ctx, void *dst, const void *src, size_t bytes, int kind, void *stream)
+{
+	static const hipMemcpyKind kinds[] = {hipMemcpyHostToDevice, hipMemcpyDeviceToHost,
+					      hipMemcpyDeviceToDevice, hipMemcpyDefault};
+	int rc = ecg_ctx_enter(ctx);
+
+	if (rc)
+		return rc;
+	if (kind < 0 || kind > 3)
+		return ecg_fail(-ECG_DER_INVAL, "memcpy: kind %d", kind);
+	HIPCHK(hipMemcpyAsync(dst, src, bytes, kinds[kind], ecg_pick_stream(ctx, stream)));
+	return 0;
+}
+
+int ecg_memset(ecg_ctx_t *ctx, void *dst, int value, size_t bytes, void *stream)
+{
+	int rc = ecg_ctx_enter(ctx);
+
+	if (rc)
+		return rc;
+	HIPCHK(hipMemsetAsync(dst, value, bytes, ecg_pick_stream(ctx, stream)));
+	return 0;
+}
+
+int ecg_stream_create(ecg_ctx_t *ctx, void **stream)
+{
+	int rc = ecg_ctx_enter(ctx);
+
+	if (rc)
+		return rc;
+	HIPCHK(hipStreamCreateWithFlags((hipStream_t *)stream, hipStreamNonBlocking));
+	return 0;
+}
+
+int ecg_stream_destroy(ecg_ctx_t *ctx, void *stream)
+{
+	int rc = ecg_ctx_enter(ctx);
+
+	if (rc)
+		return rc;
+	HIPCHK(hipStreamDestroy((hipStream_t)stream));
+	return 0;
+}
+
+int ecg_stream_sync(ecg_ctx_t *ctx, void *stream)
+{
+	int rc = ecg_ctx_enter(ctx);
+
+	if (rc)
+		return rc;
+	HIPCHK(hipStreamSynchronize(ecg_pick_stream(ctx, stream)));
+	return 0;
+}
+
+int ecg_event_create(ecg_ctx_t *ctx, void **event)
+{
+	int rc = ecg_ctx_enter(ctx);
+
+	if (rc)
+		return rc;
+	HIPCHK(hipEventCreate((hipEvent_t *)event));
+	return 0;
+}
+
+int ecg_event_destroy(ecg_ctx_t *ctx, void *event)
+{
+	int rc = ecg_ctx_enter(ctx);
+
+	if (rc)
+		return rc;
+	HIPCHK(hipEventDestroy((hipEvent_t)event));
+	return 0;
+}
+
+int ecg_event_record(ecg_ctx_t *ctx, void *event, void *stream)
+{
+	int rc = ecg_ctx_enter(ctx);
+
+	if (rc)
+		return rc;
+	HIPCHK(hipEventRecord((hipEvent_t)event, ecg_pick_stream(ctx, stream)));
+	return 0;
+}
+
+int ecg_event_elapsed_ms(ecg_ctx_t *ctx, void *start, void *stop, float *ms)
+{
+	int rc = ecg_ctx_enter(ctx);
+
+	if (rc)
+		return rc;
+	HIPCHK(hipEventSynchronize((hipEvent_t)stop));
+	HIPCHK(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
+	return 0;
+}
+
+int ecg_device_sync(ecg_ctx_t *ctx)
+{
+	int rc = ecg_ctx_enter(ctx);
+
+	if (rc)
+		return rc;
+	HIPCHK(hipDeviceSynchronize());
+	return 0;
+}
+
+int ecg_dev_copy_kernel(ecg_ctx_t *ctx, void *dst, const void *src, size_t bytes, void *stream)
+{
+	int rc = ecg_ctx_enter(ctx);
+	int e;
+
+	if (rc)
+		return rc;
+	e = ecg_k_launch_copy(src, dst, bytes, (void *)ecg_pick_stream(ctx, stream));
+	if (e)
+		return ecg_hip_fail((hipError_t)e, "copy kernel");
+	ecg_set_last_kernel("ecg_copy_kernel");
+	return 0;
+}

@@ -1,0 +1,249 @@
+/*
+ * ecg_daos.c -- DAOS EC codec surface over the MI355X engine
+ * (see include/ecg_daos.h for the reference function each one mirrors).
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../../include/ecg_daos.h"
+#include "../../../include/ecg_isal.h"
+#include "ecg_internal.h"
+
+int ecg_matmul_host(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
+		    unsigned char *const *src, unsigned char *const *dst, unsigned flags);
+
+/* OR_RS_* order of ref:src/include/daos_obj_class.h:70-80 */
+static const int g_rs_kp[ECG_OR_RS_LAST - ECG_OR_RS_FIRST + 1][2] = {
+	{2, 1}, {2, 2}, {4, 1}, {4, 2}, {8, 1}, {8, 2}, {16, 1}, {16, 2}, {4, 3}, {8, 3}, {16, 3},
+};
+#define N_RS ((int)(sizeof(g_rs_kp) / sizeof(g_rs_kp[0])))
+
+static struct ecg_obj_ec_codec g_codecs[N_RS];
+static int g_codecs_ready;
+static pthread_mutex_t g_codec_lock = PTHREAD_MUTEX_INITIALIZER;
+
+static ecg_ctx_t *g_ctx;
+static int g_ctx_rc;
+static pthread_once_t g_ctx_once = PTHREAD_ONCE_INIT;
+
+static void ctx_init(void)
+{
+	const char *env = getenv("ECG_DEVICE");
+
+	g_ctx_rc = ecg_ctx_create(env ? atoi(env) : 0, &g_ctx);
+}
+
+static int pick_ctx(ecg_ctx_t **ctx)
+{
+	if (*ctx)
+		return 0;
+	pthread_once(&g_ctx_once, ctx_init);
+	if (g_ctx_rc)
+		return g_ctx_rc;
+	*ctx = g_ctx;
+	return 0;
+}
+
+int ecg_obj_ec_class_kp(uint32_t oc_id, int *k, int *p)
+{
+	uint32_t redun = oc_id >> ECG_OC_REDUN_SHIFT;
+
+	if (redun < ECG_OR_RS_FIRST || redun > ECG_OR_RS_LAST)
+		return ecg_fail(-ECG_DER_INVAL, "oc_id 0x%x is not an EC class", oc_id);
+	*k = g_rs_kp[redun - ECG_OR_RS_FIRST][0];
+	*p = g_rs_kp[redun - ECG_OR_RS_FIRST][1];
+	return 0;
+}
+
+void ecg_obj_ec_codec_fini(void)
+{
+	int i;
+
+	pthread_mutex_lock(&g_codec_lock);
+	for (i = 0; i < N_RS; i++) {
+		free(g_codecs[i].ec_en_matrix);
+		free(g_codecs[i].ec_gftbls);
+		memset(&g_codecs[i], 0, sizeof(g_codecs[i]));
+	}
+	g_codecs_ready = 0;
+	pthread_mutex_unlock(&g_codec_lock);
+}
+
+/* obj_ec_codec_init (ref:src/object/obj_class.c:548-631): one Cauchy1
+ * matrix + ISA-L tables per EC redundancy (every group count of a (k, p)
+ * shares it; the reference builds one per class id with identical bytes). */
+int ecg_obj_ec_codec_init(void)
+{
+	int i, rc = 0;
+
+	pthread_mutex_lock(&g_codec_lock);
+	if (g_codecs_ready) {
+		pthread_mutex_unlock(&g_codec_lock);
+		return 0;
+	}
+	for (i = 0; i < N_RS; i++) {
+		struct ecg_obj_ec_codec *c = &g_codecs[i];
+		int k = g_rs_kp[i][0], p = g_rs_kp[i][1];
+
+		c->k = k;
+		c->p = p;
+		c->ec_en_matrix = malloc((size_t)(k + p) * k);
+		c->ec_gftbls = malloc((size_t)k * p * 32);
+		if (c->ec_en_matrix == NULL || c->ec_gftbls == NULL) {
+			rc = ecg_fail(-ECG_DER_NOMEM, "codec_init: malloc");
+			break;
+		}
+		ecg_gen_cauchy1(k, p, c->ec_en_matrix);
+		ec_init_tables(k, p, &c->ec_en_matrix[k * k], c->ec_gftbls);
+	}
+	g_codecs_ready = rc == 0;
+	pthread_mutex_unlock(&g_codec_lock);
+	if (rc)
+		ecg_obj_ec_codec_fini();
+	return rc;
+}
+
+struct ecg_obj_ec_codec *ecg_obj_ec_codec_get(uint32_t oc_id)
+{
+	uint32_t redun = oc_id >> ECG_OC_REDUN_SHIFT;
+
+	if (!g_codecs_ready || redun < ECG_OR_RS_FIRST || redun > ECG_OR_RS_LAST)
+		return NULL;
+	return &g_codecs[redun - ECG_OR_RS_FIRST];
+}
+
+int ecg_obj_ec_encode_buf(uint32_t oc_id, uint64_t cell_bytes, unsigned char *buffer,
+			  unsigned char *p_bufs[])
+{
+	unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
+	unsigned char *data[ECG_MAX_K];
+	ecg_ctx_t *ctx = NULL;
+	int k, p, i, rc;
+
+	rc = ecg_obj_ec_class_kp(oc_id, &k, &p);
+	if (rc)
+		return rc;
+	if (cell_bytes > 0x7fffffffULL)
+		return ecg_fail(-ECG_DER_INVAL, "encode_buf: cell %llu too large",
+				(unsigned long long)cell_bytes);
+	/* same allocation rule as the reference: leading NULL p_bufs only */
+	for (i = 0; i < p && p_bufs[i] == NULL; i++) {
+		p_bufs[i] = malloc(cell_bytes ? cell_bytes : 1);
+		if (p_bufs[i] == NULL)
+			return ecg_fail(-ECG_DER_NOMEM, "encode_buf: malloc");
+	}
+	for (i = 0; i < k; i++)
+		data[i] = buffer + (size_t)i * cell_bytes;
+	rc = pick_ctx(&ctx);
+	if (rc)
+		return rc;
+	ecg_gen_cauchy1(k, p, en);
+	return ecg_matmul_host(ctx, (int)cell_bytes, k, p, &en[k * k], data, p_bufs, 0);
+}
+
+int ecg_obj_ec_recov_codec_init(uint32_t oc_id, const uint32_t *err_list, uint32_t nerrs,
+				struct ecg_obj_ec_recov_codec *rv)
+{
+	unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
+	int k, p, rc, reused = 0;
+	uint32_t i;
+
+	if (rv == NULL || err_list == NULL || nerrs == 0)
+		return ecg_fail(-ECG_DER_INVAL, "recov_codec_init: bad arguments");
+	rc = ecg_obj_ec_class_kp(oc_id, &k, &p);
+	if (rc)
+		return rc;
+	if (nerrs > (uint32_t)p)
+		return ecg_fail(-ECG_DER_DATA_LOSS, "recov_codec_init: nerrs %u > p %d", nerrs, p);
+	memset(rv, 0, sizeof(*rv));
+	rv->k = k;
+	rv->p = p;
+	rv->er_nerrs = nerrs;
+	for (i = 0; i < nerrs; i++) {
+		rv->er_err_list[i] = err_list[i];
+		if (err_list[i] < (uint32_t)k)
+			rv->er_data_nerrs++;
+	}
+	ecg_gen_cauchy1(k, p, en);
+	rc = ecg_recov_matrix(k, p, en, err_list, (int)nerrs, rv->er_de_matrix, rv->er_dec_idx,
+			      &reused);
+	if (rc)
+		return rc;
+	rv->reused_encode = reused;
+	ec_init_tables(k, (int)nerrs, rv->er_de_matrix, rv->er_gftbls);
+	return 0;
+}
+
+int ecg_obj_ec_recov_data(ecg_ctx_t *ctx, const struct ecg_obj_ec_recov_codec *rv,
+			  uint64_t cell_sz, unsigned char *buf_stripes, uint32_t nstripes)
+{
+	int rc;
+
+	if (rv == NULL || buf_stripes == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "recov_data: NULL argument");
+	rc = pick_ctx(&ctx);
+	if (rc)
+		return rc;
+	return ecg_recover_host(ctx, rv->k, rv->p, cell_sz, nstripes, buf_stripes,
+				rv->er_err_list, (int)rv->er_nerrs, 0);
+}
+
+int ecg_obj_ec_encode_stripes(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_bytes,
+			      uint32_t nstripes, const unsigned char *data, unsigned char *parity)
+{
+	int k, p, rc;
+
+	rc = ecg_obj_ec_class_kp(oc_id, &k, &p);
+	if (rc)
+		return rc;
+	rc = pick_ctx(&ctx);
+	if (rc)
+		return rc;
+	return ecg_encode_host(ctx, k, p, cell_bytes, nstripes, data, parity, 0);
+}
+
+/* agg_update_parity (ref:src/object/srv_ec_aggregate.c:1062-1105): for the
+ * i-th updated cell, j = i-th set bit of bit_map;
+ * parity[r] ^= coef[r][j] * (old_i ^ new_i).  All updated cells of the
+ * stripe are folded into one device product. */
+int ecg_agg_update_parity(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_bytes,
+			  const uint8_t *bit_map, uint32_t cell_cnt,
+			  const unsigned char *old_cells, const unsigned char *new_cells,
+			  unsigned char *parity)
+{
+	unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
+	unsigned char coef[ECG_MAX_P * 2 * ECG_MAX_K];
+	unsigned char *src[2 * ECG_MAX_K], *dst[ECG_MAX_P];
+	uint32_t i, j;
+	int k, p, r, rc;
+
+	rc = ecg_obj_ec_class_kp(oc_id, &k, &p);
+	if (rc)
+		return rc;
+	if (cell_cnt == 0)
+		return 0;
+	if (cell_cnt > (uint32_t)k || cell_bytes > 0x7fffffffULL)
+		return ecg_fail(-ECG_DER_INVAL, "agg_update_parity: bad cell_cnt %u", cell_cnt);
+	rc = pick_ctx(&ctx);
+	if (rc)
+		return rc;
+	ecg_gen_cauchy1(k, p, en);
+	/* (old ^ new) * c == old * c ^ new * c: feed both as sources with the
+	 * same coefficient and accumulate into parity. */
+	for (i = 0, j = 0; i < cell_cnt; i++, j++) {
+		while (j < (uint32_t)k && !(bit_map[j / 8] & (1u << (j % 8))))
+			j++;
+		if (j >= (uint32_t)k)
+			return ecg_fail(-ECG_DER_INVAL, "agg_update_parity: bitmap short");
+		src[2 * i] = (unsigned char *)old_cells + (size_t)i * cell_bytes;
+		src[2 * i + 1] = (unsigned char *)new_cells + (size_t)i * cell_bytes;
+		for (r = 0; r < p; r++) {
+			coef[r * 2 * cell_cnt + 2 * i] = en[(k + r) * k + j];
+			coef[r * 2 * cell_cnt + 2 * i + 1] = en[(k + r) * k + j];
+		}
+	}
+	for (r = 0; r < p; r++)
+		dst[r] = parity + (size_t)r * cell_bytes;
+	return ecg_matmul_host(ctx, (int)cell_bytes, (int)(2 * cell_cnt), p, coef, src, dst,
+			       ECG_F_ACCUMULATE);
+}

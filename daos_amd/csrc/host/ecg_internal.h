@@ -1,0 +1,64 @@
+/*
+ * ecg_internal.h -- private declarations of the C host layer.
+ */
+#ifndef ECG_INTERNAL_H
+#define ECG_INTERNAL_H
+
+#define __HIP_PLATFORM_AMD__ 1
+#include <hip/hip_runtime_api.h>
+#include <pthread.h>
+#include <stdint.h>
+
+#include "../../../include/ecg.h"
+#include "../ecg_kabi.h"
+
+#define ECG_RCACHE 16	/* recovery-matrix cache entries per context */
+
+struct ecg_rcache_ent {
+	int valid;
+	int k, p, nerrs;
+	uint32_t err_list[ECG_MAX_P];
+	unsigned char rows[ECG_MAX_P * ECG_MAX_K];	/* data-first order */
+	uint32_t out_idx[ECG_MAX_P];			/* cell each row writes */
+	uint32_t dec_idx[ECG_MAX_K];
+	uint64_t stamp;
+};
+
+/* Host-staging buffers for the PCIe pipeline (per context, 3 slots). */
+#define ECG_NSLOT 3
+struct ecg_stage {
+	size_t dev_bytes;
+	void *dev[ECG_NSLOT];
+	hipStream_t st[ECG_NSLOT];
+	hipEvent_t done[ECG_NSLOT];
+};
+
+struct ecg_ctx {
+	int device;
+	hipStream_t stream;
+	ecg_launch_cfg_t cfg;
+	pthread_mutex_t lock;
+	struct ecg_rcache_ent rcache[ECG_RCACHE];
+	uint64_t rstamp;
+	struct ecg_stage stage;
+};
+
+/* errors (thread-local detail string) */
+int ecg_fail(int rc, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+int ecg_hip_fail(hipError_t e, const char *what);
+void ecg_set_last_kernel(const char *name);
+
+/* GF(2^8) tables (ecg_gf.c) */
+void ecg_gf_init(void);
+extern unsigned char ecg_gf_mul_tbl[256][256];
+void ecg_build_ptbl(unsigned char c, ecg_ptbl_t *t);
+/* data-first decode rows: out_idx[i] = logical cell written by rows[i] */
+int ecg_recov_rows(int k, int p, const unsigned char *en_matrix,
+		   const uint32_t *err_list, int nerrs, unsigned char *rows,
+		   uint32_t *out_idx, uint32_t *dec_idx, int *reused_encode);
+
+/* context helpers (ecg_core.c) */
+int ecg_ctx_enter(ecg_ctx_t *ctx);
+hipStream_t ecg_pick_stream(ecg_ctx_t *ctx, void *stream);
+
+#endif

@@ -1,0 +1,168 @@
+/*
+ * ecg_isal.c -- ISA-L-signature exports (see include/ecg_isal.h).
+ *
+ * Setup functions (matrices, tables) are host code, as in ISA-L.  The
+ * data-plane functions run on the MI355X through ecg_matmul_host; there is
+ * deliberately no CPU path.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../../include/ecg_isal.h"
+#include "ecg_internal.h"
+
+int ecg_matmul_host(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
+		    unsigned char *const *src, unsigned char *const *dst, unsigned flags);
+
+static ecg_ctx_t *g_ctx;
+static int g_ctx_rc;
+static pthread_once_t g_ctx_once = PTHREAD_ONCE_INIT;
+
+static void default_ctx_init(void)
+{
+	const char *env = getenv("ECG_DEVICE");
+	int dev = env ? atoi(env) : 0;
+
+	g_ctx_rc = ecg_ctx_create(dev, &g_ctx);
+}
+
+/* The ISA-L data-plane ABI is `void`: a failure cannot be returned, and
+ * silently skipping the parity would corrupt stored objects.  Fail loudly. */
+static void die(const char *fn, int rc)
+{
+	fprintf(stderr, "ecg: %s failed (rc=%d): %s\n", fn, rc, ecg_strerror());
+	abort();
+}
+
+static ecg_ctx_t *default_ctx(const char *fn)
+{
+	pthread_once(&g_ctx_once, default_ctx_init);
+	if (g_ctx_rc)
+		die(fn, g_ctx_rc);
+	return g_ctx;
+}
+
+void gf_vect_mul_init(unsigned char c, unsigned char *tbl)
+{
+	int n;
+
+	ecg_gf_init();
+	for (n = 0; n < 16; n++) {
+		tbl[n] = ecg_gf_mul_tbl[c][n];
+		tbl[16 + n] = ecg_gf_mul_tbl[c][n << 4];
+	}
+}
+
+void ec_init_tables(int k, int rows, unsigned char *a, unsigned char *gftbls)
+{
+	int i;
+
+	for (i = 0; i < k * rows; i++)
+		gf_vect_mul_init(a[i], gftbls + 32 * i);
+}
+
+static void coef_from_tables(int k, int rows, const unsigned char *gftbls, unsigned char *coef)
+{
+	int i;
+
+	for (i = 0; i < k * rows; i++)
+		coef[i] = gftbls[32 * i + 1];
+}
+
+void ec_encode_data(int len, int k, int rows, unsigned char *gftbls, unsigned char **data,
+		    unsigned char **coding)
+{
+	unsigned char coef[ECG_MAX_K * 256];
+	int rc;
+
+	if (len <= 0 || rows <= 0 || k <= 0)
+		return;
+	if (k > ECG_MAX_K || rows > 256)
+		die("ec_encode_data (k/rows out of range)", -ECG_DER_INVAL);
+	coef_from_tables(k, rows, gftbls, coef);
+	rc = ecg_matmul_host(default_ctx("ec_encode_data"), len, k, rows, coef, data, coding, 0);
+	if (rc)
+		die("ec_encode_data", rc);
+}
+
+void ec_encode_data_update(int len, int k, int rows, int vec_i, unsigned char *gftbls,
+			   unsigned char *data, unsigned char **coding)
+{
+	unsigned char coef[256];
+	unsigned char *src[1];
+	int r, rc;
+
+	if (len <= 0 || rows <= 0)
+		return;
+	if (rows > 256 || vec_i < 0 || vec_i >= k)
+		die("ec_encode_data_update (bad arguments)", -ECG_DER_INVAL);
+	for (r = 0; r < rows; r++)
+		coef[r] = gftbls[32 * (r * k + vec_i) + 1];
+	src[0] = data;
+	rc = ecg_matmul_host(default_ctx("ec_encode_data_update"), len, 1, rows, coef, src, coding,
+			     ECG_F_ACCUMULATE);
+	if (rc)
+		die("ec_encode_data_update", rc);
+}
+
+unsigned char gf_mul(unsigned char a, unsigned char b)
+{
+	return ecg_gf_mul(a, b);
+}
+
+unsigned char gf_inv(unsigned char a)
+{
+	return ecg_gf_inv(a);
+}
+
+void gf_gen_cauchy1_matrix(unsigned char *a, int m, int k)
+{
+	(void)ecg_gen_cauchy1(k, m - k, a);
+}
+
+/* ISA-L gf_gen_rs_matrix: identity, then rows of consecutive powers of
+ * successive generators 1, 2, 4, ... (Vandermonde-like; not used by DAOS). */
+void gf_gen_rs_matrix(unsigned char *a, int m, int k)
+{
+	unsigned char gen = 1;
+	int i, j;
+
+	ecg_gf_init();
+	memset(a, 0, (size_t)k * m);
+	for (i = 0; i < k; i++)
+		a[k * i + i] = 1;
+	for (i = k; i < m; i++) {
+		unsigned char v = 1;
+
+		for (j = 0; j < k; j++) {
+			a[k * i + j] = v;
+			v = ecg_gf_mul_tbl[v][gen];
+		}
+		gen = ecg_gf_mul_tbl[gen][2];
+	}
+}
+
+int gf_invert_matrix(unsigned char *in, unsigned char *out, const int n)
+{
+	return ecg_invert_matrix(in, out, n) == 0 ? 0 : -1;
+}
+
+int xor_gen(int vects, int len, void **array)
+{
+	unsigned char ones[ECG_MAX_K + 256];
+	unsigned char **v = (unsigned char **)array;
+	int rc;
+
+	if (vects < 3)
+		return 1;
+	if (len <= 0)
+		return 0;
+	if (vects - 1 > ECG_MAX_K + 256)
+		return 1;
+	memset(ones, 1, sizeof(ones));
+	rc = ecg_matmul_host(default_ctx("xor_gen"), len, vects - 1, 1, ones, v, &v[vects - 1], 0);
+	if (rc)
+		die("xor_gen", rc);
+	return 0;
+}

@@ -1,0 +1,177 @@
+/*
+ * ecg_stage.c -- synchronous host-memory product over pointer arrays: the
+ * calling convention of ISA-L ec_encode_data (k source pointers, `rows`
+ * destination pointers, arbitrary alignment and length), executed on the GPU
+ * through per-thread pinned staging.  Serves the ISA-L drop-in (ecg_isal.c)
+ * and obj_ec_encode_buf (ecg_daos.c).  One stripe per call is what every
+ * reference caller issues (ref:src/object/cli_ec.c:540, 571, 2641;
+ * ref:src/object/srv_ec_aggregate.c:693, 1136), so this path is PCIe- and
+ * launch-latency-bound by construction; the batched entry points in ecg.h
+ * are the throughput path.
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "ecg_internal.h"
+
+struct tstage {
+	ecg_ctx_t *ctx;
+	int device;
+	void *host;
+	size_t host_bytes;
+	void *dev;
+	size_t dev_bytes;
+	hipStream_t st;
+};
+
+static pthread_key_t g_key;
+static pthread_once_t g_key_once = PTHREAD_ONCE_INIT;
+
+static void tstage_release(struct tstage *t)
+{
+	if (t->st) {
+		(void)hipSetDevice(t->device);
+		(void)hipStreamSynchronize(t->st);
+		(void)hipStreamDestroy(t->st);
+	}
+	if (t->host)
+		(void)hipHostFree(t->host);
+	if (t->dev)
+		(void)hipFree(t->dev);
+	memset(t, 0, sizeof(*t));
+}
+
+static void tstage_dtor(void *p)
+{
+	if (p) {
+		tstage_release(p);
+		free(p);
+	}
+}
+
+static void key_init(void)
+{
+	pthread_key_create(&g_key, tstage_dtor);
+}
+
+static int tstage_get(ecg_ctx_t *ctx, size_t bytes, struct tstage **out)
+{
+	struct tstage *t;
+	hipError_t e;
+
+	pthread_once(&g_key_once, key_init);
+	t = pthread_getspecific(g_key);
+	if (t == NULL) {
+		t = calloc(1, sizeof(*t));
+		if (t == NULL)
+			return ecg_fail(-ECG_DER_NOMEM, "stage: calloc");
+		pthread_setspecific(g_key, t);
+	}
+	if (t->ctx != ctx || t->device != ctx->device)
+		tstage_release(t);
+	t->ctx = ctx;
+	t->device = ctx->device;
+	if (t->st == NULL) {
+		e = hipStreamCreateWithFlags(&t->st, hipStreamNonBlocking);
+		if (e != hipSuccess)
+			return ecg_hip_fail(e, "stage stream");
+	}
+	if (t->host_bytes < bytes) {
+		if (t->host)
+			(void)hipHostFree(t->host);
+		t->host = NULL;
+		t->host_bytes = 0;
+		e = hipHostMalloc(&t->host, bytes, hipHostMallocDefault);
+		if (e != hipSuccess)
+			return ecg_hip_fail(e, "stage pinned alloc");
+		t->host_bytes = bytes;
+	}
+	if (t->dev_bytes < bytes) {
+		if (t->dev)
+			(void)hipFree(t->dev);
+		t->dev = NULL;
+		t->dev_bytes = 0;
+		e = hipMalloc(&t->dev, bytes);
+		if (e != hipSuccess)
+			return ecg_hip_fail(e, "stage device alloc");
+		t->dev_bytes = bytes;
+	}
+	*out = t;
+	return 0;
+}
+
+/*
+ * dst[r][i] (^)= XOR_j coef[r*k + j] * src[j][i], i < len, host pointers.
+ * With ECG_F_ACCUMULATE the current dst bytes travel to the device first
+ * (ec_encode_data_update semantics).
+ */
+int ecg_matmul_host(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
+		    unsigned char *const *src, unsigned char *const *dst, unsigned flags)
+{
+	int64_t soff[ECG_MAX_K + 256], doff[256];
+	struct tstage *t = NULL;
+	size_t pitch, bytes;
+	unsigned char *h, *d;
+	hipError_t e;
+	int rc, j, r;
+
+	if (len < 0 || k < 1 || k > ECG_MAX_K + 256 || rows < 1 || rows > 256)
+		return ecg_fail(-ECG_DER_INVAL, "matmul_host: bad len=%d k=%d rows=%d", len,
+				k, rows);
+	if (len == 0)
+		return 0;
+	if (src == NULL || dst == NULL || coef == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "matmul_host: NULL argument");
+	rc = ecg_ctx_enter(ctx);
+	if (rc)
+		return rc;
+	pitch = ((size_t)len + 255) & ~(size_t)255;
+	bytes = pitch * (size_t)(k + rows);
+	rc = tstage_get(ctx, bytes, &t);
+	if (rc)
+		return rc;
+	h = t->host;
+	d = t->dev;
+	for (j = 0; j < k; j++) {
+		memcpy(h + j * pitch, src[j], (size_t)len);
+		soff[j] = (int64_t)(j * pitch);
+	}
+	for (r = 0; r < rows; r++) {
+		if (flags & ECG_F_ACCUMULATE)
+			memcpy(h + (k + r) * pitch, dst[r], (size_t)len);
+		doff[r] = (int64_t)((k + r) * pitch);
+	}
+	e = hipMemcpyAsync(d, h, (flags & ECG_F_ACCUMULATE) ? bytes : pitch * k,
+			   hipMemcpyHostToDevice, t->st);
+	if (e != hipSuccess)
+		return ecg_hip_fail(e, "matmul_host H2D");
+	if (k <= ECG_MAX_K) {
+		rc = ecg_matmul(ctx, k, rows, coef, (uint64_t)len, 1, d, soff, 0, d, doff, 0,
+				flags, t->st);
+	} else {
+		/* xor_gen may pass more sources than ECG_MAX_K: chain launches */
+		int j0;
+
+		rc = 0;
+		for (j0 = 0; rc == 0 && j0 < k; j0 += ECG_MAX_K) {
+			int kk = k - j0 < ECG_MAX_K ? k - j0 : ECG_MAX_K;
+			unsigned char cc[ECG_MAX_K * 256];
+
+			for (r = 0; r < rows; r++)
+				memcpy(&cc[r * kk], &coef[r * k + j0], kk);
+			rc = ecg_matmul(ctx, kk, rows, cc, (uint64_t)len, 1, d, soff + j0, 0, d,
+					doff, 0, (j0 ? ECG_F_ACCUMULATE : 0) | flags, t->st);
+		}
+	}
+	if (rc)
+		return rc;
+	e = hipMemcpyAsync(h + k * pitch, d + k * pitch, pitch * rows, hipMemcpyDeviceToHost,
+			   t->st);
+	if (e == hipSuccess)
+		e = hipStreamSynchronize(t->st);
+	if (e != hipSuccess)
+		return ecg_hip_fail(e, "matmul_host D2H");
+	for (r = 0; r < rows; r++)
+		memcpy(dst[r], h + (k + r) * pitch, (size_t)len);
+	return 0;
+}

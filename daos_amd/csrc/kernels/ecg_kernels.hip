@@ -1,0 +1,375 @@
+// ecg_kernels.hip -- CDNA4 (gfx950) kernels for the DAOS EC stripe-cell codec.
+//
+// One kernel family computes every hot-path product of SURVEY.md §8a:
+//   encode   (ISA-L ec_encode_data,          ref:src/object/cli_ec.c:540,571)
+//   recovery (DAOS obj_ec_recov_stripe,      ref:src/object/cli_ec.c:2626-2643)
+//   update   (xor_gen + ec_encode_data_update, ref:src/object/srv_ec_aggregate.c:1089-1101)
+// as  dst[s][r] (^)= XOR_j coef[r][j] * src[s][j]  over GF(2^8)/0x11d.
+//
+// Design (MI355X-first, not a port of ISA-L's SIMD):
+//  * Byte-field arithmetic on the VALU; no MFMA.  c*x is linear over
+//    GF(2), so with x = (x&0x07)^(x&0x38)^(x&0xC0) a multiply by a constant is
+//    three 8-entry byte lookups, and one v_perm_b32 does an 8-entry lookup for
+//    4 bytes at once.  Per 4 source bytes per coefficient: 3 v_perm_b32 + 1.5
+//    v_bitop3 (3-way XOR).  The selectors (3 per source dword) are shared by
+//    all output rows.  Tables travel in the kernel arguments (no device-side
+//    table copy, so launches are graph-capturable) and are staged per block
+//    into a few hundred bytes of LDS, read back as broadcasts.
+//  * Memory: each lane owns 16 B of every cell (global_load_dwordx4), a
+//    256-thread block owns a 4 KiB column of one stripe: every wave issues
+//    k x 1 KiB fully coalesced loads before any arithmetic, then p x 1 KiB
+//    dwordx4 stores.  Stripes are independent: no inter-workgroup traffic,
+//    so XCD placement only affects speed, never results.
+//  * Loads/stores are non-temporal: every cell byte is touched exactly once.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../ecg_kabi.h"
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#define CHUNK_BYTES 4096u	// 256 lanes x 16 B
+#define BLOCK 256
+
+__device__ __forceinline__ u32x4 ld_nt(const uint8_t *p)
+{
+	return __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+}
+
+__device__ __forceinline__ void st_nt(uint8_t *p, u32x4 v)
+{
+	__builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
+}
+
+// c*x for the 4 bytes of one dword, given that dword's 3 selector words.
+__device__ __forceinline__ uint32_t gf_mul4(const ecg_ptbl_t &t, uint32_t s0, uint32_t s1, uint32_t s2)
+{
+	return __builtin_amdgcn_perm(t.t0hi, t.t0lo, s0) ^
+	       __builtin_amdgcn_perm(t.t1hi, t.t1lo, s1) ^
+	       __builtin_amdgcn_perm(t.t2, t.t2, s2);
+}
+
+// Byte-granular product for the < 16-byte tail of a cell (and the
+// misaligned fallback): same tables, one byte in the low lane of a dword.
+__device__ __forceinline__ uint8_t gf_mul1(const ecg_ptbl_t &t, uint32_t x)
+{
+	return (uint8_t)gf_mul4(t, x & 7u, (x >> 3) & 7u, x >> 6);
+}
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+	return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// K, R: compile-time data cells / output rows (0 = runtime, bounded by the
+// ECG_KMAX_* maxima).  ACC: XOR into dst.  DIFF: source = src ^ src2.
+//
+// Perm tables are staged once per block from the kernel arguments into LDS,
+// cell-major: for cell j, RM x {t0lo,t0hi,t1lo,t1hi} then the rows' t2 words
+// packed 4 per 16 B.  They are re-read (wave-uniform address -> broadcast,
+// conflict-free ds_read_b128) right before cell j is consumed.  Holding them
+// in registers instead costs 5 x k x rows dwords: that overflows the SGPR
+// file at EC_8P2 (the compiler then spills through v_writelane/v_readlane)
+// and caps VGPR occupancy at 1-2 waves/SIMD for k = 16.  An empty asm on the
+// LDS base each iteration keeps LICM from hoisting the reads back out.
+template <int K, int R, bool ACC, bool DIFF>
+__global__ void __launch_bounds__(BLOCK)
+ecg_mm_kernel(const ecg_mm_params_t P)
+{
+	constexpr int KM = K ? K : ECG_KMAX_K;
+	constexpr int RM = R ? R : ECG_KMAX_R;
+	constexpr int T2V = (RM + 3) / 4;		// u32x4 holding t2 of all rows
+	constexpr int PER_J = RM + T2V;			// u32x4 per cell
+	__shared__ u32x4 s_tbl[KM * PER_J];
+	const int k = K ? K : (int)P.k;
+	const int rows = R ? R : (int)P.rows;
+	const uint64_t C = P.cell_bytes;
+	const uint32_t nchunk = (uint32_t)((C + CHUNK_BYTES - 1) / CHUNK_BYTES);
+
+	for (int i = threadIdx.x; i < KM * RM; i += BLOCK) {
+		const int j = i / RM, r = i % RM;
+		if (j < k && r < rows) {
+			const ecg_ptbl_t &t = P.tbl[r][j];
+			s_tbl[j * PER_J + r] = (u32x4){t.t0lo, t.t0hi, t.t1lo, t.t1hi};
+			reinterpret_cast<uint32_t *>(&s_tbl[j * PER_J + RM])[r] = t.t2;
+		}
+	}
+	__syncthreads();
+
+	for (uint32_t s = blockIdx.y; s < P.nstripes; s += gridDim.y) {
+		const uint8_t *sb = P.src + (int64_t)s * P.src_stripe_stride;
+		const uint8_t *sb2 = DIFF ? P.src2 + (int64_t)s * P.src2_stripe_stride : nullptr;
+		uint8_t *db = P.dst + (int64_t)s * P.dst_stripe_stride;
+
+		for (uint32_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
+			const uint64_t off = (uint64_t)ch * CHUNK_BYTES + threadIdx.x * 16u;
+			uint32_t z = 0;
+
+			asm volatile("" : "+v"(z));
+			const u32x4 *tb = s_tbl + z;
+
+			if (off + 16 <= C) {
+				u32x4 x[KM];
+#pragma unroll
+				for (int j = 0; j < KM; j++) {
+					if (j < k) {
+						x[j] = ld_nt(sb + P.src_cell_off[j] + off);
+						if (DIFF)
+							x[j] ^= ld_nt(sb2 + P.src2_cell_off[j] + off);
+					}
+				}
+				u32x4 acc[RM];
+#pragma unroll
+				for (int r = 0; r < RM; r++) {
+					if (r < rows) {
+						if (ACC)
+							acc[r] = ld_nt(db + P.dst_cell_off[r] + off);
+						else
+							acc[r] = (u32x4){0u, 0u, 0u, 0u};
+					}
+				}
+#pragma unroll
+				for (int j = 0; j < KM; j++) {
+					if (j < k) {
+						u32x4 sel0, sel1, sel2;
+#pragma unroll
+						for (int w = 0; w < 4; w++) {
+							const uint32_t v = x[j][w];
+							sel0[w] = v & 0x07070707u;
+							sel1[w] = (v >> 3) & 0x07070707u;
+							sel2[w] = (v >> 6) & 0x03030303u;
+						}
+						u32x4 t2v[T2V];
+#pragma unroll
+						for (int q = 0; q < T2V; q++)
+							t2v[q] = tb[j * PER_J + RM + q];
+#pragma unroll
+						for (int r = 0; r < RM; r++) {
+							if (r < rows) {
+								const u32x4 t = tb[j * PER_J + r];
+								const uint32_t t2 = t2v[r / 4][r % 4];
+#pragma unroll
+								for (int w = 0; w < 4; w++) {
+									const uint32_t p0 = __builtin_amdgcn_perm(t[1], t[0], sel0[w]);
+									const uint32_t p1 = __builtin_amdgcn_perm(t[3], t[2], sel1[w]);
+									const uint32_t p2 = __builtin_amdgcn_perm(t2, t2, sel2[w]);
+									acc[r][w] = xor3(acc[r][w], p0, xor3(p1, p2, 0u));
+								}
+							}
+						}
+					}
+				}
+#pragma unroll
+				for (int r = 0; r < RM; r++)
+					if (r < rows)
+						st_nt(db + P.dst_cell_off[r] + off, acc[r]);
+			} else if (off < C) {
+				// ragged tail: < 16 bytes of this lane's slot are in the cell
+				const int nb = (int)(C - off);
+
+				for (int b = 0; b < nb; b++) {
+					uint32_t o[RM];
+#pragma unroll
+					for (int r = 0; r < RM; r++)
+						o[r] = 0;
+					for (int j = 0; j < k; j++) {
+						uint32_t v = sb[P.src_cell_off[j] + off + b];
+						if (DIFF)
+							v ^= sb2[P.src2_cell_off[j] + off + b];
+						const uint32_t s0 = v & 7u, s1 = (v >> 3) & 7u, s2 = v >> 6;
+#pragma unroll
+						for (int r = 0; r < RM; r++) {
+							if (r < rows) {
+								const u32x4 t = tb[j * PER_J + r];
+								const uint32_t t2 = reinterpret_cast<const uint32_t *>(
+									&tb[j * PER_J + RM])[r];
+								o[r] ^= __builtin_amdgcn_perm(t[1], t[0], s0) ^
+									__builtin_amdgcn_perm(t[3], t[2], s1) ^
+									__builtin_amdgcn_perm(t2, t2, s2);
+							}
+						}
+					}
+#pragma unroll
+					for (int r = 0; r < RM; r++) {
+						if (r < rows) {
+							uint8_t *d = db + P.dst_cell_off[r] + off + b;
+							*d = ACC ? (uint8_t)(*d ^ o[r]) : (uint8_t)o[r];
+						}
+					}
+				}
+			}
+		}
+	}
+}
+
+// Any alignment, any length: one byte per lane-iteration.  Used only when a
+// caller hands cell bases/strides that are not 16-byte aligned.
+__global__ void __launch_bounds__(BLOCK)
+ecg_mm_byte_kernel(const ecg_mm_params_t P)
+{
+	const uint64_t C = P.cell_bytes;
+	const uint64_t total = C * P.nstripes;
+	const int k = (int)P.k, rows = (int)P.rows;
+
+	for (uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; e < total;
+	     e += (uint64_t)gridDim.x * BLOCK) {
+		const uint64_t s = e / C, i = e % C;
+		const uint8_t *sb = P.src + (int64_t)s * P.src_stripe_stride;
+		const uint8_t *sb2 = P.diff ? P.src2 + (int64_t)s * P.src2_stripe_stride : nullptr;
+		uint8_t *db = P.dst + (int64_t)s * P.dst_stripe_stride;
+		uint8_t o[ECG_KMAX_R];
+
+		for (int r = 0; r < ECG_KMAX_R; r++)
+			o[r] = 0;
+		for (int j = 0; j < k; j++) {
+			uint32_t v = sb[P.src_cell_off[j] + i];
+			if (P.diff)
+				v ^= sb2[P.src2_cell_off[j] + i];
+			for (int r = 0; r < rows; r++)
+				o[r] ^= gf_mul1(P.tbl[r][j], v);
+		}
+		for (int r = 0; r < rows; r++) {
+			uint8_t *d = db + P.dst_cell_off[r] + i;
+			*d = P.accumulate ? (uint8_t)(*d ^ o[r]) : o[r];
+		}
+	}
+}
+
+// Streaming copy, 16 B/lane, used by bench.py to measure this box's
+// achievable HBM rate next to the spec peak.
+__global__ void __launch_bounds__(BLOCK)
+ecg_copy_kernel(const uint8_t *src, uint8_t *dst, uint64_t n16)
+{
+	for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n16;
+	     i += (uint64_t)gridDim.x * BLOCK)
+		st_nt(dst + i * 16, ld_nt(src + i * 16));
+}
+
+// ---------------------------------------------------------------------------
+// Dispatch
+// ---------------------------------------------------------------------------
+typedef void (*mm_fn_t)(const ecg_mm_params_t);
+
+struct kentry {
+	int k, r, acc, diff;
+	mm_fn_t fn;
+	const char *name;
+};
+
+#define KE(K_, R_, A_, D_) \
+	{K_, R_, A_, D_, ecg_mm_kernel<K_, R_, (bool)A_, (bool)D_>, \
+	 "ecg_mm_kernel<" #K_ "," #R_ "," #A_ "," #D_ ">"}
+
+// Specialised shapes: every (k, p) of the DAOS EC classes
+// (ref:src/include/daos_obj_class.h:70-80): k in {2,4,8,16}, rows in 1..3
+// (encode rows = p; recovery rows = nerrs <= p).  Everything else runs the
+// runtime-shaped instantiation (K = R = 0).
+static const kentry g_kernels[] = {
+	KE(2, 1, 0, 0), KE(2, 2, 0, 0), KE(2, 3, 0, 0),
+	KE(4, 1, 0, 0), KE(4, 2, 0, 0), KE(4, 3, 0, 0),
+	KE(8, 1, 0, 0), KE(8, 2, 0, 0), KE(8, 3, 0, 0),
+	KE(16, 1, 0, 0), KE(16, 2, 0, 0), KE(16, 3, 0, 0),
+	KE(0, 0, 0, 0), KE(0, 0, 1, 0), KE(0, 0, 0, 1), KE(0, 0, 1, 1),
+};
+#define N_KERNELS ((uint32_t)(sizeof(g_kernels) / sizeof(g_kernels[0])))
+#define KID_BYTE N_KERNELS
+#define KID_COPY (N_KERNELS + 1)
+
+static bool aligned16(const ecg_mm_params_t *p)
+{
+	uint64_t bits = (uint64_t)(uintptr_t)p->src | (uint64_t)(uintptr_t)p->dst |
+			(uint64_t)p->src_stripe_stride | (uint64_t)p->dst_stripe_stride;
+	for (uint32_t j = 0; j < p->k; j++) {
+		bits |= (uint64_t)p->src_cell_off[j];
+		if (p->diff)
+			bits |= (uint64_t)p->src2_cell_off[j];
+	}
+	if (p->diff)
+		bits |= (uint64_t)(uintptr_t)p->src2 | (uint64_t)p->src2_stripe_stride;
+	for (uint32_t r = 0; r < p->rows; r++)
+		bits |= (uint64_t)p->dst_cell_off[r];
+	return (bits & 15u) == 0;
+}
+
+extern "C" const char *ecg_k_kernel_name(uint32_t id)
+{
+	if (id < N_KERNELS)
+		return g_kernels[id].name;
+	if (id == KID_BYTE)
+		return "ecg_mm_byte_kernel";
+	if (id == KID_COPY)
+		return "ecg_copy_kernel";
+	return "?";
+}
+
+extern "C" int ecg_k_launch_matmul(const ecg_mm_params_t *p, const ecg_launch_cfg_t *cfg,
+				   void *stream, uint32_t *kernel_id)
+{
+	hipStream_t st = (hipStream_t)stream;
+	const uint32_t variant = cfg ? cfg->variant : 0;
+	const uint64_t nchunk = (p->cell_bytes + CHUNK_BYTES - 1) / CHUNK_BYTES;
+
+	if (p->nstripes == 0 || p->cell_bytes == 0 || p->rows == 0)
+		return (int)hipSuccess;
+
+	if (variant == 2 || !aligned16(p)) {
+		uint64_t total = p->cell_bytes * p->nstripes;
+		uint64_t blocks = (total + BLOCK - 1) / BLOCK;
+		if (blocks > 8192)
+			blocks = 8192;
+		hipLaunchKernelGGL(ecg_mm_byte_kernel, dim3((uint32_t)blocks), dim3(BLOCK), 0, st, *p);
+		if (kernel_id)
+			*kernel_id = KID_BYTE;
+		return (int)hipGetLastError();
+	}
+
+	uint32_t id = N_KERNELS;
+	if (variant != 1 && !p->accumulate && !p->diff) {
+		for (uint32_t i = 0; i < N_KERNELS; i++)
+			if (g_kernels[i].k == (int)p->k && g_kernels[i].r == (int)p->rows &&
+			    !g_kernels[i].acc && !g_kernels[i].diff) {
+				id = i;
+				break;
+			}
+	}
+	if (id == N_KERNELS) {
+		for (uint32_t i = 0; i < N_KERNELS; i++)
+			if (g_kernels[i].k == 0 && g_kernels[i].acc == (int)(p->accumulate != 0) &&
+			    g_kernels[i].diff == (int)(p->diff != 0)) {
+				id = i;
+				break;
+			}
+	}
+
+	// Grid: x over the 4 KiB columns of a stripe, y over stripes; both
+	// grid-stride.  Default aims at ~8 resident 256-thread blocks per CU.
+	uint32_t gx = cfg && cfg->grid_x ? cfg->grid_x : (uint32_t)(nchunk < 65535 ? nchunk : 65535);
+	uint32_t gy;
+	if (cfg && cfg->grid_y) {
+		gy = cfg->grid_y;
+	} else {
+		uint64_t want = (2048 * 4 + gx - 1) / gx;
+		gy = (uint32_t)(want < p->nstripes ? want : p->nstripes);
+		if (gy > 65535)
+			gy = 65535;
+		if (gy == 0)
+			gy = 1;
+	}
+	hipLaunchKernelGGL(g_kernels[id].fn, dim3(gx, gy), dim3(BLOCK), 0, st, *p);
+	if (kernel_id)
+		*kernel_id = id;
+	return (int)hipGetLastError();
+}
+
+extern "C" int ecg_k_launch_copy(const void *src, void *dst, uint64_t bytes, void *stream)
+{
+	uint64_t n16 = bytes / 16;
+	uint64_t blocks = (n16 + BLOCK - 1) / BLOCK;
+	if (blocks > 256 * 32)
+		blocks = 256 * 32;
+	if (blocks == 0)
+		return (int)hipSuccess;
+	hipLaunchKernelGGL(ecg_copy_kernel, dim3((uint32_t)blocks), dim3(BLOCK), 0, (hipStream_t)stream,
+			   (const uint8_t *)src, (uint8_t *)dst, n16);
+	return (int)hipGetLastError();
+}

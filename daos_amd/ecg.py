@@ -1,0 +1,358 @@
+"""ctypes binding of libecg.so (include/ecg.h, ecg_isal.h, ecg_daos.h).
+
+This is a thin host-side mirror used by the tests and bench.py: every call
+goes through the C-ABI into the HIP kernels.  There is no Python or CPU
+implementation of the codec here -- if the shared library is missing, or no
+gfx950 device is present, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libecg.so")
+
+DER_INVAL = 1003
+DER_NOMEM = 1009
+DER_NOSYS = 1010
+DER_IO = 2001
+DER_REC2BIG = 2013
+DER_DATA_LOSS = 2026
+F_ACCUMULATE = 1
+
+u8p = C.POINTER(C.c_ubyte)
+u32p = C.POINTER(C.c_uint32)
+i64p = C.POINTER(C.c_int64)
+vp = C.c_void_p
+
+# (name, restype, argtypes) for every function of include/*.h
+_SIGS = [
+    ("ecg_device_count", C.c_int, []),
+    ("ecg_ctx_create", C.c_int, [C.c_int, C.POINTER(vp)]),
+    ("ecg_ctx_destroy", None, [vp]),
+    ("ecg_ctx_device", C.c_int, [vp]),
+    ("ecg_ctx_stream", vp, [vp]),
+    ("ecg_strerror", C.c_char_p, []),
+    ("ecg_last_kernel", C.c_char_p, []),
+    ("ecg_gf_mul", C.c_ubyte, [C.c_ubyte, C.c_ubyte]),
+    ("ecg_gf_inv", C.c_ubyte, [C.c_ubyte]),
+    ("ecg_gen_cauchy1", C.c_int, [C.c_int, C.c_int, u8p]),
+    ("ecg_invert_matrix", C.c_int, [u8p, u8p, C.c_int]),
+    ("ecg_recov_matrix", C.c_int, [C.c_int, C.c_int, u8p, u32p, C.c_int, u8p, u32p, C.POINTER(C.c_int)]),
+    ("ecg_matmul", C.c_int, [vp, C.c_int, C.c_int, u8p, C.c_uint64, C.c_uint32, vp, i64p, C.c_int64,
+                             vp, i64p, C.c_int64, C.c_uint, vp]),
+    ("ecg_encode", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, vp, C.c_int64, vp, C.c_int64,
+                             C.c_int64, vp]),
+    ("ecg_recover", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, vp, C.c_int64, u32p, C.c_int, vp]),
+    ("ecg_update", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, C.c_int, u32p, vp, vp, C.c_int64,
+                             vp, C.c_int64, C.c_int64, vp]),
+    ("ecg_matmul_host", C.c_int, [vp, C.c_int, C.c_int, C.c_int, u8p, C.POINTER(u8p), C.POINTER(u8p), C.c_uint]),
+    ("ecg_encode_host", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, vp, vp, C.c_uint32]),
+    ("ecg_recover_host", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, vp, u32p, C.c_int, C.c_uint32]),
+    ("ecg_dev_alloc", C.c_int, [vp, C.c_size_t, C.POINTER(vp)]),
+    ("ecg_dev_free", C.c_int, [vp, vp]),
+    ("ecg_host_alloc", C.c_int, [vp, C.c_size_t, C.POINTER(vp)]),
+    ("ecg_host_free", C.c_int, [vp, vp]),
+    ("ecg_memcpy", C.c_int, [vp, vp, vp, C.c_size_t, C.c_int, vp]),
+    ("ecg_memset", C.c_int, [vp, vp, C.c_int, C.c_size_t, vp]),
+    ("ecg_stream_create", C.c_int, [vp, C.POINTER(vp)]),
+    ("ecg_stream_destroy", C.c_int, [vp, vp]),
+    ("ecg_stream_sync", C.c_int, [vp, vp]),
+    ("ecg_event_create", C.c_int, [vp, C.POINTER(vp)]),
+    ("ecg_event_destroy", C.c_int, [vp, vp]),
+    ("ecg_event_record", C.c_int, [vp, vp, vp]),
+    ("ecg_event_elapsed_ms", C.c_int, [vp, vp, vp, C.POINTER(C.c_float)]),
+    ("ecg_device_sync", C.c_int, [vp]),
+    ("ecg_dev_copy_kernel", C.c_int, [vp, vp, vp, C.c_size_t, vp]),
+    ("ecg_set_launch", C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_uint32]),
+    # ISA-L drop-in (ecg_isal.h)
+    ("ec_init_tables", None, [C.c_int, C.c_int, u8p, u8p]),
+    ("ec_encode_data", None, [C.c_int, C.c_int, C.c_int, u8p, C.POINTER(u8p), C.POINTER(u8p)]),
+    ("ec_encode_data_update", None, [C.c_int, C.c_int, C.c_int, C.c_int, u8p, u8p, C.POINTER(u8p)]),
+    ("gf_vect_mul_init", None, [C.c_ubyte, u8p]),
+    ("gf_mul", C.c_ubyte, [C.c_ubyte, C.c_ubyte]),
+    ("gf_inv", C.c_ubyte, [C.c_ubyte]),
+    ("gf_gen_rs_matrix", None, [u8p, C.c_int, C.c_int]),
+    ("gf_gen_cauchy1_matrix", None, [u8p, C.c_int, C.c_int]),
+    ("gf_invert_matrix", C.c_int, [u8p, u8p, C.c_int]),
+    ("xor_gen", C.c_int, [C.c_int, C.c_int, C.POINTER(vp)]),
+    # DAOS codec surface (ecg_daos.h)
+    ("ecg_obj_ec_codec_init", C.c_int, []),
+    ("ecg_obj_ec_codec_fini", None, []),
+    ("ecg_obj_ec_codec_get", vp, [C.c_uint32]),
+    ("ecg_obj_ec_class_kp", C.c_int, [C.c_uint32, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    ("ecg_obj_ec_encode_buf", C.c_int, [C.c_uint32, C.c_uint64, u8p, C.POINTER(u8p)]),
+    ("ecg_obj_ec_recov_codec_init", C.c_int, [C.c_uint32, u32p, C.c_uint32, vp]),
+    ("ecg_obj_ec_recov_data", C.c_int, [vp, vp, C.c_uint64, u8p, C.c_uint32]),
+    ("ecg_obj_ec_encode_stripes", C.c_int, [vp, C.c_uint32, C.c_uint64, C.c_uint32, u8p, u8p]),
+    ("ecg_agg_update_parity", C.c_int, [vp, C.c_uint32, C.c_uint64, u8p, C.c_uint32, u8p, u8p, u8p]),
+]
+
+EXPORTED = [n for n, _, _ in _SIGS]
+
+_lib = None
+
+
+class EcgError(RuntimeError):
+    def __init__(self, rc: int, what: str):
+        self.rc = rc
+        super().__init__(f"{what}: rc={rc} ({lib().ecg_strerror().decode(errors='replace')})")
+
+
+def lib():
+    """Load libecg.so (built in-tree by __graft_entry__.build()).  Raises if absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in _SIGS:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _chk(rc: int, what: str):
+    if rc != 0:
+        raise EcgError(rc, what)
+
+
+def _u8(a: np.ndarray):
+    return a.ctypes.data_as(u8p)
+
+
+def _u32(seq) -> C.Array:
+    return (C.c_uint32 * max(1, len(seq)))(*seq)
+
+
+def _i64(seq) -> C.Array:
+    return (C.c_int64 * max(1, len(seq)))(*seq)
+
+
+def device_count() -> int:
+    return lib().ecg_device_count()
+
+
+def last_kernel() -> str:
+    return lib().ecg_last_kernel().decode()
+
+
+# ---------------------------------------------------------------- host math
+def gf_mul(a: int, b: int) -> int:
+    return lib().ecg_gf_mul(a, b)
+
+
+def gf_inv(a: int) -> int:
+    return lib().ecg_gf_inv(a)
+
+
+def cauchy1(k: int, p: int) -> np.ndarray:
+    m = np.zeros((k + p) * k, dtype=np.uint8)
+    _chk(lib().ecg_gen_cauchy1(k, p, _u8(m)), "gen_cauchy1")
+    return m.reshape(k + p, k)
+
+
+def invert(mat: np.ndarray):
+    n = mat.shape[0]
+    a = np.ascontiguousarray(mat, dtype=np.uint8).copy()
+    out = np.zeros((n, n), dtype=np.uint8)
+    rc = lib().ecg_invert_matrix(_u8(a), _u8(out), n)
+    return None if rc else out
+
+
+def recov_matrix(k: int, p: int, err_list: Sequence[int]):
+    """-> (rows [nerrs, k] in err_list order, dec_idx [k], reused_encode)."""
+    en = cauchy1(k, p).reshape(-1).copy()
+    rows = np.zeros(max(1, len(err_list)) * k, dtype=np.uint8)
+    dec = (C.c_uint32 * k)()
+    reused = C.c_int(0)
+    _chk(lib().ecg_recov_matrix(k, p, _u8(en), _u32(err_list), len(err_list), _u8(rows), dec, C.byref(reused)),
+         "recov_matrix")
+    return rows.reshape(-1, k)[: len(err_list)], np.array(list(dec), dtype=np.uint32), bool(reused.value)
+
+
+# ---------------------------------------------------------------- device side
+class DeviceBuffer:
+    def __init__(self, ctx: "Context", nbytes: int):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = vp()
+        _chk(lib().ecg_dev_alloc(ctx.h, self.nbytes, C.byref(p)), "dev_alloc")
+        self.ptr = p.value
+
+    def upload(self, arr: np.ndarray, offset: int = 0, stream=None):
+        a = np.ascontiguousarray(arr)
+        assert offset + a.nbytes <= self.nbytes
+        _chk(lib().ecg_memcpy(self.ctx.h, self.ptr + offset, a.ctypes.data, a.nbytes, 0, stream), "H2D")
+        self.ctx.sync(stream)
+
+    def download(self, nbytes: int | None = None, offset: int = 0, stream=None) -> np.ndarray:
+        n = self.nbytes - offset if nbytes is None else nbytes
+        out = np.empty(n, dtype=np.uint8)
+        _chk(lib().ecg_memcpy(self.ctx.h, out.ctypes.data, self.ptr + offset, n, 1, stream), "D2H")
+        self.ctx.sync(stream)
+        return out
+
+    def fill(self, value: int, stream=None):
+        _chk(lib().ecg_memset(self.ctx.h, self.ptr, value, self.nbytes, stream), "memset")
+
+    def free(self):
+        if self.ptr:
+            _chk(lib().ecg_dev_free(self.ctx.h, self.ptr), "dev_free")
+            self.ptr = 0
+
+
+class HostBuffer:
+    """Pinned host memory exposed as a numpy uint8 array."""
+
+    def __init__(self, ctx: "Context", nbytes: int):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = vp()
+        _chk(lib().ecg_host_alloc(ctx.h, self.nbytes, C.byref(p)), "host_alloc")
+        self.ptr = p.value
+        self.array = np.ctypeslib.as_array((C.c_ubyte * self.nbytes).from_address(self.ptr))
+
+    def free(self):
+        if self.ptr:
+            self.array = None
+            _chk(lib().ecg_host_free(self.ctx.h, self.ptr), "host_free")
+            self.ptr = 0
+
+
+class Context:
+    """One per device; mirrors ecg_ctx_t."""
+
+    def __init__(self, device: int = 0):
+        h = vp()
+        _chk(lib().ecg_ctx_create(device, C.byref(h)), f"ctx_create(device={device})")
+        self.h = h.value
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib().ecg_ctx_destroy(self.h)
+            self.h = None
+
+    # plumbing
+    def alloc(self, nbytes: int) -> DeviceBuffer:
+        return DeviceBuffer(self, nbytes)
+
+    def host_alloc(self, nbytes: int) -> HostBuffer:
+        return HostBuffer(self, nbytes)
+
+    def to_device(self, arr: np.ndarray) -> DeviceBuffer:
+        a = np.ascontiguousarray(arr, dtype=np.uint8)
+        b = DeviceBuffer(self, max(1, a.nbytes))
+        b.upload(a)
+        return b
+
+    def sync(self, stream=None):
+        _chk(lib().ecg_stream_sync(self.h, stream), "stream_sync")
+
+    def stream(self):
+        s = vp()
+        _chk(lib().ecg_stream_create(self.h, C.byref(s)), "stream_create")
+        return s.value
+
+    def destroy_stream(self, s):
+        _chk(lib().ecg_stream_destroy(self.h, s), "stream_destroy")
+
+    def event(self):
+        e = vp()
+        _chk(lib().ecg_event_create(self.h, C.byref(e)), "event_create")
+        return e.value
+
+    def record(self, ev, stream=None):
+        _chk(lib().ecg_event_record(self.h, ev, stream), "event_record")
+
+    def elapsed_ms(self, a, b) -> float:
+        ms = C.c_float()
+        _chk(lib().ecg_event_elapsed_ms(self.h, a, b, C.byref(ms)), "event_elapsed")
+        return ms.value
+
+    def destroy_event(self, e):
+        _chk(lib().ecg_event_destroy(self.h, e), "event_destroy")
+
+    def set_launch(self, grid_x: int = 0, grid_y: int = 0, variant: int = 0):
+        _chk(lib().ecg_set_launch(self.h, grid_x, grid_y, variant), "set_launch")
+
+    def copy_kernel(self, dst: int, src: int, nbytes: int, stream=None):
+        _chk(lib().ecg_dev_copy_kernel(self.h, dst, src, nbytes, stream), "copy_kernel")
+
+    # codec
+    def matmul(self, coef: np.ndarray, cell_bytes: int, nstripes: int, src: int, src_off, src_stride: int,
+               dst: int, dst_off, dst_stride: int, flags: int = 0, stream=None):
+        coef = np.ascontiguousarray(coef, dtype=np.uint8)
+        rows, k = coef.shape
+        _chk(lib().ecg_matmul(self.h, k, rows, _u8(coef), cell_bytes, nstripes, src, _i64(src_off), src_stride,
+                              dst, _i64(dst_off), dst_stride, flags, stream), "matmul")
+
+    def encode(self, k: int, p: int, cell_bytes: int, nstripes: int, data: int, data_stripe_stride: int,
+               parity: int, parity_cell_stride: int, parity_stripe_stride: int, stream=None):
+        _chk(lib().ecg_encode(self.h, k, p, cell_bytes, nstripes, data, data_stripe_stride, parity,
+                              parity_cell_stride, parity_stripe_stride, stream), "encode")
+
+    def recover(self, k: int, p: int, cell_bytes: int, nstripes: int, stripes: int, stripe_stride: int,
+                err_list: Sequence[int], stream=None):
+        _chk(lib().ecg_recover(self.h, k, p, cell_bytes, nstripes, stripes, stripe_stride, _u32(err_list),
+                               len(err_list), stream), "recover")
+
+    def update(self, k: int, p: int, cell_bytes: int, nstripes: int, cell_idx: Sequence[int], old: int, new: int,
+               upd_stripe_stride: int, parity: int, parity_cell_stride: int, parity_stripe_stride: int,
+               stream=None):
+        _chk(lib().ecg_update(self.h, k, p, cell_bytes, nstripes, len(cell_idx), _u32(cell_idx), old, new,
+                              upd_stripe_stride, parity, parity_cell_stride, parity_stripe_stride, stream),
+             "update")
+
+    def encode_host(self, k: int, p: int, cell_bytes: int, nstripes: int, data: np.ndarray, parity: np.ndarray,
+                    chunk: int = 0):
+        _chk(lib().ecg_encode_host(self.h, k, p, cell_bytes, nstripes, data.ctypes.data, parity.ctypes.data,
+                                   chunk), "encode_host")
+
+    def recover_host(self, k: int, p: int, cell_bytes: int, nstripes: int, stripes: np.ndarray,
+                     err_list: Sequence[int], chunk: int = 0):
+        _chk(lib().ecg_recover_host(self.h, k, p, cell_bytes, nstripes, stripes.ctypes.data, _u32(err_list),
+                                    len(err_list), chunk), "recover_host")
+
+    def matmul_host(self, coef: np.ndarray, src: Sequence[np.ndarray], dst: Sequence[np.ndarray], flags: int = 0):
+        coef = np.ascontiguousarray(coef, dtype=np.uint8)
+        rows, k = coef.shape
+        n = src[0].shape[0]
+        sp = (u8p * k)(*[_u8(s) for s in src])
+        dp = (u8p * rows)(*[_u8(d) for d in dst])
+        _chk(lib().ecg_matmul_host(self.h, n, k, rows, _u8(coef), sp, dp, flags), "matmul_host")
+
+
+# ---------------------------------------------------------------- ISA-L drop-in
+def isal_init_tables(coef: np.ndarray) -> np.ndarray:
+    rows, k = coef.shape
+    t = np.zeros(rows * k * 32, dtype=np.uint8)
+    c = np.ascontiguousarray(coef, dtype=np.uint8)
+    lib().ec_init_tables(k, rows, _u8(c), _u8(t))
+    return t
+
+
+def isal_encode_data(gftbls: np.ndarray, k: int, rows: int, data: Sequence[np.ndarray],
+                     coding: Sequence[np.ndarray]):
+    n = data[0].shape[0]
+    sp = (u8p * k)(*[_u8(d) for d in data])
+    dp = (u8p * rows)(*[_u8(c) for c in coding])
+    lib().ec_encode_data(n, k, rows, _u8(gftbls), sp, dp)
+
+
+def isal_encode_data_update(gftbls: np.ndarray, k: int, rows: int, vec_i: int, delta: np.ndarray,
+                            coding: Sequence[np.ndarray]):
+    dp = (u8p * rows)(*[_u8(c) for c in coding])
+    lib().ec_encode_data_update(delta.shape[0], k, rows, vec_i, _u8(gftbls), _u8(delta), dp)
+
+
+def isal_xor_gen(arrs: Sequence[np.ndarray]) -> int:
+    v = (vp * len(arrs))(*[a.ctypes.data for a in arrs])
+    return lib().xor_gen(len(arrs), arrs[0].shape[0], v)

@@ -1,0 +1,178 @@
+/*
+ * ecg.h -- MI355X-native Reed-Solomon erasure-coding engine for DAOS EC
+ * objects: the core C-ABI.
+ *
+ * Plain C, host pointers / device pointers / sizes only (no HIP, no torch
+ * types).  Streams are opaque `void *` (a hipStream_t; NULL = the context's
+ * own stream).  Every function returns 0 or a negative DAOS errno
+ * (ref:src/include/daos_errno.h); ecg_strerror() gives the detail of the last
+ * failure on the calling thread.  All entry points are thread-safe.
+ *
+ * What this replaces: the arithmetic boundary of DAOS's EC
+ * object class -- ISA-L ec_encode_data / ec_encode_data_update / xor_gen as
+ * called from ref:src/object/cli_ec.c:540,571,2641,
+ * ref:src/object/srv_ec_aggregate.c:693,1092,1099,1136 -- batched over stripes
+ * and executed by hand-written gfx950 kernels on device-resident cells.
+ * The ISA-L-signature drop-in is ecg_isal.h; the DAOS codec surface
+ * (obj_ec_codec_*, obj_ec_encode_buf, recovery codec) is ecg_daos.h.
+ *
+ * Arithmetic is GF(2^8) with polynomial 0x11d and generator 2, bit-exact with
+ * ISA-L's ec_encode_data_base (and therefore with every ISA-L SIMD path).
+ */
+#ifndef ECG_H
+#define ECG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Negative DAOS errno values (ref:src/include/daos_errno.h). */
+#define ECG_DER_INVAL		1003
+#define ECG_DER_NOMEM		1009
+#define ECG_DER_NOSYS		1010	/* no gfx950 device / HIP runtime */
+#define ECG_DER_IO		2001	/* HIP runtime or kernel failure */
+#define ECG_DER_REC2BIG		2013
+#define ECG_DER_DATA_LOSS	2026	/* more erasures than parity cells */
+
+/* Limits (ref:src/object/obj_ec.h:16-20, ref:src/object/obj_class.c:587-601). */
+#define ECG_MAX_K		64
+#define ECG_MAX_P		8
+
+/* Flags for ecg_matmul */
+#define ECG_F_ACCUMULATE	0x1u	/* dst ^= product (else dst = product) */
+
+typedef struct ecg_ctx ecg_ctx_t;
+
+/* ---- context / device ---------------------------------------------------- */
+/* Number of usable (gfx950) HIP devices; 0 when none.  Never fails. */
+int ecg_device_count(void);
+/* Binds a context to `device` (index into the visible HIP devices).
+ * -ECG_DER_NOSYS when the device is absent or not gfx950: there is no CPU
+ * fallback in the product path. */
+int ecg_ctx_create(int device, ecg_ctx_t **ctx);
+void ecg_ctx_destroy(ecg_ctx_t *ctx);
+int ecg_ctx_device(const ecg_ctx_t *ctx);
+/* The context's default stream (used when a call passes stream == NULL). */
+void *ecg_ctx_stream(ecg_ctx_t *ctx);
+const char *ecg_strerror(void);
+/* Name of the kernel the last ecg_* compute call on this thread launched. */
+const char *ecg_last_kernel(void);
+
+/* ---- field and matrices (host; setup only) ------------------------------- */
+unsigned char ecg_gf_mul(unsigned char a, unsigned char b);
+unsigned char ecg_gf_inv(unsigned char a);
+/* (k+p) x k Cauchy1 encode matrix: identity rows then 1/(i ^ j), the matrix
+ * DAOS builds per EC class (ref:src/object/obj_class.c:611-617). */
+int ecg_gen_cauchy1(int k, int p, unsigned char *en_matrix);
+/* n x n inverse over GF(2^8); `in` is destroyed; -ECG_DER_INVAL if singular. */
+int ecg_invert_matrix(unsigned char *in, unsigned char *out, int n);
+/* DAOS recovery codec (ref:src/object/cli_ec.c:2152-2250): for LOGICAL error
+ * indices err_list[nerrs] (cells 0..k-1 data, k..k+p-1 parity) produce the
+ * decode rows (nerrs x k, in err_list order), dec_idx[k] (the surviving cells
+ * they consume) and *reused_encode (1 when all p parity cells and no data
+ * cell are lost: rows are then the encode parity rows and dec_idx = 0..k-1,
+ * ref:src/object/cli_ec.c:2205-2210).  -ECG_DER_DATA_LOSS when nerrs > p. */
+int ecg_recov_matrix(int k, int p, const unsigned char *en_matrix,
+		     const uint32_t *err_list, int nerrs, unsigned char *de_rows,
+		     uint32_t *dec_idx, int *reused_encode);
+
+/* ---- device-resident batched codec (the hot path) ----------------------- */
+/*
+ * dst cell r of stripe s  (^)=  XOR_{j<k} coef[r*k + j] * (src cell j of s)
+ * for every byte i < cell_bytes and every stripe s < nstripes, where
+ *   src cell j of s = src + s*src_stripe_stride + src_cell_off[j]
+ *   dst cell r of s = dst + s*dst_stripe_stride + dst_cell_off[r]
+ * All pointers are device pointers.  k <= 64, rows <= 8 (larger k is split
+ * into accumulating launches).  16-byte aligned cells take the vector
+ * kernels; anything else runs a byte kernel (same results, slower).
+ * Asynchronous on `stream`.
+ */
+int ecg_matmul(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef,
+	       uint64_t cell_bytes, uint32_t nstripes,
+	       const void *src, const int64_t *src_cell_off, int64_t src_stripe_stride,
+	       void *dst, const int64_t *dst_cell_off, int64_t dst_stripe_stride,
+	       unsigned flags, void *stream);
+
+/* Full-stripe encode with the Cauchy1 matrix (ISA-L ec_encode_data with the
+ * DAOS codec tables).  Data cell j of stripe s at
+ *   data + s*data_stripe_stride + j*cell_bytes,
+ * parity cell r of stripe s at
+ *   parity + r*parity_cell_stride + s*parity_stripe_stride.
+ * Client write layout (ref:src/object/cli_ec.c:75-97,638-640): data [S][k][C],
+ * parity [p][S][C] => data_stripe_stride = k*C, parity_cell_stride = S*C,
+ * parity_stripe_stride = C.  Recovery layout [S][k+p][C] => parity = data +
+ * k*C, parity_cell_stride = C, both stripe strides (k+p)*C. */
+int ecg_encode(ecg_ctx_t *ctx, int k, int p, uint64_t cell_bytes, uint32_t nstripes,
+	       const void *data, int64_t data_stripe_stride,
+	       void *parity, int64_t parity_cell_stride, int64_t parity_stripe_stride,
+	       void *stream);
+
+/* In-place degraded-read / rebuild recovery over stripes laid out
+ * [S][k+p][cell_bytes] in logical cell order, stripe s at
+ * stripes + s*stripe_stride (obj_ec_recov_data, ref:src/object/cli_ec.c:
+ * 2814-2885).  Erased cells (logical indices) are regenerated from the first
+ * k survivors.  Decode matrices are cached per (k, p, err_list). */
+int ecg_recover(ecg_ctx_t *ctx, int k, int p, uint64_t cell_bytes, uint32_t nstripes,
+		void *stripes, int64_t stripe_stride,
+		const uint32_t *err_list, int nerrs, void *stream);
+
+/* Aggregation delta parity update (xor_gen + ec_encode_data_update fused,
+ * ref:src/object/srv_ec_aggregate.c:1062-1105), batched over stripes:
+ *   parity[r] ^= XOR_u coef[r][cell_idx[u]] * (old[u] ^ new[u])
+ * for the nupd updated data cells of each stripe.  Cell u of stripe s:
+ *   old_cells + s*old_stripe_stride + u*cell_bytes (same for new_cells);
+ * parity cell r of stripe s: parity + r*parity_cell_stride + s*parity_stripe_stride. */
+int ecg_update(ecg_ctx_t *ctx, int k, int p, uint64_t cell_bytes, uint32_t nstripes,
+	       int nupd, const uint32_t *cell_idx,
+	       const void *old_cells, const void *new_cells, int64_t upd_stripe_stride,
+	       void *parity, int64_t parity_cell_stride, int64_t parity_stripe_stride,
+	       void *stream);
+
+/* ---- host-resident pipeline (PCIe-inclusive) ---------------------------- */
+/* One stripe, ISA-L ec_encode_data calling convention: host pointers
+ * src[k], dst[rows] (any alignment), `len` bytes each;
+ * dst[r] (^)= XOR_j coef[r*k+j] * src[j].  Executed on the GPU through
+ * per-thread pinned staging; synchronous.  k may exceed ECG_MAX_K (xor_gen). */
+int ecg_matmul_host(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
+		    unsigned char *const *src, unsigned char *const *dst, unsigned flags);
+/* Encode host-resident stripes (data [S][k][C], parity [p][S][C] in host
+ * memory; pinned memory from ecg_host_alloc is fastest) by streaming chunks
+ * of `chunk_stripes` through device staging on 3 rotating streams
+ * (H2D / kernel / D2H overlap).  Synchronous. */
+int ecg_encode_host(ecg_ctx_t *ctx, int k, int p, uint64_t cell_bytes, uint32_t nstripes,
+		    const void *data, void *parity, uint32_t chunk_stripes);
+/* Same for recovery over host [S][k+p][C] stripes: only survivors travel
+ * H2D, only regenerated cells travel D2H.  Synchronous. */
+int ecg_recover_host(ecg_ctx_t *ctx, int k, int p, uint64_t cell_bytes, uint32_t nstripes,
+		     void *stripes, const uint32_t *err_list, int nerrs,
+		     uint32_t chunk_stripes);
+
+/* ---- memory / streams / timing plumbing --------------------------------- */
+int ecg_dev_alloc(ecg_ctx_t *ctx, size_t bytes, void **ptr);
+int ecg_dev_free(ecg_ctx_t *ctx, void *ptr);
+int ecg_host_alloc(ecg_ctx_t *ctx, size_t bytes, void **ptr);	/* pinned */
+int ecg_host_free(ecg_ctx_t *ctx, void *ptr);
+/* kind: 0 H2D, 1 D2H, 2 D2D, 3 default (runtime infers). Async on stream. */
+int ecg_memcpy(ecg_ctx_t *ctx, void *dst, const void *src, size_t bytes, int kind, void *stream);
+int ecg_memset(ecg_ctx_t *ctx, void *dst, int value, size_t bytes, void *stream);
+int ecg_stream_create(ecg_ctx_t *ctx, void **stream);
+int ecg_stream_destroy(ecg_ctx_t *ctx, void *stream);
+int ecg_stream_sync(ecg_ctx_t *ctx, void *stream);
+int ecg_event_create(ecg_ctx_t *ctx, void **event);
+int ecg_event_destroy(ecg_ctx_t *ctx, void *event);
+int ecg_event_record(ecg_ctx_t *ctx, void *event, void *stream);
+int ecg_event_elapsed_ms(ecg_ctx_t *ctx, void *start, void *stop, float *ms);
+int ecg_device_sync(ecg_ctx_t *ctx);
+/* Streaming device copy (16 B/lane) used to measure achievable HBM rate. */
+int ecg_dev_copy_kernel(ecg_ctx_t *ctx, void *dst, const void *src, size_t bytes, void *stream);
+
+/* ---- launch tuning (benchmarks; 0 = default) ---------------------------- */
+int ecg_set_launch(ecg_ctx_t *ctx, uint32_t grid_x, uint32_t grid_y, uint32_t variant);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

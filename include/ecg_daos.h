@@ -1,0 +1,113 @@
+/*
+ * ecg_daos.h -- the DAOS EC codec surface (src/object/obj_ec.h) backed by
+ * the MI355X engine.
+ *
+ * Mirrors, with the same argument meaning, return codes and buffer
+ * ownership, the codec functions of ref:src/object/obj_ec.h:731-845 and
+ * ref:src/object/cli_ec.c.  DAOS-private aggregates (dc_object,
+ * obj_reasb_req, daos_oclass_attr) are replaced by the scalars the codec
+ * actually consumes (class id, k, p, cell bytes, LOGICAL cell indices --
+ * the obj_ec_shard_off physical->logical mapping stays in the caller).
+ * Names carry an ecg_ prefix so the library links next to libdaos; the
+ * maintainer's glue forwards the reference functions here.
+ *
+ *   ecg_obj_ec_codec_init/fini/get  <- obj_ec_codec_init/fini/get
+ *                                      ref:src/object/obj_class.c:511-649
+ *   ecg_obj_ec_encode_buf           <- obj_ec_encode_buf
+ *                                      ref:src/object/cli_ec.c:548-573
+ *   ecg_obj_ec_recov_codec_init     <- obj_ec_recov_codec_alloc + _init
+ *                                      ref:src/object/cli_ec.c:1953-1993, 2152-2250
+ *   ecg_obj_ec_recov_data           <- obj_ec_recov_data's stripe loop over
+ *                                      obj_ec_recov_stripe
+ *                                      ref:src/object/cli_ec.c:2626-2643, 2814-2885
+ *   ecg_obj_ec_encode_stripes       <- obj_ec_recx_encode's stripe loop
+ *                                      ref:src/object/cli_ec.c:593-663
+ *   ecg_agg_update_parity           <- agg_update_parity
+ *                                      ref:src/object/srv_ec_aggregate.c:1062-1105
+ */
+#ifndef ECG_DAOS_H
+#define ECG_DAOS_H
+
+#include <stdint.h>
+
+#include "ecg.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Object class id = (redundancy << 24) | group count
+ * (ref:src/include/daos_obj_class.h:22-23); EC redundancy OR_RS_2P1 = 32 ..
+ * OR_RS_16P3 = 42 (ref:src/include/daos_obj_class.h:70-80). */
+#define ECG_OC_REDUN_SHIFT	24
+#define ECG_OR_RS_FIRST		32
+#define ECG_OR_RS_LAST		42
+
+/* struct obj_ec_codec (ref:src/object/obj_ec.h:33-41) + its k, p. */
+struct ecg_obj_ec_codec {
+	unsigned char *ec_en_matrix;	/* (k+p) x k Cauchy1 */
+	unsigned char *ec_gftbls;	/* k*p*32 ISA-L-layout tables */
+	int k;
+	int p;
+};
+
+/* struct obj_ec_recov_codec (ref:src/object/obj_ec.h:213-224). */
+struct ecg_obj_ec_recov_codec {
+	unsigned char er_gftbls[ECG_MAX_K * ECG_MAX_P * 32];
+	unsigned char er_de_matrix[ECG_MAX_P * ECG_MAX_K];	/* err_list order */
+	uint32_t er_dec_idx[ECG_MAX_K];
+	uint32_t er_err_list[ECG_MAX_P];			/* logical cells */
+	uint32_t er_nerrs;
+	uint32_t er_data_nerrs;
+	int k;
+	int p;
+	int reused_encode;	/* all-parity-lost shortcut (cli_ec.c:2205-2210) */
+};
+
+/* 0, or -ECG_DER_NOMEM. Idempotent. */
+int ecg_obj_ec_codec_init(void);
+void ecg_obj_ec_codec_fini(void);
+/* NULL when oc_id is not an EC class (or init has not run). */
+struct ecg_obj_ec_codec *ecg_obj_ec_codec_get(uint32_t oc_id);
+/* The k, p of an EC class id; -ECG_DER_INVAL if not EC. */
+int ecg_obj_ec_class_kp(uint32_t oc_id, int *k, int *p);
+
+/* Encode one contiguous stripe buffer[k*cell_bytes] into p_bufs[p].  As in
+ * the reference, leading NULL entries of p_bufs are allocated here
+ * (cell_bytes each, caller frees with free()).  0 / -ECG_DER_NOMEM /
+ * -ECG_DER_INVAL (not an EC class).  Runs on the GPU (synchronous). */
+int ecg_obj_ec_encode_buf(uint32_t oc_id, uint64_t cell_bytes, unsigned char *buffer,
+			  unsigned char *p_bufs[]);
+
+/* Build the recovery codec for LOGICAL erased cells err_list[nerrs].
+ * 0 / -ECG_DER_DATA_LOSS (nerrs > p) / -ECG_DER_INVAL. */
+int ecg_obj_ec_recov_codec_init(uint32_t oc_id, const uint32_t *err_list, uint32_t nerrs,
+				struct ecg_obj_ec_recov_codec *recov);
+
+/* Regenerate the erased cells of `nstripes` host stripes laid out
+ * [nstripes][k+p][cell_sz] (the recovery buffer of ref:src/object/cli_ec.c:
+ * 2449-2464), in place, on device ctx (NULL = process default device). */
+int ecg_obj_ec_recov_data(ecg_ctx_t *ctx, const struct ecg_obj_ec_recov_codec *recov,
+			  uint64_t cell_sz, unsigned char *buf_stripes, uint32_t nstripes);
+
+/* Full-stripe encode of host stripes: data [S][k][C] (user sgl order),
+ * parity [p][S][C] (oer_pbufs layout, ref:src/object/cli_ec.c:75-97). */
+int ecg_obj_ec_encode_stripes(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_bytes,
+			      uint32_t nstripes, const unsigned char *data,
+			      unsigned char *parity);
+
+/* agg_update_parity for one stripe, host buffers as in the reference:
+ * old/new replica cells [cell_cnt][C] (AGG_IOV_ODATA / AGG_IOV_DATA),
+ * parity [p][C] updated in place; bit_map marks the updated data cells.
+ * The reference's diff buffer (AGG_IOV_DIFF) is not needed: old ^ new is
+ * fused on the device.  (Hole zeroing, agg_diff_preprocess, is applied by
+ * the caller to `new_cells` beforehand by copying `old` over hole ranges.) */
+int ecg_agg_update_parity(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_bytes,
+			  const uint8_t *bit_map, uint32_t cell_cnt,
+			  const unsigned char *old_cells, const unsigned char *new_cells,
+			  unsigned char *parity);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,159 @@
+"""ctypes wrapper for the C oracle (oracle/build/libecg_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py.  The product (daos_amd/) never imports this.
+See oracle/ec_ref.h for what is restated and why parity is "unpinned" by
+reference fixtures.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "libecg_oracle.so")
+_lib = None
+
+u8p = C.POINTER(C.c_ubyte)
+u32p = C.POINTER(C.c_uint32)
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.ref_gf_mul.restype = C.c_ubyte
+        L.ref_gf_mul.argtypes = [C.c_ubyte, C.c_ubyte]
+        L.ref_gf_inv.restype = C.c_ubyte
+        L.ref_gf_inv.argtypes = [C.c_ubyte]
+        L.ref_gf_gen_cauchy1_matrix.argtypes = [u8p, C.c_int, C.c_int]
+        L.ref_gf_invert_matrix.argtypes = [u8p, u8p, C.c_int]
+        L.ref_gf_invert_matrix.restype = C.c_int
+        L.ref_ec_init_tables.argtypes = [C.c_int, C.c_int, u8p, u8p]
+        L.ref_ec_encode_data.argtypes = [C.c_int, C.c_int, C.c_int, u8p, C.POINTER(u8p), C.POINTER(u8p)]
+        L.ref_simd_encode_data.argtypes = L.ref_ec_encode_data.argtypes
+        L.ref_ec_encode_data_update.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, u8p, u8p, C.POINTER(u8p)]
+        L.ref_xor_gen.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+        L.ref_xor_gen.restype = C.c_int
+        L.ref_obj_ec_recov_codec_init.argtypes = [C.c_int, C.c_int, u8p, u32p, C.c_int, u8p, u32p, u32p,
+                                                  u8p, C.POINTER(C.c_int)]
+        L.ref_obj_ec_recov_codec_init.restype = C.c_int
+        L.ref_encode_batch.argtypes = [C.c_int, C.c_int, C.c_uint64, C.c_uint32, u8p, u8p, C.c_int]
+        L.ref_simd_encode_batch.argtypes = L.ref_encode_batch.argtypes
+        L.ref_recov_batch.argtypes = [C.c_int, C.c_int, u8p, u32p, u32p, C.c_uint64, C.c_uint64, C.c_uint32,
+                                      u8p, C.c_int]
+        L.ref_simd_recov_batch.argtypes = L.ref_recov_batch.argtypes
+        L.ref_simd_variant.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(u8p)
+
+
+def _p32(a: np.ndarray):
+    return a.ctypes.data_as(u32p)
+
+
+def gf_mul(a: int, b: int) -> int:
+    return lib().ref_gf_mul(a, b)
+
+
+def gf_inv(a: int) -> int:
+    return lib().ref_gf_inv(a)
+
+
+def cauchy1(k: int, p: int) -> np.ndarray:
+    m = np.zeros((k + p) * k, dtype=np.uint8)
+    lib().ref_gf_gen_cauchy1_matrix(_p(m), k + p, k)
+    return m.reshape(k + p, k)
+
+
+def invert(mat: np.ndarray):
+    n = mat.shape[0]
+    a = np.ascontiguousarray(mat, dtype=np.uint8).copy()
+    out = np.zeros((n, n), dtype=np.uint8)
+    rc = lib().ref_gf_invert_matrix(_p(a), _p(out), n)
+    return None if rc else out
+
+
+def init_tables(coef: np.ndarray) -> np.ndarray:
+    rows, k = coef.shape
+    t = np.zeros(rows * k * 32, dtype=np.uint8)
+    c = np.ascontiguousarray(coef, dtype=np.uint8)
+    lib().ref_ec_init_tables(k, rows, _p(c), _p(t))
+    return t
+
+
+def _ptr_array(arrs):
+    return (u8p * len(arrs))(*[_p(a) for a in arrs])
+
+
+def encode_data(coef: np.ndarray, cells: np.ndarray, simd: bool = False) -> np.ndarray:
+    """ec_encode_data over k cells [k, len] with coefficient matrix [rows, k]."""
+    rows, k = coef.shape
+    cells = np.ascontiguousarray(cells, dtype=np.uint8)
+    n = cells.shape[1]
+    out = np.zeros((rows, n), dtype=np.uint8)
+    tb = init_tables(coef)
+    f = lib().ref_simd_encode_data if simd else lib().ref_ec_encode_data
+    f(n, k, rows, _p(tb), _ptr_array([cells[j] for j in range(k)]), _ptr_array([out[r] for r in range(rows)]))
+    return out
+
+
+def encode_data_update(coef: np.ndarray, vec_i: int, delta: np.ndarray, parity: np.ndarray) -> np.ndarray:
+    rows, k = coef.shape
+    par = np.ascontiguousarray(parity, dtype=np.uint8).copy()
+    d = np.ascontiguousarray(delta, dtype=np.uint8)
+    tb = init_tables(coef)
+    lib().ref_ec_encode_data_update(d.shape[0], k, rows, vec_i, _p(tb), _p(d), _ptr_array([par[r] for r in range(rows)]))
+    return par
+
+
+def xor_gen(arrs) -> int:
+    vp = (C.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    return lib().ref_xor_gen(len(arrs), arrs[0].shape[0], vp)
+
+
+def recov_codec(k: int, p: int, err_list):
+    """Returns (rc, de_matrix [nerrs,k], dec_idx [k], err_list, gftbls, reused)."""
+    en = cauchy1(k, p).reshape(-1).copy()
+    nerrs = len(err_list)
+    el = np.array(list(err_list) + [0] * 8, dtype=np.uint32)
+    de = np.zeros(max(nerrs, 1) * k, dtype=np.uint8)
+    dec = np.zeros(k, dtype=np.uint32)
+    oel = np.zeros(8, dtype=np.uint32)
+    gt = np.zeros(k * p * 32, dtype=np.uint8)
+    reused = C.c_int(0)
+    rc = lib().ref_obj_ec_recov_codec_init(k, p, _p(en), _p32(el), nerrs, _p(de), _p32(dec), _p32(oel),
+                                           _p(gt), C.byref(reused))
+    return rc, de.reshape(-1, k)[:nerrs], dec, oel[:nerrs].copy(), gt, bool(reused.value)
+
+
+def encode_batch(k: int, p: int, C_: int, S: int, data: np.ndarray, nthreads: int = 1, simd: bool = False):
+    parity = np.zeros(p * S * C_, dtype=np.uint8)
+    f = lib().ref_simd_encode_batch if simd else lib().ref_encode_batch
+    f(k, p, C_, S, _p(data), _p(parity), nthreads)
+    return parity
+
+
+def recov_batch(k: int, nerrs: int, gftbls, dec_idx, err_list, C_: int, stride: int, S: int,
+                stripes: np.ndarray, nthreads: int = 1, simd: bool = False):
+    f = lib().ref_simd_recov_batch if simd else lib().ref_recov_batch
+    f(k, nerrs, _p(gftbls), _p32(np.ascontiguousarray(dec_idx, dtype=np.uint32)),
+      _p32(np.ascontiguousarray(err_list, dtype=np.uint32)), C_, stride, S, _p(stripes), nthreads)
+
+
+def simd_variant() -> int:
+    return lib().ref_simd_variant()

@@ -1,0 +1,37 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a gfx950 GPU (runs on the MI355X box)")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from oracle import ref
+
+    ref.lib()
+    return ref
+
+
+@pytest.fixture(scope="session")
+def ecglib():
+    from daos_amd import ecg
+
+    ecg.lib()
+    return ecg
+
+
+@pytest.fixture(scope="session")
+def ctx(ecglib):
+    if ecglib.device_count() < 1:
+        pytest.fail("no gfx950 device visible: GPU tests must run on the MI355X box")
+    c = ecglib.Context(0)
+    yield c
+    c.close()

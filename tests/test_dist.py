@@ -1,0 +1,62 @@
+"""Multi-rank control path of bench.py on CPU (gloo, world_size 2).
+
+The data path has no collective (stripes are independent); the
+only cross-rank operations are the barrier and the max of the elapsed time.
+"""
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_gloo_barrier_and_max_two_ranks(tmp_path):
+    script = tmp_path / "w.py"
+    script.write_text(textwrap.dedent(f"""
+        import os, sys, time
+        sys.path.insert(0, {ROOT!r})
+        import bench
+        world, rank, local = bench.dist_init()
+        assert world == 2 and local == rank
+        bench.barrier(world)
+        t = 0.25 if rank == 1 else 0.1
+        m = bench.max_over_ranks(world, t)
+        assert abs(m - 0.25) < 1e-12, m
+        bench.barrier(world)
+        print("rank", rank, "ok", m)
+    """))
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = [p.communicate(timeout=300)[0] for p in procs]
+    for r, (p, o) in enumerate(zip(procs, outs)):
+        assert p.returncode == 0, o
+        assert f"rank {r} ok" in o
+
+
+def test_weak_scaling_accounting():
+    """value counts every rank's stripes: N x per-GPU user bytes / max time."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    class FakeCtx:
+        pass
+
+    wl = bench.Workload.__new__(bench.Workload)
+    wl.k, wl.p, wl.C, wl.S, wl.err = 4, 2, 1 << 20, 1024, [0, 1]
+    assert wl.user_bytes_per_step() == 2 * 4 * (1 << 20) * 1024
+    assert wl.alg_bytes_per_launch() == (6 * (1 << 20) * 1024, 6 * (1 << 20) * 1024)
