@@ -1,0 +1,55 @@
+#!/bin/bash
+# GPU-box driver for one gpurun call.  Every GPU step has its own time limit;
+# any fault / abort / segfault / timeout ends the call (no retries).  Test
+# failures (pytest exit 1) are not faults and do not stop later steps.
+#   tools/gpu_run.sh [smoke] [tests] [bench] [prof] [pmc] [fulltests]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+
+step() {   # name timeout cmd...
+	local name=$1 to=$2
+	shift 2
+	echo "== $name: $*"
+	timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+	local rc=$?
+	echo "== $name rc=$rc"
+	tail -n 12 "gpurun_out/$name.log"
+	return $rc
+}
+
+for what in "$@"; do
+	case $what in
+	smoke)
+		step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+		;;
+	tests)
+		step pytest_gpu 900 python -m pytest tests -q -m gpu -p no:cacheprovider -k "not full_size and not degraded_decode"
+		rc=$?; [ $rc -le 1 ] || exit $rc
+		;;
+	fulltests)
+		step pytest_gpu_full 900 python -m pytest tests -q -m gpu -p no:cacheprovider -k "full_size or degraded_decode"
+		rc=$?; [ $rc -le 1 ] || exit $rc
+		;;
+	bench)
+		step bench 900 python bench.py || exit $?
+		;;
+	prof)
+		rm -rf gpurun_out/prof
+		step rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
+			-- python3 bench.py --steps 10 --warmup 2 --no-detail --no-cpu || exit $?
+		;;
+	pmc)
+		rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
+		step rocprof_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run \
+			-- python3 bench.py --steps 4 --warmup 1 --no-detail --no-cpu --profile-only || exit $?
+		step rocprof_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run \
+			-- python3 bench.py --steps 4 --warmup 1 --no-detail --no-cpu --profile-only || exit $?
+		;;
+	*)
+		echo "unknown step $what"; exit 2
+		;;
+	esac
+done
+echo "== all done"
