@@ -717,16 +717,20 @@ int ecg_device_sync(ecg_ctx_t *ctx)
 	return 0;
 }
 
-int ecg_dev_copy_kernel(ecg_ctx_t *ctx, void *dst, const void *src, size_t bytes, void *stream)
+int ecg_dev_copy_kernel(ecg_ctx_t *ctx, void *dst, const void *src, size_t bytes, int mode,
+			void *stream)
 {
 	int rc = ecg_ctx_enter(ctx);
+	uint32_t kid = 0;
 	int e;
 
 	if (rc)
 		return rc;
-	e = ecg_k_launch_copy(src, dst, bytes, (void *)ecg_pick_stream(ctx, stream));
+	if (mode < 0 || mode > 2)
+		return ecg_fail(-ECG_DER_INVAL, "copy kernel: mode %d", mode);
+	e = ecg_k_launch_copy(src, dst, bytes, mode, (void *)ecg_pick_stream(ctx, stream), &kid);
 	if (e)
 		return ecg_hip_fail((hipError_t)e, "copy kernel");
-	ecg_set_last_kernel("ecg_copy_kernel");
+	ecg_set_last_kernel(ecg_k_kernel_name(kid));
 	return 0;
 }

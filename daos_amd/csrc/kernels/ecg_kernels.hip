@@ -61,6 +61,28 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 	return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
+// Tuning variants (VAR bits; 0 = the shipped default):
+//   bit 0: plain (temporal) loads instead of non-temporal
+//   bit 1: plain stores instead of non-temporal
+//   bit 2: two stripes per iteration (s and s + gridDim.y): 2x the loads in
+//          flight per wave before any arithmetic
+template <bool NT>
+__device__ __forceinline__ u32x4 ld(const uint8_t *p)
+{
+	if (NT)
+		return ld_nt(p);
+	return *reinterpret_cast<const u32x4 *>(p);
+}
+
+template <bool NT>
+__device__ __forceinline__ void st(uint8_t *p, u32x4 v)
+{
+	if (NT)
+		st_nt(p, v);
+	else
+		*reinterpret_cast<u32x4 *>(p) = v;
+}
+
 // K, R: compile-time data cells / output rows (0 = runtime, bounded by the
 // ECG_KMAX_* maxima).  ACC: XOR into dst.  DIFF: source = src ^ src2.
 //
@@ -71,8 +93,8 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 // in registers instead costs 5 x k x rows dwords: that overflows the SGPR
 // file at EC_8P2 (the compiler then spills through v_writelane/v_readlane)
 // and caps VGPR occupancy at 1-2 waves/SIMD for k = 16.  An empty asm on the
-// LDS base each iteration keeps LICM from hoisting the reads back out.
-template <int K, int R, bool ACC, bool DIFF>
+// LDS index each iteration keeps LICM from hoisting the reads back out.
+template <int K, int R, bool ACC, bool DIFF, int VAR = 0>
 __global__ void __launch_bounds__(BLOCK)
 ecg_mm_kernel(const ecg_mm_params_t P)
 {
@@ -80,6 +102,9 @@ ecg_mm_kernel(const ecg_mm_params_t P)
 	constexpr int RM = R ? R : ECG_KMAX_R;
 	constexpr int T2V = (RM + 3) / 4;		// u32x4 holding t2 of all rows
 	constexpr int PER_J = RM + T2V;			// u32x4 per cell
+	constexpr bool NTL = !(VAR & 1);
+	constexpr bool NTS = !(VAR & 2);
+	constexpr int U = (VAR & 4) ? 2 : 1;
 	__shared__ u32x4 s_tbl[KM * PER_J];
 	const int k = K ? K : (int)P.k;
 	const int rows = R ? R : (int)P.rows;
@@ -96,10 +121,19 @@ ecg_mm_kernel(const ecg_mm_params_t P)
 	}
 	__syncthreads();
 
-	for (uint32_t s = blockIdx.y; s < P.nstripes; s += gridDim.y) {
-		const uint8_t *sb = P.src + (int64_t)s * P.src_stripe_stride;
-		const uint8_t *sb2 = DIFF ? P.src2 + (int64_t)s * P.src2_stripe_stride : nullptr;
-		uint8_t *db = P.dst + (int64_t)s * P.dst_stripe_stride;
+	for (uint32_t s0 = blockIdx.y; s0 < P.nstripes; s0 += gridDim.y * U) {
+		const uint8_t *sb[U];
+		const uint8_t *sb2[U];
+		uint8_t *db[U];
+		bool live[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const uint32_t s = s0 + u * gridDim.y;
+			live[u] = s < P.nstripes;
+			sb[u] = P.src + (int64_t)s * P.src_stripe_stride;
+			sb2[u] = DIFF ? P.src2 + (int64_t)s * P.src2_stripe_stride : nullptr;
+			db[u] = P.dst + (int64_t)s * P.dst_stripe_stride;
+		}
 
 		for (uint32_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
 			const uint64_t off = (uint64_t)ch * CHUNK_BYTES + threadIdx.x * 16u;
@@ -109,91 +143,105 @@ ecg_mm_kernel(const ecg_mm_params_t P)
 			const u32x4 *tb = s_tbl + z;
 
 			if (off + 16 <= C) {
-				u32x4 x[KM];
+				u32x4 x[U][KM];
 #pragma unroll
-				for (int j = 0; j < KM; j++) {
-					if (j < k) {
-						x[j] = ld_nt(sb + P.src_cell_off[j] + off);
-						if (DIFF)
-							x[j] ^= ld_nt(sb2 + P.src2_cell_off[j] + off);
-					}
-				}
-				u32x4 acc[RM];
+				for (int u = 0; u < U; u++) {
+					if (u == 0 || live[u]) {
 #pragma unroll
-				for (int r = 0; r < RM; r++) {
-					if (r < rows) {
-						if (ACC)
-							acc[r] = ld_nt(db + P.dst_cell_off[r] + off);
-						else
-							acc[r] = (u32x4){0u, 0u, 0u, 0u};
-					}
-				}
-#pragma unroll
-				for (int j = 0; j < KM; j++) {
-					if (j < k) {
-						u32x4 sel0, sel1, sel2;
-#pragma unroll
-						for (int w = 0; w < 4; w++) {
-							const uint32_t v = x[j][w];
-							sel0[w] = v & 0x07070707u;
-							sel1[w] = (v >> 3) & 0x07070707u;
-							sel2[w] = (v >> 6) & 0x03030303u;
+						for (int j = 0; j < KM; j++) {
+							if (j < k) {
+								x[u][j] = ld<NTL>(sb[u] + P.src_cell_off[j] + off);
+								if (DIFF)
+									x[u][j] ^= ld<NTL>(sb2[u] + P.src2_cell_off[j] + off);
+							}
 						}
-						u32x4 t2v[T2V];
+					}
+				}
 #pragma unroll
-						for (int q = 0; q < T2V; q++)
-							t2v[q] = tb[j * PER_J + RM + q];
+				for (int u = 0; u < U; u++) {
+					if (u > 0 && !live[u])
+						break;
+					u32x4 acc[RM];
 #pragma unroll
-						for (int r = 0; r < RM; r++) {
-							if (r < rows) {
-								const u32x4 t = tb[j * PER_J + r];
-								const uint32_t t2 = t2v[r / 4][r % 4];
+					for (int r = 0; r < RM; r++) {
+						if (r < rows) {
+							if (ACC)
+								acc[r] = ld<NTL>(db[u] + P.dst_cell_off[r] + off);
+							else
+								acc[r] = (u32x4){0u, 0u, 0u, 0u};
+						}
+					}
 #pragma unroll
-								for (int w = 0; w < 4; w++) {
-									const uint32_t p0 = __builtin_amdgcn_perm(t[1], t[0], sel0[w]);
-									const uint32_t p1 = __builtin_amdgcn_perm(t[3], t[2], sel1[w]);
-									const uint32_t p2 = __builtin_amdgcn_perm(t2, t2, sel2[w]);
-									acc[r][w] = xor3(acc[r][w], p0, xor3(p1, p2, 0u));
+					for (int j = 0; j < KM; j++) {
+						if (j < k) {
+							u32x4 sel0, sel1, sel2;
+#pragma unroll
+							for (int w = 0; w < 4; w++) {
+								const uint32_t v = x[u][j][w];
+								sel0[w] = v & 0x07070707u;
+								sel1[w] = (v >> 3) & 0x07070707u;
+								sel2[w] = (v >> 6) & 0x03030303u;
+							}
+							u32x4 t2v[T2V];
+#pragma unroll
+							for (int q = 0; q < T2V; q++)
+								t2v[q] = tb[j * PER_J + RM + q];
+#pragma unroll
+							for (int r = 0; r < RM; r++) {
+								if (r < rows) {
+									const u32x4 t = tb[j * PER_J + r];
+									const uint32_t t2 = t2v[r / 4][r % 4];
+#pragma unroll
+									for (int w = 0; w < 4; w++) {
+										const uint32_t p0 = __builtin_amdgcn_perm(t[1], t[0], sel0[w]);
+										const uint32_t p1 = __builtin_amdgcn_perm(t[3], t[2], sel1[w]);
+										const uint32_t p2 = __builtin_amdgcn_perm(t2, t2, sel2[w]);
+										acc[r][w] = xor3(acc[r][w], p0, xor3(p1, p2, 0u));
+									}
 								}
 							}
 						}
 					}
-				}
 #pragma unroll
-				for (int r = 0; r < RM; r++)
-					if (r < rows)
-						st_nt(db + P.dst_cell_off[r] + off, acc[r]);
+					for (int r = 0; r < RM; r++)
+						if (r < rows)
+							st<NTS>(db[u] + P.dst_cell_off[r] + off, acc[r]);
+				}
 			} else if (off < C) {
 				// ragged tail: < 16 bytes of this lane's slot are in the cell
 				const int nb = (int)(C - off);
 
-				for (int b = 0; b < nb; b++) {
-					uint32_t o[RM];
+				for (int u = 0; u < U; u++) {
+					if (!live[u])
+						break;
+					for (int b = 0; b < nb; b++) {
+						uint32_t o[RM];
 #pragma unroll
-					for (int r = 0; r < RM; r++)
-						o[r] = 0;
-					for (int j = 0; j < k; j++) {
-						uint32_t v = sb[P.src_cell_off[j] + off + b];
-						if (DIFF)
-							v ^= sb2[P.src2_cell_off[j] + off + b];
-						const uint32_t s0 = v & 7u, s1 = (v >> 3) & 7u, s2 = v >> 6;
+						for (int r = 0; r < RM; r++)
+							o[r] = 0;
+						for (int j = 0; j < k; j++) {
+							uint32_t v = sb[u][P.src_cell_off[j] + off + b];
+							if (DIFF)
+								v ^= sb2[u][P.src2_cell_off[j] + off + b];
+							const uint32_t s0_ = v & 7u, s1_ = (v >> 3) & 7u, s2_ = v >> 6;
+#pragma unroll
+							for (int r = 0; r < RM; r++) {
+								if (r < rows) {
+									const u32x4 t = tb[j * PER_J + r];
+									const uint32_t t2 = reinterpret_cast<const uint32_t *>(
+										&tb[j * PER_J + RM])[r];
+									o[r] ^= __builtin_amdgcn_perm(t[1], t[0], s0_) ^
+										__builtin_amdgcn_perm(t[3], t[2], s1_) ^
+										__builtin_amdgcn_perm(t2, t2, s2_);
+								}
+							}
+						}
 #pragma unroll
 						for (int r = 0; r < RM; r++) {
 							if (r < rows) {
-								const u32x4 t = tb[j * PER_J + r];
-								const uint32_t t2 = reinterpret_cast<const uint32_t *>(
-									&tb[j * PER_J + RM])[r];
-								o[r] ^= __builtin_amdgcn_perm(t[1], t[0], s0) ^
-									__builtin_amdgcn_perm(t[3], t[2], s1) ^
-									__builtin_amdgcn_perm(t2, t2, s2);
+								uint8_t *d = db[u] + P.dst_cell_off[r] + off + b;
+								*d = ACC ? (uint8_t)(*d ^ o[r]) : (uint8_t)o[r];
 							}
-						}
-					}
-#pragma unroll
-					for (int r = 0; r < RM; r++) {
-						if (r < rows) {
-							uint8_t *d = db + P.dst_cell_off[r] + off + b;
-							*d = ACC ? (uint8_t)(*d ^ o[r]) : (uint8_t)o[r];
 						}
 					}
 				}
@@ -235,14 +283,48 @@ ecg_mm_byte_kernel(const ecg_mm_params_t P)
 	}
 }
 
-// Streaming copy, 16 B/lane, used by bench.py to measure this box's
-// achievable HBM rate next to the spec peak.
+// Streaming kernels used by bench.py to measure this box's achievable HBM
+// rates next to the spec peak: mode 0 copy, 1 read-only (XOR-reduce, one
+// 16 B word per thread written), 2 write-only.  16 B per lane, 4 accesses in
+// flight per lane per iteration.
+template <int MODE>
 __global__ void __launch_bounds__(BLOCK)
-ecg_copy_kernel(const uint8_t *src, uint8_t *dst, uint64_t n16)
+ecg_stream_kernel(const uint8_t *src, uint8_t *dst, uint64_t n16)
 {
-	for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n16;
-	     i += (uint64_t)gridDim.x * BLOCK)
-		st_nt(dst + i * 16, ld_nt(src + i * 16));
+	const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+	uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+	u32x4 acc = (u32x4){0u, 0u, 0u, 0u};
+
+	for (; i + 3 * stride < n16; i += 4 * stride) {
+		if (MODE == 2) {
+			const u32x4 v = (u32x4){(uint32_t)i, 1u, 2u, 3u};
+#pragma unroll
+			for (int q = 0; q < 4; q++)
+				st_nt(dst + (i + q * stride) * 16, v);
+		} else {
+			u32x4 v[4];
+#pragma unroll
+			for (int q = 0; q < 4; q++)
+				v[q] = ld_nt(src + (i + q * stride) * 16);
+#pragma unroll
+			for (int q = 0; q < 4; q++) {
+				if (MODE == 0)
+					st_nt(dst + (i + q * stride) * 16, v[q]);
+				else
+					acc ^= v[q];
+			}
+		}
+	}
+	for (; i < n16; i += stride) {
+		if (MODE == 0)
+			st_nt(dst + i * 16, ld_nt(src + i * 16));
+		else if (MODE == 1)
+			acc ^= ld_nt(src + i * 16);
+		else
+			st_nt(dst + i * 16, (u32x4){(uint32_t)i, 1u, 2u, 3u});
+	}
+	if (MODE == 1)
+		st_nt(dst + ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) * 16, acc);
 }
 
 // ---------------------------------------------------------------------------
@@ -251,14 +333,17 @@ ecg_copy_kernel(const uint8_t *src, uint8_t *dst, uint64_t n16)
 typedef void (*mm_fn_t)(const ecg_mm_params_t);
 
 struct kentry {
-	int k, r, acc, diff;
+	int k, r, acc, diff, var;
 	mm_fn_t fn;
 	const char *name;
 };
 
 #define KE(K_, R_, A_, D_) \
-	{K_, R_, A_, D_, ecg_mm_kernel<K_, R_, (bool)A_, (bool)D_>, \
+	{K_, R_, A_, D_, 0, ecg_mm_kernel<K_, R_, (bool)A_, (bool)D_, 0>, \
 	 "ecg_mm_kernel<" #K_ "," #R_ "," #A_ "," #D_ ">"}
+#define KV(K_, R_, V_) \
+	{K_, R_, 0, 0, V_, ecg_mm_kernel<K_, R_, false, false, V_>, \
+	 "ecg_mm_kernel<" #K_ "," #R_ ",0,0,var" #V_ ">"}
 
 // Specialised shapes: every (k, p) of the DAOS EC classes
 // (ref:src/include/daos_obj_class.h:70-80): k in {2,4,8,16}, rows in 1..3
@@ -270,10 +355,16 @@ static const kentry g_kernels[] = {
 	KE(8, 1, 0, 0), KE(8, 2, 0, 0), KE(8, 3, 0, 0),
 	KE(16, 1, 0, 0), KE(16, 2, 0, 0), KE(16, 3, 0, 0),
 	KE(0, 0, 0, 0), KE(0, 0, 1, 0), KE(0, 0, 0, 1), KE(0, 0, 1, 1),
+	// tuning variants (ECG launch variant 16 + VAR) for the bench shapes
+	KV(4, 2, 1), KV(4, 2, 2), KV(4, 2, 3), KV(4, 2, 4), KV(4, 2, 5), KV(4, 2, 6), KV(4, 2, 7),
+	KV(8, 2, 1), KV(8, 2, 2), KV(8, 2, 3), KV(8, 2, 4), KV(8, 2, 5), KV(8, 2, 6), KV(8, 2, 7),
+	KV(16, 2, 1), KV(16, 2, 2), KV(16, 2, 3), KV(16, 2, 4), KV(16, 2, 5), KV(16, 2, 6), KV(16, 2, 7),
 };
 #define N_KERNELS ((uint32_t)(sizeof(g_kernels) / sizeof(g_kernels[0])))
 #define KID_BYTE N_KERNELS
 #define KID_COPY (N_KERNELS + 1)
+#define KID_READ (N_KERNELS + 2)
+#define KID_WRITE (N_KERNELS + 3)
 
 static bool aligned16(const ecg_mm_params_t *p)
 {
@@ -298,7 +389,11 @@ extern "C" const char *ecg_k_kernel_name(uint32_t id)
 	if (id == KID_BYTE)
 		return "ecg_mm_byte_kernel";
 	if (id == KID_COPY)
-		return "ecg_copy_kernel";
+		return "ecg_stream_kernel<copy>";
+	if (id == KID_READ)
+		return "ecg_stream_kernel<read>";
+	if (id == KID_WRITE)
+		return "ecg_stream_kernel<write>";
 	return "?";
 }
 
@@ -324,17 +419,19 @@ extern "C" int ecg_k_launch_matmul(const ecg_mm_params_t *p, const ecg_launch_cf
 	}
 
 	uint32_t id = N_KERNELS;
+	const int want_var = variant >= 16 ? (int)variant - 16 : 0;
 	if (variant != 1 && !p->accumulate && !p->diff) {
 		for (uint32_t i = 0; i < N_KERNELS; i++)
 			if (g_kernels[i].k == (int)p->k && g_kernels[i].r == (int)p->rows &&
-			    !g_kernels[i].acc && !g_kernels[i].diff) {
+			    !g_kernels[i].acc && !g_kernels[i].diff && g_kernels[i].var == want_var) {
 				id = i;
 				break;
 			}
 	}
 	if (id == N_KERNELS) {
 		for (uint32_t i = 0; i < N_KERNELS; i++)
-			if (g_kernels[i].k == 0 && g_kernels[i].acc == (int)(p->accumulate != 0) &&
+			if (g_kernels[i].k == 0 && g_kernels[i].var == 0 &&
+			    g_kernels[i].acc == (int)(p->accumulate != 0) &&
 			    g_kernels[i].diff == (int)(p->diff != 0)) {
 				id = i;
 				break;
@@ -361,15 +458,27 @@ extern "C" int ecg_k_launch_matmul(const ecg_mm_params_t *p, const ecg_launch_cf
 	return (int)hipGetLastError();
 }
 
-extern "C" int ecg_k_launch_copy(const void *src, void *dst, uint64_t bytes, void *stream)
+extern "C" int ecg_k_launch_copy(const void *src, void *dst, uint64_t bytes, int mode, void *stream,
+				 uint32_t *kernel_id)
 {
-	uint64_t n16 = bytes / 16;
-	uint64_t blocks = (n16 + BLOCK - 1) / BLOCK;
-	if (blocks > 256 * 32)
-		blocks = 256 * 32;
+	const uint64_t n16 = bytes / 16;
+	uint64_t blocks = (n16 + 4 * BLOCK - 1) / (4 * BLOCK);
+	hipStream_t st = (hipStream_t)stream;
+
+	if (blocks > 256 * 8)
+		blocks = 256 * 8;
 	if (blocks == 0)
 		return (int)hipSuccess;
-	hipLaunchKernelGGL(ecg_copy_kernel, dim3((uint32_t)blocks), dim3(BLOCK), 0, (hipStream_t)stream,
-			   (const uint8_t *)src, (uint8_t *)dst, n16);
+	if (mode == 1)
+		hipLaunchKernelGGL(ecg_stream_kernel<1>, dim3((uint32_t)blocks), dim3(BLOCK), 0, st,
+				   (const uint8_t *)src, (uint8_t *)dst, n16);
+	else if (mode == 2)
+		hipLaunchKernelGGL(ecg_stream_kernel<2>, dim3((uint32_t)blocks), dim3(BLOCK), 0, st,
+				   (const uint8_t *)src, (uint8_t *)dst, n16);
+	else
+		hipLaunchKernelGGL(ecg_stream_kernel<0>, dim3((uint32_t)blocks), dim3(BLOCK), 0, st,
+				   (const uint8_t *)src, (uint8_t *)dst, n16);
+	if (kernel_id)
+		*kernel_id = mode == 1 ? KID_READ : mode == 2 ? KID_WRITE : KID_COPY;
 	return (int)hipGetLastError();
 }

@@ -67,7 +67,7 @@ _SIGS = [
     ("ecg_event_record", C.c_int, [vp, vp, vp]),
     ("ecg_event_elapsed_ms", C.c_int, [vp, vp, vp, C.POINTER(C.c_float)]),
     ("ecg_device_sync", C.c_int, [vp]),
-    ("ecg_dev_copy_kernel", C.c_int, [vp, vp, vp, C.c_size_t, vp]),
+    ("ecg_dev_copy_kernel", C.c_int, [vp, vp, vp, C.c_size_t, C.c_int, vp]),
     ("ecg_set_launch", C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_uint32]),
     # ISA-L drop-in (ecg_isal.h)
     ("ec_init_tables", None, [C.c_int, C.c_int, u8p, u8p]),
@@ -283,8 +283,9 @@ class Context:
     def set_launch(self, grid_x: int = 0, grid_y: int = 0, variant: int = 0):
         _chk(lib().ecg_set_launch(self.h, grid_x, grid_y, variant), "set_launch")
 
-    def copy_kernel(self, dst: int, src: int, nbytes: int, stream=None):
-        _chk(lib().ecg_dev_copy_kernel(self.h, dst, src, nbytes, stream), "copy_kernel")
+    def copy_kernel(self, dst: int, src: int, nbytes: int, mode: int = 0, stream=None):
+        """mode 0 copy, 1 read-only, 2 write-only (HBM rate probes)."""
+        _chk(lib().ecg_dev_copy_kernel(self.h, dst, src, nbytes, mode, stream), "copy_kernel")
 
     # codec
     def matmul(self, coef: np.ndarray, cell_bytes: int, nstripes: int, src: int, src_off, src_stride: int,
