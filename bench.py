@@ -297,7 +297,7 @@ def main():
     kernel_name = f"ecg_mm_kernel<{k},{p},0,0>"
     traffic = None
     pmc = pmc_traffic()
-    if pmc and pmc.get("kernel", "").replace(" ", "").startswith(f"ecg_mm_kernel<{k},{p},"[:len(pmc["kernel"].replace(" ", ""))]):
+    if pmc and pmc.get("kernel", "").replace(" ", "") == f"ecg_mm_kernel<{k},{p}":
         traffic = pmc.get("hbm_bytes_per_launch")
 
     out = {

@@ -61,8 +61,7 @@ typedef struct ecg_mm_params {
 typedef struct ecg_launch_cfg {
 	uint32_t grid_x;	/* chunks per stripe handled in parallel */
 	uint32_t grid_y;	/* stripes handled in parallel */
-	uint32_t variant;	/* 0 auto, 1 force generic, 2 force byte kernel,
-				 * 16+v tuning variant v of a specialised shape */
+	uint32_t variant;	/* 0 auto, 1 force generic, 2 force byte kernel */
 	uint32_t pad;
 } ecg_launch_cfg_t;
 
@@ -75,7 +74,7 @@ int ecg_k_launch_matmul(const ecg_mm_params_t *p, const ecg_launch_cfg_t *cfg,
 /* Streaming kernels used only to measure the box's achievable HBM rates:
  * mode 0 copy, 1 read-only, 2 write-only. */
 int ecg_k_launch_copy(const void *src, void *dst, uint64_t bytes, int mode, void *stream,
-		      uint32_t *kernel_id);
+		      uint32_t max_blocks, uint32_t *kernel_id);
 const char *ecg_k_kernel_name(uint32_t kernel_id);
 #ifdef __cplusplus
 }

@@ -728,7 +728,8 @@ int ecg_dev_copy_kernel(ecg_ctx_t *ctx, void *dst, const void *src, size_t bytes
 		return rc;
 	if (mode < 0 || mode > 2)
 		return ecg_fail(-ECG_DER_INVAL, "copy kernel: mode %d", mode);
-	e = ecg_k_launch_copy(src, dst, bytes, mode, (void *)ecg_pick_stream(ctx, stream), &kid);
+	e = ecg_k_launch_copy(src, dst, bytes, mode, (void *)ecg_pick_stream(ctx, stream),
+			      ctx->cfg.grid_x, &kid);
 	if (e)
 		return ecg_hip_fail((hipError_t)e, "copy kernel");
 	ecg_set_last_kernel(ecg_k_kernel_name(kid));

@@ -61,26 +61,129 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 	return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
-// Tuning variants (VAR bits; 0 = the shipped default):
-//   bit 0: plain (temporal) loads instead of non-temporal
-//   bit 1: plain stores instead of non-temporal
-//   bit 2: two stripes per iteration (s and s + gridDim.y): 2x the loads in
-//          flight per wave before any arithmetic
-template <bool NT>
-__device__ __forceinline__ u32x4 ld(const uint8_t *p)
+// One (stripe, 4 KiB column) item of the product.  Addresses are a
+// wave-uniform 64-bit base per cell (SGPRs) plus the lane's 32-bit offset.
+// The uniform cell offsets are passed through an empty asm per item so LICM
+// cannot hoist k+rows 64-bit pointers out of the stripe loop (they land in
+// VGPRs and spill at EC_8P2/EC_16P2).
+template <int KM, int RM, bool ACC, bool DIFF>
+__device__ __forceinline__ void mm_item(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
+					uint32_t s, uint64_t cbase, uint32_t lo)
 {
-	if (NT)
-		return ld_nt(p);
-	return *reinterpret_cast<const u32x4 *>(p);
+	constexpr int T2V = (RM + 3) / 4;
+	constexpr int PER_J = RM + T2V;
+	const int64_t s_src = (int64_t)s * P.src_stripe_stride + (int64_t)cbase;
+	const int64_t s_src2 = DIFF ? (int64_t)s * P.src2_stripe_stride + (int64_t)cbase : 0;
+	const int64_t s_dst = (int64_t)s * P.dst_stripe_stride + (int64_t)cbase;
+
+	u32x4 x[KM];
+#pragma unroll
+	for (int j = 0; j < KM; j++) {
+		if (j < k) {
+			int64_t o = P.src_cell_off[j] + s_src;
+			asm volatile("" : "+s"(o));
+			x[j] = ld_nt(P.src + o + lo);
+			if (DIFF) {
+				int64_t o2 = P.src2_cell_off[j] + s_src2;
+				asm volatile("" : "+s"(o2));
+				x[j] ^= ld_nt(P.src2 + o2 + lo);
+			}
+		}
+	}
+	u32x4 acc[RM];
+#pragma unroll
+	for (int r = 0; r < RM; r++) {
+		if (r < rows) {
+			if (ACC) {
+				int64_t o = P.dst_cell_off[r] + s_dst;
+				asm volatile("" : "+s"(o));
+				acc[r] = ld_nt(P.dst + o + lo);
+			} else {
+				acc[r] = (u32x4){0u, 0u, 0u, 0u};
+			}
+		}
+	}
+#pragma unroll
+	for (int j = 0; j < KM; j++) {
+		if (j < k) {
+			u32x4 sel0, sel1, sel2;
+#pragma unroll
+			for (int w = 0; w < 4; w++) {
+				const uint32_t v = x[j][w];
+				sel0[w] = v & 0x07070707u;
+				sel1[w] = (v >> 3) & 0x07070707u;
+				sel2[w] = (v >> 6) & 0x03030303u;
+			}
+			u32x4 t2v[T2V];
+#pragma unroll
+			for (int q = 0; q < T2V; q++)
+				t2v[q] = tb[j * PER_J + RM + q];
+#pragma unroll
+			for (int r = 0; r < RM; r++) {
+				if (r < rows) {
+					const u32x4 t = tb[j * PER_J + r];
+					const uint32_t t2 = t2v[r / 4][r % 4];
+#pragma unroll
+					for (int w = 0; w < 4; w++) {
+						const uint32_t p0 = __builtin_amdgcn_perm(t[1], t[0], sel0[w]);
+						const uint32_t p1 = __builtin_amdgcn_perm(t[3], t[2], sel1[w]);
+						const uint32_t p2 = __builtin_amdgcn_perm(t2, t2, sel2[w]);
+						acc[r][w] = xor3(acc[r][w], p0, xor3(p1, p2, 0u));
+					}
+				}
+			}
+		}
+	}
+#pragma unroll
+	for (int r = 0; r < RM; r++) {
+		if (r < rows) {
+			int64_t o = P.dst_cell_off[r] + s_dst;
+			asm volatile("" : "+s"(o));
+			st_nt(P.dst + o + lo, acc[r]);
+		}
+	}
 }
 
-template <bool NT>
-__device__ __forceinline__ void st(uint8_t *p, u32x4 v)
+// Ragged tail: fewer than 16 bytes of this lane's slot are inside the cell.
+template <int RM, bool ACC, bool DIFF>
+__device__ __forceinline__ void mm_tail(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
+				     uint32_t s, uint64_t off, int nb)
 {
-	if (NT)
-		st_nt(p, v);
-	else
-		*reinterpret_cast<u32x4 *>(p) = v;
+	constexpr int T2V = (RM + 3) / 4;
+	constexpr int PER_J = RM + T2V;
+	const uint8_t *sb = P.src + (int64_t)s * P.src_stripe_stride;
+	const uint8_t *sb2 = DIFF ? P.src2 + (int64_t)s * P.src2_stripe_stride : nullptr;
+	uint8_t *db = P.dst + (int64_t)s * P.dst_stripe_stride;
+
+	for (int b = 0; b < nb; b++) {
+		uint32_t o[RM];
+#pragma unroll
+		for (int r = 0; r < RM; r++)
+			o[r] = 0;
+		for (int j = 0; j < k; j++) {
+			uint32_t v = sb[P.src_cell_off[j] + off + b];
+			if (DIFF)
+				v ^= sb2[P.src2_cell_off[j] + off + b];
+			const uint32_t s0 = v & 7u, s1 = (v >> 3) & 7u, s2 = v >> 6;
+#pragma unroll
+			for (int r = 0; r < RM; r++) {
+				if (r < rows) {
+					const u32x4 t = tb[j * PER_J + r];
+					const uint32_t t2 = reinterpret_cast<const uint32_t *>(&tb[j * PER_J + RM])[r];
+					o[r] ^= __builtin_amdgcn_perm(t[1], t[0], s0) ^
+						__builtin_amdgcn_perm(t[3], t[2], s1) ^
+						__builtin_amdgcn_perm(t2, t2, s2);
+				}
+			}
+		}
+#pragma unroll
+		for (int r = 0; r < RM; r++) {
+			if (r < rows) {
+				uint8_t *d = db + P.dst_cell_off[r] + off + b;
+				*d = ACC ? (uint8_t)(*d ^ o[r]) : (uint8_t)o[r];
+			}
+		}
+	}
 }
 
 // K, R: compile-time data cells / output rows (0 = runtime, bounded by the
@@ -93,8 +196,8 @@ __device__ __forceinline__ void st(uint8_t *p, u32x4 v)
 // in registers instead costs 5 x k x rows dwords: that overflows the SGPR
 // file at EC_8P2 (the compiler then spills through v_writelane/v_readlane)
 // and caps VGPR occupancy at 1-2 waves/SIMD for k = 16.  An empty asm on the
-// LDS index each iteration keeps LICM from hoisting the reads back out.
-template <int K, int R, bool ACC, bool DIFF, int VAR = 0>
+// LDS index each item keeps LICM from hoisting the reads back out.
+template <int K, int R, bool ACC, bool DIFF>
 __global__ void __launch_bounds__(BLOCK)
 ecg_mm_kernel(const ecg_mm_params_t P)
 {
@@ -102,14 +205,12 @@ ecg_mm_kernel(const ecg_mm_params_t P)
 	constexpr int RM = R ? R : ECG_KMAX_R;
 	constexpr int T2V = (RM + 3) / 4;		// u32x4 holding t2 of all rows
 	constexpr int PER_J = RM + T2V;			// u32x4 per cell
-	constexpr bool NTL = !(VAR & 1);
-	constexpr bool NTS = !(VAR & 2);
-	constexpr int U = (VAR & 4) ? 2 : 1;
 	__shared__ u32x4 s_tbl[KM * PER_J];
 	const int k = K ? K : (int)P.k;
 	const int rows = R ? R : (int)P.rows;
 	const uint64_t C = P.cell_bytes;
 	const uint32_t nchunk = (uint32_t)((C + CHUNK_BYTES - 1) / CHUNK_BYTES);
+	const uint32_t lo = threadIdx.x * 16u;
 
 	for (int i = threadIdx.x; i < KM * RM; i += BLOCK) {
 		const int j = i / RM, r = i % RM;
@@ -121,130 +222,24 @@ ecg_mm_kernel(const ecg_mm_params_t P)
 	}
 	__syncthreads();
 
-	for (uint32_t s0 = blockIdx.y; s0 < P.nstripes; s0 += gridDim.y * U) {
-		const uint8_t *sb[U];
-		const uint8_t *sb2[U];
-		uint8_t *db[U];
-		bool live[U];
-#pragma unroll
-		for (int u = 0; u < U; u++) {
-			const uint32_t s = s0 + u * gridDim.y;
-			live[u] = s < P.nstripes;
-			sb[u] = P.src + (int64_t)s * P.src_stripe_stride;
-			sb2[u] = DIFF ? P.src2 + (int64_t)s * P.src2_stripe_stride : nullptr;
-			db[u] = P.dst + (int64_t)s * P.dst_stripe_stride;
-		}
-
+	// Normally one item per block (grid = columns x stripes); the loops only
+	// stride when a grid dimension would exceed 65535.
+	for (uint32_t s = blockIdx.y; s < P.nstripes; s += gridDim.y) {
 		for (uint32_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
-			const uint64_t off = (uint64_t)ch * CHUNK_BYTES + threadIdx.x * 16u;
+			const uint64_t cbase = (uint64_t)ch * CHUNK_BYTES;
 			uint32_t z = 0;
 
 			asm volatile("" : "+v"(z));
 			const u32x4 *tb = s_tbl + z;
 
-			if (off + 16 <= C) {
-				u32x4 x[U][KM];
-#pragma unroll
-				for (int u = 0; u < U; u++) {
-					if (u == 0 || live[u]) {
-#pragma unroll
-						for (int j = 0; j < KM; j++) {
-							if (j < k) {
-								x[u][j] = ld<NTL>(sb[u] + P.src_cell_off[j] + off);
-								if (DIFF)
-									x[u][j] ^= ld<NTL>(sb2[u] + P.src2_cell_off[j] + off);
-							}
-						}
-					}
-				}
-#pragma unroll
-				for (int u = 0; u < U; u++) {
-					if (u > 0 && !live[u])
-						break;
-					u32x4 acc[RM];
-#pragma unroll
-					for (int r = 0; r < RM; r++) {
-						if (r < rows) {
-							if (ACC)
-								acc[r] = ld<NTL>(db[u] + P.dst_cell_off[r] + off);
-							else
-								acc[r] = (u32x4){0u, 0u, 0u, 0u};
-						}
-					}
-#pragma unroll
-					for (int j = 0; j < KM; j++) {
-						if (j < k) {
-							u32x4 sel0, sel1, sel2;
-#pragma unroll
-							for (int w = 0; w < 4; w++) {
-								const uint32_t v = x[u][j][w];
-								sel0[w] = v & 0x07070707u;
-								sel1[w] = (v >> 3) & 0x07070707u;
-								sel2[w] = (v >> 6) & 0x03030303u;
-							}
-							u32x4 t2v[T2V];
-#pragma unroll
-							for (int q = 0; q < T2V; q++)
-								t2v[q] = tb[j * PER_J + RM + q];
-#pragma unroll
-							for (int r = 0; r < RM; r++) {
-								if (r < rows) {
-									const u32x4 t = tb[j * PER_J + r];
-									const uint32_t t2 = t2v[r / 4][r % 4];
-#pragma unroll
-									for (int w = 0; w < 4; w++) {
-										const uint32_t p0 = __builtin_amdgcn_perm(t[1], t[0], sel0[w]);
-										const uint32_t p1 = __builtin_amdgcn_perm(t[3], t[2], sel1[w]);
-										const uint32_t p2 = __builtin_amdgcn_perm(t2, t2, sel2[w]);
-										acc[r][w] = xor3(acc[r][w], p0, xor3(p1, p2, 0u));
-									}
-								}
-							}
-						}
-					}
-#pragma unroll
-					for (int r = 0; r < RM; r++)
-						if (r < rows)
-							st<NTS>(db[u] + P.dst_cell_off[r] + off, acc[r]);
-				}
-			} else if (off < C) {
-				// ragged tail: < 16 bytes of this lane's slot are in the cell
-				const int nb = (int)(C - off);
-
-				for (int u = 0; u < U; u++) {
-					if (!live[u])
-						break;
-					for (int b = 0; b < nb; b++) {
-						uint32_t o[RM];
-#pragma unroll
-						for (int r = 0; r < RM; r++)
-							o[r] = 0;
-						for (int j = 0; j < k; j++) {
-							uint32_t v = sb[u][P.src_cell_off[j] + off + b];
-							if (DIFF)
-								v ^= sb2[u][P.src2_cell_off[j] + off + b];
-							const uint32_t s0_ = v & 7u, s1_ = (v >> 3) & 7u, s2_ = v >> 6;
-#pragma unroll
-							for (int r = 0; r < RM; r++) {
-								if (r < rows) {
-									const u32x4 t = tb[j * PER_J + r];
-									const uint32_t t2 = reinterpret_cast<const uint32_t *>(
-										&tb[j * PER_J + RM])[r];
-									o[r] ^= __builtin_amdgcn_perm(t[1], t[0], s0_) ^
-										__builtin_amdgcn_perm(t[3], t[2], s1_) ^
-										__builtin_amdgcn_perm(t2, t2, s2_);
-								}
-							}
-						}
-#pragma unroll
-						for (int r = 0; r < RM; r++) {
-							if (r < rows) {
-								uint8_t *d = db[u] + P.dst_cell_off[r] + off + b;
-								*d = ACC ? (uint8_t)(*d ^ o[r]) : (uint8_t)o[r];
-							}
-						}
-					}
-				}
+			// wave-uniform test first: every full 4 KiB column (all of them
+			// when C % 4096 == 0) takes the vector path with no lane mask
+			if (cbase + CHUNK_BYTES <= C) {
+				mm_item<KM, RM, ACC, DIFF>(P, tb, k, rows, s, cbase, lo);
+			} else if (cbase + lo + 16 <= C) {
+				mm_item<KM, RM, ACC, DIFF>(P, tb, k, rows, s, cbase, lo);
+			} else if (cbase + lo < C) {
+				mm_tail<RM, ACC, DIFF>(P, tb, k, rows, s, cbase + lo, (int)(C - cbase - lo));
 			}
 		}
 	}
@@ -333,17 +328,15 @@ ecg_stream_kernel(const uint8_t *src, uint8_t *dst, uint64_t n16)
 typedef void (*mm_fn_t)(const ecg_mm_params_t);
 
 struct kentry {
-	int k, r, acc, diff, var;
+	int k, r, acc, diff;
 	mm_fn_t fn;
 	const char *name;
 };
 
 #define KE(K_, R_, A_, D_) \
-	{K_, R_, A_, D_, 0, ecg_mm_kernel<K_, R_, (bool)A_, (bool)D_, 0>, \
+	{K_, R_, A_, D_, ecg_mm_kernel<K_, R_, (bool)A_, (bool)D_>, \
 	 "ecg_mm_kernel<" #K_ "," #R_ "," #A_ "," #D_ ">"}
-#define KV(K_, R_, V_) \
-	{K_, R_, 0, 0, V_, ecg_mm_kernel<K_, R_, false, false, V_>, \
-	 "ecg_mm_kernel<" #K_ "," #R_ ",0,0,var" #V_ ">"}
+
 
 // Specialised shapes: every (k, p) of the DAOS EC classes
 // (ref:src/include/daos_obj_class.h:70-80): k in {2,4,8,16}, rows in 1..3
@@ -355,10 +348,6 @@ static const kentry g_kernels[] = {
 	KE(8, 1, 0, 0), KE(8, 2, 0, 0), KE(8, 3, 0, 0),
 	KE(16, 1, 0, 0), KE(16, 2, 0, 0), KE(16, 3, 0, 0),
 	KE(0, 0, 0, 0), KE(0, 0, 1, 0), KE(0, 0, 0, 1), KE(0, 0, 1, 1),
-	// tuning variants (ECG launch variant 16 + VAR) for the bench shapes
-	KV(4, 2, 1), KV(4, 2, 2), KV(4, 2, 3), KV(4, 2, 4), KV(4, 2, 5), KV(4, 2, 6), KV(4, 2, 7),
-	KV(8, 2, 1), KV(8, 2, 2), KV(8, 2, 3), KV(8, 2, 4), KV(8, 2, 5), KV(8, 2, 6), KV(8, 2, 7),
-	KV(16, 2, 1), KV(16, 2, 2), KV(16, 2, 3), KV(16, 2, 4), KV(16, 2, 5), KV(16, 2, 6), KV(16, 2, 7),
 };
 #define N_KERNELS ((uint32_t)(sizeof(g_kernels) / sizeof(g_kernels[0])))
 #define KID_BYTE N_KERNELS
@@ -419,39 +408,32 @@ extern "C" int ecg_k_launch_matmul(const ecg_mm_params_t *p, const ecg_launch_cf
 	}
 
 	uint32_t id = N_KERNELS;
-	const int want_var = variant >= 16 ? (int)variant - 16 : 0;
 	if (variant != 1 && !p->accumulate && !p->diff) {
 		for (uint32_t i = 0; i < N_KERNELS; i++)
 			if (g_kernels[i].k == (int)p->k && g_kernels[i].r == (int)p->rows &&
-			    !g_kernels[i].acc && !g_kernels[i].diff && g_kernels[i].var == want_var) {
+			    !g_kernels[i].acc && !g_kernels[i].diff) {
 				id = i;
 				break;
 			}
 	}
 	if (id == N_KERNELS) {
 		for (uint32_t i = 0; i < N_KERNELS; i++)
-			if (g_kernels[i].k == 0 && g_kernels[i].var == 0 &&
-			    g_kernels[i].acc == (int)(p->accumulate != 0) &&
+			if (g_kernels[i].k == 0 && g_kernels[i].acc == (int)(p->accumulate != 0) &&
 			    g_kernels[i].diff == (int)(p->diff != 0)) {
 				id = i;
 				break;
 			}
 	}
 
-	// Grid: x over the 4 KiB columns of a stripe, y over stripes; both
-	// grid-stride.  Default aims at ~8 resident 256-thread blocks per CU.
+	// Grid: x over the 4 KiB columns of a stripe, y over stripes, one
+	// (stripe, column) item per block.  Measured on MI355X (tools/tune2.py,
+	// profiles/r01/tune2.json): one-shot blocks beat a ~8 blocks/CU
+	// grid-stride grid by 15-30 % on every shape (EC_4P2 encode 4.7 ->
+	// 6.2 TB/s) -- the dispatcher refills CUs faster than a resident block
+	// re-issues its next item's loads.  Both loops still stride for
+	// grids beyond 65535.
 	uint32_t gx = cfg && cfg->grid_x ? cfg->grid_x : (uint32_t)(nchunk < 65535 ? nchunk : 65535);
-	uint32_t gy;
-	if (cfg && cfg->grid_y) {
-		gy = cfg->grid_y;
-	} else {
-		uint64_t want = (2048 * 4 + gx - 1) / gx;
-		gy = (uint32_t)(want < p->nstripes ? want : p->nstripes);
-		if (gy > 65535)
-			gy = 65535;
-		if (gy == 0)
-			gy = 1;
-	}
+	uint32_t gy = cfg && cfg->grid_y ? cfg->grid_y : (p->nstripes < 65535 ? p->nstripes : 65535);
 	hipLaunchKernelGGL(g_kernels[id].fn, dim3(gx, gy), dim3(BLOCK), 0, st, *p);
 	if (kernel_id)
 		*kernel_id = id;
@@ -459,14 +441,16 @@ extern "C" int ecg_k_launch_matmul(const ecg_mm_params_t *p, const ecg_launch_cf
 }
 
 extern "C" int ecg_k_launch_copy(const void *src, void *dst, uint64_t bytes, int mode, void *stream,
-				 uint32_t *kernel_id)
+				 uint32_t max_blocks, uint32_t *kernel_id)
 {
 	const uint64_t n16 = bytes / 16;
 	uint64_t blocks = (n16 + 4 * BLOCK - 1) / (4 * BLOCK);
 	hipStream_t st = (hipStream_t)stream;
 
-	if (blocks > 256 * 8)
-		blocks = 256 * 8;
+	if (max_blocks == 0)
+		max_blocks = 1u << 20;
+	if (blocks > max_blocks)
+		blocks = max_blocks;
 	if (blocks == 0)
 		return (int)hipSuccess;
 	if (mode == 1)

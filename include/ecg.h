@@ -168,14 +168,13 @@ int ecg_event_elapsed_ms(ecg_ctx_t *ctx, void *start, void *stop, float *ms);
 int ecg_device_sync(ecg_ctx_t *ctx);
 /* Streaming kernels (16 B/lane) used to measure the achievable HBM rate:
  * mode 0 copy src->dst, 1 read-only (dst receives 16 B per thread of the
- * launch, <= 8 MiB), 2 write-only (fills dst). */
+ * launch, <= 8 MiB), 2 write-only (fills dst).  ecg_set_launch's grid_x, when
+ * set, caps the block count (default: one 4 x 16 B slice per thread). */
 int ecg_dev_copy_kernel(ecg_ctx_t *ctx, void *dst, const void *src, size_t bytes, int mode,
 			void *stream);
 
 /* ---- launch tuning (benchmarks; 0 = default) ----------------------------
- * variant: 0 auto, 1 runtime-shaped kernel, 2 byte kernel, 16+v tuning
- * variant v (bit0 plain loads, bit1 plain stores, bit2 two stripes per
- * iteration) of the EC_4P2 / EC_8P2 / EC_16P2 kernels. */
+ * variant: 0 auto, 1 runtime-shaped kernel, 2 byte kernel. */
 int ecg_set_launch(ecg_ctx_t *ctx, uint32_t grid_x, uint32_t grid_y, uint32_t variant);
 
 #ifdef __cplusplus

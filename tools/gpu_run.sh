@@ -47,6 +47,15 @@ for what in "$@"; do
 		step rocprof_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run \
 			-- python3 bench.py --steps 4 --warmup 1 --no-detail --no-cpu --profile-only || exit $?
 		;;
+	tune)
+		step tune 600 python tools/tune.py || exit $?
+		;;
+	tune2)
+		step tune2 600 python tools/tune2.py || exit $?
+		;;
+	tune3)
+		step tune3 600 python tools/tune3.py || exit $?
+		;;
 	*)
 		echo "unknown step $what"; exit 2
 		;;
