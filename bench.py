@@ -166,20 +166,36 @@ def time_kernel(ctx, fn, iters):
     return ms[len(ms) // 2]
 
 
-def detail_rows(ctx, iters=5):
+def measured_ceilings(ctx, iters=7):
+    """This box's streaming rates (GB/s), each mode at its best measured
+    geometry (profiles/r01/tune2*.json): reads with 512 persistent blocks,
+    writes / copies with one 4 x 16 B slice per thread."""
+    n = 2 << 30
+    a, b = ctx.alloc(n), ctx.alloc(n)
+    a.fill(0x3C)
+    out = {}
+    for mode, name, nbytes, blocks in ((0, "copy", 2 * n, 0), (1, "read", n, 512), (2, "write", n, 0)):
+        ctx.set_launch(blocks, 0, 0)
+        ms = time_kernel(ctx, lambda: ctx.copy_kernel(b.ptr, a.ptr, n, mode), iters)
+        out[name] = round(nbytes / ms / 1e6, 1)
+    ctx.set_launch(0, 0, 0)
+    a.free()
+    b.free()
+    return out
+
+
+def mix_ceiling(ceil, read_frac):
+    """Time-weighted ceiling for a read/write mix from the measured rates."""
+    return 1.0 / (read_frac / ceil["read"] + (1 - read_frac) / ceil["write"])
+
+
+def detail_rows(ctx, ceil, iters=7):
     """Extra device-resident rows (per GPU): the north-star EC_8P2 encode,
-    EC_8P2 2-erasure decode, EC_16P2 128 KiB encode, and this box's measured
-    HBM copy rate.  Median kernel time over `iters` launches."""
+    EC_8P2 2-erasure decode, EC_16P2 128 KiB encode, EC_2P1 128 KiB encode.
+    Median kernel time over `iters` launches."""
     from daos_amd import ecg
 
     rows = {}
-    # HBM copy ceiling (2 GiB read + 2 GiB write)
-    n = 2 << 30
-    a, b = ctx.alloc(n), ctx.alloc(n)
-    ms = time_kernel(ctx, lambda: ctx.copy_kernel(b.ptr, a.ptr, n), iters)
-    rows["hbm_copy"] = {"GBps": round(2 * n / ms / 1e6, 1), "frac_of_spec": round(2 * n / ms / 1e6 / HBM_PEAK_GBS, 4)}
-    a.free()
-    b.free()
     for name, k, p, C, S, mode in (("EC_8P2_1MiB_encode", 8, 2, 1 << 20, 512, "enc"),
                                    ("EC_8P2_1MiB_decode_d0d1", 8, 2, 1 << 20, 512, "dec"),
                                    ("EC_16P2_128KiB_encode", 16, 2, 128 << 10, 1024, "enc"),
@@ -190,18 +206,20 @@ def detail_rows(ctx, iters=5):
         if mode == "enc":
             fn = (lambda buf=buf, k=k, p=p, C=C, S=S, st=st:
                   ctx.encode(k, p, C, S, buf.ptr, st, buf.ptr + k * C, C, st))
-            alg = (k + p) * C * S
+            rd, wr = k, p
         else:
             ctx.encode(k, p, C, S, buf.ptr, st, buf.ptr + k * C, C, st)
             fn = (lambda buf=buf, k=k, p=p, C=C, S=S, st=st:
                   ctx.recover(k, p, C, S, buf.ptr, st, [0, 1]))
-            alg = (k + 2) * C * S
+            rd, wr = k, 2
         ms = time_kernel(ctx, fn, iters)
+        alg = (rd + wr) * C * S
         gbs = alg / ms / 1e6
-        rows[name] = {"GiBps_user": round(k * C * S / ms / 1e3 / GIB * 1e6, 1), "alg_GBps": round(gbs, 1),
+        mix = mix_ceiling(ceil, rd / (rd + wr))
+        rows[name] = {"GiBps_user": round(k * C * S / (ms / 1e3) / GIB, 1), "alg_GBps": round(gbs, 1),
                       "roofline_frac": round(gbs / HBM_PEAK_GBS, 4),
-                      "frac_of_measured_copy": round(gbs / rows["hbm_copy"]["GBps"], 4),
-                      "kernel": ecg.last_kernel(), "ms": round(ms, 3)}
+                      "measured_mix_ceiling_GBps": round(mix, 1), "frac_of_measured_mix": round(gbs / mix, 4),
+                      "kernel": ecg.last_kernel(), "ms": round(ms, 4)}
         buf.free()
     return rows
 
@@ -259,8 +277,12 @@ def main():
 
     from daos_amd import ecg
 
-    torch.cuda.set_device(local)
-    ctx = ecg.Context(local)
+    ndev = ecg.device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py: no gfx950 device visible")
+    dev = local % ndev          # > 1 rank per GPU only when rehearsing on a 1-GPU box
+    torch.cuda.set_device(dev)
+    ctx = ecg.Context(dev)
     k, p, C, S = args.k, args.p, args.cell, args.stripes
     wl = Workload(ctx, k, p, C, S)
 
@@ -325,9 +347,14 @@ def main():
                      "decode_ms_median": round(dec_ms[len(dec_ms) // 2], 4)},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_detail:
-        out["detail"] = detail_rows(ctx)
     wl.free()
+    if rank == 0 and world == 1 and not args.no_detail:
+        ceil = measured_ceilings(ctx)
+        mix = mix_ceiling(ceil, k / (k + p))
+        out["roofline"]["measured_stream_GBps"] = ceil
+        out["roofline"]["measured_mix_ceiling_GBps"] = round(mix, 1)
+        out["roofline"]["frac_of_measured_mix"] = round(achieved / mix, 4)
+        out["detail"] = detail_rows(ctx, ceil)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(k, p, C, args.cpu_seconds)
     if rank == 0:

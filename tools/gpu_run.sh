@@ -53,6 +53,13 @@ for what in "$@"; do
 	tune2)
 		step tune2 600 python tools/tune2.py || exit $?
 		;;
+	pcie)
+		step pcie 600 python tools/bench_pcie.py || exit $?
+		;;
+	dist2)
+		step dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+			--master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 || exit $?
+		;;
 	tune3)
 		step tune3 600 python tools/tune3.py || exit $?
 		;;
