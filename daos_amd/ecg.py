@@ -53,6 +53,12 @@ _SIGS = [
     ("ecg_matmul_host", C.c_int, [vp, C.c_int, C.c_int, C.c_int, u8p, C.POINTER(u8p), C.POINTER(u8p), C.c_uint]),
     ("ecg_encode_host", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, vp, vp, C.c_uint32]),
     ("ecg_recover_host", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, vp, u32p, C.c_int, C.c_uint32]),
+    ("ecg_queue_create", C.c_int, [vp, vp, C.POINTER(vp)]),
+    ("ecg_queue_destroy", None, [vp]),
+    ("ecg_queue_encode", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.POINTER(u8p), C.POINTER(u8p), vp, vp]),
+    ("ecg_queue_recover", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, u8p, u32p, C.c_int, vp, vp]),
+    ("ecg_queue_flush", C.c_int, [vp]),
+    ("ecg_queue_stats", C.c_int, [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("ecg_dev_alloc", C.c_int, [vp, C.c_size_t, C.POINTER(vp)]),
     ("ecg_dev_free", C.c_int, [vp, vp]),
     ("ecg_host_alloc", C.c_int, [vp, C.c_size_t, C.POINTER(vp)]),
@@ -329,6 +335,61 @@ class Context:
         sp = (u8p * k)(*[_u8(s) for s in src])
         dp = (u8p * rows)(*[_u8(d) for d in dst])
         _chk(lib().ecg_matmul_host(self.h, n, k, rows, _u8(coef), sp, dp, flags), "matmul_host")
+
+
+class QueueAttr(C.Structure):
+    _fields_ = [("max_batch", C.c_uint32), ("max_wait_us", C.c_uint32), ("max_cell_bytes", C.c_uint64)]
+
+
+DONE_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_int)
+
+
+class Queue:
+    """ecg_queue_t: one-stripe requests from many threads -> batched launches.
+    Completion is reported through a C callback; this wrapper records rc per
+    request id (callbacks run on the queue's worker thread)."""
+
+    def __init__(self, ctx: Context, max_batch: int = 0, max_wait_us: int = 0, max_cell_bytes: int = 0):
+        self.ctx = ctx
+        h = vp()
+        attr = QueueAttr(max_batch, max_wait_us, max_cell_bytes)
+        _chk(lib().ecg_queue_create(ctx.h, C.byref(attr), C.byref(h)), "queue_create")
+        self.h = h.value
+        self.done = {}
+        self._keep = {}
+
+        def _cb(arg, rc):          # arg = request id + 1 (a NULL void* would arrive as None)
+            self.done[arg - 1] = rc
+
+        self._cb = DONE_CB(_cb)
+
+    def encode(self, rid: int, k: int, p: int, data, parity):
+        C_ = data[0].shape[0]
+        sp = (u8p * k)(*[_u8(d) for d in data])
+        dp = (u8p * p)(*[_u8(d) for d in parity])
+        self._keep[rid] = (data, parity)
+        _chk(lib().ecg_queue_encode(self.h, k, p, C_, sp, dp, self._cb, rid + 1), "queue_encode")
+
+    def recover(self, rid: int, k: int, p: int, stripe: np.ndarray, err_list):
+        C_ = stripe.shape[-1]
+        self._keep[rid] = stripe
+        _chk(lib().ecg_queue_recover(self.h, k, p, C_, _u8(stripe), _u32(err_list), len(err_list), self._cb,
+                                     rid + 1),
+             "queue_recover")
+
+    def flush(self):
+        _chk(lib().ecg_queue_flush(self.h), "queue_flush")
+        self._keep.clear()
+
+    def stats(self):
+        r, b = C.c_uint64(), C.c_uint64()
+        _chk(lib().ecg_queue_stats(self.h, C.byref(r), C.byref(b)), "queue_stats")
+        return r.value, b.value
+
+    def close(self):
+        if self.h:
+            lib().ecg_queue_destroy(self.h)
+            self.h = None
 
 
 # ---------------------------------------------------------------- ISA-L drop-in

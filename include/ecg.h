@@ -150,6 +150,42 @@ int ecg_recover_host(ecg_ctx_t *ctx, int k, int p, uint64_t cell_bytes, uint32_t
 		     void *stripes, const uint32_t *err_list, int nerrs,
 		     uint32_t chunk_stripes);
 
+/* ---- batching facade for one-stripe callers ------------------------------
+ * Every reference caller issues ONE stripe per codec call (client write
+ * ref:src/object/cli_ec.c:627-659, rebuild ref:src/object/srv_obj_migrate.c:
+ * 1116-1177, aggregation ULTs on the offload xstream ref:src/object/
+ * srv_ec_aggregate.c:701-734).  An ecg_queue accepts such requests from any
+ * number of threads, coalesces compatible ones (same op, k, p, cell size and
+ * erasure set) into one device batch, and completes each request through its
+ * callback -- the place DAOS sets its ABT_eventual (srv_ec_aggregate.c:696).
+ * Host buffers must stay valid until the callback runs.  Callbacks run on the
+ * queue's worker thread and must not block on the queue. */
+typedef struct ecg_queue ecg_queue_t;
+typedef void (*ecg_done_cb_t)(void *arg, int rc);
+
+typedef struct ecg_queue_attr {
+	uint32_t max_batch;	/* stripes per device batch (default 256) */
+	uint32_t max_wait_us;	/* how long a lone request may wait for company (default 50) */
+	uint64_t max_cell_bytes; /* staging sized for this cell size (default 1 MiB) */
+} ecg_queue_attr_t;
+
+/* attr may be NULL for defaults. */
+int ecg_queue_create(ecg_ctx_t *ctx, const ecg_queue_attr_t *attr, ecg_queue_t **q);
+/* Drains outstanding requests (their callbacks run) then frees the queue. */
+void ecg_queue_destroy(ecg_queue_t *q);
+/* Encode one stripe: data[k] -> parity[p] (host pointers, cell_bytes each). */
+int ecg_queue_encode(ecg_queue_t *q, int k, int p, uint64_t cell_bytes,
+		     unsigned char *const *data, unsigned char *const *parity,
+		     ecg_done_cb_t cb, void *arg);
+/* Recover one stripe in place: `stripe` is [k+p][cell_bytes] host memory in
+ * logical cell order; err_list holds the erased logical cells. */
+int ecg_queue_recover(ecg_queue_t *q, int k, int p, uint64_t cell_bytes, unsigned char *stripe,
+		      const uint32_t *err_list, int nerrs, ecg_done_cb_t cb, void *arg);
+/* Block until every request submitted before the call has completed. */
+int ecg_queue_flush(ecg_queue_t *q);
+/* Counters: requests completed, device batches launched. */
+int ecg_queue_stats(ecg_queue_t *q, uint64_t *requests, uint64_t *batches);
+
 /* ---- memory / streams / timing plumbing --------------------------------- */
 int ecg_dev_alloc(ecg_ctx_t *ctx, size_t bytes, void **ptr);
 int ecg_dev_free(ecg_ctx_t *ctx, void *ptr);

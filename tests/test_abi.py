@@ -19,6 +19,7 @@ def declared_functions():
         txt = open(os.path.join(ROOT, h)).read()
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
         txt = re.sub(r"#.*", "", txt)
+        txt = re.sub(r"typedef[^;]*;", "", txt)
         for m in re.finditer(r"\b([a-z_][a-z0-9_]*)\s*\(", txt):
             if m.group(1) not in ("if", "for", "while", "sizeof", "return") and m.group(1) not in names:
                 names.append(m.group(1))

@@ -395,3 +395,89 @@ def test_config3_ec8p2_1mib_degraded_decode(ctx, oracle):
     got = buf.download().reshape(S, k + p, C_)
     assert np.array_equal(got[:, :k], data)
     buf.free()
+
+
+
+# --------------------------------------------------------------- batching facade
+def test_queue_batches_concurrent_one_stripe_calls(ctx, oracle, ecglib):
+    """8 threads x 40 one-stripe EC_8P2 encodes (the reference's calling
+    pattern) complete bit-exact and are coalesced into far fewer launches."""
+    import threading
+
+    k, p, C_ = 8, 2, 32768
+    q = ecglib.Queue(ctx, max_batch=64, max_wait_us=2000)
+    en = oracle.cauchy1(k, p)
+    jobs = {}
+    for t in range(8):                 # inputs ready before the burst of calls
+        for i in range(40):
+            rid = t * 1000 + i
+            jobs[rid] = ([rand(C_, rid * 16 + j) for j in range(k)], [np.zeros(C_, dtype=np.uint8) for _ in range(p)])
+
+    def worker(t):
+        for i in range(40):
+            rid = t * 1000 + i
+            q.encode(rid, k, p, *jobs[rid])
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    q.flush()
+    nreq, nbatch = q.stats()
+    assert nreq == 320 and len(q.done) == 320
+    assert all(rc == 0 for rc in q.done.values())
+    assert nbatch < nreq / 4, (nreq, nbatch)
+    for rid, (data, par) in jobs.items():
+        want = oracle.encode_data(en[k:], np.stack(data))
+        assert np.array_equal(np.stack(par), want), rid
+    q.close()
+
+
+def test_queue_mixed_classes_and_recovery(ctx, oracle, ecglib):
+    """Interleaved encode 4P2 / encode 8P3 (odd cell size) / recover with two
+    different erasure sets: each class batched separately, all bit-exact."""
+    q = ecglib.Queue(ctx, max_batch=16, max_wait_us=100)
+    checks = []
+    rid = 0
+    for i in range(24):
+        kind = i % 4
+        if kind == 0:
+            k, p, C_ = 4, 2, 4096
+        elif kind == 1:
+            k, p, C_ = 8, 3, 933
+        else:
+            k, p, C_ = 4, 2, 8192
+        data = rand((k, C_), 7000 + i)
+        en = oracle.cauchy1(k, p)
+        par = oracle.encode_data(en[k:], data)
+        if kind < 2:
+            outp = [np.zeros(C_, dtype=np.uint8) for _ in range(p)]
+            q.encode(rid, k, p, list(data), outp)
+            checks.append((rid, lambda outp=outp, par=par: np.array_equal(np.stack(outp), par)))
+        else:
+            stripe = np.concatenate([data, par]).copy()
+            err = [0, 5] if kind == 2 else [3]
+            broken = stripe.copy()
+            broken[err] = 0
+            q.recover(rid, k, p, broken, err)
+            checks.append((rid, lambda broken=broken, stripe=stripe: np.array_equal(broken, stripe)))
+        rid += 1
+    q.flush()
+    for r, ok in checks:
+        assert q.done[r] == 0 and ok(), r
+    nreq, nbatch = q.stats()
+    assert nreq == 24 and nbatch >= 4
+    q.close()
+
+
+def test_queue_destroy_drains(ctx, oracle, ecglib):
+    k, p, C_ = 2, 1, 4096
+    q = ecglib.Queue(ctx, max_batch=1000, max_wait_us=1000000)   # would wait 1 s for company
+    data = [rand(C_, 1), rand(C_, 2)]
+    par = [np.zeros(C_, dtype=np.uint8)]
+    q.encode(1, k, p, data, par)
+    keep = q.done
+    q.close()                       # must drain: callback runs before destroy returns
+    assert keep.get(1) == 0
+    assert np.array_equal(par[0], oracle.encode_data(oracle.cauchy1(k, p)[k:], np.stack(data))[0])

@@ -60,6 +60,15 @@ for what in "$@"; do
 		step dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
 			--master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 || exit $?
 		;;
+	tune4)
+		step tune4 600 python tools/tune4.py || exit $?
+		;;
+	tune5)
+		step tune5 600 python tools/tune5.py || exit $?
+		;;
+	tune6)
+		step tune6 600 python tools/tune6.py || exit $?
+		;;
 	tune3)
 		step tune3 600 python tools/tune3.py || exit $?
 		;;
