@@ -35,6 +35,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 GIB = float(1 << 30)
+PARITY_ROW_PAD = 4096
 HBM_PEAK_GBS = 8000.0          # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 ROUND = "r01"
 
@@ -103,8 +104,12 @@ class Workload:
 
     def __init__(self, ctx, k, p, C, S, err=(0, 1), config_id=2):
         self.ctx, self.k, self.p, self.C, self.S, self.err = ctx, k, p, C, S, list(err)
+        # Parity rows [p][S][C] at a pitch of S*C + 4 KiB: rows exactly a power
+        # of two apart alias in HBM and cost EC_8P2 encode ~10 %
+        # (profiles/r01/tune5_parity_row_aliasing.json, tune6_pitch.json).
+        self.prow = S * C + PARITY_ROW_PAD
         self.data = ctx.alloc(S * k * C)
-        self.parity = ctx.alloc(p * S * C)
+        self.parity = ctx.alloc(p * self.prow)
         self.stripes = ctx.alloc(S * (k + p) * C)
         fill_device(ctx, self.data, S * k * C, config_id)
         # recovery buffer: a consistent [S][k+p][C] image (encode in place)
@@ -119,7 +124,7 @@ class Workload:
         ev = [c.event() for _ in range(4)] if timed else None
         if timed:
             c.record(ev[0])
-        c.encode(k, p, C, S, self.data.ptr, k * C, self.parity.ptr, S * C, C)
+        c.encode(k, p, C, S, self.data.ptr, k * C, self.parity.ptr, self.prow, C)
         if timed:
             c.record(ev[1])
             c.record(ev[2])
@@ -336,7 +341,8 @@ def main():
         "dtype": "u8",
         "data": "synthetic: xoshiro256** stripes seeded 0xDA05EC00+id (BASELINE.md §3), device-resident",
         "config": {"workload": f"EC_{k}P{p} {C >> 10} KiB cells x {S} stripes per GPU: encode (data [S][k][C] -> "
-                               f"parity [p][S][C]) + degraded decode of cells d0,d1 in [S][k+p][C]",
+                               f"parity [p][S][C], row pitch S*C+4KiB) + degraded decode of cells d0,d1 in "
+                               f"[S][k+p][C]",
                    "k": k, "p": p, "cell_bytes": C, "stripes_per_gpu": S, "erasures": wl.err,
                    "parallelism": f"stripe-sharded x{world}, no collective"},
         "roofline": {"bound": "hbm", "kernel": kernel_name, "achieved": round(achieved, 1),

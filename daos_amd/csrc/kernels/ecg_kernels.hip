@@ -352,6 +352,8 @@ static const kentry g_kernels[] = {
 #define N_KERNELS ((uint32_t)(sizeof(g_kernels) / sizeof(g_kernels[0])))
 
 
+
+
 #define KID_BYTE N_KERNELS
 #define KID_COPY (N_KERNELS + 1)
 #define KID_READ (N_KERNELS + 2)
@@ -385,6 +387,7 @@ extern "C" const char *ecg_k_kernel_name(uint32_t id)
 		return "ecg_stream_kernel<read>";
 	if (id == KID_WRITE)
 		return "ecg_stream_kernel<write>";
+
 
 	return "?";
 }

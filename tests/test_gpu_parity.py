@@ -481,3 +481,4 @@ def test_queue_destroy_drains(ctx, oracle, ecglib):
     q.close()                       # must drain: callback runs before destroy returns
     assert keep.get(1) == 0
     assert np.array_equal(par[0], oracle.encode_data(oracle.cauchy1(k, p)[k:], np.stack(data))[0])
+

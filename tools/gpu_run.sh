@@ -69,6 +69,9 @@ for what in "$@"; do
 	tune6)
 		step tune6 600 python tools/tune6.py || exit $?
 		;;
+	tune7)
+		step tune7 600 python tools/tune7.py || exit $?
+		;;
 	tune3)
 		step tune3 600 python tools/tune3.py || exit $?
 		;;
