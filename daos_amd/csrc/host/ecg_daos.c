@@ -202,18 +202,55 @@ int ecg_obj_ec_encode_stripes(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_byte
 	return ecg_encode_host(ctx, k, p, cell_bytes, nstripes, data, parity, 0);
 }
 
-/* agg_update_parity (ref:src/object/srv_ec_aggregate.c:1062-1105): for the
- * i-th updated cell, j = i-th set bit of bit_map;
- * parity[r] ^= coef[r][j] * (old_i ^ new_i).  All updated cells of the
- * stripe are folded into one device product. */
-int ecg_agg_update_parity(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_bytes,
+static int bit_isset(const uint8_t *bm, uint32_t j)
+{
+	return (bm[j / 8] >> (j % 8)) & 1u;
+}
+
+/* The byte ranges of cell `cell_idx` that agg_diff_preprocess zeroes in the
+ * diff (ref:src/object/srv_ec_aggregate.c:1006-1058) -- between and after the
+ * new extents, the tail only once some extent has touched the cell
+ * (hole_off > 0) -- get `old` copied over `dst`, so old ^ dst is zero there. */
+static void for_each_hole(uint64_t len, uint64_t rsize, uint32_t cell_idx, const uint64_t *es,
+			  const uint64_t *en, uint32_t n, unsigned char *dst, const unsigned char *old)
+{
+	const uint64_t cs = (uint64_t)cell_idx * len, ce = cs + len;
+	uint64_t hole_off = 0;
+	uint32_t i;
+
+	for (i = 0; i < n; i++) {
+		const uint64_t estart = es[i], eend = es[i] + en[i];
+		uint64_t hole_end;
+
+		if (estart >= ce)
+			break;
+		if (eend <= cs)
+			continue;
+		hole_end = cs + hole_off;
+		if (estart > hole_end)
+			memcpy(dst + hole_off * rsize, old + hole_off * rsize, (estart - hole_end) * rsize);
+		hole_off = eend - cs;
+	}
+	if (hole_off > 0 && hole_off < len)
+		memcpy(dst + hole_off * rsize, old + hole_off * rsize, (len - hole_off) * rsize);
+}
+
+/* agg_update_parity: parity[r] ^= coef[r][j] * (old_i ^ new_i'), where new_i'
+ * is new_i with holes replaced by old_i (so the diff is zero there, exactly
+ * the reference's memset of the diff).  (old ^ new') * c == old*c ^ new'*c,
+ * so both feed the same device product as two sources with equal
+ * coefficients, accumulated into parity. */
+int ecg_agg_update_parity(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_recs, uint64_t rsize,
 			  const uint8_t *bit_map, uint32_t cell_cnt,
 			  const unsigned char *old_cells, const unsigned char *new_cells,
+			  const uint64_t *ext_start, const uint64_t *ext_nr, uint32_t n_ext,
 			  unsigned char *parity)
 {
 	unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
 	unsigned char coef[ECG_MAX_P * 2 * ECG_MAX_K];
 	unsigned char *src[2 * ECG_MAX_K], *dst[ECG_MAX_P];
+	unsigned char *masked = NULL;
+	const uint64_t cb = cell_recs * rsize;
 	uint32_t i, j;
 	int k, p, r, rc;
 
@@ -222,28 +259,125 @@ int ecg_agg_update_parity(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_bytes,
 		return rc;
 	if (cell_cnt == 0)
 		return 0;
-	if (cell_cnt > (uint32_t)k || cell_bytes > 0x7fffffffULL)
-		return ecg_fail(-ECG_DER_INVAL, "agg_update_parity: bad cell_cnt %u", cell_cnt);
+	if (cell_cnt > (uint32_t)k || cb == 0 || cb > 0x7fffffffULL || bit_map == NULL ||
+	    (n_ext && (ext_start == NULL || ext_nr == NULL)))
+		return ecg_fail(-ECG_DER_INVAL, "agg_update_parity: bad arguments");
 	rc = pick_ctx(&ctx);
 	if (rc)
 		return rc;
+	if (n_ext) {
+		masked = malloc((size_t)cb * cell_cnt);
+		if (masked == NULL)
+			return ecg_fail(-ECG_DER_NOMEM, "agg_update_parity: malloc");
+	}
 	ecg_gen_cauchy1(k, p, en);
-	/* (old ^ new) * c == old * c ^ new * c: feed both as sources with the
-	 * same coefficient and accumulate into parity. */
 	for (i = 0, j = 0; i < cell_cnt; i++, j++) {
-		while (j < (uint32_t)k && !(bit_map[j / 8] & (1u << (j % 8))))
+		const unsigned char *o = old_cells + (size_t)i * cb;
+		const unsigned char *nw = new_cells + (size_t)i * cb;
+
+		while (j < (uint32_t)k && !bit_isset(bit_map, j))
 			j++;
-		if (j >= (uint32_t)k)
-			return ecg_fail(-ECG_DER_INVAL, "agg_update_parity: bitmap short");
-		src[2 * i] = (unsigned char *)old_cells + (size_t)i * cell_bytes;
-		src[2 * i + 1] = (unsigned char *)new_cells + (size_t)i * cell_bytes;
+		if (j >= (uint32_t)k) {
+			free(masked);
+			return ecg_fail(-ECG_DER_INVAL, "agg_update_parity: bitmap has < %u cells", cell_cnt);
+		}
+		if (masked) {
+			unsigned char *m = masked + (size_t)i * cb;
+
+			memcpy(m, nw, cb);
+			for_each_hole(cell_recs, rsize, j, ext_start, ext_nr, n_ext, m, o);
+			nw = m;
+		}
+		src[2 * i] = (unsigned char *)o;
+		src[2 * i + 1] = (unsigned char *)nw;
 		for (r = 0; r < p; r++) {
 			coef[r * 2 * cell_cnt + 2 * i] = en[(k + r) * k + j];
 			coef[r * 2 * cell_cnt + 2 * i + 1] = en[(k + r) * k + j];
 		}
 	}
 	for (r = 0; r < p; r++)
-		dst[r] = parity + (size_t)r * cell_bytes;
-	return ecg_matmul_host(ctx, (int)cell_bytes, (int)(2 * cell_cnt), p, coef, src, dst,
-			       ECG_F_ACCUMULATE);
+		dst[r] = parity + (size_t)r * cb;
+	rc = ecg_matmul_host(ctx, (int)cb, (int)(2 * cell_cnt), p, coef, src, dst, ECG_F_ACCUMULATE);
+	free(masked);
+	return rc;
+}
+
+int ecg_agg_recalc_parity(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cb, const uint8_t *bit_map,
+			  uint32_t cell_cnt, const unsigned char *rbuf, const unsigned char *lbuf,
+			  unsigned char *parity)
+{
+	unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
+	unsigned char *data[ECG_MAX_K], *dst[ECG_MAX_P];
+	uint32_t rr = 0, ll = 0;
+	int k, p, i, rc;
+
+	rc = ecg_obj_ec_class_kp(oc_id, &k, &p);
+	if (rc)
+		return rc;
+	if (cb == 0 || cb > 0x7fffffffULL || bit_map == NULL || cell_cnt > (uint32_t)k)
+		return ecg_fail(-ECG_DER_INVAL, "agg_recalc_parity: bad arguments");
+	for (i = 0; i < k; i++) {
+		if (bit_isset(bit_map, (uint32_t)i))
+			data[i] = (unsigned char *)rbuf + (size_t)rr++ * cb;
+		else
+			data[i] = (unsigned char *)lbuf + (size_t)ll++ * cb;
+	}
+	if (rr != cell_cnt)	/* D_ASSERT(r == cell_cnt) in the reference */
+		return ecg_fail(-ECG_DER_INVAL, "agg_recalc_parity: bitmap has %u cells, not %u", rr,
+				cell_cnt);
+	rc = pick_ctx(&ctx);
+	if (rc)
+		return rc;
+	for (i = 0; i < p; i++)
+		dst[i] = parity + (size_t)i * cb;
+	ecg_gen_cauchy1(k, p, en);
+	return ecg_matmul_host(ctx, (int)cb, k, p, &en[k * k], data, dst, 0);
+}
+
+uint64_t ecg_obj_ec_singv_cell_bytes(uint32_t oc_id, uint64_t iod_size)
+{
+	uint64_t c;
+	int k, p;
+
+	if (ecg_obj_ec_class_kp(oc_id, &k, &p))
+		return 0;
+	c = iod_size / (uint64_t)k + (iod_size % (uint64_t)k != 0);
+	return (c + 7) & ~7ull;		/* OBJ_EC_SINGV_CELL_ALIGN */
+}
+
+int ecg_obj_ec_singv_encode(uint32_t oc_id, uint64_t iod_size, const unsigned char *value,
+			    unsigned char *p_bufs[])
+{
+	unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
+	unsigned char *data[ECG_MAX_K];
+	unsigned char *cells;
+	ecg_ctx_t *ctx = NULL;
+	uint64_t cb;
+	int k, p, i, rc;
+
+	rc = ecg_obj_ec_class_kp(oc_id, &k, &p);
+	if (rc)
+		return rc;
+	cb = ecg_obj_ec_singv_cell_bytes(oc_id, iod_size);
+	if (iod_size == 0 || value == NULL || cb > 0x7fffffffULL)
+		return ecg_fail(-ECG_DER_INVAL, "singv_encode: bad arguments");
+	for (i = 0; i < p && p_bufs[i] == NULL; i++) {
+		p_bufs[i] = malloc(cb);
+		if (p_bufs[i] == NULL)
+			return ecg_fail(-ECG_DER_NOMEM, "singv_encode: malloc");
+	}
+	/* the last data cell is zero padded (ref:src/object/cli_ec.c:494-503) */
+	cells = calloc((size_t)k, cb);
+	if (cells == NULL)
+		return ecg_fail(-ECG_DER_NOMEM, "singv_encode: calloc");
+	memcpy(cells, value, iod_size);
+	for (i = 0; i < k; i++)
+		data[i] = cells + (size_t)i * cb;
+	rc = pick_ctx(&ctx);
+	if (rc == 0) {
+		ecg_gen_cauchy1(k, p, en);
+		rc = ecg_matmul_host(ctx, (int)cb, k, p, &en[k * k], data, p_bufs, 0);
+	}
+	free(cells);
+	return rc;
 }

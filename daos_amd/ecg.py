@@ -95,7 +95,11 @@ _SIGS = [
     ("ecg_obj_ec_recov_codec_init", C.c_int, [C.c_uint32, u32p, C.c_uint32, vp]),
     ("ecg_obj_ec_recov_data", C.c_int, [vp, vp, C.c_uint64, u8p, C.c_uint32]),
     ("ecg_obj_ec_encode_stripes", C.c_int, [vp, C.c_uint32, C.c_uint64, C.c_uint32, u8p, u8p]),
-    ("ecg_agg_update_parity", C.c_int, [vp, C.c_uint32, C.c_uint64, u8p, C.c_uint32, u8p, u8p, u8p]),
+    ("ecg_agg_update_parity", C.c_int, [vp, C.c_uint32, C.c_uint64, C.c_uint64, u8p, C.c_uint32, u8p, u8p,
+                                        C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_uint32, u8p]),
+    ("ecg_agg_recalc_parity", C.c_int, [vp, C.c_uint32, C.c_uint64, u8p, C.c_uint32, u8p, u8p, u8p]),
+    ("ecg_obj_ec_singv_cell_bytes", C.c_uint64, [C.c_uint32, C.c_uint64]),
+    ("ecg_obj_ec_singv_encode", C.c_int, [C.c_uint32, C.c_uint64, u8p, C.POINTER(u8p)]),
 ]
 
 EXPORTED = [n for n, _, _ in _SIGS]

@@ -22,8 +22,12 @@
  *                                      ref:src/object/cli_ec.c:2626-2643, 2814-2885
  *   ecg_obj_ec_encode_stripes       <- obj_ec_recx_encode's stripe loop
  *                                      ref:src/object/cli_ec.c:593-663
- *   ecg_agg_update_parity           <- agg_update_parity
- *                                      ref:src/object/srv_ec_aggregate.c:1062-1105
+ *   ecg_agg_update_parity           <- agg_update_parity + agg_diff_preprocess
+ *                                      ref:src/object/srv_ec_aggregate.c:1006-1105
+ *   ecg_agg_recalc_parity           <- agg_recalc_parity
+ *                                      ref:src/object/srv_ec_aggregate.c:1110-1138
+ *   ecg_obj_ec_singv_cell_bytes /   <- obj_ec_singv_cell_bytes, obj_ec_singv_encode
+ *   ecg_obj_ec_singv_encode            ref:src/object/obj_ec.h:421-434, cli_ec.c:1447-1465
  */
 #ifndef ECG_DAOS_H
 #define ECG_DAOS_H
@@ -96,16 +100,42 @@ int ecg_obj_ec_encode_stripes(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_byte
 			      uint32_t nstripes, const unsigned char *data,
 			      unsigned char *parity);
 
-/* agg_update_parity for one stripe, host buffers as in the reference:
- * old/new replica cells [cell_cnt][C] (AGG_IOV_ODATA / AGG_IOV_DATA),
- * parity [p][C] updated in place; bit_map marks the updated data cells.
- * The reference's diff buffer (AGG_IOV_DIFF) is not needed: old ^ new is
- * fused on the device.  (Hole zeroing, agg_diff_preprocess, is applied by
- * the caller to `new_cells` beforehand by copying `old` over hole ranges.) */
-int ecg_agg_update_parity(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_bytes,
+/* agg_update_parity + agg_diff_preprocess for one stripe
+ * (ref:src/object/srv_ec_aggregate.c:1006-1105), host buffers as in the
+ * reference: old/new replica cells [cell_cnt][C] (AGG_IOV_ODATA /
+ * AGG_IOV_DATA), parity [p][C] updated in place, C = cell_recs * rsize.  The
+ * i-th updated cell is the i-th set bit of bit_map.  ext_start/ext_nr are the
+ * stripe's new-data extents in records relative to the stripe start, sorted
+ * (the reference's as_dextents with holes and old epochs already skipped);
+ * bytes of an updated cell outside them count as unchanged, with the
+ * reference's exact rules (no extent touching the cell -> whole cell counts;
+ * n_ext = 0 -> no hole processing).  old ^ new is fused on the device: no
+ * AGG_IOV_DIFF buffer. */
+int ecg_agg_update_parity(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_recs, uint64_t rsize,
 			  const uint8_t *bit_map, uint32_t cell_cnt,
 			  const unsigned char *old_cells, const unsigned char *new_cells,
+			  const uint64_t *ext_start, const uint64_t *ext_nr, uint32_t n_ext,
 			  unsigned char *parity);
+
+/* agg_recalc_parity (ref:src/object/srv_ec_aggregate.c:1110-1138): re-encode
+ * a stripe whose data cells come from two buffers -- cell j from rbuf (fetched
+ * from peers) when bit j of bit_map is set, else from lbuf (local replicas),
+ * each consumed in order.  parity [p][cell_bytes]. */
+int ecg_agg_recalc_parity(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_bytes,
+			  const uint8_t *bit_map, uint32_t cell_cnt, const unsigned char *rbuf,
+			  const unsigned char *lbuf, unsigned char *parity);
+
+/* obj_ec_singv_cell_bytes (ref:src/object/obj_ec.h:421-434): cell size of an
+ * evenly distributed single value of iod_size bytes. 0 if not an EC class. */
+uint64_t ecg_obj_ec_singv_cell_bytes(uint32_t oc_id, uint64_t iod_size);
+
+/* Single-value encode (obj_ec_singv_encode / obj_ec_stripe_encode's singv
+ * branch, ref:src/object/cli_ec.c:476-546, 1447-1465): the value is split into
+ * k cells of ecg_obj_ec_singv_cell_bytes, the last one zero padded, and the p
+ * parity cells are written to p_bufs (leading NULL entries allocated here, as
+ * obj_ec_encode_buf; caller frees). */
+int ecg_obj_ec_singv_encode(uint32_t oc_id, uint64_t iod_size, const unsigned char *value,
+			    unsigned char *p_bufs[]);
 
 #ifdef __cplusplus
 }

@@ -348,3 +348,93 @@ void ref_recov_batch(int k, int nerrs, const unsigned char *gftbls,
 		ref_obj_ec_recov_stripe(k, nerrs, gftbls, dec_idx, err_list,
 					stripes + (uint64_t)s * stripe_stride, C);
 }
+
+/* agg_diff_preprocess, ref:src/object/srv_ec_aggregate.c:1006-1058, restated
+ * with the stripe start already subtracted from the extents. */
+void ref_agg_diff_preprocess(unsigned char *diff, uint64_t len, uint64_t rsize,
+			     unsigned int cell_idx, const uint64_t *ext_start,
+			     const uint64_t *ext_nr, unsigned int n_ext)
+{
+	uint64_t cell_start = (uint64_t)cell_idx * len;
+	uint64_t cell_end = cell_start + len;
+	uint64_t hole_off = 0;
+	unsigned int i;
+
+	for (i = 0; i < n_ext; i++) {
+		uint64_t estart = ext_start[i];
+		uint64_t eend = estart + ext_nr[i];
+		uint64_t hole_end;
+
+		if (estart >= cell_end)
+			break;
+		if (eend <= cell_start)
+			continue;
+		hole_end = cell_start + hole_off;
+		if (estart > hole_end)
+			memset(diff + hole_off * rsize, 0, (estart - hole_end) * rsize);
+		hole_off = eend - cell_start;
+	}
+	if (hole_off > 0 && hole_off < len)
+		memset(diff + hole_off * rsize, 0, (len - hole_off) * rsize);
+}
+
+int ref_agg_update_parity(int k, int p, uint64_t len, uint64_t rsize, const uint8_t *bit_map,
+			  unsigned int cell_cnt, const unsigned char *obuf,
+			  const unsigned char *nbuf, const uint64_t *ext_start,
+			  const uint64_t *ext_nr, unsigned int n_ext, unsigned char *parity)
+{
+	unsigned char en[(64 + 8) * 64], tbls[64 * 8 * 32];
+	unsigned char *pb[8];
+	uint64_t cb = len * rsize;
+	unsigned char *diff = malloc(cb ? cb : 1);
+	unsigned int i, j;
+	int r;
+
+	if (diff == NULL)
+		return -REF_DER_NOMEM;
+	ref_gf_gen_cauchy1_matrix(en, k + p, k);
+	ref_ec_init_tables(k, p, &en[k * k], tbls);
+	for (r = 0; r < p; r++)
+		pb[r] = parity + (uint64_t)r * cb;
+	for (i = 0, j = 0; i < cell_cnt; i++, j++) {
+		void *v[3];
+
+		v[0] = (void *)(obuf + (uint64_t)i * cb);
+		v[1] = (void *)(nbuf + (uint64_t)i * cb);
+		v[2] = diff;
+		ref_xor_gen(3, (int)cb, v);
+		while (!(bit_map[j / 8] & (1u << (j % 8))))
+			j++;
+		ref_agg_diff_preprocess(diff, len, rsize, j, ext_start, ext_nr, n_ext);
+		ref_ec_encode_data_update((int)cb, k, p, (int)j, tbls, diff, pb);
+	}
+	free(diff);
+	return 0;
+}
+
+uint64_t ref_singv_cell_bytes(uint64_t rec_gsize, int k)
+{
+	uint64_t c = rec_gsize / (uint64_t)k;
+
+	if (rec_gsize % (uint64_t)k)
+		c++;
+	return (c + 7) & ~7ull;
+}
+
+void ref_singv_encode(int k, int p, uint64_t iod_size, const unsigned char *value,
+		      unsigned char **p_bufs)
+{
+	uint64_t cb = ref_singv_cell_bytes(iod_size, k);
+	unsigned char *cells = calloc((size_t)k, cb);
+	unsigned char en[(64 + 8) * 64], tbls[64 * 8 * 32];
+	unsigned char *data[64];
+	int j;
+
+	memcpy(cells, value, iod_size);		/* last cell keeps its zero padding */
+	for (j = 0; j < k; j++)
+		data[j] = cells + (uint64_t)j * cb;
+	ref_gf_gen_cauchy1_matrix(en, k + p, k);
+	ref_ec_init_tables(k, p, &en[k * k], tbls);
+	ref_ec_encode_data((int)cb, k, p, tbls, data, p_bufs);
+	free(cells);
+}

@@ -88,6 +88,29 @@ void ref_obj_ec_encode_buf(int k, int p, const unsigned char *en_matrix,
                            uint64_t cell_bytes, const unsigned char *buffer,
                            unsigned char **p_bufs);
 
+/* ---- aggregation / single-value helpers ---- */
+/* agg_diff_preprocess (ref:src/object/srv_ec_aggregate.c:1006-1058): zero the
+ * parts of `diff` (one cell, len records of rsize bytes, cell index cell_idx)
+ * not covered by the new-data extents.  Extents are (start, nr) in records
+ * relative to the stripe start, sorted, as the reference's as_dextents list
+ * (holes / old-epoch extents already filtered out by the caller). */
+void ref_agg_diff_preprocess(unsigned char *diff, uint64_t len, uint64_t rsize,
+                             unsigned int cell_idx, const uint64_t *ext_start,
+                             const uint64_t *ext_nr, unsigned int n_ext);
+/* agg_update_parity (ref:src/object/srv_ec_aggregate.c:1062-1105): for the
+ * i-th updated cell (cell index = i-th set bit of bit_map): diff = old ^ new,
+ * preprocess, ec_encode_data_update into parity[p][cell_bytes]. */
+int ref_agg_update_parity(int k, int p, uint64_t len, uint64_t rsize, const uint8_t *bit_map,
+                          unsigned int cell_cnt, const unsigned char *obuf,
+                          const unsigned char *nbuf, const uint64_t *ext_start,
+                          const uint64_t *ext_nr, unsigned int n_ext, unsigned char *parity);
+/* obj_ec_singv_cell_bytes (ref:src/object/obj_ec.h:421-434). */
+uint64_t ref_singv_cell_bytes(uint64_t rec_gsize, int k);
+/* Single-value encode (ref:src/object/cli_ec.c:476-546 singv branch,
+ * 1447-1465): value split into k cells of cell_bytes, last one zero padded. */
+void ref_singv_encode(int k, int p, uint64_t iod_size, const unsigned char *value,
+                      unsigned char **p_bufs);
+
 /* ---- batch helpers used by tests / cpu_baseline (layouts of SURVEY §8a) ---- */
 /* Encode S stripes: data [S][k][C] -> parity [p][S][C] (obj_ec_pbufs_init
  * layout, ref:src/object/cli_ec.c:75-97, 638-640). nthreads<=1: serial. */

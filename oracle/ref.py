@@ -54,6 +54,14 @@ def lib():
                                       u8p, C.c_int]
         L.ref_simd_recov_batch.argtypes = L.ref_recov_batch.argtypes
         L.ref_simd_variant.restype = C.c_int
+        u64p = C.POINTER(C.c_uint64)
+        L.ref_agg_diff_preprocess.argtypes = [u8p, C.c_uint64, C.c_uint64, C.c_uint, u64p, u64p, C.c_uint]
+        L.ref_agg_update_parity.argtypes = [C.c_int, C.c_int, C.c_uint64, C.c_uint64, u8p, C.c_uint, u8p, u8p,
+                                            u64p, u64p, C.c_uint, u8p]
+        L.ref_agg_update_parity.restype = C.c_int
+        L.ref_singv_cell_bytes.argtypes = [C.c_uint64, C.c_int]
+        L.ref_singv_cell_bytes.restype = C.c_uint64
+        L.ref_singv_encode.argtypes = [C.c_int, C.c_int, C.c_uint64, u8p, C.POINTER(u8p)]
         _lib = L
     return _lib
 
@@ -157,3 +165,38 @@ def recov_batch(k: int, nerrs: int, gftbls, dec_idx, err_list, C_: int, stride: 
 
 def simd_variant() -> int:
     return lib().ref_simd_variant()
+
+
+def _u64(seq):
+    return (C.c_uint64 * max(1, len(seq)))(*seq)
+
+
+def agg_diff_preprocess(diff: np.ndarray, len_: int, rsize: int, cell_idx: int, exts):
+    d = np.ascontiguousarray(diff, dtype=np.uint8).copy()
+    lib().ref_agg_diff_preprocess(_p(d), len_, rsize, cell_idx, _u64([e[0] for e in exts]),
+                                  _u64([e[1] for e in exts]), len(exts))
+    return d
+
+
+def agg_update_parity(k: int, p: int, len_: int, rsize: int, bit_map: bytes, old: np.ndarray, new: np.ndarray,
+                      exts, parity: np.ndarray) -> np.ndarray:
+    par = np.ascontiguousarray(parity, dtype=np.uint8).copy()
+    bm = np.frombuffer(bytes(bit_map), dtype=np.uint8).copy()
+    o = np.ascontiguousarray(old, dtype=np.uint8)
+    n = np.ascontiguousarray(new, dtype=np.uint8)
+    rc = lib().ref_agg_update_parity(k, p, len_, rsize, _p(bm), o.shape[0], _p(o), _p(n),
+                                     _u64([e[0] for e in exts]), _u64([e[1] for e in exts]), len(exts), _p(par))
+    assert rc == 0
+    return par
+
+
+def singv_cell_bytes(size: int, k: int) -> int:
+    return lib().ref_singv_cell_bytes(size, k)
+
+
+def singv_encode(k: int, p: int, value: np.ndarray) -> np.ndarray:
+    cb = singv_cell_bytes(value.size, k)
+    out = np.zeros((p, cb), dtype=np.uint8)
+    v = np.ascontiguousarray(value, dtype=np.uint8)
+    lib().ref_singv_encode(k, p, v.size, _p(v), _ptr_array([out[r] for r in range(p)]))
+    return out

@@ -302,9 +302,9 @@ def test_daos_encode_stripes_and_agg_update(ecglib, oracle, ctx):
     new = rand((2, cell), 81)
     parity = par[:, 0].copy()
     bitmap = np.array([0b1010], dtype=np.uint8)
-    assert L.ecg_agg_update_parity(None, oc, cell, bitmap.ctypes.data_as(ecglib.u8p), 2,
+    assert L.ecg_agg_update_parity(None, oc, cell, 1, bitmap.ctypes.data_as(ecglib.u8p), 2,
                                    old.ctypes.data_as(ecglib.u8p), new.ctypes.data_as(ecglib.u8p),
-                                   parity.ctypes.data_as(ecglib.u8p)) == 0
+                                   None, None, 0, parity.ctypes.data_as(ecglib.u8p)) == 0
     d2 = data[0].copy()
     d2[[1, 3]] = new
     assert np.array_equal(parity, oracle.encode_data(oracle.cauchy1(k, p)[k:], d2))
@@ -482,3 +482,78 @@ def test_queue_destroy_drains(ctx, oracle, ecglib):
     assert keep.get(1) == 0
     assert np.array_equal(par[0], oracle.encode_data(oracle.cauchy1(k, p)[k:], np.stack(data))[0])
 
+
+
+# --------------------------------------------------------------- aggregation / single value
+def _u64(seq):
+    return (C.c_uint64 * max(1, len(seq)))(*seq)
+
+
+@pytest.mark.parametrize("exts", [
+    [],                                   # n_ext = 0: no hole processing
+    [(2 * 64 + 5, 10), (2 * 64 + 30, 4)],  # holes before, between and after (cell 2)
+    [(0, 3 * 64)],                        # covers cells 0-2 entirely
+    [(3 * 64 + 60, 40)],                  # overruns cell 3's end: no tail zeroing
+    [(7 * 64, 8)],                        # touches no updated cell -> whole diffs kept
+])
+def test_agg_update_parity_holes(ctx, oracle, ecglib, exts):
+    """agg_update_parity + agg_diff_preprocess semantics, including the
+    reference's rules for cells no extent touches (ref:src/object/
+    srv_ec_aggregate.c:1006-1105), vs the oracle restatement."""
+    L = ecglib.lib()
+    oc = (37 << 24) | 1                      # EC_8P2
+    k, p, recs, rsize = 8, 2, 64, 8          # 512-byte cells
+    cb = recs * rsize
+    bitmap = bytes([0b00001110])             # cells 1, 2, 3 updated
+    old = rand((3, cb), 90)
+    new = rand((3, cb), 91)
+    parity = rand((p, cb), 92)
+    want = oracle.agg_update_parity(k, p, recs, rsize, bitmap, old, new, exts, parity)
+    got = parity.copy()
+    bm = np.frombuffer(bitmap, dtype=np.uint8).copy()
+    rc = L.ecg_agg_update_parity(None, oc, recs, rsize, bm.ctypes.data_as(ecglib.u8p), 3,
+                                 old.ctypes.data_as(ecglib.u8p), new.ctypes.data_as(ecglib.u8p),
+                                 _u64([e[0] for e in exts]) if exts else None,
+                                 _u64([e[1] for e in exts]) if exts else None, len(exts),
+                                 got.ctypes.data_as(ecglib.u8p))
+    assert rc == 0
+    assert np.array_equal(got, want)
+
+
+def test_agg_recalc_parity(ctx, oracle, ecglib):
+    L = ecglib.lib()
+    oc = (41 << 24) | 1                      # EC_8P3
+    k, p, cb = 8, 3, 4096 + 8
+    bitmap = np.array([0b10010110], dtype=np.uint8)     # cells 1,2,4,7 from peers
+    rbuf = rand((4, cb), 93)
+    lbuf = rand((4, cb), 94)
+    parity = np.zeros((p, cb), dtype=np.uint8)
+    assert L.ecg_agg_recalc_parity(None, oc, cb, bitmap.ctypes.data_as(ecglib.u8p), 4,
+                                   rbuf.ctypes.data_as(ecglib.u8p), lbuf.ctypes.data_as(ecglib.u8p),
+                                   parity.ctypes.data_as(ecglib.u8p)) == 0
+    data = np.stack([rbuf[[1, 2, 4, 7].index(j)] if j in (1, 2, 4, 7) else lbuf[[0, 3, 5, 6].index(j)]
+                     for j in range(k)])
+    assert np.array_equal(parity, oracle.encode_data(oracle.cauchy1(k, p)[k:], data))
+
+
+@pytest.mark.parametrize("oc,size", [((32 << 24) | 1, 8569), ((35 << 24) | 1, 8569), ((37 << 24) | 1, 8569),
+                                     ((42 << 24) | 1, 8569), ((35 << 24) | 1, 4 * 1048576 + 347),
+                                     ((39 << 24) | 1, 65536 + 3)])
+def test_singv_encode(ctx, oracle, ecglib, oc, size):
+    """Single values of the reference's test sizes (LARGE_SINGLE_VALUE_SIZE
+    8569, DATA_SIZE 4 MiB + 347; ref:src/tests/suite/daos_rebuild_common.c:
+    654-658): zero-padded last cell, parity vs the oracle restatement."""
+    L = ecglib.lib()
+    kk, pp = C.c_int(), C.c_int()
+    L.ecg_obj_ec_class_kp(oc, C.byref(kk), C.byref(pp))
+    k, p = kk.value, pp.value
+    cb = L.ecg_obj_ec_singv_cell_bytes(oc, size)
+    assert cb == oracle.singv_cell_bytes(size, k)
+    value = rand(size, size)
+    pbufs = (ecglib.u8p * p)()
+    assert L.ecg_obj_ec_singv_encode(oc, size, value.ctypes.data_as(ecglib.u8p), pbufs) == 0
+    got = np.stack([np.ctypeslib.as_array(pbufs[r], shape=(cb,)).copy() for r in range(p)])
+    libc = C.CDLL(None)
+    for r in range(p):
+        libc.free(C.cast(pbufs[r], C.c_void_p))
+    assert np.array_equal(got, oracle.singv_encode(k, p, value))

@@ -124,9 +124,10 @@ def test_recovery_all_patterns(oracle, k, p):
     for pat in pats:
         rc, de, dec, el, gt, reused = oracle.recov_codec(k, p, list(pat))
         assert rc == 0
-        src = stripe[dec] if not reused else stripe[:k]
-        out = oracle.encode_data(de if not reused else en[k:], src) if not reused else \
-            oracle.encode_data(en[k:], stripe[:k])
+        if reused:      # all parity lost: plain re-encode (ref:src/object/cli_ec.c:2205-2210)
+            out = oracle.encode_data(en[k:], stripe[:k])
+        else:
+            out = oracle.encode_data(de, stripe[dec])
         for i, e in enumerate(el):
             assert np.array_equal(out[i], stripe[e]), (pat, e)
         # numpy restatement builds the same rows
@@ -181,3 +182,24 @@ def test_batch_helpers(oracle):
     en = oracle.cauchy1(k, p)
     for s in range(S):
         assert np.array_equal(par.reshape(p, S, C)[:, s], oracle.encode_data(en[k:], d[s]))
+
+
+def test_singv_cell_bytes(oracle):
+    # obj_ec_singv_cell_bytes: ceil(size / k) rounded up to 8 (ref:src/object/obj_ec.h:421-434)
+    assert oracle.singv_cell_bytes(8569, 2) == 4288
+    assert oracle.singv_cell_bytes(8569, 4) == 2144
+    assert oracle.singv_cell_bytes(8569, 16) == 536
+    assert oracle.singv_cell_bytes(4096, 4) == 1024
+
+
+def test_agg_diff_preprocess_rules(oracle):
+    """Restatement of ref:src/object/srv_ec_aggregate.c:1006-1058 on a cell of
+    8 records x 4 bytes (cell index 1 = records 8..15)."""
+    d = np.full(32, 0xFF, np.uint8)
+    out = oracle.agg_diff_preprocess(d, 8, 4, 1, [(9, 2), (13, 1)]).reshape(8, 4)[:, 0]
+    assert list(out) == [0, 255, 255, 0, 0, 255, 0, 0]
+    # no extent touches the cell: nothing zeroed (hole_off stays 0)
+    assert (oracle.agg_diff_preprocess(d, 8, 4, 1, [(0, 4)]) == 0xFF).all()
+    # extent running past the cell end: no tail zeroing
+    out = oracle.agg_diff_preprocess(d, 8, 4, 1, [(12, 10)]).reshape(8, 4)[:, 0]
+    assert list(out) == [0, 0, 0, 0, 255, 255, 255, 255]
