@@ -39,21 +39,37 @@ PARITY_ROW_PAD = 4096
 HBM_PEAK_GBS = 8000.0          # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 ROUND = "r01"
 
+# name -> (k, p, cell bytes, stripes, ops, strong scaling?)
+WORKLOADS = {
+    "enc_dec_4p2": (4, 2, 1 << 20, 1024, ("enc", "dec"), False),
+    "dec_8p2": (8, 2, 1 << 20, 512, ("dec",), False),
+    "enc_16p2_strong": (16, 2, 128 << 10, 8192, ("enc",), True),
+}
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--k", type=int, default=4)
-    ap.add_argument("--p", type=int, default=2)
-    ap.add_argument("--cell", type=int, default=1 << 20)
-    ap.add_argument("--stripes", type=int, default=1024, help="stripes per GPU")
+    ap.add_argument("--workload", default="enc_dec_4p2", choices=sorted(WORKLOADS),
+                    help="enc_dec_4p2 = BASELINE configs[1] (+ its decode); dec_8p2 = configs[2]; "
+                         "enc_16p2_strong = configs[3] (8192 stripes split across ranks)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
     ap.add_argument("--no-detail", action="store_true", help="skip the extra per-config rows")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-only", action="store_true", help="just the timed loop (for rocprofv3)")
     return ap.parse_args()
+
+
+def describe(name, k, p, C, S, ops):
+    parts = []
+    if "enc" in ops:
+        parts.append("encode (data [S][k][C] -> parity [p][S][C], row pitch S*C+4KiB)")
+    if "dec" in ops:
+        parts.append("degraded decode of cells d0,d1 in [S][k+p][C]")
+    per = "per GPU" if not WORKLOADS[name][5] else "on this rank (8192 total, split)"
+    return f"EC_{k}P{p} {C >> 10} KiB cells x {S} stripes {per}: " + " + ".join(parts)
 
 
 def dist_init():
@@ -102,8 +118,9 @@ def fill_device(ctx, buf, nbytes, config_id, chunk=256 << 20):
 class Workload:
     """One rank's EC batch: encode (client layout) + decode (recovery layout)."""
 
-    def __init__(self, ctx, k, p, C, S, err=(0, 1), config_id=2):
+    def __init__(self, ctx, k, p, C, S, ops=("enc", "dec"), err=(0, 1), config_id=2):
         self.ctx, self.k, self.p, self.C, self.S, self.err = ctx, k, p, C, S, list(err)
+        self.ops = tuple(ops)
         # Parity rows [p][S][C] at a pitch of S*C + 4 KiB: rows exactly a power
         # of two apart alias in HBM and cost EC_8P2 encode ~10 %
         # (profiles/r01/tune5_parity_row_aliasing.json, tune6_pitch.json).
@@ -121,34 +138,38 @@ class Workload:
 
     def step(self, timed=False):
         c, k, p, C, S = self.ctx, self.k, self.p, self.C, self.S
-        ev = [c.event() for _ in range(4)] if timed else None
+        evs = []
+        for op in self.ops:
+            ev = (c.event(), c.event()) if timed else None
+            if timed:
+                c.record(ev[0])
+            if op == "enc":
+                c.encode(k, p, C, S, self.data.ptr, k * C, self.parity.ptr, self.prow, C)
+            else:
+                c.recover(k, p, C, S, self.stripes.ptr, (k + p) * C, self.err)
+            if timed:
+                c.record(ev[1])
+                evs.append(ev)
         if timed:
-            c.record(ev[0])
-        c.encode(k, p, C, S, self.data.ptr, k * C, self.parity.ptr, self.prow, C)
-        if timed:
-            c.record(ev[1])
-            c.record(ev[2])
-        c.recover(k, p, C, S, self.stripes.ptr, (k + p) * C, self.err)
-        if timed:
-            c.record(ev[3])
-            self.events.append(ev)
+            self.events.append(evs)
 
     def kernel_ms(self):
-        """(encode_ms, decode_ms) per timed step, read after the timed region."""
-        out = []
-        for ev in self.events:
-            out.append((self.ctx.elapsed_ms(ev[0], ev[1]), self.ctx.elapsed_ms(ev[2], ev[3])))
-            for e in ev:
-                self.ctx.destroy_event(e)
+        """{op: [ms per timed step]}, read after the timed region."""
+        out = {op: [] for op in self.ops}
+        for evs in self.events:
+            for op, (a, b) in zip(self.ops, evs):
+                out[op].append(self.ctx.elapsed_ms(a, b))
+                self.ctx.destroy_event(a)
+                self.ctx.destroy_event(b)
         self.events = []
         return out
 
     def user_bytes_per_step(self):
-        return 2 * self.k * self.C * self.S
+        return len(self.ops) * self.k * self.C * self.S
 
-    def alg_bytes_per_launch(self):
+    def alg_bytes(self, op):
         # encode: read k, write p cells; decode: read k survivors, write nerrs
-        return (self.k + self.p) * self.C * self.S, (self.k + len(self.err)) * self.C * self.S
+        return (self.k + (self.p if op == "enc" else len(self.err))) * self.C * self.S
 
     def free(self):
         for b in (self.data, self.parity, self.stripes):
@@ -229,10 +250,10 @@ def detail_rows(ctx, ceil, iters=7):
     return rows
 
 
-def cpu_baseline(k, p, C, budget_s):
+def cpu_baseline(k, p, C, budget_s, ops=("enc", "dec")):
     """Oracle SIMD restatement (ISA-L-equivalent), OpenMP over stripes, on a
-    bounded sample: 32 stripes of the same workload, encode + {d0,d1} decode,
-    repeated until ~budget_s of CPU time."""
+    bounded sample: 32 stripes of the same workload (same ops), repeated until
+    ~budget_s of CPU time."""
     import numpy as np
 
     from oracle import ref
@@ -255,13 +276,15 @@ def cpu_baseline(k, p, C, budget_s):
     user = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
-        ref.encode_batch(k, p, C, S, data, nthreads=cores, simd=True)
-        ref.recov_batch(k, 2, gt, dec, el, C, (k + p) * C, S, stripes, nthreads=cores, simd=True)
-        user += 2 * k * C * S
+        if "enc" in ops:
+            ref.encode_batch(k, p, C, S, data, nthreads=cores, simd=True)
+        if "dec" in ops:
+            ref.recov_batch(k, 2, gt, dec, el, C, (k + p) * C, S, stripes, nthreads=cores, simd=True)
+        user += len(ops) * k * C * S
     dt = time.perf_counter() - t0
     variant = {0: "scalar", 1: "avx2-vpshufb", 2: "gfni-avx512"}[ref.simd_variant()]
     return {"value": round(user / dt / GIB, 3), "unit": "GiB/s", "cores": cores, "kind": "port",
-            "sample": f"EC_{k}P{p} {C >> 10} KiB cells, {S} stripes, encode + d0,d1 decode, repeated "
+            "sample": f"EC_{k}P{p} {C >> 10} KiB cells, {S} stripes, {' + '.join(ops)}, repeated "
                       f"{dt:.1f} s; ISA-L-equivalent restatement ({variant}, OpenMP)"}
 
 
@@ -288,8 +311,10 @@ def main():
     dev = local % ndev          # > 1 rank per GPU only when rehearsing on a 1-GPU box
     torch.cuda.set_device(dev)
     ctx = ecg.Context(dev)
-    k, p, C, S = args.k, args.p, args.cell, args.stripes
-    wl = Workload(ctx, k, p, C, S)
+    k, p, C, S, ops, strong = WORKLOADS[args.workload]
+    if strong:                      # configs[3]: a fixed stripe total split across ranks
+        S = S // world + (1 if rank < S % world else 0)
+    wl = Workload(ctx, k, p, C, S, ops=ops)
 
     for _ in range(args.warmup):
         wl.step()
@@ -312,19 +337,21 @@ def main():
         ctx.close()
         return
 
-    user = wl.user_bytes_per_step() * args.steps * world
+    if strong:      # the fixed total, however it was split
+        user = WORKLOADS[args.workload][3] * k * C * len(ops) * args.steps
+    else:           # every rank processed the same batch
+        user = wl.user_bytes_per_step() * args.steps * world
     value = user / elapsed / GIB
     kms = wl.kernel_ms()
-    enc_ms = sorted(m[0] for m in kms)
-    dec_ms = sorted(m[1] for m in kms)
-    enc_alg, dec_alg = wl.alg_bytes_per_launch()
-    mean_launch_ms = (sum(enc_ms) + sum(dec_ms)) / (2 * len(enc_ms))
-    alg_per_launch = (enc_alg + dec_alg) / 2
+    launches = [(op, ms) for op in ops for ms in kms[op]]
+    mean_launch_ms = sum(ms for _, ms in launches) / len(launches)
+    alg_per_launch = sum(wl.alg_bytes(op) for op, _ in launches) / len(launches)
     achieved = alg_per_launch / (mean_launch_ms / 1e3) / 1e9
     kernel_name = f"ecg_mm_kernel<{k},{p},0,0>"
     traffic = None
     pmc = pmc_traffic()
-    if pmc and pmc.get("kernel", "").replace(" ", "") == f"ecg_mm_kernel<{k},{p}":
+    if pmc and pmc.get("kernel", "").replace(" ", "") == f"ecg_mm_kernel<{k},{p}" and \
+            pmc.get("alg_bytes_per_launch") == int(alg_per_launch):
         traffic = pmc.get("hbm_bytes_per_launch")
 
     out = {
@@ -336,33 +363,31 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic: xoshiro256** stripes seeded 0xDA05EC00+id (BASELINE.md §3), device-resident",
-        "config": {"workload": f"EC_{k}P{p} {C >> 10} KiB cells x {S} stripes per GPU: encode (data [S][k][C] -> "
-                               f"parity [p][S][C], row pitch S*C+4KiB) + degraded decode of cells d0,d1 in "
-                               f"[S][k+p][C]",
-                   "k": k, "p": p, "cell_bytes": C, "stripes_per_gpu": S, "erasures": wl.err,
+        "config": {"workload": describe(args.workload, k, p, C, S, ops),
+                   "name": args.workload, "k": k, "p": p, "cell_bytes": C, "stripes_per_gpu": S,
+                   "erasures": wl.err if "dec" in ops else [],
                    "parallelism": f"stripe-sharded x{world}, no collective"},
         "roofline": {"bound": "hbm", "kernel": kernel_name, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "alg_bytes_per_launch": int(alg_per_launch),
                      "mean_launch_ms": round(mean_launch_ms, 4),
-                     "encode_ms_median": round(enc_ms[len(enc_ms) // 2], 4),
-                     "decode_ms_median": round(dec_ms[len(dec_ms) // 2], 4)},
+                     **{f"{op}_ms_median": round(sorted(kms[op])[len(kms[op]) // 2], 4) for op in ops}},
         "cpu_baseline": None,
     }
     wl.free()
     if rank == 0 and world == 1 and not args.no_detail:
         ceil = measured_ceilings(ctx)
-        mix = mix_ceiling(ceil, k / (k + p))
+        mix = mix_ceiling(ceil, k / (k + p))      # enc (k in, p out) and dec (k in, 2 out) alike at p = 2
         out["roofline"]["measured_stream_GBps"] = ceil
         out["roofline"]["measured_mix_ceiling_GBps"] = round(mix, 1)
         out["roofline"]["frac_of_measured_mix"] = round(achieved / mix, 4)
         out["detail"] = detail_rows(ctx, ceil)
     if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(k, p, C, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(k, p, C, args.cpu_seconds, ops)
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()

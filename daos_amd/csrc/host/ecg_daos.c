@@ -141,6 +141,16 @@ int ecg_obj_ec_encode_buf(uint32_t oc_id, uint64_t cell_bytes, unsigned char *bu
 	return ecg_matmul_host(ctx, (int)cell_bytes, k, p, &en[k * k], data, p_bufs, 0);
 }
 
+struct ecg_obj_ec_recov_codec *ecg_obj_ec_recov_codec_alloc(void)
+{
+	return calloc(1, sizeof(struct ecg_obj_ec_recov_codec));
+}
+
+void ecg_obj_ec_recov_codec_free(struct ecg_obj_ec_recov_codec *recov)
+{
+	free(recov);
+}
+
 int ecg_obj_ec_recov_codec_init(uint32_t oc_id, const uint32_t *err_list, uint32_t nerrs,
 				struct ecg_obj_ec_recov_codec *rv)
 {

@@ -92,6 +92,8 @@ _SIGS = [
     ("ecg_obj_ec_codec_get", vp, [C.c_uint32]),
     ("ecg_obj_ec_class_kp", C.c_int, [C.c_uint32, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("ecg_obj_ec_encode_buf", C.c_int, [C.c_uint32, C.c_uint64, u8p, C.POINTER(u8p)]),
+    ("ecg_obj_ec_recov_codec_alloc", vp, []),
+    ("ecg_obj_ec_recov_codec_free", None, [vp]),
     ("ecg_obj_ec_recov_codec_init", C.c_int, [C.c_uint32, u32p, C.c_uint32, vp]),
     ("ecg_obj_ec_recov_data", C.c_int, [vp, vp, C.c_uint64, u8p, C.c_uint32]),
     ("ecg_obj_ec_encode_stripes", C.c_int, [vp, C.c_uint32, C.c_uint64, C.c_uint32, u8p, u8p]),

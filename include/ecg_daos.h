@@ -83,6 +83,12 @@ int ecg_obj_ec_class_kp(uint32_t oc_id, int *k, int *p);
 int ecg_obj_ec_encode_buf(uint32_t oc_id, uint64_t cell_bytes, unsigned char *buffer,
 			  unsigned char *p_bufs[]);
 
+/* obj_ec_recov_codec_alloc (ref:src/object/cli_ec.c:1953-1993): heap
+ * allocation of a recovery codec (the struct is ~17 KiB -- too large for an
+ * Argobots ULT stack).  NULL on allocation failure. */
+struct ecg_obj_ec_recov_codec *ecg_obj_ec_recov_codec_alloc(void);
+void ecg_obj_ec_recov_codec_free(struct ecg_obj_ec_recov_codec *recov);
+
 /* Build the recovery codec for LOGICAL erased cells err_list[nerrs].
  * 0 / -ECG_DER_DATA_LOSS (nerrs > p) / -ECG_DER_INVAL. */
 int ecg_obj_ec_recov_codec_init(uint32_t oc_id, const uint32_t *err_list, uint32_t nerrs,

@@ -57,6 +57,10 @@ def test_weak_scaling_accounting():
         pass
 
     wl = bench.Workload.__new__(bench.Workload)
-    wl.k, wl.p, wl.C, wl.S, wl.err = 4, 2, 1 << 20, 1024, [0, 1]
+    wl.k, wl.p, wl.C, wl.S, wl.err, wl.ops = 4, 2, 1 << 20, 1024, [0, 1], ("enc", "dec")
     assert wl.user_bytes_per_step() == 2 * 4 * (1 << 20) * 1024
-    assert wl.alg_bytes_per_launch() == (6 * (1 << 20) * 1024, 6 * (1 << 20) * 1024)
+    assert wl.alg_bytes("enc") == wl.alg_bytes("dec") == 6 * (1 << 20) * 1024
+    wl.k, wl.p, wl.ops = 16, 2, ("enc",)
+    assert wl.user_bytes_per_step() == 16 * (1 << 20) * 1024
+    assert set(bench.WORKLOADS) == {"enc_dec_4p2", "dec_8p2", "enc_16p2_strong"}
+    assert bench.WORKLOADS["enc_dec_4p2"][:4] == (4, 2, 1 << 20, 1024)      # BASELINE configs[1]

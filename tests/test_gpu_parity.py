@@ -281,11 +281,13 @@ def test_daos_encode_buf_and_recovery(ecglib, oracle, ctx):
     broken = stripes.copy()
     err = [1, 9]
     broken[:, err] = 0
-    rv = (C.c_ubyte * 32768)()             # >= sizeof(struct ecg_obj_ec_recov_codec)
+    rv = L.ecg_obj_ec_recov_codec_alloc()
+    assert rv
     assert L.ecg_obj_ec_recov_codec_init(oc, (C.c_uint32 * 2)(*err), 2, rv) == 0
     assert L.ecg_obj_ec_recov_data(None, rv, cell, broken.ctypes.data_as(ecglib.u8p), S) == 0
     assert np.array_equal(broken, stripes)
     assert L.ecg_obj_ec_recov_codec_init(oc, (C.c_uint32 * 3)(0, 1, 2), 3, rv) == -ecglib.DER_DATA_LOSS
+    L.ecg_obj_ec_recov_codec_free(rv)
 
 
 def test_daos_encode_stripes_and_agg_update(ecglib, oracle, ctx):
