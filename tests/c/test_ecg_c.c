@@ -1,0 +1,282 @@
+/*
+ * test_ecg_c.c -- native C driver for the libecg C-ABI, checked against the
+ * CPU oracle (oracle/ec_ref.c, test infrastructure).
+ *
+ * Host-only checks always run.  With a gfx950 device present it also runs
+ * the device paths, including ISA-L-convention calls from many pthreads at
+ * once (the reference calls ec_encode_data concurrently from client threads
+ * and engine xstreams) and the batching queue.
+ * Built plain and with -fsanitize=address,undefined on the host code
+ * (tests/c/Makefile).  Exit status 0 = pass.
+ */
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "ec_ref.h"
+#include "ecg.h"
+#include "ecg_daos.h"
+#include "ecg_isal.h"
+
+static int g_fail;
+
+#define CHECK(cond, ...)                                               \
+	do {                                                           \
+		if (!(cond)) {                                         \
+			fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+			fprintf(stderr, __VA_ARGS__);                  \
+			fprintf(stderr, "\n");                         \
+			g_fail++;                                      \
+		}                                                      \
+	} while (0)
+
+static uint64_t g_rng = 0xDA05EC00ull;
+
+static unsigned char rnd(void)
+{
+	g_rng ^= g_rng << 13;
+	g_rng ^= g_rng >> 7;
+	g_rng ^= g_rng << 17;
+	return (unsigned char)(g_rng >> 24);
+}
+
+static void fill(unsigned char *p, size_t n)
+{
+	for (size_t i = 0; i < n; i++)
+		p[i] = rnd();
+}
+
+static void host_checks(void)
+{
+	static const int kp[][2] = {{2, 1}, {2, 2}, {4, 1}, {4, 2}, {4, 3}, {8, 1}, {8, 2},
+				    {8, 3}, {16, 1}, {16, 2}, {16, 3}};
+	unsigned char a[(64 + 8) * 64], b[(64 + 8) * 64];
+	size_t t;
+
+	for (int x = 0; x < 256; x++)
+		for (int y = 0; y < 256; y += 3)
+			CHECK(gf_mul(x, y) == ref_gf_mul(x, y), "gf_mul %d %d", x, y);
+	for (t = 0; t < sizeof(kp) / sizeof(kp[0]); t++) {
+		int k = kp[t][0], p = kp[t][1];
+
+		gf_gen_cauchy1_matrix(a, k + p, k);
+		ref_gf_gen_cauchy1_matrix(b, k + p, k);
+		CHECK(memcmp(a, b, (size_t)(k + p) * k) == 0, "cauchy %d+%d", k, p);
+		/* every single and double erasure: data-first decode rows equal
+		 * the reference's obj_ec_recov_codec_init rows */
+		for (int e0 = 0; e0 < k + p; e0++) {
+			for (int e1 = e0; e1 < k + p; e1++) {
+				uint32_t err[2] = {(uint32_t)e0, (uint32_t)e1};
+				int nerrs = e1 == e0 ? 1 : 2, reused = 0, rreused = 0;
+				unsigned char rows[8 * 64], rrows[8 * 64], tb[64 * 8 * 32];
+				uint32_t dec[64], rdec[64], rel[8];
+
+				if (nerrs > p)
+					continue;
+				CHECK(ecg_recov_matrix(k, p, a, err, nerrs, rows, dec, &reused) == 0,
+				      "recov %d+%d", k, p);
+				CHECK(ref_obj_ec_recov_codec_init(k, p, b, err, nerrs, rrows, rdec, rel, tb,
+								  &rreused) == 0, "ref recov");
+				CHECK(reused == rreused, "reused %d+%d", k, p);
+				if (!reused)
+					CHECK(memcmp(rows, rrows, (size_t)nerrs * k) == 0 &&
+					      memcmp(dec, rdec, sizeof(uint32_t) * k) == 0,
+					      "rows %d+%d {%d,%d}", k, p, e0, e1);
+			}
+		}
+	}
+	{
+		uint32_t err[3] = {0, 1, 2};
+		unsigned char rows[8 * 64];
+		uint32_t dec[64];
+		int reused;
+
+		CHECK(ecg_recov_matrix(4, 2, a, err, 3, rows, dec, &reused) == -ECG_DER_DATA_LOSS,
+		      "data loss");
+	}
+	CHECK(ecg_obj_ec_codec_init() == 0, "codec_init");
+	CHECK(ecg_obj_ec_codec_get((37u << 24) | 1) != NULL, "codec_get 8P2");
+	CHECK(ecg_obj_ec_codec_get((1u << 24) | 1) == NULL, "codec_get RP");
+	ecg_obj_ec_codec_fini();
+}
+
+/* ---- device checks -------------------------------------------------------- */
+struct tjob {
+	int k, p, len, iters, id;
+	int fails;
+};
+
+static void *isal_thread(void *arg)
+{
+	struct tjob *j = arg;
+	unsigned char en[(16 + 4) * 16], tb[16 * 4 * 32], rtb[16 * 4 * 32];
+	unsigned char *data[16], *par[4], *want[4];
+	uint64_t st = 0x9E3779B97F4A7C15ull * (uint64_t)(j->id + 1);
+
+	gf_gen_cauchy1_matrix(en, j->k + j->p, j->k);
+	ec_init_tables(j->k, j->p, &en[j->k * j->k], tb);
+	ref_ec_init_tables(j->k, j->p, &en[j->k * j->k], rtb);
+	for (int c = 0; c < j->k; c++)
+		data[c] = malloc(j->len);
+	for (int r = 0; r < j->p; r++) {
+		par[r] = malloc(j->len);
+		want[r] = malloc(j->len);
+	}
+	for (int it = 0; it < j->iters; it++) {
+		for (int c = 0; c < j->k; c++)
+			for (int i = 0; i < j->len; i++) {
+				st ^= st << 13;
+				st ^= st >> 7;
+				st ^= st << 17;
+				data[c][i] = (unsigned char)st;
+			}
+		ec_encode_data(j->len, j->k, j->p, tb, data, par);
+		ref_ec_encode_data(j->len, j->k, j->p, rtb, data, want);
+		for (int r = 0; r < j->p; r++)
+			j->fails += memcmp(par[r], want[r], j->len) != 0;
+	}
+	for (int c = 0; c < j->k; c++)
+		free(data[c]);
+	for (int r = 0; r < j->p; r++) {
+		free(par[r]);
+		free(want[r]);
+	}
+	return NULL;
+}
+
+struct qdone {
+	pthread_mutex_t lock;
+	int done, bad;
+};
+
+static void qcb(void *arg, int rc)
+{
+	struct qdone *d = arg;
+
+	pthread_mutex_lock(&d->lock);
+	d->done++;
+	d->bad += rc != 0;
+	pthread_mutex_unlock(&d->lock);
+}
+
+static void device_checks(void)
+{
+	enum { NT = 12 };
+	pthread_t th[NT];
+	struct tjob jobs[NT];
+	ecg_ctx_t *ctx = NULL;
+	int t;
+
+	/* concurrent ISA-L-convention calls, mixed shapes and odd lengths */
+	for (t = 0; t < NT; t++) {
+		static const int shapes[][3] = {{4, 2, 4096}, {8, 2, 933}, {16, 3, 8569}, {2, 1, 37}};
+
+		jobs[t] = (struct tjob){shapes[t % 4][0], shapes[t % 4][1], shapes[t % 4][2], 20, t, 0};
+		pthread_create(&th[t], NULL, isal_thread, &jobs[t]);
+	}
+	for (t = 0; t < NT; t++) {
+		pthread_join(th[t], NULL);
+		CHECK(jobs[t].fails == 0, "thread %d: %d mismatches", t, jobs[t].fails);
+	}
+
+	/* batched device encode + recovery through ecg.h */
+	CHECK(ecg_ctx_create(0, &ctx) == 0, "ctx_create: %s", ecg_strerror());
+	if (ctx == NULL)
+		return;
+	{
+		const int k = 8, p = 2, S = 6;
+		const uint64_t C = 65536 + 16;
+		const size_t sst = (size_t)(k + p) * C;
+		unsigned char *h = malloc(S * sst), *g = malloc(S * sst);
+		unsigned char en[10 * 8], tb[8 * 2 * 32], *src[8], *dst[2];
+		void *d = NULL;
+		uint32_t err[2] = {1, 8};
+
+		fill(h, S * sst);
+		CHECK(ecg_dev_alloc(ctx, S * sst, &d) == 0, "dev_alloc");
+		CHECK(ecg_memcpy(ctx, d, h, S * sst, 0, NULL) == 0, "h2d");
+		CHECK(ecg_encode(ctx, k, p, C, S, d, (int64_t)sst, (char *)d + k * C, (int64_t)C,
+				 (int64_t)sst, NULL) == 0, "encode: %s", ecg_strerror());
+		CHECK(ecg_memcpy(ctx, g, d, S * sst, 1, NULL) == 0 && ecg_stream_sync(ctx, NULL) == 0,
+		      "d2h");
+		ref_gf_gen_cauchy1_matrix(en, k + p, k);
+		ref_ec_init_tables(k, p, &en[k * k], tb);
+		for (int s = 0; s < S; s++) {
+			unsigned char want0[65536 + 16], want1[65536 + 16];
+
+			for (int c = 0; c < k; c++)
+				src[c] = g + s * sst + c * C;
+			dst[0] = want0;
+			dst[1] = want1;
+			ref_ec_encode_data((int)C, k, p, tb, src, dst);
+			CHECK(memcmp(want0, g + s * sst + k * C, C) == 0 &&
+			      memcmp(want1, g + s * sst + (k + 1) * C, C) == 0, "parity stripe %d", s);
+		}
+		/* wipe d1 and p0, recover on device */
+		memcpy(h, g, S * sst);
+		for (int s = 0; s < S; s++) {
+			memset(h + s * sst + 1 * C, 0, C);
+			memset(h + s * sst + 8 * C, 0, C);
+		}
+		CHECK(ecg_memcpy(ctx, d, h, S * sst, 0, NULL) == 0, "h2d 2");
+		CHECK(ecg_recover(ctx, k, p, C, S, d, (int64_t)sst, err, 2, NULL) == 0, "recover");
+		CHECK(ecg_memcpy(ctx, h, d, S * sst, 1, NULL) == 0 && ecg_stream_sync(ctx, NULL) == 0,
+		      "d2h 2");
+		CHECK(memcmp(h, g, S * sst) == 0, "recovered stripes");
+		ecg_dev_free(ctx, d);
+		free(h);
+		free(g);
+	}
+	/* batching queue from several threads' worth of submissions */
+	{
+		ecg_queue_t *q = NULL;
+		struct qdone qd = {PTHREAD_MUTEX_INITIALIZER, 0, 0};
+		enum { N = 64 };
+		const int k = 4, p = 2, C = 4096 + 8;
+		unsigned char *cells = malloc((size_t)N * (k + p) * C);
+		unsigned char en[6 * 4], tb[4 * 2 * 32];
+
+		fill(cells, (size_t)N * (k + p) * C);
+		CHECK(ecg_queue_create(ctx, NULL, &q) == 0, "queue_create");
+		for (int i = 0; i < N; i++) {
+			unsigned char *data[4], *par[2];
+
+			for (int c = 0; c < k; c++)
+				data[c] = cells + ((size_t)i * (k + p) + c) * C;
+			for (int r = 0; r < p; r++)
+				par[r] = cells + ((size_t)i * (k + p) + k + r) * C;
+			CHECK(ecg_queue_encode(q, k, p, C, data, par, qcb, &qd) == 0, "queue_encode");
+		}
+		CHECK(ecg_queue_flush(q) == 0 && qd.done == N && qd.bad == 0, "queue done %d bad %d",
+		      qd.done, qd.bad);
+		ref_gf_gen_cauchy1_matrix(en, k + p, k);
+		ref_ec_init_tables(k, p, &en[k * k], tb);
+		for (int i = 0; i < N; i++) {
+			unsigned char *src[4], *dst[2], w0[4096 + 8], w1[4096 + 8];
+
+			for (int c = 0; c < k; c++)
+				src[c] = cells + ((size_t)i * (k + p) + c) * C;
+			dst[0] = w0;
+			dst[1] = w1;
+			ref_ec_encode_data(C, k, p, tb, src, dst);
+			CHECK(memcmp(w0, cells + ((size_t)i * (k + p) + k) * C, C) == 0 &&
+			      memcmp(w1, cells + ((size_t)i * (k + p) + k + 1) * C, C) == 0, "queue stripe %d",
+			      i);
+		}
+		ecg_queue_destroy(q);
+		free(cells);
+	}
+	ecg_ctx_destroy(ctx);
+}
+
+int main(void)
+{
+	host_checks();
+	if (ecg_device_count() > 0)
+		device_checks();
+	else
+		printf("no gfx950 device: host-only checks\n");
+	printf("%s (%d failures)\n", g_fail ? "FAIL" : "PASS", g_fail);
+	return g_fail ? 1 : 0;
+}

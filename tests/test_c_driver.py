@@ -1,0 +1,44 @@
+"""Runs the native C driver (tests/c/test_ecg_c.c): the C-ABI exercised from
+C, plain and with ASan/UBSan on the host code, checked against the oracle.
+Without a GPU only its host-side checks run; under -m gpu the device paths
+(concurrent ISA-L calls from 12 pthreads, batched encode/recover, queue)."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+BIN = os.path.join(ROOT, "build", "ctest")
+
+
+@pytest.fixture(scope="module")
+def cbins():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "c")], check=True)
+    return os.path.join(BIN, "test_ecg_c"), os.path.join(BIN, "test_ecg_c_asan")
+
+
+def _run(path, gpu):
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:use_sigaltstack=0", UBSAN_OPTIONS="print_stacktrace=1")
+    if not gpu:
+        env["HIP_VISIBLE_DEVICES"] = ""       # host-only half
+    r = subprocess.run([path], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "PASS" in r.stdout
+    return r.stdout
+
+
+def test_c_driver_host(cbins):
+    for b in cbins:
+        _run(b, gpu=False)
+
+
+@pytest.mark.gpu
+def test_c_driver_device(cbins):
+    out = _run(cbins[0], gpu=True)
+    assert "host-only" not in out
+
+
+@pytest.mark.gpu
+def test_c_driver_device_asan(cbins):
+    out = _run(cbins[1], gpu=True)
+    assert "host-only" not in out
