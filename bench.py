@@ -273,11 +273,12 @@ def cpu_baseline(k, p, C, budget_s, ops=("enc", "dec")):
     sv[:, k:] = par.transpose(1, 0, 2)
     rc, de, dec, el, gt, reused = ref.recov_codec(k, p, [0, 1])
     assert rc == 0
+    pout = np.empty(p * S * C, dtype=np.uint8)     # reused: no page faults in the timed loop
     user = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
         if "enc" in ops:
-            ref.encode_batch(k, p, C, S, data, nthreads=cores, simd=True)
+            ref.encode_batch(k, p, C, S, data, nthreads=cores, simd=True, out=pout)
         if "dec" in ops:
             ref.recov_batch(k, 2, gt, dec, el, C, (k + p) * C, S, stripes, nthreads=cores, simd=True)
         user += len(ops) * k * C * S

@@ -8,14 +8,22 @@
  * launch- and PCIe-latency bound.  The queue turns N concurrent
  * one-stripe calls into one device product over N stripes.
  *
- * Structure: a FIFO guarded by a mutex, one worker thread.  The worker takes
- * the oldest request's "class" (op, k, p, cell size, erasure set), waits up to
- * max_wait_us for more of the same class unless max_batch are already queued,
- * gathers the batch into pinned staging with a 64-byte-aligned cell pitch (so
- * the vector kernels apply for any cell size), runs one ecg_matmul on the
- * device, scatters the results back and fires each request's callback.
+ * Structure: NSLOT pinned staging slots, each owned by one request class
+ * (op, k, p, cell size, erasure set) while it fills:
+ *   FREE -> FILLING -> READY -> INFLIGHT -> FREE
+ * A submitter reserves a stripe index in a FILLING slot of its class (or
+ * opens a FREE slot), copies its input cells into the slot's pinned staging
+ * itself -- so gathers run in parallel on the callers' threads -- and
+ * returns.  The worker thread closes a slot when it is full or its oldest
+ * request has waited max_wait_us (or a flush is pending), launches
+ * H2D(inputs) -> kernel -> D2H(outputs) on the slot's own stream, and polls
+ * in-flight slots; when one completes it scatters the outputs to the
+ * requests' buffers and fires their callbacks.  Slots in different states
+ * overlap: one fills while another's H2D, another's kernel and another's D2H
+ * run.  Staging layout per slot: inputs [n][k][pitch], outputs
+ * [n][rows][pitch] (pitch = cell size rounded to 64 B), so only inputs
+ * cross H2D and only outputs cross D2H.
  */
-#include <errno.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -24,37 +32,51 @@
 
 #define OP_ENCODE 0
 #define OP_RECOVER 1
+#define NSLOT 4
+
+enum slot_state { S_FREE, S_FILLING, S_READY, S_INFLIGHT };
 
 struct qreq {
-	struct qreq *next;
 	int op, k, p, nerrs;
 	uint64_t C;
-	unsigned char *src[ECG_MAX_K];
-	unsigned char *dst[ECG_MAX_P];
-	unsigned char *stripe;
-	uint32_t err[ECG_MAX_P];
+	unsigned char *dst[ECG_MAX_P];	/* where each output row goes */
 	ecg_done_cb_t cb;
 	void *arg;
-	uint64_t t_ns;
+};
+
+struct qslot {
+	enum slot_state state;
+	/* class */
+	int op, k, p, nerrs, rows;
+	uint64_t C, pitch;
+	uint32_t err[ECG_MAX_P];
+	unsigned char coef[ECG_MAX_P * ECG_MAX_K];
+	uint32_t dec_idx[ECG_MAX_K], out_idx[ECG_MAX_P];
+	/* fill state */
+	uint32_t cap, reserved, filled;
+	uint64_t t_open_ns;
+	struct qreq *reqs;		/* cap entries */
+	/* staging */
+	unsigned char *host;		/* pinned: inputs then outputs */
+	unsigned char *dev;
+	size_t bytes;
+	hipStream_t st;
+	hipEvent_t done;
+	int rc;
 };
 
 struct ecg_queue {
 	ecg_ctx_t *ctx;
 	ecg_queue_attr_t attr;
-	uint64_t staging_bytes;
+	size_t slot_bytes;
 	pthread_mutex_t lock;
-	pthread_cond_t cv_work;
-	pthread_cond_t cv_done;
-	struct qreq *head, *tail;
-	uint64_t submitted, completed, batches;
-	uint64_t flush_target;	/* a flush waits for this many completions */
+	pthread_cond_t cv_work;		/* worker wakeups */
+	pthread_cond_t cv_slot;		/* a slot became FREE or gained room */
+	pthread_cond_t cv_done;		/* completions (flush) */
+	struct qslot slot[NSLOT];
+	uint64_t submitted, completed, batches, flush_target;
 	int stop;
 	pthread_t worker;
-	unsigned char *host;
-	size_t host_bytes;
-	unsigned char *dev;
-	size_t dev_bytes;
-	hipStream_t st;
 };
 
 static uint64_t now_ns(void)
@@ -65,11 +87,15 @@ static uint64_t now_ns(void)
 	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
 }
 
-static int same_class(const struct qreq *a, const struct qreq *b)
+static void abs_deadline(struct timespec *ts, uint64_t wait_ns)
 {
-	return a->op == b->op && a->k == b->k && a->p == b->p && a->C == b->C &&
-	       a->nerrs == b->nerrs &&
-	       (a->op != OP_RECOVER || memcmp(a->err, b->err, sizeof(uint32_t) * a->nerrs) == 0);
+	clock_gettime(CLOCK_REALTIME, ts);
+	ts->tv_sec += (time_t)(wait_ns / 1000000000ull);
+	ts->tv_nsec += (long)(wait_ns % 1000000000ull);
+	if (ts->tv_nsec >= 1000000000L) {
+		ts->tv_sec++;
+		ts->tv_nsec -= 1000000000L;
+	}
 }
 
 static uint64_t pitch_of(uint64_t C)
@@ -77,214 +103,202 @@ static uint64_t pitch_of(uint64_t C)
 	return (C + 63) & ~63ull;
 }
 
-/* Stripes of this class that fit one batch. */
-static uint32_t batch_limit(const struct ecg_queue *q, const struct qreq *r)
+static int slot_matches(const struct qslot *s, int op, int k, int p, uint64_t C,
+			const uint32_t *err, int nerrs)
 {
-	uint64_t per = pitch_of(r->C) * (uint64_t)(r->k + r->p);
-	uint64_t n = per ? q->staging_bytes / per : q->attr.max_batch;
-
-	if (n < 1)
-		n = 1;
-	if (n > q->attr.max_batch)
-		n = q->attr.max_batch;
-	return (uint32_t)n;
+	return s->state == S_FILLING && s->reserved < s->cap && s->op == op && s->k == k &&
+	       s->p == p && s->C == C && s->nerrs == nerrs &&
+	       (op != OP_RECOVER || memcmp(s->err, err, sizeof(uint32_t) * nerrs) == 0);
 }
 
-static int staging_reserve(struct ecg_queue *q, size_t bytes)
+/* Assign a FREE slot to a class: decode rows for recovery, capacity from the
+ * slot's staging bytes. */
+static int slot_open(struct ecg_queue *q, struct qslot *s, int op, int k, int p, uint64_t C,
+		     const uint32_t *err, int nerrs)
 {
-	hipError_t e;
+	unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
+	uint64_t per;
+	int j, reused, rc;
 
-	if (q->host_bytes < bytes) {
-		if (q->host)
-			(void)hipHostFree(q->host);
-		q->host = NULL;
-		q->host_bytes = 0;
-		e = hipHostMalloc((void **)&q->host, bytes, hipHostMallocDefault);
-		if (e != hipSuccess)
-			return ecg_hip_fail(e, "queue pinned staging");
-		q->host_bytes = bytes;
-	}
-	if (q->dev_bytes < bytes) {
-		if (q->dev)
-			(void)hipFree(q->dev);
-		q->dev = NULL;
-		q->dev_bytes = 0;
-		e = hipMalloc((void **)&q->dev, bytes);
-		if (e != hipSuccess)
-			return ecg_hip_fail(e, "queue device staging");
-		q->dev_bytes = bytes;
-	}
-	return 0;
-}
-
-/* Run one batch of same-class requests.  Staging layout: stripe i at
- * i*(k+p)*pitch, cell c at c*pitch inside it (logical order, as the
- * reference's recovery buffer). */
-static int run_batch(struct ecg_queue *q, struct qreq **b, uint32_t n)
-{
-	const struct qreq *r0 = b[0];
-	const int k = r0->k, p = r0->p;
-	const uint64_t C = r0->C, pitch = pitch_of(C);
-	const uint64_t sstride = pitch * (uint64_t)(k + p);
-	unsigned char coef[ECG_MAX_P * ECG_MAX_K];
-	uint32_t out_idx[ECG_MAX_P], dec_idx[ECG_MAX_K];
-	int64_t soff[ECG_MAX_K], doff[ECG_MAX_P];
-	int rows, rc, reused, j;
-	uint32_t i;
-	hipError_t e;
-
-	rc = ecg_ctx_enter(q->ctx);
-	if (rc)
-		return rc;
-	rc = staging_reserve(q, (size_t)(sstride * n));
-	if (rc)
-		return rc;
-	if (r0->op == OP_ENCODE) {
-		unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
-
-		ecg_gen_cauchy1(k, p, en);
-		memcpy(coef, &en[k * k], (size_t)p * k);
-		rows = p;
+	s->op = op;
+	s->k = k;
+	s->p = p;
+	s->C = C;
+	s->pitch = pitch_of(C);
+	s->nerrs = nerrs;
+	ecg_gen_cauchy1(k, p, en);
+	if (op == OP_ENCODE) {
+		s->rows = p;
+		memcpy(s->coef, &en[k * k], (size_t)p * k);
 		for (j = 0; j < k; j++)
-			dec_idx[j] = (uint32_t)j;
+			s->dec_idx[j] = (uint32_t)j;
 		for (j = 0; j < p; j++)
-			out_idx[j] = (uint32_t)(k + j);
+			s->out_idx[j] = (uint32_t)(k + j);
 	} else {
-		unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
-
-		ecg_gen_cauchy1(k, p, en);
-		rc = ecg_recov_rows(k, p, en, r0->err, r0->nerrs, coef, out_idx, dec_idx, &reused);
+		memcpy(s->err, err, sizeof(uint32_t) * nerrs);
+		rc = ecg_recov_rows(k, p, en, err, nerrs, s->coef, s->out_idx, s->dec_idx, &reused);
 		if (rc)
 			return rc;
-		rows = r0->nerrs;
+		s->rows = nerrs;
 	}
-	/* gather the cells the product reads */
-	for (i = 0; i < n; i++) {
-		unsigned char *s = q->host + i * sstride;
-
-		for (j = 0; j < k; j++) {
-			const unsigned char *from = b[i]->op == OP_ENCODE ? b[i]->src[j]
-					: b[i]->stripe + (uint64_t)dec_idx[j] * C;
-
-			memcpy(s + (uint64_t)dec_idx[j] * pitch, from, C);
-		}
-	}
-	e = hipMemcpyAsync(q->dev, q->host, (size_t)(sstride * n), hipMemcpyHostToDevice, q->st);
-	if (e != hipSuccess)
-		return ecg_hip_fail(e, "queue H2D");
-	for (j = 0; j < k; j++)
-		soff[j] = (int64_t)(dec_idx[j] * pitch);
-	for (j = 0; j < rows; j++)
-		doff[j] = (int64_t)(out_idx[j] * pitch);
-	rc = ecg_matmul(q->ctx, k, rows, coef, C, n, q->dev, soff, (int64_t)sstride, q->dev, doff,
-			(int64_t)sstride, 0, q->st);
-	if (rc)
-		return rc;
-	e = hipMemcpyAsync(q->host, q->dev, (size_t)(sstride * n), hipMemcpyDeviceToHost, q->st);
-	if (e == hipSuccess)
-		e = hipStreamSynchronize(q->st);
-	if (e != hipSuccess)
-		return ecg_hip_fail(e, "queue D2H");
-	/* scatter the cells the product wrote */
-	for (i = 0; i < n; i++) {
-		const unsigned char *s = q->host + i * sstride;
-
-		for (j = 0; j < rows; j++) {
-			unsigned char *to = b[i]->op == OP_ENCODE ? b[i]->dst[j]
-					: b[i]->stripe + (uint64_t)out_idx[j] * C;
-
-			memcpy(to, s + (uint64_t)out_idx[j] * pitch, C);
-		}
-	}
+	per = s->pitch * (uint64_t)(k + s->rows);
+	s->cap = (uint32_t)(q->slot_bytes / per);
+	if (s->cap > q->attr.max_batch)
+		s->cap = q->attr.max_batch;
+	if (s->cap == 0)
+		return ecg_fail(-ECG_DER_REC2BIG, "queue: one stripe (%llu B) exceeds a slot",
+				(unsigned long long)per);
+	s->reserved = 0;
+	s->filled = 0;
+	s->rc = 0;
+	s->t_open_ns = now_ns();
+	s->state = S_FILLING;
 	return 0;
+}
+
+static void close_due_slots(struct ecg_queue *q, uint64_t t, int force)
+{
+	for (int i = 0; i < NSLOT; i++) {
+		struct qslot *s = &q->slot[i];
+
+		if (s->state == S_FILLING && s->reserved > 0 &&
+		    (force || s->reserved == s->cap ||
+		     t >= s->t_open_ns + (uint64_t)q->attr.max_wait_us * 1000ull))
+			s->state = S_READY;
+	}
+}
+
+/* READY and fully copied in: launch H2D -> product -> D2H (lock held; only
+ * enqueues asynchronous work). */
+static void launch_slot(struct ecg_queue *q, struct qslot *s)
+{
+	const uint32_t n = s->reserved;
+	const uint64_t in_stride = s->pitch * (uint64_t)s->k;
+	const uint64_t out_stride = s->pitch * (uint64_t)s->rows;
+	unsigned char *dout = s->dev + (size_t)in_stride * s->cap;
+	int64_t soff[ECG_MAX_K], doff[ECG_MAX_P];
+	hipError_t e;
+	int j, rc;
+
+	for (j = 0; j < s->k; j++)
+		soff[j] = (int64_t)(j * s->pitch);
+	for (j = 0; j < s->rows; j++)
+		doff[j] = (int64_t)(j * s->pitch);
+	e = hipMemcpyAsync(s->dev, s->host, (size_t)in_stride * n, hipMemcpyHostToDevice, s->st);
+	rc = e == hipSuccess ? 0 : ecg_hip_fail(e, "queue H2D");
+	if (rc == 0)
+		rc = ecg_matmul(q->ctx, s->k, s->rows, s->coef, s->C, n, s->dev, soff, (int64_t)in_stride,
+				dout, doff, (int64_t)out_stride, 0, s->st);
+	if (rc == 0) {
+		e = hipMemcpyAsync(s->host + (size_t)in_stride * s->cap, dout, (size_t)out_stride * n,
+				   hipMemcpyDeviceToHost, s->st);
+		if (e == hipSuccess)
+			e = hipEventRecord(s->done, s->st);
+		if (e != hipSuccess)
+			rc = ecg_hip_fail(e, "queue D2H");
+	}
+	s->rc = rc;
+	s->state = S_INFLIGHT;
+	q->batches++;
+}
+
+/* Outputs back to the requests, then callbacks (lock NOT held). */
+static void finish_slot(struct qslot *s)
+{
+	const uint64_t in_stride = s->pitch * (uint64_t)s->k;
+	const uint64_t out_stride = s->pitch * (uint64_t)s->rows;
+	const unsigned char *out = s->host + (size_t)in_stride * s->cap;
+
+	for (uint32_t i = 0; i < s->reserved; i++) {
+		struct qreq *r = &s->reqs[i];
+
+		if (s->rc == 0)
+			for (int j = 0; j < s->rows; j++)
+				memcpy(r->dst[j], out + i * out_stride + j * s->pitch, s->C);
+		if (r->cb)
+			r->cb(r->arg, s->rc);
+	}
 }
 
 static void *worker_main(void *argp)
 {
 	struct ecg_queue *q = argp;
-	struct qreq **batch = calloc(q->attr.max_batch, sizeof(*batch));
 
-	if (batch == NULL)
-		abort();
 	(void)hipSetDevice(q->ctx->device);
 	pthread_mutex_lock(&q->lock);
 	for (;;) {
-		struct qreq *r, *prev, *next;
-		uint32_t n = 0, limit, avail = 0;
-		int rc;
+		int busy = 0, idle = 1;
+		uint64_t t = now_ns(), next = UINT64_MAX;
 
-		if (q->head == NULL) {
-			if (q->stop)
-				break;
-			pthread_cond_wait(&q->cv_work, &q->lock);
+		close_due_slots(q, t, q->stop || q->completed < q->flush_target);
+		for (int i = 0; i < NSLOT; i++) {
+			struct qslot *s = &q->slot[i];
+
+			if (s->state == S_READY && s->filled == s->reserved) {
+				launch_slot(q, s);
+				idle = 0;
+			}
+		}
+		for (int i = 0; i < NSLOT; i++) {
+			struct qslot *s = &q->slot[i];
+
+			if (s->state == S_INFLIGHT) {
+				hipError_t e = hipEventQuery(s->done);
+
+				if (e == hipErrorNotReady) {
+					busy = 1;
+					continue;
+				}
+				if (e != hipSuccess && s->rc == 0)
+					s->rc = ecg_hip_fail(e, "queue batch");
+				pthread_mutex_unlock(&q->lock);
+				finish_slot(s);
+				pthread_mutex_lock(&q->lock);
+				q->completed += s->reserved;
+				s->state = S_FREE;
+				pthread_cond_broadcast(&q->cv_slot);
+				pthread_cond_broadcast(&q->cv_done);
+				idle = 0;
+			} else if (s->state == S_FILLING && s->reserved > 0) {
+				uint64_t dl = s->t_open_ns + (uint64_t)q->attr.max_wait_us * 1000ull;
+
+				if (dl < next)
+					next = dl;
+			} else if (s->state == S_READY) {
+				busy = 1;	/* waiting for a submitter's copy to land */
+			}
+		}
+		if (!idle)
 			continue;
-		}
-		limit = batch_limit(q, q->head);
-		for (r = q->head; r && avail < limit; r = r->next)
-			avail += same_class(r, q->head);
-		if (avail < limit && !q->stop && q->completed >= q->flush_target) {
-			uint64_t deadline = q->head->t_ns + (uint64_t)q->attr.max_wait_us * 1000ull;
-			uint64_t t = now_ns();
+		if (q->stop) {
+			int live = 0;
 
-			if (t < deadline) {
-				struct timespec ts;
-
-				clock_gettime(CLOCK_REALTIME, &ts);
-				t = deadline - t;
-				ts.tv_sec += (time_t)(t / 1000000000ull);
-				ts.tv_nsec += (long)(t % 1000000000ull);
-				if (ts.tv_nsec >= 1000000000L) {
-					ts.tv_sec++;
-					ts.tv_nsec -= 1000000000L;
-				}
-				pthread_cond_timedwait(&q->cv_work, &q->lock, &ts);
-				continue;
-			}
+			for (int i = 0; i < NSLOT; i++)
+				live += q->slot[i].state != S_FREE;
+			if (!live)
+				break;
 		}
-		/* unlink up to `limit` requests of the head's class, FIFO order */
 		{
-			struct qreq *key = q->head;
+			struct timespec ts;
+			uint64_t wait = busy ? 20000ull : 100000000ull;	/* poll in-flight work */
 
-			prev = NULL;
-			for (r = q->head; r && n < limit; r = next) {
-				next = r->next;
-				if (same_class(r, key)) {
-					if (prev)
-						prev->next = next;
-					else
-						q->head = next;
-					if (q->tail == r)
-						q->tail = prev;
-					r->next = NULL;
-					batch[n++] = r;
-				} else {
-					prev = r;
-				}
+			if (next != UINT64_MAX)
+				wait = next > t ? (next - t < wait ? next - t : wait) : 0;
+			if (wait) {
+				abs_deadline(&ts, wait);
+				pthread_cond_timedwait(&q->cv_work, &q->lock, &ts);
 			}
 		}
-		pthread_mutex_unlock(&q->lock);
-		rc = run_batch(q, batch, n);
-		for (uint32_t i = 0; i < n; i++) {
-			if (batch[i]->cb)
-				batch[i]->cb(batch[i]->arg, rc);
-			free(batch[i]);
-		}
-		pthread_mutex_lock(&q->lock);
-		q->completed += n;
-		q->batches++;
-		pthread_cond_broadcast(&q->cv_done);
 	}
 	pthread_mutex_unlock(&q->lock);
-	free(batch);
 	return NULL;
 }
 
 int ecg_queue_create(ecg_ctx_t *ctx, const ecg_queue_attr_t *attr, ecg_queue_t **out)
 {
 	struct ecg_queue *q;
-	pthread_condattr_t ca;
-	hipError_t e;
-	int rc;
+	hipError_t e = hipSuccess;
+	int rc, i;
 
 	if (ctx == NULL || out == NULL)
 		return ecg_fail(-ECG_DER_INVAL, "queue_create: NULL argument");
@@ -303,25 +317,52 @@ int ecg_queue_create(ecg_ctx_t *ctx, const ecg_queue_attr_t *attr, ecg_queue_t *
 		q->attr.max_wait_us = 50;
 	if (q->attr.max_cell_bytes == 0)
 		q->attr.max_cell_bytes = 1 << 20;
-	/* staging for a full batch of 8+2 stripes at max_cell_bytes, capped at
-	 * 512 MiB (larger classes just get proportionally fewer stripes) */
-	q->staging_bytes = pitch_of(q->attr.max_cell_bytes) * 10ull * q->attr.max_batch;
-	if (q->staging_bytes > (512ull << 20))
-		q->staging_bytes = 512ull << 20;
+	/* a slot holds max_batch stripes of 8+2 cells of max_cell_bytes, capped
+	 * at 128 MiB (bigger classes get proportionally fewer stripes) */
+	q->slot_bytes = (size_t)pitch_of(q->attr.max_cell_bytes) * 10u * q->attr.max_batch;
+	if (q->slot_bytes > (128u << 20))
+		q->slot_bytes = 128u << 20;
+	if (q->slot_bytes < (size_t)pitch_of(q->attr.max_cell_bytes) * (ECG_MAX_K + ECG_MAX_P))
+		q->slot_bytes = (size_t)pitch_of(q->attr.max_cell_bytes) * (ECG_MAX_K + ECG_MAX_P);
 	pthread_mutex_init(&q->lock, NULL);
-	pthread_condattr_init(&ca);
-	pthread_cond_init(&q->cv_work, &ca);
-	pthread_cond_init(&q->cv_done, &ca);
-	pthread_condattr_destroy(&ca);
-	e = hipStreamCreateWithFlags(&q->st, hipStreamNonBlocking);
-	if (e != hipSuccess) {
-		free(q);
-		return ecg_hip_fail(e, "queue stream");
+	pthread_cond_init(&q->cv_work, NULL);
+	pthread_cond_init(&q->cv_slot, NULL);
+	pthread_cond_init(&q->cv_done, NULL);
+	for (i = 0; i < NSLOT && e == hipSuccess; i++) {
+		struct qslot *s = &q->slot[i];
+
+		s->reqs = calloc(q->attr.max_batch, sizeof(*s->reqs));
+		if (s->reqs == NULL) {
+			e = hipErrorOutOfMemory;
+			break;
+		}
+		s->bytes = q->slot_bytes;
+		e = hipHostMalloc((void **)&s->host, s->bytes, hipHostMallocDefault);
+		if (e == hipSuccess)
+			e = hipMalloc((void **)&s->dev, s->bytes);
+		if (e == hipSuccess)
+			e = hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking);
+		if (e == hipSuccess)
+			e = hipEventCreateWithFlags(&s->done, hipEventDisableTiming);
 	}
-	if (pthread_create(&q->worker, NULL, worker_main, q) != 0) {
-		(void)hipStreamDestroy(q->st);
+	if (e == hipSuccess && pthread_create(&q->worker, NULL, worker_main, q) != 0)
+		e = hipErrorOutOfMemory;
+	if (e != hipSuccess) {
+		for (i = 0; i < NSLOT; i++) {
+			struct qslot *s = &q->slot[i];
+
+			if (s->host)
+				(void)hipHostFree(s->host);
+			if (s->dev)
+				(void)hipFree(s->dev);
+			if (s->st)
+				(void)hipStreamDestroy(s->st);
+			if (s->done)
+				(void)hipEventDestroy(s->done);
+			free(s->reqs);
+		}
 		free(q);
-		return ecg_fail(-ECG_DER_NOMEM, "queue_create: pthread_create");
+		return ecg_hip_fail(e, "queue_create");
 	}
 	*out = q;
 	return 0;
@@ -334,35 +375,90 @@ void ecg_queue_destroy(ecg_queue_t *q)
 	pthread_mutex_lock(&q->lock);
 	q->stop = 1;
 	pthread_cond_broadcast(&q->cv_work);
+	pthread_cond_broadcast(&q->cv_slot);
 	pthread_mutex_unlock(&q->lock);
 	pthread_join(q->worker, NULL);
 	(void)hipSetDevice(q->ctx->device);
-	if (q->host)
-		(void)hipHostFree(q->host);
-	if (q->dev)
-		(void)hipFree(q->dev);
-	(void)hipStreamDestroy(q->st);
+	for (int i = 0; i < NSLOT; i++) {
+		struct qslot *s = &q->slot[i];
+
+		(void)hipHostFree(s->host);
+		(void)hipFree(s->dev);
+		(void)hipStreamDestroy(s->st);
+		(void)hipEventDestroy(s->done);
+		free(s->reqs);
+	}
 	pthread_cond_destroy(&q->cv_work);
+	pthread_cond_destroy(&q->cv_slot);
 	pthread_cond_destroy(&q->cv_done);
 	pthread_mutex_destroy(&q->lock);
 	free(q);
 }
 
-static int enqueue(struct ecg_queue *q, struct qreq *r)
+/* Reserve a stripe index in a slot of this class (opening one if needed),
+ * copy the inputs in without the lock, then publish. */
+static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const uint32_t *err,
+		  int nerrs, unsigned char *const *src, unsigned char *stripe,
+		  unsigned char *const *dst, ecg_done_cb_t cb, void *arg)
 {
-	r->t_ns = now_ns();
+	struct qslot *s = NULL;
+	uint32_t idx;
+	int i, rc = 0;
+
 	pthread_mutex_lock(&q->lock);
-	if (q->stop) {
-		pthread_mutex_unlock(&q->lock);
-		free(r);
-		return ecg_fail(-ECG_DER_INVAL, "queue is being destroyed");
+	while (s == NULL) {
+		if (q->stop) {
+			pthread_mutex_unlock(&q->lock);
+			return ecg_fail(-ECG_DER_INVAL, "queue is being destroyed");
+		}
+		for (i = 0; i < NSLOT && s == NULL; i++)
+			if (slot_matches(&q->slot[i], op, k, p, C, err, nerrs))
+				s = &q->slot[i];
+		for (i = 0; i < NSLOT && s == NULL; i++) {
+			if (q->slot[i].state == S_FREE) {
+				rc = slot_open(q, &q->slot[i], op, k, p, C, err, nerrs);
+				if (rc) {
+					q->slot[i].state = S_FREE;
+					pthread_mutex_unlock(&q->lock);
+					return rc;
+				}
+				s = &q->slot[i];
+			}
+		}
+		if (s == NULL) {
+			pthread_cond_broadcast(&q->cv_work);	/* make the worker drain */
+			pthread_cond_wait(&q->cv_slot, &q->lock);
+		}
 	}
-	if (q->tail)
-		q->tail->next = r;
-	else
-		q->head = r;
-	q->tail = r;
+	idx = s->reserved++;
 	q->submitted++;
+	if (s->reserved == s->cap)
+		s->state = S_READY;
+	pthread_mutex_unlock(&q->lock);
+
+	{
+		struct qreq *r = &s->reqs[idx];
+		unsigned char *in = s->host + (size_t)idx * s->pitch * (uint64_t)k;
+
+		r->op = op;
+		r->k = k;
+		r->p = p;
+		r->C = C;
+		r->nerrs = nerrs;
+		r->cb = cb;
+		r->arg = arg;
+		for (i = 0; i < k; i++) {
+			const unsigned char *from = op == OP_ENCODE ? src[i]
+					: stripe + (uint64_t)s->dec_idx[i] * C;
+
+			memcpy(in + (uint64_t)i * s->pitch, from, C);
+		}
+		for (i = 0; i < s->rows; i++)
+			r->dst[i] = op == OP_ENCODE ? dst[i] : stripe + (uint64_t)s->out_idx[i] * C;
+	}
+
+	pthread_mutex_lock(&q->lock);
+	s->filled++;
 	pthread_cond_signal(&q->cv_work);
 	pthread_mutex_unlock(&q->lock);
 	return 0;
@@ -371,55 +467,31 @@ static int enqueue(struct ecg_queue *q, struct qreq *r)
 int ecg_queue_encode(ecg_queue_t *q, int k, int p, uint64_t C, unsigned char *const *data,
 		     unsigned char *const *parity, ecg_done_cb_t cb, void *arg)
 {
-	struct qreq *r;
-	int j;
-
 	if (q == NULL || data == NULL || parity == NULL || k < 1 || k > ECG_MAX_K || p < 1 ||
 	    p > ECG_MAX_P || C == 0)
 		return ecg_fail(-ECG_DER_INVAL, "queue_encode: bad arguments");
-	r = calloc(1, sizeof(*r));
-	if (r == NULL)
-		return ecg_fail(-ECG_DER_NOMEM, "queue_encode: calloc");
-	r->op = OP_ENCODE;
-	r->k = k;
-	r->p = p;
-	r->C = C;
-	for (j = 0; j < k; j++)
-		r->src[j] = data[j];
-	for (j = 0; j < p; j++)
-		r->dst[j] = parity[j];
-	r->cb = cb;
-	r->arg = arg;
-	return enqueue(q, r);
+	return submit(q, OP_ENCODE, k, p, C, NULL, 0, data, NULL, parity, cb, arg);
 }
 
 int ecg_queue_recover(ecg_queue_t *q, int k, int p, uint64_t C, unsigned char *stripe,
 		      const uint32_t *err_list, int nerrs, ecg_done_cb_t cb, void *arg)
 {
-	struct qreq *r;
-	int i;
+	int i, j;
 
 	if (q == NULL || stripe == NULL || err_list == NULL || k < 1 || k > ECG_MAX_K || p < 1 ||
 	    p > ECG_MAX_P || C == 0 || nerrs < 1)
 		return ecg_fail(-ECG_DER_INVAL, "queue_recover: bad arguments");
 	if (nerrs > p)
 		return ecg_fail(-ECG_DER_DATA_LOSS, "queue_recover: %d erasures > p=%d", nerrs, p);
-	for (i = 0; i < nerrs; i++)
+	for (i = 0; i < nerrs; i++) {
 		if (err_list[i] >= (uint32_t)(k + p))
 			return ecg_fail(-ECG_DER_INVAL, "queue_recover: cell %u", err_list[i]);
-	r = calloc(1, sizeof(*r));
-	if (r == NULL)
-		return ecg_fail(-ECG_DER_NOMEM, "queue_recover: calloc");
-	r->op = OP_RECOVER;
-	r->k = k;
-	r->p = p;
-	r->C = C;
-	r->stripe = stripe;
-	r->nerrs = nerrs;
-	memcpy(r->err, err_list, sizeof(uint32_t) * nerrs);
-	r->cb = cb;
-	r->arg = arg;
-	return enqueue(q, r);
+		for (j = 0; j < i; j++)
+			if (err_list[j] == err_list[i])
+				return ecg_fail(-ECG_DER_INVAL, "queue_recover: duplicate cell %u",
+						err_list[i]);
+	}
+	return submit(q, OP_RECOVER, k, p, C, err_list, nerrs, NULL, stripe, NULL, cb, arg);
 }
 
 int ecg_queue_flush(ecg_queue_t *q)

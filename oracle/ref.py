@@ -149,8 +149,9 @@ def recov_codec(k: int, p: int, err_list):
     return rc, de.reshape(-1, k)[:nerrs], dec, oel[:nerrs].copy(), gt, bool(reused.value)
 
 
-def encode_batch(k: int, p: int, C_: int, S: int, data: np.ndarray, nthreads: int = 1, simd: bool = False):
-    parity = np.zeros(p * S * C_, dtype=np.uint8)
+def encode_batch(k: int, p: int, C_: int, S: int, data: np.ndarray, nthreads: int = 1, simd: bool = False,
+                 out: np.ndarray | None = None):
+    parity = np.zeros(p * S * C_, dtype=np.uint8) if out is None else out
     f = lib().ref_simd_encode_batch if simd else lib().ref_encode_batch
     f(k, p, C_, S, _p(data), _p(parity), nthreads)
     return parity

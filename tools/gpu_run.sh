@@ -72,6 +72,19 @@ for what in "$@"; do
 	tune7)
 		step tune7 600 python tools/tune7.py || exit $?
 		;;
+	qbench)
+		make -C tests/c > /dev/null || exit 2
+		for c in 32768 131072 1048576; do
+			for t in 8 16; do
+				step qbench_${c}_$t 300 ./build/ctest/queue_bench $c $t || exit $?
+			done
+		done
+		cat gpurun_out/qbench_*.log | grep '^{' > gpurun_out/qbench.jsonl
+		;;
+	ctest)
+		make -C tests/c > /dev/null || exit 2
+		step ctest 300 ./build/ctest/test_ecg_c || exit $?
+		;;
 	tune3)
 		step tune3 600 python tools/tune3.py || exit $?
 		;;

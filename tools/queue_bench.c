@@ -1,0 +1,134 @@
+/*
+ * queue_bench.c -- one-stripe callers, the reference's calling pattern
+ * (SURVEY §0.6): T pthreads each encode N stripes of EC_k+p with C-byte
+ * cells, one stripe per call, via
+ *   isal : ec_encode_data()        (synchronous ISA-L drop-in, GPU per call)
+ *   queue: ecg_queue_encode()      (batching facade, async completion)
+ *   cpu  : ref_simd_encode_data()  (ISA-L-equivalent CPU restatement, the
+ *                                   baseline DAOS runs today)
+ * and prints one JSON line of GiB/s (user data).  Bench infrastructure.
+ */
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "ec_ref.h"
+#include "ecg.h"
+#include "ecg_isal.h"
+
+static int K = 8, P = 2, T = 8, N = 64;
+static uint64_t CB = 128 << 10;
+static unsigned char *g_cells;		/* T * N stripes of (K + P) cells */
+static unsigned char g_tbls[64 * 8 * 32];
+static ecg_queue_t *g_q;
+static int g_mode;			/* 0 isal, 1 queue, 2 cpu */
+
+struct cnt {
+	pthread_mutex_t lock;
+	pthread_cond_t cv;
+	long done;
+};
+static struct cnt g_cnt = {PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, 0};
+
+static double now(void)
+{
+	struct timespec ts;
+
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+static void done_cb(void *arg, int rc)
+{
+	(void)arg;
+	if (rc)
+		fprintf(stderr, "request failed rc=%d\n", rc);
+	pthread_mutex_lock(&g_cnt.lock);
+	g_cnt.done++;
+	pthread_cond_broadcast(&g_cnt.cv);
+	pthread_mutex_unlock(&g_cnt.lock);
+}
+
+static void *worker(void *arg)
+{
+	long t = (long)arg;
+
+	for (int i = 0; i < N; i++) {
+		unsigned char *s = g_cells + ((size_t)t * N + i) * (K + P) * CB;
+		unsigned char *data[64], *par[8];
+
+		for (int c = 0; c < K; c++)
+			data[c] = s + c * CB;
+		for (int r = 0; r < P; r++)
+			par[r] = s + (K + r) * CB;
+		if (g_mode == 0)
+			ec_encode_data((int)CB, K, P, g_tbls, data, par);
+		else if (g_mode == 1)
+			ecg_queue_encode(g_q, K, P, CB, data, par, done_cb, NULL);
+		else
+			ref_simd_encode_data((int)CB, K, P, g_tbls, data, par);
+	}
+	return NULL;
+}
+
+static double run(int mode)
+{
+	pthread_t th[64];
+	double t0, t1;
+
+	g_mode = mode;
+	g_cnt.done = 0;
+	t0 = now();
+	for (long t = 0; t < T; t++)
+		pthread_create(&th[t], NULL, worker, (void *)t);
+	for (int t = 0; t < T; t++)
+		pthread_join(th[t], NULL);
+	if (mode == 1) {
+		pthread_mutex_lock(&g_cnt.lock);
+		while (g_cnt.done < (long)T * N)
+			pthread_cond_wait(&g_cnt.cv, &g_cnt.lock);
+		pthread_mutex_unlock(&g_cnt.lock);
+	}
+	t1 = now();
+	return (double)T * N * K * CB / (t1 - t0) / (1 << 30);
+}
+
+int main(int argc, char **argv)
+{
+	unsigned char en[(64 + 8) * 64];
+	ecg_ctx_t *ctx = NULL;
+	ecg_queue_attr_t qa = {256, 100, 0};
+	double isal, queue, cpu;
+	uint64_t reqs = 0, batches = 0;
+
+	if (argc > 1)
+		CB = strtoull(argv[1], NULL, 0);
+	if (argc > 2)
+		T = atoi(argv[2]);
+	g_cells = malloc((size_t)T * N * (K + P) * CB);
+	for (size_t i = 0; i < (size_t)T * N * (K + P) * CB; i++)
+		g_cells[i] = (unsigned char)(i * 2654435761u >> 13);
+	gf_gen_cauchy1_matrix(en, K + P, K);
+	ec_init_tables(K, P, &en[K * K], g_tbls);
+	if (ecg_ctx_create(0, &ctx) || ecg_queue_create(ctx, &qa, &g_q)) {
+		fprintf(stderr, "no device: %s\n", ecg_strerror());
+		return 1;
+	}
+	run(0);			/* warm up staging / code objects */
+	isal = run(0);
+	run(1);
+	queue = run(1);
+	ecg_queue_stats(g_q, &reqs, &batches);
+	cpu = run(2);
+	printf("{\"k\": %d, \"p\": %d, \"cell_bytes\": %llu, \"threads\": %d, \"stripes_per_thread\": %d, "
+	       "\"isal_one_stripe_GiBps\": %.2f, \"queue_GiBps\": %.2f, \"queue_requests\": %llu, "
+	       "\"queue_batches\": %llu, \"cpu_gfni_same_threads_GiBps\": %.2f}\n",
+	       K, P, (unsigned long long)CB, T, N, isal, queue, (unsigned long long)reqs,
+	       (unsigned long long)batches, cpu);
+	ecg_queue_destroy(g_q);
+	ecg_ctx_destroy(ctx);
+	free(g_cells);
+	return 0;
+}
