@@ -10,17 +10,17 @@
  *
  * Structure: NSLOT pinned staging slots, each owned by one request class
  * (op, k, p, cell size, erasure set) while it fills:
- *   FREE -> FILLING -> READY -> INFLIGHT -> FREE
+ *   FREE -> FILLING -> READY -> INFLIGHT -> DONE -> FREE
  * A submitter reserves a stripe index in a FILLING slot of its class (or
  * opens a FREE slot), copies its input cells into the slot's pinned staging
  * itself -- so gathers run in parallel on the callers' threads -- and
  * returns.  The worker thread closes a slot when it is full or its oldest
  * request has waited max_wait_us (or a flush is pending), launches
  * H2D(inputs) -> kernel -> D2H(outputs) on the slot's own stream, and polls
- * in-flight slots; when one completes it scatters the outputs to the
- * requests' buffers and fires their callbacks.  Slots in different states
- * overlap: one fills while another's H2D, another's kernel and another's D2H
- * run.  Staging layout per slot: inputs [n][k][pitch], outputs
+ * in-flight slots; when one completes, NFIN completion threads scatter the
+ * outputs to the requests' buffers and fire their callbacks.  Slots in
+ * different states overlap: one fills while another's H2D, another's kernel
+ * and another's D2H run.  Staging layout per slot: inputs [n][k][pitch], outputs
  * [n][rows][pitch] (pitch = cell size rounded to 64 B), so only inputs
  * cross H2D and only outputs cross D2H.
  */
@@ -33,8 +33,9 @@
 #define OP_ENCODE 0
 #define OP_RECOVER 1
 #define NSLOT 4
+#define NFIN 4		/* completion threads: output scatter + callbacks */
 
-enum slot_state { S_FREE, S_FILLING, S_READY, S_INFLIGHT };
+enum slot_state { S_FREE, S_FILLING, S_READY, S_INFLIGHT, S_DONE };
 
 struct qreq {
 	int op, k, p, nerrs;
@@ -54,6 +55,7 @@ struct qslot {
 	uint32_t dec_idx[ECG_MAX_K], out_idx[ECG_MAX_P];
 	/* fill state */
 	uint32_t cap, reserved, filled;
+	uint32_t fin_next, fin_done;	/* completion progress (S_DONE) */
 	uint64_t t_open_ns;
 	struct qreq *reqs;		/* cap entries */
 	/* staging */
@@ -73,10 +75,13 @@ struct ecg_queue {
 	pthread_cond_t cv_work;		/* worker wakeups */
 	pthread_cond_t cv_slot;		/* a slot became FREE or gained room */
 	pthread_cond_t cv_done;		/* completions (flush) */
+	pthread_cond_t cv_fin;		/* a slot reached S_DONE */
 	struct qslot slot[NSLOT];
 	uint64_t submitted, completed, batches, flush_target;
-	int stop;
+	int stop, worker_exited;
 	pthread_t worker;
+	pthread_t fin[NFIN];
+	int nfin;
 };
 
 static uint64_t now_ns(void)
@@ -202,22 +207,57 @@ static void launch_slot(struct ecg_queue *q, struct qslot *s)
 	q->batches++;
 }
 
-/* Outputs back to the requests, then callbacks (lock NOT held). */
-static void finish_slot(struct qslot *s)
+/* One request's outputs back to its buffers, then its callback (lock NOT
+ * held). */
+static void finish_req(struct qslot *s, uint32_t i)
 {
 	const uint64_t in_stride = s->pitch * (uint64_t)s->k;
 	const uint64_t out_stride = s->pitch * (uint64_t)s->rows;
-	const unsigned char *out = s->host + (size_t)in_stride * s->cap;
+	const unsigned char *out = s->host + (size_t)in_stride * s->cap + i * out_stride;
+	struct qreq *r = &s->reqs[i];
 
-	for (uint32_t i = 0; i < s->reserved; i++) {
-		struct qreq *r = &s->reqs[i];
+	if (s->rc == 0)
+		for (int j = 0; j < s->rows; j++)
+			memcpy(r->dst[j], out + j * s->pitch, s->C);
+	if (r->cb)
+		r->cb(r->arg, s->rc);
+}
 
-		if (s->rc == 0)
-			for (int j = 0; j < s->rows; j++)
-				memcpy(r->dst[j], out + i * out_stride + j * s->pitch, s->C);
-		if (r->cb)
-			r->cb(r->arg, s->rc);
+/* Completion threads: claim requests of S_DONE slots one at a time, so the
+ * host-side scatter of a batch runs on NFIN threads; the last one frees the
+ * slot. */
+static void *fin_main(void *argp)
+{
+	struct ecg_queue *q = argp;
+
+	pthread_mutex_lock(&q->lock);
+	for (;;) {
+		struct qslot *s = NULL;
+		uint32_t i;
+
+		for (int j = 0; j < NSLOT && s == NULL; j++)
+			if (q->slot[j].state == S_DONE && q->slot[j].fin_next < q->slot[j].reserved)
+				s = &q->slot[j];
+		if (s == NULL) {
+			if (q->stop && q->worker_exited)
+				break;
+			pthread_cond_wait(&q->cv_fin, &q->lock);
+			continue;
+		}
+		i = s->fin_next++;
+		pthread_mutex_unlock(&q->lock);
+		finish_req(s, i);
+		pthread_mutex_lock(&q->lock);
+		if (++s->fin_done == s->reserved) {
+			q->completed += s->reserved;
+			s->state = S_FREE;
+			pthread_cond_broadcast(&q->cv_slot);
+			pthread_cond_broadcast(&q->cv_done);
+			pthread_cond_signal(&q->cv_work);
+		}
 	}
+	pthread_mutex_unlock(&q->lock);
+	return NULL;
 }
 
 static void *worker_main(void *argp)
@@ -251,13 +291,10 @@ static void *worker_main(void *argp)
 				}
 				if (e != hipSuccess && s->rc == 0)
 					s->rc = ecg_hip_fail(e, "queue batch");
-				pthread_mutex_unlock(&q->lock);
-				finish_slot(s);
-				pthread_mutex_lock(&q->lock);
-				q->completed += s->reserved;
-				s->state = S_FREE;
-				pthread_cond_broadcast(&q->cv_slot);
-				pthread_cond_broadcast(&q->cv_done);
+				s->fin_next = 0;
+				s->fin_done = 0;
+				s->state = S_DONE;
+				pthread_cond_broadcast(&q->cv_fin);
 				idle = 0;
 			} else if (s->state == S_FILLING && s->reserved > 0) {
 				uint64_t dl = s->t_open_ns + (uint64_t)q->attr.max_wait_us * 1000ull;
@@ -290,6 +327,8 @@ static void *worker_main(void *argp)
 			}
 		}
 	}
+	q->worker_exited = 1;
+	pthread_cond_broadcast(&q->cv_fin);
 	pthread_mutex_unlock(&q->lock);
 	return NULL;
 }
@@ -328,6 +367,7 @@ int ecg_queue_create(ecg_ctx_t *ctx, const ecg_queue_attr_t *attr, ecg_queue_t *
 	pthread_cond_init(&q->cv_work, NULL);
 	pthread_cond_init(&q->cv_slot, NULL);
 	pthread_cond_init(&q->cv_done, NULL);
+	pthread_cond_init(&q->cv_fin, NULL);
 	for (i = 0; i < NSLOT && e == hipSuccess; i++) {
 		struct qslot *s = &q->slot[i];
 
@@ -345,8 +385,22 @@ int ecg_queue_create(ecg_ctx_t *ctx, const ecg_queue_attr_t *attr, ecg_queue_t *
 		if (e == hipSuccess)
 			e = hipEventCreateWithFlags(&s->done, hipEventDisableTiming);
 	}
+	for (i = 0; i < NFIN && e == hipSuccess; i++) {
+		if (pthread_create(&q->fin[i], NULL, fin_main, q) != 0)
+			e = hipErrorOutOfMemory;
+		else
+			q->nfin++;
+	}
 	if (e == hipSuccess && pthread_create(&q->worker, NULL, worker_main, q) != 0)
 		e = hipErrorOutOfMemory;
+	if (e != hipSuccess && q->nfin) {
+		pthread_mutex_lock(&q->lock);
+		q->stop = q->worker_exited = 1;
+		pthread_cond_broadcast(&q->cv_fin);
+		pthread_mutex_unlock(&q->lock);
+		for (i = 0; i < q->nfin; i++)
+			pthread_join(q->fin[i], NULL);
+	}
 	if (e != hipSuccess) {
 		for (i = 0; i < NSLOT; i++) {
 			struct qslot *s = &q->slot[i];
@@ -378,6 +432,8 @@ void ecg_queue_destroy(ecg_queue_t *q)
 	pthread_cond_broadcast(&q->cv_slot);
 	pthread_mutex_unlock(&q->lock);
 	pthread_join(q->worker, NULL);
+	for (int i = 0; i < q->nfin; i++)
+		pthread_join(q->fin[i], NULL);
 	(void)hipSetDevice(q->ctx->device);
 	for (int i = 0; i < NSLOT; i++) {
 		struct qslot *s = &q->slot[i];
@@ -391,6 +447,7 @@ void ecg_queue_destroy(ecg_queue_t *q)
 	pthread_cond_destroy(&q->cv_work);
 	pthread_cond_destroy(&q->cv_slot);
 	pthread_cond_destroy(&q->cv_done);
+	pthread_cond_destroy(&q->cv_fin);
 	pthread_mutex_destroy(&q->lock);
 	free(q);
 }
