@@ -65,6 +65,38 @@ typedef struct ecg_launch_cfg {
 	uint32_t pad;
 } ecg_launch_cfg_t;
 
+/*
+ * Chunked checksums (DAOS csummer semantics, ref:src/common/checksum.c:467-497):
+ * n_ext extents at src + e*ext_stride, each ext_bytes long and cut into
+ * nchunks chunks: chunk 0 = [0, first_bytes), chunk c >= 1 =
+ * [first_bytes + (c-1)*chunk_bytes, ... + chunk_bytes) clipped to ext_bytes.
+ * out[e*nchunks + c] = hash of that chunk (2, 4 or 8 bytes, little-endian).
+ * CRC tables (host-built, ecg_csum.c) at tbl: W-bit words T
+ *   sl[NB][256]  slice tables: sl[j][v] = CRC state after byte v then j zero bytes
+ *   sh[NB][256]  "shift by ECG_CSUM_STRIDE zero bytes" as a byte-wise linear map
+ *   k[64]        x^(8*16*(63-lane)) mod P, for the final per-lane shift
+ * with NB = W/8, T = uint32_t (W <= 32) or uint64_t (W = 64).
+ */
+#define ECG_CSUM_STRIDE 1024	/* bytes a wave consumes per step (64 lanes x 16 B) */
+#define ECG_KID_CSUM 1000	/* kernel ids of the checksum kernels start here */
+
+typedef struct ecg_csum_params {
+	const uint8_t *src;
+	uint8_t *out;
+	const void *tbl;
+	int64_t ext_stride;
+	uint64_t ext_bytes;
+	uint64_t first_bytes;
+	uint64_t chunk_bytes;
+	uint64_t init;			/* CRC register before the first byte */
+	uint64_t xorout;		/* XORed into the final register */
+	uint64_t poly;			/* reflected (or MSB-first for crc16) polynomial */
+	uint32_t n_ext;
+	uint32_t nchunks;
+	uint32_t type;			/* DAOS hash type: 1 crc16, 2 crc32, 3 crc64, 7 adler32 */
+	uint32_t pad;
+} ecg_csum_params_t;
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -75,6 +107,10 @@ int ecg_k_launch_matmul(const ecg_mm_params_t *p, const ecg_launch_cfg_t *cfg,
  * mode 0 copy, 1 read-only, 2 write-only. */
 int ecg_k_launch_copy(const void *src, void *dst, uint64_t bytes, int mode, void *stream,
 		      uint32_t max_blocks, uint32_t *kernel_id);
+/* Chunked checksums (kernels/ecg_csum_kernels.hip). max_blocks 0 = default. */
+int ecg_k_launch_csum(const ecg_csum_params_t *p, void *stream, uint32_t max_blocks,
+		      uint32_t *kernel_id);
+const char *ecg_k_csum_kernel_name(uint32_t kernel_id);
 const char *ecg_k_kernel_name(uint32_t kernel_id);
 #ifdef __cplusplus
 }

@@ -1,0 +1,237 @@
+/*
+ * ecg_csum.c -- host side of the chunked checksums (include/ecg_csum.h):
+ * CRC tables built from the polynomials, per-context device copies, chunk
+ * geometry of an extent (ref:src/common/checksum.c:1444-1565), launch.
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "ecg_internal.h"
+#include "../../../include/ecg_csum.h"
+
+struct crc_def {
+	int width;
+	int refl;
+	uint64_t poly;		/* reflected for refl, MSB-first otherwise */
+	uint64_t init, xorout;
+};
+
+/* ISA-L crc16_t10dif / crc32_iscsi / crc64_ecma_refl as DAOS calls them
+ * (seed 0; crc64 inverts the register on entry and exit). */
+static const struct crc_def g_defs[4] = {
+	[ECG_HASH_CRC16] = {16, 0, 0x8BB7, 0, 0},
+	[ECG_HASH_CRC32] = {32, 1, 0x82F63B78u, 0, 0},
+	[ECG_HASH_CRC64] = {64, 1, 0xC96C5795D7870F42ull, ~0ull, ~0ull},
+};
+
+int ecg_csum_len(int type)
+{
+	switch (type) {
+	case ECG_HASH_CRC16:
+		return 2;
+	case ECG_HASH_CRC32:
+	case ECG_HASH_ADLER32:
+		return 4;
+	case ECG_HASH_CRC64:
+		return 8;
+	default:
+		return -ECG_DER_NOTSUPPORTED;
+	}
+}
+
+uint64_t ecg_csum_record_chunksize(uint64_t chunksize, uint64_t rec_size)
+{
+	if (rec_size == 0 || chunksize == 0)
+		return 0;
+	if (rec_size > chunksize)
+		return rec_size;
+	return chunksize / rec_size * rec_size;
+}
+
+uint32_t ecg_csum_chunk_count(uint64_t chunksize, uint64_t rec_size, uint64_t rx_idx,
+			      uint64_t rx_nr)
+{
+	const uint64_t rcs = ecg_csum_record_chunksize(chunksize, rec_size);
+	uint64_t per, lo, hi_end;
+
+	if (rcs == 0 || rx_nr == 0)
+		return 0;
+	if (rx_nr == 1)
+		return 1;
+	per = rcs / rec_size;
+	lo = rx_idx / per;
+	hi_end = (rx_idx + (rx_nr - 1)) / per;
+	return (uint32_t)(hi_end - lo + 1);
+}
+
+/* CRC register after one zero byte: c * x^8 mod P */
+static uint64_t zero_byte(const struct crc_def *d, uint64_t c)
+{
+	const uint64_t mask = d->width == 64 ? ~0ull : (1ull << d->width) - 1;
+
+	for (int b = 0; b < 8; b++) {
+		if (d->refl)
+			c = (c & 1) ? (c >> 1) ^ d->poly : c >> 1;
+		else
+			c = ((c >> (d->width - 1)) & 1) ? ((c << 1) & mask) ^ d->poly : (c << 1) & mask;
+	}
+	return c;
+}
+
+/* Device table image (layout in ecg_kabi.h): sl[NB][256], sh[NB][256], k[64],
+ * entries of 4 (W <= 32) or 8 (W = 64) bytes. */
+static void *build_crc_tables(const struct crc_def *d, size_t *bytes)
+{
+	const int nb = d->width / 8, es = d->width == 64 ? 8 : 4;
+	const size_t n = (size_t)nb * 256 * 2 + 64;
+	uint64_t *t = calloc(n, sizeof(uint64_t));
+	uint64_t basis[64];
+	unsigned char *img;
+
+	if (t == NULL)
+		return NULL;
+	/* sl[j][v]: register after byte v (from zero) and then j zero bytes */
+	for (int v = 0; v < 256; v++) {
+		uint64_t c = d->refl ? (uint64_t)v : (uint64_t)v << (d->width - 8);
+
+		c = zero_byte(d, c);
+		for (int j = 0; j < nb; j++) {
+			t[(size_t)j * 256 + v] = c;
+			c = zero_byte(d, c);
+		}
+	}
+	/* sh: register bit i moved through ECG_CSUM_STRIDE zero bytes */
+	for (int i = 0; i < d->width; i++) {
+		uint64_t c = 1ull << i;
+
+		for (int z = 0; z < ECG_CSUM_STRIDE; z++)
+			c = zero_byte(d, c);
+		basis[i] = c;
+	}
+	for (int j = 0; j < nb; j++)
+		for (int v = 0; v < 256; v++) {
+			uint64_t c = 0;
+
+			for (int b = 0; b < 8; b++)
+				if (v & (1 << b))
+					c ^= basis[8 * j + b];
+			t[(size_t)nb * 256 + (size_t)j * 256 + v] = c;
+		}
+	/* k[lane] = x^(8*16*(63-lane)) mod P, i.e. "1" through that many zero bytes */
+	for (int l = 0; l < 64; l++) {
+		uint64_t c = d->refl ? 1ull << (d->width - 1) : 1;
+
+		for (int z = 0; z < 16 * (63 - l); z++)
+			c = zero_byte(d, c);
+		t[(size_t)nb * 512 + l] = c;
+	}
+	*bytes = n * (size_t)es;
+	if (es == 8)
+		return t;
+	img = malloc(*bytes);
+	if (img)
+		for (size_t i = 0; i < n; i++) {
+			uint32_t w = (uint32_t)t[i];
+
+			memcpy(img + 4 * i, &w, 4);
+		}
+	free(t);
+	return img;
+}
+
+/* Device copy of a type's tables, built once per context (ctx->lock). */
+static int crc_tables(ecg_ctx_t *ctx, int type, const void **out)
+{
+	int rc = 0;
+
+	pthread_mutex_lock(&ctx->lock);
+	if (ctx->csum_tbl[type] == NULL) {
+		size_t bytes = 0;
+		void *img = build_crc_tables(&g_defs[type], &bytes), *dev = NULL;
+		hipError_t e;
+
+		if (img == NULL) {
+			rc = ecg_fail(-ECG_DER_NOMEM, "csum tables");
+		} else {
+			e = hipMalloc(&dev, bytes);
+			if (e == hipSuccess)
+				e = hipMemcpy(dev, img, bytes, hipMemcpyHostToDevice);
+			if (e != hipSuccess) {
+				if (dev)
+					(void)hipFree(dev);
+				rc = ecg_hip_fail(e, "csum tables");
+			} else {
+				ctx->csum_tbl[type] = dev;
+			}
+			free(img);
+		}
+	}
+	*out = ctx->csum_tbl[type];
+	pthread_mutex_unlock(&ctx->lock);
+	return rc;
+}
+
+void ecg_csum_ctx_fini(ecg_ctx_t *ctx)
+{
+	for (int i = 0; i < ECG_NCSUM_TBL; i++)
+		if (ctx->csum_tbl[i]) {
+			(void)hipFree(ctx->csum_tbl[i]);
+			ctx->csum_tbl[i] = NULL;
+		}
+}
+
+int ecg_csum_extents(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_size,
+		     uint64_t rx_idx, uint64_t rx_nr, const void *buf, int64_t ext_stride,
+		     uint32_t n_ext, void *csums, void *stream)
+{
+	ecg_csum_params_t prm;
+	const uint64_t rcs = ecg_csum_record_chunksize(chunksize, rec_size);
+	uint64_t per, first_end;
+	uint32_t kid = 0;
+	int rc, e;
+
+	if (ctx == NULL || (n_ext && rx_nr && (buf == NULL || csums == NULL)) || rcs == 0)
+		return ecg_fail(-ECG_DER_INVAL, "csum_extents: bad arguments");
+	if (ecg_csum_len(type) < 0)
+		return ecg_fail(-ECG_DER_NOTSUPPORTED, "csum_extents: hash type %d not supported",
+				type);
+	if (rx_nr > UINT64_MAX / rec_size || (rx_nr && rx_nr - 1 > UINT64_MAX - rx_idx))
+		return ecg_fail(-ECG_DER_INVAL, "csum_extents: extent overflows");
+	if (n_ext == 0 || rx_nr == 0)
+		return 0;
+	rc = ecg_ctx_enter(ctx);
+	if (rc)
+		return rc;
+	memset(&prm, 0, sizeof(prm));
+	if (type != ECG_HASH_ADLER32) {
+		rc = crc_tables(ctx, type, &prm.tbl);
+		if (rc)
+			return rc;
+		prm.poly = g_defs[type].poly;
+		prm.init = g_defs[type].init;
+		prm.xorout = g_defs[type].xorout;
+	}
+	/* chunk 0 runs from rx_idx to the end of its aligned chunk (clipped);
+	 * the rest are whole chunks, the last one clipped
+	 * (csum_recx_chunkidx2range, ref:src/common/checksum.c:1489-1565) */
+	per = rcs / rec_size;
+	first_end = rx_idx - rx_idx % per + (per - 1);
+	if (first_end < rx_idx)		/* csum_chunk_align_ceiling overflow guard */
+		first_end = UINT64_MAX;
+	if (first_end > rx_idx + (rx_nr - 1))
+		first_end = rx_idx + (rx_nr - 1);
+	prm.src = buf;
+	prm.out = csums;
+	prm.ext_stride = ext_stride;
+	prm.ext_bytes = rx_nr * rec_size;
+	prm.first_bytes = (first_end - rx_idx + 1) * rec_size;
+	prm.chunk_bytes = rcs;
+	prm.n_ext = n_ext;
+	prm.nchunks = ecg_csum_chunk_count(chunksize, rec_size, rx_idx, rx_nr);
+	prm.type = (uint32_t)type;
+	e = ecg_k_launch_csum(&prm, (void *)ecg_pick_stream(ctx, stream), ctx->csum_blocks, &kid);
+	if (e != 0)
+		return ecg_hip_fail((hipError_t)e, "csum kernel launch");
+	ecg_set_last_kernel(ecg_k_kernel_name(kid));
+	return 0;
+}

@@ -41,6 +41,9 @@ struct ecg_ctx {
 	struct ecg_rcache_ent rcache[ECG_RCACHE];
 	uint64_t rstamp;
 	struct ecg_stage stage;
+#define ECG_NCSUM_TBL 4
+	void *csum_tbl[ECG_NCSUM_TBL];	/* device CRC tables by hash type (ecg_csum.c) */
+	uint32_t csum_blocks;		/* csum grid cap, 0 = kernel default */
 };
 
 /* errors (thread-local detail string) */
@@ -56,6 +59,9 @@ void ecg_build_ptbl(unsigned char c, ecg_ptbl_t *t);
 int ecg_recov_rows(int k, int p, const unsigned char *en_matrix,
 		   const uint32_t *err_list, int nerrs, unsigned char *rows,
 		   uint32_t *out_idx, uint32_t *dec_idx, int *reused_encode);
+
+/* checksums (ecg_csum.c) */
+void ecg_csum_ctx_fini(ecg_ctx_t *ctx);
 
 /* context helpers (ecg_core.c) */
 int ecg_ctx_enter(ecg_ctx_t *ctx);

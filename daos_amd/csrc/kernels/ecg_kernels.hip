@@ -387,7 +387,8 @@ extern "C" const char *ecg_k_kernel_name(uint32_t id)
 		return "ecg_stream_kernel<read>";
 	if (id == KID_WRITE)
 		return "ecg_stream_kernel<write>";
-
+	if (id >= ECG_KID_CSUM)
+		return ecg_k_csum_kernel_name(id);
 
 	return "?";
 }

@@ -102,7 +102,15 @@ _SIGS = [
     ("ecg_agg_recalc_parity", C.c_int, [vp, C.c_uint32, C.c_uint64, u8p, C.c_uint32, u8p, u8p, u8p]),
     ("ecg_obj_ec_singv_cell_bytes", C.c_uint64, [C.c_uint32, C.c_uint64]),
     ("ecg_obj_ec_singv_encode", C.c_int, [C.c_uint32, C.c_uint64, u8p, C.POINTER(u8p)]),
+    # chunked checksums (ecg_csum.h)
+    ("ecg_csum_len", C.c_int, [C.c_int]),
+    ("ecg_csum_record_chunksize", C.c_uint64, [C.c_uint64, C.c_uint64]),
+    ("ecg_csum_chunk_count", C.c_uint32, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64]),
+    ("ecg_csum_extents", C.c_int, [vp, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, vp, C.c_int64,
+                                   C.c_uint32, vp, vp]),
 ]
+
+HASH_CRC16, HASH_CRC32, HASH_CRC64, HASH_ADLER32 = 1, 2, 3, 7
 
 EXPORTED = [n for n, _, _ in _SIGS]
 
@@ -323,6 +331,12 @@ class Context:
         _chk(lib().ecg_update(self.h, k, p, cell_bytes, nstripes, len(cell_idx), _u32(cell_idx), old, new,
                               upd_stripe_stride, parity, parity_cell_stride, parity_stripe_stride, stream),
              "update")
+
+    def csum_extents(self, htype: int, chunksize: int, rec_size: int, rx_idx: int, rx_nr: int, buf: int,
+                     ext_stride: int, n_ext: int, csums: int, stream=None):
+        """Device checksums of n_ext extents (include/ecg_csum.h): csums[n_ext][nchunks]."""
+        _chk(lib().ecg_csum_extents(self.h, htype, chunksize, rec_size, rx_idx, rx_nr, buf, ext_stride, n_ext,
+                                    csums, stream), "csum_extents")
 
     def encode_host(self, k: int, p: int, cell_bytes: int, nstripes: int, data: np.ndarray, parity: np.ndarray,
                     chunk: int = 0):

@@ -137,6 +137,25 @@ void ref_simd_recov_batch(int k, int nerrs, const unsigned char *gftbls,
                           uint64_t C, uint64_t stripe_stride, uint32_t S,
                           unsigned char *stripes, int nthreads);
 
+/* ---- chunked checksums (oracle/csum_ref.c) ---- */
+#define REF_HASH_CRC16   1
+#define REF_HASH_CRC32   2
+#define REF_HASH_CRC64   3
+#define REF_HASH_ADLER32 7
+uint16_t ref_crc16_t10dif(uint16_t seed, const unsigned char *buf, uint64_t len);
+uint32_t ref_crc32_iscsi(const unsigned char *buf, uint64_t len, uint32_t seed);
+uint64_t ref_crc64_ecma_refl(uint64_t seed, const unsigned char *buf, uint64_t len);
+uint32_t ref_adler32(uint32_t seed, const unsigned char *buf, uint64_t len);
+int ref_csum_len(int type);
+uint64_t ref_csum_record_chunksize(uint64_t chunksize, uint64_t rec_size);
+uint32_t ref_csum_chunk_count(uint64_t rec_chunksize, uint64_t rec_size, uint64_t rx_idx,
+			      uint64_t rx_nr);
+uint32_t ref_csum_extent(int type, uint64_t chunksize, uint64_t rec_size, uint64_t rx_idx,
+			 uint64_t rx_nr, const unsigned char *buf, unsigned char *out);
+void ref_csum_extents(int type, uint64_t chunksize, uint64_t rec_size, uint64_t rx_idx,
+		      uint64_t rx_nr, const unsigned char *buf, int64_t ext_stride, uint32_t n_ext,
+		      unsigned char *out, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

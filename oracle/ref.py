@@ -59,6 +59,22 @@ def lib():
         L.ref_agg_update_parity.argtypes = [C.c_int, C.c_int, C.c_uint64, C.c_uint64, u8p, C.c_uint, u8p, u8p,
                                             u64p, u64p, C.c_uint, u8p]
         L.ref_agg_update_parity.restype = C.c_int
+        L.ref_crc16_t10dif.restype = C.c_uint16
+        L.ref_crc16_t10dif.argtypes = [C.c_uint16, u8p, C.c_uint64]
+        L.ref_crc32_iscsi.restype = C.c_uint32
+        L.ref_crc32_iscsi.argtypes = [u8p, C.c_uint64, C.c_uint32]
+        L.ref_crc64_ecma_refl.restype = C.c_uint64
+        L.ref_crc64_ecma_refl.argtypes = [C.c_uint64, u8p, C.c_uint64]
+        L.ref_adler32.restype = C.c_uint32
+        L.ref_adler32.argtypes = [C.c_uint32, u8p, C.c_uint64]
+        L.ref_csum_record_chunksize.restype = C.c_uint64
+        L.ref_csum_record_chunksize.argtypes = [C.c_uint64, C.c_uint64]
+        L.ref_csum_chunk_count.restype = C.c_uint32
+        L.ref_csum_chunk_count.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64]
+        L.ref_csum_extent.restype = C.c_uint32
+        L.ref_csum_extent.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, u8p, u8p]
+        L.ref_csum_extents.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, u8p, C.c_int64,
+                                       C.c_uint32, u8p, C.c_int]
         L.ref_singv_cell_bytes.argtypes = [C.c_uint64, C.c_int]
         L.ref_singv_cell_bytes.restype = C.c_uint64
         L.ref_singv_encode.argtypes = [C.c_int, C.c_int, C.c_uint64, u8p, C.POINTER(u8p)]
@@ -201,3 +217,49 @@ def singv_encode(k: int, p: int, value: np.ndarray) -> np.ndarray:
     v = np.ascontiguousarray(value, dtype=np.uint8)
     lib().ref_singv_encode(k, p, v.size, _p(v), _ptr_array([out[r] for r in range(p)]))
     return out
+
+
+# ---- chunked checksums (oracle/csum_ref.c) ----
+HASH_CRC16, HASH_CRC32, HASH_CRC64, HASH_ADLER32 = 1, 2, 3, 7
+CSUM_LEN = {HASH_CRC16: 2, HASH_CRC32: 4, HASH_CRC64: 8, HASH_ADLER32: 4}
+_CSUM_DT = {2: np.uint16, 4: np.uint32, 8: np.uint64}
+
+
+def crc16_t10dif(seed: int, data) -> int:
+    b = np.frombuffer(bytes(data), dtype=np.uint8).copy()
+    return lib().ref_crc16_t10dif(seed, _p(b), b.size)
+
+
+def crc32_iscsi(data, seed: int) -> int:
+    b = np.frombuffer(bytes(data), dtype=np.uint8).copy()
+    return lib().ref_crc32_iscsi(_p(b), b.size, seed)
+
+
+def crc64_ecma_refl(seed: int, data) -> int:
+    b = np.frombuffer(bytes(data), dtype=np.uint8).copy()
+    return lib().ref_crc64_ecma_refl(seed, _p(b), b.size)
+
+
+def adler32(seed: int, data) -> int:
+    b = np.frombuffer(bytes(data), dtype=np.uint8).copy()
+    return lib().ref_adler32(seed, _p(b), b.size)
+
+
+def csum_record_chunksize(chunksize: int, rec_size: int) -> int:
+    return lib().ref_csum_record_chunksize(chunksize, rec_size)
+
+
+def csum_chunk_count(chunksize: int, rec_size: int, rx_idx: int, rx_nr: int) -> int:
+    return lib().ref_csum_chunk_count(csum_record_chunksize(chunksize, rec_size), rec_size, rx_idx, rx_nr)
+
+
+def csum_extents(htype: int, chunksize: int, rec_size: int, rx_idx: int, rx_nr: int, buf: np.ndarray,
+                 ext_stride: int = 0, n_ext: int = 1, nthreads: int = 8) -> np.ndarray:
+    """Checksums [n_ext][nchunks] (uint16/32/64) of n_ext extents at buf + e*ext_stride."""
+    n = csum_chunk_count(chunksize, rec_size, rx_idx, rx_nr)
+    cl = CSUM_LEN[htype]
+    out = np.zeros(max(1, n_ext * n * cl), dtype=np.uint8)
+    b = np.ascontiguousarray(buf, dtype=np.uint8).reshape(-1)
+    lib().ref_csum_extents(htype, chunksize, rec_size, rx_idx, rx_nr, _p(b), ext_stride, n_ext, _p(out),
+                           nthreads)
+    return out[:n_ext * n * cl].view(_CSUM_DT[cl]).reshape(n_ext, n)

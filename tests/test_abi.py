@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
-HEADERS = ["include/ecg.h", "include/ecg_isal.h", "include/ecg_daos.h"]
+HEADERS = ["include/ecg.h", "include/ecg_isal.h", "include/ecg_daos.h", "include/ecg_csum.h"]
 
 
 def declared_functions():

@@ -1,0 +1,135 @@
+"""GPU parity of the chunked checksums (include/ecg_csum.h) against the CPU
+oracle (oracle/csum_ref.c, pinned in tests/test_csum_oracle.py).
+
+Bit-exact: every checksum of every chunk must equal the oracle's.  Covers the
+DAOS hash types (crc16 / crc32 / crc64 / adler32), the csummer's chunk
+geometry (unaligned record index, records larger than the chunk, partial first
+and last chunks, single record), the 16-byte-aligned and byte-granular kernel
+paths, batched extents, and the rebuild pattern it exists for: parity cells
+regenerated on the device, then checksummed without leaving HBM
+(ref:src/object/srv_obj_migrate.c:1096-1181).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TYPES = (1, 2, 3, 7)
+DT = {2: np.uint16, 4: np.uint32, 8: np.uint64}
+
+
+def _dev_csum(ecglib, ctx, htype, cs, rb, idx, nr, host, ext_stride=0, n_ext=1, offset=0):
+    """Upload host bytes at device offset `offset`, checksum on the device, return [n_ext][n]."""
+    L = ecglib.lib()
+    n = L.ecg_csum_chunk_count(cs, rb, idx, nr)
+    cl = L.ecg_csum_len(htype)
+    buf = ecglib.DeviceBuffer(ctx, offset + max(1, host.nbytes))
+    out = ecglib.DeviceBuffer(ctx, max(8, n_ext * n * cl))
+    try:
+        buf.upload(host, offset=offset)
+        out.fill(0xA5)
+        ctx.csum_extents(htype, cs, rb, idx, nr, buf.ptr + offset, ext_stride, n_ext, out.ptr)
+        ctx.sync()
+        assert "crc" in L.ecg_last_kernel().decode() or "adler" in L.ecg_last_kernel().decode()
+        return out.download(n_ext * n * cl).view(DT[cl]).reshape(n_ext, n)
+    finally:
+        buf.free()
+        out.free()
+
+
+GEOMS = [
+    # (chunksize, rec_size, rx_idx, rx_nr)
+    (32768, 1, 0, 1 << 20),            # DAOS default chunk over a 1 MiB cell
+    (16384, 1, 0, 5 << 16),            # ftest cksum_size 16 KiB
+    (32768, 1, 100, 200000),           # unaligned index: partial first + last chunk
+    (4096, 8, 3, 10000),               # 8-byte records
+    (32768, 6, 7, 30001),              # record size not dividing the chunk (rec chunk 32766)
+    (4096, 65536, 5, 9),               # records larger than the chunk: one chunk per record
+    (1024, 1, 0, 1),                   # single record
+    (64, 1, 0, 1000),                  # tiny chunks (4 pieces) + tails
+    (1 << 20, 1, 0, (1 << 20) + 15),   # one big chunk + 15-byte tail chunk
+    (24, 1, 0, 1000),                  # chunk not a multiple of 16: byte path
+]
+
+
+@pytest.mark.parametrize("htype", TYPES)
+@pytest.mark.parametrize("geom", GEOMS)
+def test_csum_parity(oracle, ecglib, ctx, htype, geom):
+    cs, rb, idx, nr = geom
+    rng = np.random.default_rng(hash((htype,) + geom) & 0xFFFFFFFF)
+    host = rng.integers(0, 256, rb * nr, dtype=np.uint8)
+    got = _dev_csum(ecglib, ctx, htype, cs, rb, idx, nr, host)
+    want = oracle.csum_extents(htype, cs, rb, idx, nr, host)
+    assert got.shape == want.shape
+    assert np.array_equal(got, want), np.argwhere(got != want)[:5]
+
+
+@pytest.mark.parametrize("htype", TYPES)
+@pytest.mark.parametrize("offset", [1, 3, 8, 15])
+def test_csum_unaligned_base(oracle, ecglib, ctx, htype, offset):
+    """Extents starting off a 16-byte boundary take the byte-granular kernel."""
+    rng = np.random.default_rng(offset)
+    host = rng.integers(0, 256, 100000, dtype=np.uint8)
+    got = _dev_csum(ecglib, ctx, htype, 4096, 1, 0, host.size, host, offset=offset)
+    assert "bytes" in ecglib.lib().ecg_last_kernel().decode()
+    assert np.array_equal(got, oracle.csum_extents(htype, 4096, 1, 0, host.size, host))
+
+
+@pytest.mark.parametrize("htype", TYPES)
+def test_csum_batched_extents(oracle, ecglib, ctx, htype):
+    """64 cells of 256 KiB + 4 KiB pitch, one launch."""
+    C, pitch, n = 256 << 10, (256 << 10) + 4096, 64
+    rng = np.random.default_rng(htype + 100)
+    host = rng.integers(0, 256, pitch * n, dtype=np.uint8)
+    got = _dev_csum(ecglib, ctx, htype, 32768, 1, 0, C, host, ext_stride=pitch, n_ext=n)
+    want = oracle.csum_extents(htype, 32768, 1, 0, C, host, ext_stride=pitch, n_ext=n)
+    assert np.array_equal(got, want)
+
+
+def test_csum_special_data(oracle, ecglib, ctx):
+    """All-zero and all-0xFF chunks (crc64's inverted register must still fold in)."""
+    for fill in (0x00, 0xFF):
+        host = np.full(300000, fill, dtype=np.uint8)
+        for htype in TYPES:
+            got = _dev_csum(ecglib, ctx, htype, 32768, 1, 0, host.size, host)
+            assert np.array_equal(got, oracle.csum_extents(htype, 32768, 1, 0, host.size, host)), (fill, htype)
+
+
+def test_csum_errors(ecglib, ctx):
+    L = ecglib.lib()
+    buf = ecglib.DeviceBuffer(ctx, 4096)
+    try:
+        assert L.ecg_csum_extents(ctx.h, 5, 4096, 1, 0, 4096, buf.ptr, 0, 1, buf.ptr, None) == -2037
+        assert L.ecg_csum_extents(ctx.h, 2, 0, 1, 0, 4096, buf.ptr, 0, 1, buf.ptr, None) == -1003
+        assert L.ecg_csum_extents(ctx.h, 2, 4096, 0, 0, 4096, buf.ptr, 0, 1, buf.ptr, None) == -1003
+        assert L.ecg_csum_extents(ctx.h, 2, 4096, 1, 0, 0, buf.ptr, 0, 1, buf.ptr, None) == 0
+    finally:
+        buf.free()
+
+
+@pytest.mark.parametrize("htype", (1, 2, 3))
+def test_rebuild_parity_then_csum(oracle, ecglib, ctx, htype):
+    """Rebuild pattern: encode EC_8P2 parity on the device, checksum the
+    regenerated parity cells in place (32 KiB chunks), compare with the oracle
+    encode + oracle checksums."""
+    k, p, C, S = 8, 2, 1 << 20, 16
+    rng = np.random.default_rng(7)
+    data = rng.integers(0, 256, S * k * C, dtype=np.uint8)
+    d = ecglib.DeviceBuffer(ctx, data.nbytes)
+    par = ecglib.DeviceBuffer(ctx, p * S * C)
+    cl = ecglib.lib().ecg_csum_len(htype)
+    out = ecglib.DeviceBuffer(ctx, p * S * (C // 32768) * cl)
+    try:
+        d.upload(data)
+        ctx.encode(k, p, C, S, d.ptr, k * C, par.ptr, S * C, C)
+        # parity cells are [p][S][C]: p*S extents of C bytes at pitch C
+        ctx.csum_extents(htype, 32768, 1, 0, C, par.ptr, C, p * S, out.ptr)
+        ctx.sync()
+        got = out.download().view(DT[cl]).reshape(p * S, -1)
+        want_par = oracle.encode_batch(k, p, C, S, data, nthreads=8, simd=True)
+        want = oracle.csum_extents(htype, 32768, 1, 0, C, want_par, ext_stride=C, n_ext=p * S)
+        assert np.array_equal(got, want)
+    finally:
+        d.free()
+        par.free()
+        out.free()
