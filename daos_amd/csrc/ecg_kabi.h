@@ -75,10 +75,19 @@ typedef struct ecg_launch_cfg {
  *   sl[NB][256]  slice tables: sl[j][v] = CRC state after byte v then j zero bytes
  *   sh[NB][256]  "shift by ECG_CSUM_STRIDE zero bytes" as a byte-wise linear map
  *   k[64]        x^(8*16*(63-lane)) mod P, for the final per-lane shift
+ *   sh4k[NB][256] shift by ECG_MMCS_STRIDE zero bytes (fused kernels)
+ *   k256[256]    x^(8*16*(255-thread)) mod P (fused kernels)
  * with NB = W/8, T = uint32_t (W <= 32) or uint64_t (W = 64).
  */
 #define ECG_CSUM_STRIDE 1024	/* bytes a wave consumes per step (64 lanes x 16 B) */
 #define ECG_KID_CSUM 1000	/* kernel ids of the checksum kernels start here */
+
+#define ECG_MMCS_STRIDE 4096	/* fused kernels: 256 threads x 16 B per step */
+#define ECG_CSUM_TBL_ENTRIES(NB) (3 * (NB) * 256 + 64 + 256)
+#define ECG_CSUM_OFF_SH(NB) ((NB) * 256)
+#define ECG_CSUM_OFF_K64(NB) (2 * (NB) * 256)
+#define ECG_CSUM_OFF_SH4K(NB) (2 * (NB) * 256 + 64)
+#define ECG_CSUM_OFF_K256(NB) (3 * (NB) * 256 + 64)
 
 typedef struct ecg_csum_params {
 	const uint8_t *src;
@@ -97,6 +106,26 @@ typedef struct ecg_csum_params {
 	uint32_t pad;
 } ecg_csum_params_t;
 
+/*
+ * Fused product + checksum: a launch of the GF product (ecg_mm_params_t)
+ * that also checksums every output cell it writes, chunk by chunk, while the
+ * bytes are still in registers.  Each output cell starts on a chunk boundary;
+ * chunk_bytes is a multiple of ECG_MMCS_STRIDE; cell_bytes a multiple of 16.
+ * out[(row_slot[r] * nstripes + s) * nch + c] = checksum of chunk c of output
+ * row r of stripe s.  tail_fix = x^(-8Z) mod P undoes the Z zero bytes that
+ * pad the last chunk of a cell to a whole number of 4 KiB steps.
+ */
+typedef struct ecg_mmcs_params {
+	const void *tbl;
+	uint8_t *out;
+	uint64_t chunk_bytes;
+	uint64_t init, xorout, poly;
+	uint64_t tail_fix;
+	uint32_t nch;
+	uint32_t type;
+	uint32_t row_slot[ECG_KMAX_R];
+} ecg_mmcs_params_t;
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -107,6 +136,10 @@ int ecg_k_launch_matmul(const ecg_mm_params_t *p, const ecg_launch_cfg_t *cfg,
  * mode 0 copy, 1 read-only, 2 write-only. */
 int ecg_k_launch_copy(const void *src, void *dst, uint64_t bytes, int mode, void *stream,
 		      uint32_t max_blocks, uint32_t *kernel_id);
+/* Fused product + checksum (kernels/ecg_kernels.hip).  Returns 1 (and
+ * launches nothing) when the operands are not 16-byte aligned. */
+int ecg_k_launch_matmul_csum(const ecg_mm_params_t *p, const ecg_mmcs_params_t *q,
+			     const ecg_launch_cfg_t *cfg, void *stream, uint32_t *kernel_id);
 /* Chunked checksums (kernels/ecg_csum_kernels.hip). max_blocks 0 = default. */
 int ecg_k_launch_csum(const ecg_csum_params_t *p, void *stream, uint32_t max_blocks,
 		      uint32_t *kernel_id);

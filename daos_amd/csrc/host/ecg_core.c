@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include "ecg_internal.h"
+#include "../../../include/ecg_csum.h"
 
 static __thread char t_err[512];
 static __thread const char *t_last_kernel = "";
@@ -385,6 +386,151 @@ int ecg_recover(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 	if (rc)
 		return rc;
 	return recover_with(ctx, &ent, C, S, stripes, stripe_stride, stream);
+}
+
+/*
+ * Product + chunked checksums of every output cell (include/ecg_csum.h).  One
+ * fused launch when the shape allows (CRC types, k <= 16, rows <= 8, 16-byte
+ * aligned cells, record chunk a multiple of 4 KiB); otherwise the product
+ * followed by one ecg_csum_extents launch per output row -- both on the
+ * device, the fused path only saves the re-read of the outputs.
+ * csums[row_slot[r]][s][chunk].
+ */
+static int matmul_csum(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, uint64_t C,
+		       uint32_t S, const void *src, const int64_t *soff, int64_t sstride, void *dst,
+		       const int64_t *doff, int64_t dstride, int type, uint64_t chunksize,
+		       uint64_t rec_size, void *csums, const uint32_t *row_slot, void *stream)
+{
+	const int cl = ecg_csum_len(type);
+	ecg_mmcs_params_t q;
+	hipStream_t st;
+	uint32_t nch;
+	int fused = 0, rc, r;
+
+	if (cl < 0)
+		return ecg_fail(-ECG_DER_NOTSUPPORTED, "csum: hash type %d not supported", type);
+	if (csums == NULL || rec_size == 0 || chunksize == 0 || C % rec_size)
+		return ecg_fail(-ECG_DER_INVAL, "csum: bad chunk/record size or NULL csums");
+	if (C == 0 || S == 0)
+		return 0;
+	rc = ecg_ctx_enter(ctx);
+	if (rc)
+		return rc;
+	ecg_gf_init();
+	st = ecg_pick_stream(ctx, stream);
+	if (k <= ECG_KMAX_K && rows <= ECG_KMAX_R) {
+		fused = ecg_csum_fused_params(ctx, type, chunksize, rec_size, C, csums, &q);
+		if (fused < 0)
+			return fused;
+	}
+	if (fused) {
+		ecg_mm_params_t *prm = calloc(1, sizeof(*prm));
+		uint32_t kid = 0;
+		int e, j;
+
+		if (prm == NULL)
+			return ecg_fail(-ECG_DER_NOMEM, "matmul_csum: calloc");
+		prm->src = src;
+		prm->dst = dst;
+		prm->src_stripe_stride = sstride;
+		prm->dst_stripe_stride = dstride;
+		prm->cell_bytes = C;
+		prm->nstripes = S;
+		prm->k = (uint32_t)k;
+		prm->rows = (uint32_t)rows;
+		for (j = 0; j < k; j++)
+			prm->src_cell_off[j] = soff[j];
+		for (r = 0; r < rows; r++) {
+			prm->dst_cell_off[r] = doff[r];
+			q.row_slot[r] = row_slot[r];
+			for (j = 0; j < k; j++)
+				ecg_build_ptbl(coef[(size_t)r * k + j], &prm->tbl[r][j]);
+		}
+		e = ecg_k_launch_matmul_csum(prm, &q, &ctx->cfg, (void *)st, &kid);
+		free(prm);
+		if (e == 0) {
+			ecg_set_last_kernel(ecg_k_kernel_name(kid));
+			return 0;
+		}
+		if (e != 1)
+			return ecg_hip_fail((hipError_t)e, "fused kernel launch");
+		/* e == 1: operands not 16-byte aligned -> two-pass path */
+	}
+	rc = matmul2(ctx, k, rows, coef, C, S, src, soff, sstride, NULL, NULL, 0, dst, doff, dstride,
+		     0, (void *)st);
+	if (rc)
+		return rc;
+	nch = ecg_csum_chunk_count(chunksize, rec_size, 0, C / rec_size);
+	for (r = 0; r < rows; r++) {
+		rc = ecg_csum_extents(ctx, type, chunksize, rec_size, 0, C / rec_size,
+				      (const uint8_t *)dst + doff[r], dstride, S,
+				      (uint8_t *)csums + (uint64_t)row_slot[r] * S * nch * (uint64_t)cl,
+				      (void *)st);
+		if (rc)
+			return rc;
+	}
+	return 0;
+}
+
+int ecg_encode_csum(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S, const void *data,
+		    int64_t data_stripe_stride, void *parity, int64_t parity_cell_stride,
+		    int64_t parity_stripe_stride, int type, uint64_t chunksize, uint64_t rec_size,
+		    void *csums, void *stream)
+{
+	unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
+	int64_t soff[ECG_MAX_K], doff[ECG_MAX_P];
+	uint32_t slot[ECG_MAX_P];
+	int i, rc;
+
+	rc = check_kp(k, p);
+	if (rc)
+		return rc;
+	if (data == NULL || parity == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "encode_csum: NULL buffer");
+	ecg_gen_cauchy1(k, p, en);
+	for (i = 0; i < k; i++)
+		soff[i] = (int64_t)i * (int64_t)C;
+	for (i = 0; i < p; i++) {
+		doff[i] = (int64_t)i * parity_cell_stride;
+		slot[i] = (uint32_t)i;
+	}
+	return matmul_csum(ctx, k, p, &en[k * k], C, S, data, soff, data_stripe_stride, parity, doff,
+			   parity_stripe_stride, type, chunksize, rec_size, csums, slot, stream);
+}
+
+int ecg_recover_csum(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S, void *stripes,
+		     int64_t stripe_stride, const uint32_t *err_list, int nerrs, int type,
+		     uint64_t chunksize, uint64_t rec_size, void *csums, void *stream)
+{
+	struct ecg_rcache_ent ent;
+	int64_t soff[ECG_MAX_K], doff[ECG_MAX_P];
+	uint32_t slot[ECG_MAX_P];
+	int i, j, rc;
+
+	rc = check_kp(k, p);
+	if (rc)
+		return rc;
+	if (err_list == NULL || stripes == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "recover_csum: NULL argument");
+	if (nerrs > p)
+		return ecg_fail(-ECG_DER_DATA_LOSS, "recover_csum: %d erasures > p=%d", nerrs, p);
+	if (nerrs <= 0)
+		return 0;
+	rc = recov_lookup(ctx, k, p, err_list, nerrs, &ent);
+	if (rc)
+		return rc;
+	for (i = 0; i < ent.k; i++)
+		soff[i] = (int64_t)ent.dec_idx[i] * (int64_t)C;
+	for (i = 0; i < ent.nerrs; i++) {
+		doff[i] = (int64_t)ent.out_idx[i] * (int64_t)C;
+		slot[i] = 0;
+		for (j = 0; j < nerrs; j++)	/* checksum rows in err_list order */
+			if (err_list[j] == ent.out_idx[i])
+				slot[i] = (uint32_t)j;
+	}
+	return matmul_csum(ctx, ent.k, ent.nerrs, ent.rows, C, S, stripes, soff, stripe_stride,
+			   stripes, doff, stripe_stride, type, chunksize, rec_size, csums, slot,
+			   stream);
 }
 
 int ecg_update(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,

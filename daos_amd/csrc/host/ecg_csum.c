@@ -78,15 +78,81 @@ static uint64_t zero_byte(const struct crc_def *d, uint64_t c)
 	return c;
 }
 
-/* Device table image (layout in ecg_kabi.h): sl[NB][256], sh[NB][256], k[64],
- * entries of 4 (W <= 32) or 8 (W = 64) bytes. */
+/* "1" in the register representation */
+static uint64_t crc_one(const struct crc_def *d)
+{
+	return d->refl ? 1ull << (d->width - 1) : 1;
+}
+
+/* a * b mod P (same representations as the device mulmod) */
+static uint64_t crc_mulmod(const struct crc_def *d, uint64_t a, uint64_t b)
+{
+	const uint64_t mask = d->width == 64 ? ~0ull : (1ull << d->width) - 1;
+	uint64_t p = 0;
+
+	for (int i = d->width - 1; i >= 0; i--) {
+		if (d->refl) {
+			if ((a >> i) & 1)
+				p ^= b;
+			b = (b & 1) ? (b >> 1) ^ d->poly : b >> 1;
+		} else {
+			p = ((p >> (d->width - 1)) & 1) ? ((p << 1) & mask) ^ d->poly : (p << 1) & mask;
+			if ((a >> i) & 1)
+				p ^= b;
+		}
+	}
+	return p;
+}
+
+/* x^(-8z) mod P: x^-1 = (P - 1) / x since P(0) = 1 */
+static uint64_t crc_unshift(const struct crc_def *d, uint64_t z)
+{
+	const uint64_t mask = d->width == 64 ? ~0ull : (1ull << d->width) - 1;
+	const uint64_t xinv = d->refl ? (((d->poly << 1) & mask) | 1)
+				      : ((1ull << (d->width - 1)) | (d->poly >> 1));
+	uint64_t r = crc_one(d), b = xinv;
+
+	for (uint64_t e = 8 * z; e; e >>= 1) {	/* square and multiply */
+		if (e & 1)
+			r = crc_mulmod(d, r, b);
+		b = crc_mulmod(d, b, b);
+	}
+	return r;
+}
+
+/* linear map "shift by n zero bytes" as NB byte tables at t */
+static void build_shift(const struct crc_def *d, int n, uint64_t *t)
+{
+	const int nb = d->width / 8;
+	uint64_t basis[64];
+
+	for (int i = 0; i < d->width; i++) {
+		uint64_t c = 1ull << i;
+
+		for (int z = 0; z < n; z++)
+			c = zero_byte(d, c);
+		basis[i] = c;
+	}
+	for (int j = 0; j < nb; j++)
+		for (int v = 0; v < 256; v++) {
+			uint64_t c = 0;
+
+			for (int b = 0; b < 8; b++)
+				if (v & (1 << b))
+					c ^= basis[8 * j + b];
+			t[(size_t)j * 256 + v] = c;
+		}
+}
+
+/* Device table image (layout in ecg_kabi.h): sl, sh (1 KiB), k64, sh4k,
+ * k256; entries of 4 (W <= 32) or 8 (W = 64) bytes. */
 static void *build_crc_tables(const struct crc_def *d, size_t *bytes)
 {
 	const int nb = d->width / 8, es = d->width == 64 ? 8 : 4;
-	const size_t n = (size_t)nb * 256 * 2 + 64;
+	const size_t n = ECG_CSUM_TBL_ENTRIES(nb);
 	uint64_t *t = calloc(n, sizeof(uint64_t));
-	uint64_t basis[64];
 	unsigned char *img;
+	uint64_t c;
 
 	if (t == NULL)
 		return NULL;
@@ -100,30 +166,17 @@ static void *build_crc_tables(const struct crc_def *d, size_t *bytes)
 			c = zero_byte(d, c);
 		}
 	}
-	/* sh: register bit i moved through ECG_CSUM_STRIDE zero bytes */
-	for (int i = 0; i < d->width; i++) {
-		uint64_t c = 1ull << i;
-
-		for (int z = 0; z < ECG_CSUM_STRIDE; z++)
+	build_shift(d, ECG_CSUM_STRIDE, t + ECG_CSUM_OFF_SH(nb));
+	build_shift(d, ECG_MMCS_STRIDE, t + ECG_CSUM_OFF_SH4K(nb));
+	/* k64[lane] = x^(8*16*(63-lane)), k256[t] = x^(8*16*(255-t)) mod P:
+	 * "1" moved through that many zero bytes, walking down from the last */
+	c = crc_one(d);
+	for (int l = 255; l >= 0; l--) {
+		if (l >= 192)
+			t[ECG_CSUM_OFF_K64(nb) + (l - 192)] = c;
+		t[ECG_CSUM_OFF_K256(nb) + l] = c;
+		for (int z = 0; z < 16; z++)
 			c = zero_byte(d, c);
-		basis[i] = c;
-	}
-	for (int j = 0; j < nb; j++)
-		for (int v = 0; v < 256; v++) {
-			uint64_t c = 0;
-
-			for (int b = 0; b < 8; b++)
-				if (v & (1 << b))
-					c ^= basis[8 * j + b];
-			t[(size_t)nb * 256 + (size_t)j * 256 + v] = c;
-		}
-	/* k[lane] = x^(8*16*(63-lane)) mod P, i.e. "1" through that many zero bytes */
-	for (int l = 0; l < 64; l++) {
-		uint64_t c = d->refl ? 1ull << (d->width - 1) : 1;
-
-		for (int z = 0; z < 16 * (63 - l); z++)
-			c = zero_byte(d, c);
-		t[(size_t)nb * 512 + l] = c;
 	}
 	*bytes = n * (size_t)es;
 	if (es == 8)
@@ -234,4 +287,46 @@ int ecg_csum_extents(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_
 		return ecg_hip_fail((hipError_t)e, "csum kernel launch");
 	ecg_set_last_kernel(ecg_k_kernel_name(kid));
 	return 0;
+}
+
+int ecg_set_csum_launch(ecg_ctx_t *ctx, uint32_t max_blocks)
+{
+	if (ctx == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "set_csum_launch: NULL context");
+	ctx->csum_blocks = max_blocks;
+	return 0;
+}
+
+/* Fused product + checksum parameters (ecg_kabi.h) for output cells of C
+ * bytes that start on chunk boundaries.  Returns 1 when the fused kernels
+ * can take the request, 0 when the caller must run the product and
+ * ecg_csum_extents separately, < 0 on error. */
+int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_size,
+			  uint64_t C, void *csums, ecg_mmcs_params_t *q)
+{
+	const uint64_t rcs = ecg_csum_record_chunksize(chunksize, rec_size);
+	const struct crc_def *d;
+	uint64_t last, z;
+	int rc;
+
+	memset(q, 0, sizeof(*q));
+	if (type != ECG_HASH_CRC16 && type != ECG_HASH_CRC32 && type != ECG_HASH_CRC64)
+		return 0;
+	if (rcs == 0 || rcs % ECG_MMCS_STRIDE || C % 16 || C % rec_size)
+		return 0;
+	d = &g_defs[type];
+	rc = crc_tables(ctx, type, &q->tbl);
+	if (rc)
+		return rc;
+	q->out = csums;
+	q->chunk_bytes = rcs;
+	q->nch = (uint32_t)((C + rcs - 1) / rcs);
+	q->init = d->init;
+	q->xorout = d->xorout;
+	q->poly = d->poly;
+	q->type = (uint32_t)type;
+	last = C - (uint64_t)(q->nch - 1) * rcs;
+	z = (last + ECG_MMCS_STRIDE - 1) / ECG_MMCS_STRIDE * ECG_MMCS_STRIDE - last;
+	q->tail_fix = crc_unshift(d, z);
+	return 1;
 }

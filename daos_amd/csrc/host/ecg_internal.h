@@ -62,6 +62,8 @@ int ecg_recov_rows(int k, int p, const unsigned char *en_matrix,
 
 /* checksums (ecg_csum.c) */
 void ecg_csum_ctx_fini(ecg_ctx_t *ctx);
+int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_size,
+			  uint64_t C, void *csums, ecg_mmcs_params_t *q);
 
 /* context helpers (ecg_core.c) */
 int ecg_ctx_enter(ecg_ctx_t *ctx);

@@ -25,6 +25,7 @@
 #include <stdint.h>
 
 #include "../ecg_kabi.h"
+#include "ecg_crc_dev.h"
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -66,9 +67,9 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 // The uniform cell offsets are passed through an empty asm per item so LICM
 // cannot hoist k+rows 64-bit pointers out of the stripe loop (they land in
 // VGPRs and spill at EC_8P2/EC_16P2).
-template <int KM, int RM, bool ACC, bool DIFF>
+template <int KM, int RM, bool ACC, bool DIFF, bool KEEP = false>
 __device__ __forceinline__ void mm_item(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
-					uint32_t s, uint64_t cbase, uint32_t lo)
+					uint32_t s, uint64_t cbase, uint32_t lo, u32x4 *keep = nullptr)
 {
 	constexpr int T2V = (RM + 3) / 4;
 	constexpr int PER_J = RM + T2V;
@@ -140,6 +141,8 @@ __device__ __forceinline__ void mm_item(const ecg_mm_params_t &P, const u32x4 *t
 			int64_t o = P.dst_cell_off[r] + s_dst;
 			asm volatile("" : "+s"(o));
 			st_nt(P.dst + o + lo, acc[r]);
+			if (KEEP)
+				keep[r] = acc[r];
 		}
 	}
 }
@@ -241,6 +244,120 @@ ecg_mm_kernel(const ecg_mm_params_t P)
 			} else if (cbase + lo < C) {
 				mm_tail<RM, ACC, DIFF>(P, tb, k, rows, s, cbase + lo, (int)(C - cbase - lo));
 			}
+		}
+	}
+}
+
+// Fused product + checksum of every output cell (ecg_kabi.h, ecg_mmcs_params).
+// Block = one (stripe, checksum chunk) item; it walks the chunk's 4 KiB
+// columns, computing and storing the outputs exactly as ecg_mm_kernel does,
+// and folds each thread's 16-byte output piece into a per-row Horner CRC
+// (acc = shift_4KiB(acc) ^ crc(piece)).  At the end of the chunk every
+// thread multiplies by x^(8*16*(255-t)) mod P, the block XOR-reduces, a
+// ragged last chunk is corrected by tail_fix, and the checksum is stored.
+// The outputs are never re-read from HBM: the checksum costs LDS lookups on
+// p/(k+p) of the traffic instead of a second pass over the regenerated
+// cells (ref:src/object/srv_obj_migrate.c:1156 checksums them after encode).
+template <int K, int R, int W, bool REFL>
+__global__ void __launch_bounds__(BLOCK)
+ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
+{
+	using T = typename ecg_crc::reg<W>::T;
+	constexpr int NB = W / 8;
+	constexpr int KM = K ? K : ECG_KMAX_K;
+	constexpr int RM = R ? R : ECG_KMAX_R;
+	constexpr int T2V = (RM + 3) / 4;
+	constexpr int PER_J = RM + T2V;
+	__shared__ u32x4 s_tbl[KM * PER_J];
+	__shared__ T s_sl[NB * 256];
+	__shared__ T s_sh[NB * 256];
+	__shared__ T s_red[BLOCK / 64][RM];
+	const int k = K ? K : (int)P.k;
+	const int rows = R ? R : (int)P.rows;
+	const uint64_t C = P.cell_bytes;
+	const uint32_t lo = threadIdx.x * 16u;
+	const T *gt = (const T *)Q.tbl;
+
+	for (int i = threadIdx.x; i < KM * RM; i += BLOCK) {
+		const int j = i / RM, r = i % RM;
+		if (j < k && r < rows) {
+			const ecg_ptbl_t &t = P.tbl[r][j];
+			s_tbl[j * PER_J + r] = (u32x4){t.t0lo, t.t0hi, t.t1lo, t.t1hi};
+			reinterpret_cast<uint32_t *>(&s_tbl[j * PER_J + RM])[r] = t.t2;
+		}
+	}
+	for (int i = threadIdx.x; i < NB * 256; i += BLOCK) {
+		s_sl[i] = gt[i];
+		s_sh[i] = gt[ECG_CSUM_OFF_SH4K(NB) + i];
+	}
+	const T kt = gt[ECG_CSUM_OFF_K256(NB) + threadIdx.x];
+	const T poly = (T)Q.poly;
+	__syncthreads();
+
+	for (uint32_t s = blockIdx.y; s < P.nstripes; s += gridDim.y) {
+		for (uint32_t c = blockIdx.x; c < Q.nch; c += gridDim.x) {
+			const uint64_t c0 = (uint64_t)c * Q.chunk_bytes;
+			const uint64_t clen = C - c0 < Q.chunk_bytes ? C - c0 : Q.chunk_bytes;
+			const uint32_t m = (uint32_t)((clen + CHUNK_BYTES - 1) / CHUNK_BYTES);
+			T crc[RM];
+
+#pragma unroll
+			for (int r = 0; r < RM; r++)
+				crc[r] = 0;
+			for (uint32_t i = 0; i < m; i++) {
+				const uint64_t cbase = c0 + (uint64_t)i * CHUNK_BYTES;
+				const bool have = cbase + lo + 16 <= C;	// C % 16 == 0
+				u32x4 outv[RM];
+				uint32_t z = 0;
+
+				asm volatile("" : "+v"(z));
+				const u32x4 *tb = s_tbl + z;
+				if (cbase + CHUNK_BYTES <= C)
+					mm_item<KM, RM, false, false, true>(P, tb, k, rows, s, cbase, lo, outv);
+				else if (have)
+					mm_item<KM, RM, false, false, true>(P, tb, k, rows, s, cbase, lo, outv);
+#pragma unroll
+				for (int r = 0; r < RM; r++) {
+					if (r < rows) {
+						crc[r] = ecg_crc::lin_map<W>(crc[r], s_sh);
+						if (have) {
+							uint32_t d[4] = {outv[r][0], outv[r][1], outv[r][2], outv[r][3]};
+							if (i == 0 && threadIdx.x == 0) {	// initial register
+								d[0] ^= (uint32_t)Q.init;
+								if constexpr (W == 64)
+									d[1] ^= (uint32_t)(Q.init >> 32);
+							}
+							crc[r] ^= ecg_crc::piece_crc<W, REFL>(d, s_sl);
+						}
+					}
+				}
+			}
+#pragma unroll
+			for (int r = 0; r < RM; r++) {
+				if (r < rows) {
+					T v = ecg_crc::mulmod<W, REFL>(kt, crc[r], poly);
+					v = ecg_crc::wave_xor(v);
+					if ((threadIdx.x & 63) == 0)
+						s_red[threadIdx.x >> 6][r] = v;
+				}
+			}
+			__syncthreads();
+			if ((int)threadIdx.x < rows) {
+				const int r = threadIdx.x;
+				T v = 0;
+#pragma unroll
+				for (int w = 0; w < BLOCK / 64; w++)
+					v ^= s_red[w][r];
+				if (clen & (CHUNK_BYTES - 1))
+					v = ecg_crc::mulmod<W, REFL>((T)Q.tail_fix, v, poly);
+				v ^= (T)Q.xorout;
+				const uint64_t slot = ((uint64_t)Q.row_slot[r] * P.nstripes + s) * Q.nch + c;
+				if constexpr (W == 16)
+					((uint16_t *)Q.out)[slot] = (uint16_t)v;
+				else
+					((T *)Q.out)[slot] = v;
+			}
+			__syncthreads();
 		}
 	}
 }
@@ -354,6 +471,27 @@ static const kentry g_kernels[] = {
 
 
 
+typedef void (*mmcs_fn_t)(const ecg_mm_params_t, const ecg_mmcs_params_t);
+
+struct csentry {
+	int k, r, type;
+	mmcs_fn_t fn;
+	const char *name;
+};
+
+#define CSE(K_, R_, T_, W_, RF_, N_) \
+	{K_, R_, T_, ecg_mm_csum_kernel<K_, R_, W_, RF_>, "ecg_mm_csum_kernel<" #K_ "," #R_ "," N_ ">"}
+#define CSE3(K_, R_) CSE(K_, R_, 1, 16, false, "crc16"), CSE(K_, R_, 2, 32, true, "crc32"), \
+		     CSE(K_, R_, 3, 64, true, "crc64")
+
+static const csentry g_cskernels[] = {
+	CSE3(2, 1), CSE3(2, 2), CSE3(2, 3), CSE3(4, 1), CSE3(4, 2), CSE3(4, 3),
+	CSE3(8, 1), CSE3(8, 2), CSE3(8, 3), CSE3(16, 1), CSE3(16, 2), CSE3(16, 3),
+	CSE3(0, 0),
+};
+#define N_CSKERNELS ((uint32_t)(sizeof(g_cskernels) / sizeof(g_cskernels[0])))
+#define KID_FUSED 500u		/* fused kernel ids: KID_FUSED + index */
+
 #define KID_BYTE N_KERNELS
 #define KID_COPY (N_KERNELS + 1)
 #define KID_READ (N_KERNELS + 2)
@@ -389,6 +527,8 @@ extern "C" const char *ecg_k_kernel_name(uint32_t id)
 		return "ecg_stream_kernel<write>";
 	if (id >= ECG_KID_CSUM)
 		return ecg_k_csum_kernel_name(id);
+	if (id >= KID_FUSED && id < KID_FUSED + N_CSKERNELS)
+		return g_cskernels[id - KID_FUSED].name;
 
 	return "?";
 }
@@ -471,5 +611,37 @@ extern "C" int ecg_k_launch_copy(const void *src, void *dst, uint64_t bytes, int
 				   (const uint8_t *)src, (uint8_t *)dst, n16);
 	if (kernel_id)
 		*kernel_id = mode == 1 ? KID_READ : mode == 2 ? KID_WRITE : KID_COPY;
+	return (int)hipGetLastError();
+}
+
+extern "C" int ecg_k_launch_matmul_csum(const ecg_mm_params_t *p, const ecg_mmcs_params_t *q,
+				       const ecg_launch_cfg_t *cfg, void *stream, uint32_t *kernel_id)
+{
+	uint32_t id = N_CSKERNELS;
+
+	if (p->nstripes == 0 || p->cell_bytes == 0 || p->rows == 0)
+		return (int)hipSuccess;
+	if (!aligned16(p) || p->accumulate || p->diff || (p->cell_bytes & 15u) ||
+	    (q->chunk_bytes % CHUNK_BYTES) || q->chunk_bytes == 0)
+		return 1;
+	for (uint32_t i = 0; i < N_CSKERNELS; i++)
+		if (g_cskernels[i].type == (int)q->type && g_cskernels[i].k == (int)p->k &&
+		    g_cskernels[i].r == (int)p->rows) {
+			id = i;
+			break;
+		}
+	if (id == N_CSKERNELS)
+		for (uint32_t i = 0; i < N_CSKERNELS; i++)
+			if (g_cskernels[i].type == (int)q->type && g_cskernels[i].k == 0) {
+				id = i;
+				break;
+			}
+	if (id == N_CSKERNELS)
+		return (int)hipErrorInvalidValue;
+	uint32_t gx = cfg && cfg->grid_x ? cfg->grid_x : (q->nch < 65535 ? q->nch : 65535);
+	uint32_t gy = cfg && cfg->grid_y ? cfg->grid_y : (p->nstripes < 65535 ? p->nstripes : 65535);
+	hipLaunchKernelGGL(g_cskernels[id].fn, dim3(gx, gy), dim3(BLOCK), 0, (hipStream_t)stream, *p, *q);
+	if (kernel_id)
+		*kernel_id = KID_FUSED + id;
 	return (int)hipGetLastError();
 }

@@ -108,6 +108,11 @@ _SIGS = [
     ("ecg_csum_chunk_count", C.c_uint32, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64]),
     ("ecg_csum_extents", C.c_int, [vp, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, vp, C.c_int64,
                                    C.c_uint32, vp, vp]),
+    ("ecg_set_csum_launch", C.c_int, [vp, C.c_uint32]),
+    ("ecg_encode_csum", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, vp, C.c_int64, vp, C.c_int64,
+                                  C.c_int64, C.c_int, C.c_uint64, C.c_uint64, vp, vp]),
+    ("ecg_recover_csum", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, vp, C.c_int64, u32p, C.c_int,
+                                   C.c_int, C.c_uint64, C.c_uint64, vp, vp]),
 ]
 
 HASH_CRC16, HASH_CRC32, HASH_CRC64, HASH_ADLER32 = 1, 2, 3, 7
@@ -337,6 +342,18 @@ class Context:
         """Device checksums of n_ext extents (include/ecg_csum.h): csums[n_ext][nchunks]."""
         _chk(lib().ecg_csum_extents(self.h, htype, chunksize, rec_size, rx_idx, rx_nr, buf, ext_stride, n_ext,
                                     csums, stream), "csum_extents")
+
+    def encode_csum(self, k: int, p: int, cell_bytes: int, nstripes: int, data: int, data_stripe_stride: int,
+                    parity: int, parity_cell_stride: int, parity_stripe_stride: int, htype: int, chunksize: int,
+                    rec_size: int, csums: int, stream=None):
+        _chk(lib().ecg_encode_csum(self.h, k, p, cell_bytes, nstripes, data, data_stripe_stride, parity,
+                                   parity_cell_stride, parity_stripe_stride, htype, chunksize, rec_size, csums,
+                                   stream), "encode_csum")
+
+    def recover_csum(self, k: int, p: int, cell_bytes: int, nstripes: int, stripes: int, stripe_stride: int,
+                     err_list: Sequence[int], htype: int, chunksize: int, rec_size: int, csums: int, stream=None):
+        _chk(lib().ecg_recover_csum(self.h, k, p, cell_bytes, nstripes, stripes, stripe_stride, _u32(err_list),
+                                    len(err_list), htype, chunksize, rec_size, csums, stream), "recover_csum")
 
     def encode_host(self, k: int, p: int, cell_bytes: int, nstripes: int, data: np.ndarray, parity: np.ndarray,
                     chunk: int = 0):

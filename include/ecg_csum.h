@@ -63,6 +63,34 @@ int ecg_csum_extents(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_
 		     uint64_t rx_idx, uint64_t rx_nr, const void *buf, int64_t ext_stride,
 		     uint32_t n_ext, void *csums, void *stream);
 
+/* Encode with checksums of the parity cells it writes, in one pass: the same
+ * operands as ecg_encode (include/ecg.h), plus the hash type, the csummer's
+ * chunk size and record size (cell_bytes must be a multiple of rec_size;
+ * every parity cell is checksummed as an extent that starts on a chunk
+ * boundary, as DAOS cells do when the cell's record count is a multiple of
+ * the chunk's).  csums: device memory, [p][nstripes][nch] checksums of
+ * ecg_csum_len(type) bytes, nch = ecg_csum_chunk_count(chunksize, rec_size, 0,
+ * cell_bytes / rec_size).  Replaces obj_ec_encode_buf + daos_csummer_calc_iods
+ * on the rebuild path (ref:src/object/srv_obj_migrate.c:1122-1160).
+ * CRC types with a 4 KiB-multiple record chunk and 16-byte aligned cells run
+ * as one fused kernel that never re-reads the parity; other shapes run the
+ * product and ecg_csum_extents back to back on the stream. */
+int ecg_encode_csum(ecg_ctx_t *ctx, int k, int p, uint64_t cell_bytes, uint32_t nstripes,
+		    const void *data, int64_t data_stripe_stride, void *parity,
+		    int64_t parity_cell_stride, int64_t parity_stripe_stride, int type,
+		    uint64_t chunksize, uint64_t rec_size, void *csums, void *stream);
+
+/* Recover erased cells in place (as ecg_recover) and checksum them:
+ * csums[nerrs][nstripes][nch] in err_list order (degraded-read / rebuild of
+ * data cells, ref:src/object/cli_ec.c:2626-2643 then the csummer). */
+int ecg_recover_csum(ecg_ctx_t *ctx, int k, int p, uint64_t cell_bytes, uint32_t nstripes,
+		     void *stripes, int64_t stripe_stride, const uint32_t *err_list, int nerrs,
+		     int type, uint64_t chunksize, uint64_t rec_size, void *csums, void *stream);
+
+/* Launch tuning: cap on checksum workgroups (4 chunks in flight each, grid-
+ * stride beyond); 0 restores the default. */
+int ecg_set_csum_launch(ecg_ctx_t *ctx, uint32_t max_blocks);
+
 #ifdef __cplusplus
 }
 #endif

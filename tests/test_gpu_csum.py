@@ -133,3 +133,128 @@ def test_rebuild_parity_then_csum(oracle, ecglib, ctx, htype):
         d.free()
         par.free()
         out.free()
+
+
+# ---- fused product + checksum (ecg_encode_csum / ecg_recover_csum) ----------
+
+def _want_cell_csums(oracle, htype, cs, rb, cells):
+    """oracle checksums of each cell (rows of `cells`), as extents at index 0."""
+    C = cells.shape[-1]
+    flat = np.ascontiguousarray(cells.reshape(-1, C))
+    return oracle.csum_extents(htype, cs, rb, 0, C // rb, flat.reshape(-1), ext_stride=C, n_ext=flat.shape[0])
+
+
+FUSED = [
+    # (k, p, C, S, chunksize, rec_size, htype)
+    (2, 1, 1 << 20, 4, 32768, 1, 2),
+    (4, 2, 1 << 20, 6, 32768, 1, 2),
+    (8, 2, 1 << 20, 4, 32768, 1, 2),
+    (8, 2, 1 << 20, 4, 32768, 1, 1),
+    (8, 2, 1 << 20, 4, 32768, 1, 3),
+    (16, 2, 128 << 10, 8, 16384, 1, 2),
+    (8, 3, 256 << 10, 5, 4096, 1, 3),
+    (4, 1, 65536 + 48, 3, 32768, 1, 2),       # ragged last chunk (not a 4 KiB multiple)
+    (4, 2, 100000, 3, 8192, 8, 1),            # 8-byte records, ragged
+    (16, 3, 40960, 3, 12288, 4096, 3),        # records of 4 KiB, 3 per chunk
+]
+
+
+@pytest.mark.parametrize("case", FUSED)
+def test_encode_csum_fused(oracle, ecglib, ctx, case):
+    k, p, C, S, cs, rb, htype = case
+    L = ecglib.lib()
+    nch = L.ecg_csum_chunk_count(cs, rb, 0, C // rb)
+    cl = L.ecg_csum_len(htype)
+    rng = np.random.default_rng(sum(case))
+    data = rng.integers(0, 256, S * k * C, dtype=np.uint8)
+    d = ctx.to_device(data)
+    par = ctx.alloc(p * S * C)
+    out = ctx.alloc(p * S * nch * cl)
+    try:
+        ctx.encode_csum(k, p, C, S, d.ptr, k * C, par.ptr, S * C, C, htype, cs, rb, out.ptr)
+        ctx.sync()
+        assert "ecg_mm_csum_kernel" in L.ecg_last_kernel().decode(), L.ecg_last_kernel()
+        got_par = par.download().reshape(p, S, C)
+        want_par = oracle.encode_batch(k, p, C, S, data, nthreads=8, simd=True).reshape(p, S, C)
+        assert np.array_equal(got_par, want_par)
+        got = out.download().view(DT[cl]).reshape(p, S, nch)
+        want = _want_cell_csums(oracle, htype, cs, rb, want_par).reshape(p, S, nch)
+        assert np.array_equal(got, want), np.argwhere(got != want)[:5]
+    finally:
+        d.free(); par.free(); out.free()
+
+
+@pytest.mark.parametrize("errs", [[3, 9], [9, 3], [8, 9], [0], [0, 1], [5]])
+@pytest.mark.parametrize("htype", (2, 3))
+def test_recover_csum_fused(oracle, ecglib, ctx, errs, htype):
+    k, p, C, S, cs = 8, 2, 256 << 10, 6, 32768
+    L = ecglib.lib()
+    nch = C // cs
+    cl = L.ecg_csum_len(htype)
+    rng = np.random.default_rng(len(errs) * 10 + htype)
+    data = rng.integers(0, 256, (S, k, C), dtype=np.uint8)
+    en = oracle.cauchy1(k, p)
+    stripes = np.zeros((S, k + p, C), dtype=np.uint8)
+    for s in range(S):
+        stripes[s, :k] = data[s]
+        stripes[s, k:] = oracle.encode_data(en[k:], data[s])
+    broken = stripes.copy()
+    broken[:, errs] = 0
+    d = ctx.to_device(broken)
+    out = ctx.alloc(len(errs) * S * nch * cl)
+    try:
+        ctx.recover_csum(k, p, C, S, d.ptr, (k + p) * C, errs, htype, cs, 1, out.ptr)
+        ctx.sync()
+        got_st = d.download().reshape(S, k + p, C)
+        assert np.array_equal(got_st, stripes)
+        got = out.download().view(DT[cl]).reshape(len(errs), S, nch)
+        for i, e in enumerate(errs):
+            want = _want_cell_csums(oracle, htype, cs, 1, stripes[:, e])
+            assert np.array_equal(got[i], want), (e, i)
+    finally:
+        d.free(); out.free()
+
+
+@pytest.mark.parametrize("variant", ["adler32", "chunk_not_4k", "unaligned", "k_over_16"])
+def test_encode_csum_fallback(oracle, ecglib, ctx, variant):
+    """Shapes the fused kernel does not take run product + checksum launches."""
+    k, p, C, S, cs, rb, htype, off = 4, 2, 1 << 18, 3, 32768, 1, 2, 0
+    if variant == "adler32":
+        htype = 7
+    elif variant == "chunk_not_4k":
+        cs = 6000
+    elif variant == "unaligned":
+        off = 4
+    else:
+        k = 20
+    L = ecglib.lib()
+    nch = L.ecg_csum_chunk_count(cs, rb, 0, C // rb)
+    cl = L.ecg_csum_len(htype)
+    rng = np.random.default_rng(3)
+    data = rng.integers(0, 256, S * k * C, dtype=np.uint8)
+    d = ctx.alloc(data.nbytes + 64)
+    d.upload(data, offset=off)
+    par = ctx.alloc(p * S * C + 64)
+    out = ctx.alloc(p * S * nch * cl)
+    try:
+        ctx.encode_csum(k, p, C, S, d.ptr + off, k * C, par.ptr + off, S * C, C, htype, cs, rb, out.ptr)
+        ctx.sync()
+        assert "ecg_mm_csum_kernel" not in L.ecg_last_kernel().decode()
+        want_par = oracle.encode_batch(k, p, C, S, data, nthreads=8, simd=True).reshape(p, S, C)
+        assert np.array_equal(par.download(p * S * C, offset=off).reshape(p, S, C), want_par)
+        got = out.download().view(DT[cl]).reshape(p, S, nch)
+        assert np.array_equal(got, _want_cell_csums(oracle, htype, cs, rb, want_par).reshape(p, S, nch))
+    finally:
+        d.free(); par.free(); out.free()
+
+
+def test_encode_csum_errors(ecglib, ctx):
+    L = ecglib.lib()
+    b = ctx.alloc(1 << 16)
+    try:
+        assert L.ecg_encode_csum(ctx.h, 4, 2, 4096, 1, b.ptr, 4 * 4096, b.ptr, 4096, 4096, 4, 4096, 1, b.ptr,
+                                 None) == -2037
+        assert L.ecg_encode_csum(ctx.h, 4, 2, 4097, 1, b.ptr, 4 * 4097, b.ptr, 4097, 4097, 2, 4096, 2, b.ptr,
+                                 None) == -1003          # cell not a multiple of the record size
+    finally:
+        b.free()
