@@ -37,22 +37,45 @@ def main():
     out = ctx.alloc(n * (C // 4096) * 8)
     res = {}
     for htype in (1, 2, 3, 7):
-        for cs in (4096, 16384, 32768, 1 << 20):
-            for blocks in (0, 1024, 2048, 8192, 65536):
+        for cs in (4096, 32768, 1 << 20):
+            for blocks in (0, 8192):
                 L.ecg_set_csum_launch(ctx.h, blocks)
                 ms = timed(lambda: ctx.csum_extents(htype, cs, 1, 0, C, buf.ptr, C, n, out.ptr))
                 res[f"{NAMES[htype]}_cs{cs >> 10}K_b{blocks}"] = {
                     "ms": round(ms, 4), "GBps": round(C * n / ms / 1e6, 1), "kernel": L.ecg_last_kernel().decode()}
         L.ecg_set_csum_launch(ctx.h, 0)
-    # rebuild pattern: EC_8P2 encode of 64 stripes then crc32 of the parity cells
-    k, p, S = 8, 2, 64
-    data = ctx.alloc(S * k * C)
-    par = ctx.alloc(p * S * C + 4096)
-    data.fill(0x3C)
-    enc = timed(lambda: ctx.encode(k, p, C, S, data.ptr, k * C, par.ptr, S * C + 4096, C))
-    crc = timed(lambda: ctx.csum_extents(2, 32768, 1, 0, C, par.ptr, C, p * S, out.ptr))
-    res["rebuild_8p2_encode_ms"] = round(enc, 4)
-    res["rebuild_8p2_parity_crc32_ms"] = round(crc, 4)
+    # rebuild pattern: encode alone / encode then checksum launches / fused
+    for (k, p, C2, S, tag) in ((8, 2, 1 << 20, 256, "8p2_1M"), (4, 2, 1 << 20, 512, "4p2_1M"),
+                               (16, 2, 128 << 10, 1024, "16p2_128K")):
+        data = ctx.alloc(S * k * C2)
+        par = ctx.alloc(p * S * C2 + 4096)
+        cs_out = ctx.alloc(p * S * (C2 // 32768) * 8)
+        data.upload(blk[: min(blk.size, S * k * C2)])
+        pitch = S * C2 + 4096
+        enc = timed(lambda: ctx.encode(k, p, C2, S, data.ptr, k * C2, par.ptr, pitch, C2))
+        for htype in ((1, 2, 3) if tag == "8p2_1M" else (2,)):
+            def two_pass():
+                ctx.encode(k, p, C2, S, data.ptr, k * C2, par.ptr, pitch, C2)
+                for r in range(p):
+                    ctx.csum_extents(htype, 32768, 1, 0, C2, par.ptr + r * pitch, C2, S, cs_out.ptr)
+            sep = timed(two_pass)
+            fus = timed(lambda: ctx.encode_csum(k, p, C2, S, data.ptr, k * C2, par.ptr, pitch, C2, htype, 32768, 1,
+                                                cs_out.ptr))
+            alg = (k + p) * C2 * S
+            res[f"enc_{tag}_{NAMES[htype]}"] = {
+                "encode_ms": round(enc, 4), "encode_then_csum_ms": round(sep, 4), "fused_ms": round(fus, 4),
+                "encode_GBps": round(alg / enc / 1e6, 1), "fused_GBps": round(alg / fus / 1e6, 1),
+                "fused_overhead_vs_encode": round(fus / enc - 1, 4), "fused_kernel": L.ecg_last_kernel().decode()}
+        if tag == "8p2_1M":
+            st = ctx.alloc(S * (k + p) * C2)
+            st.fill(0x11)
+            rec = timed(lambda: ctx.recover(k, p, C2, S, st.ptr, (k + p) * C2, [0, 1]))
+            recf = timed(lambda: ctx.recover_csum(k, p, C2, S, st.ptr, (k + p) * C2, [0, 1], 2, 32768, 1,
+                                                  cs_out.ptr))
+            res["rec_8p2_1M_crc32"] = {"recover_ms": round(rec, 4), "fused_ms": round(recf, 4),
+                                      "fused_overhead": round(recf / rec - 1, 4)}
+            st.free()
+        data.free(); par.free(); cs_out.free()
     print(json.dumps(res, indent=0))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     json.dump(res, open(os.path.join(ROOT, "gpurun_out", "bench_csum.json"), "w"), indent=1)

@@ -85,6 +85,9 @@ for what in "$@"; do
 		make -C tests/c > /dev/null || exit 2
 		step ctest 300 ./build/ctest/test_ecg_c || exit $?
 		;;
+	tune8)
+		step tune8 600 python tools/tune8.py || exit $?
+		;;
 	csum)
 		step bench_csum 600 python tools/bench_csum.py || exit $?
 		;;
