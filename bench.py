@@ -247,6 +247,31 @@ def detail_rows(ctx, ceil, iters=7):
                       "measured_mix_ceiling_GBps": round(mix, 1), "frac_of_measured_mix": round(gbs / mix, 4),
                       "kernel": ecg.last_kernel(), "ms": round(ms, 4)}
         buf.free()
+    # checksums of regenerated cells (include/ecg_csum.h): EC_8P2 encode with
+    # crc32 over 32 KiB chunks of the parity, fused vs the product alone, and
+    # the standalone checksum kernel over 1 GiB of 1 MiB cells
+    k, p, C, S = 8, 2, 1 << 20, 512
+    data = ctx.alloc(S * k * C)
+    fill_device(ctx, data, S * k * C, 8)
+    pitch = S * C + PARITY_ROW_PAD
+    par = ctx.alloc(p * pitch)
+    out = ctx.alloc(p * S * (C // 32768) * 4)
+    enc = time_kernel(ctx, lambda: ctx.encode(k, p, C, S, data.ptr, k * C, par.ptr, pitch, C), iters)
+    fus = time_kernel(ctx, lambda: ctx.encode_csum(k, p, C, S, data.ptr, k * C, par.ptr, pitch, C,
+                                                   ecg.HASH_CRC32, 32768, 1, out.ptr), iters)
+    alg = (k + p) * C * S
+    rows["EC_8P2_1MiB_encode_crc32_32KiB_fused"] = {
+        "GiBps_user": round(k * C * S / (fus / 1e3) / GIB, 1), "alg_GBps": round(alg / fus / 1e6, 1),
+        "roofline_frac": round(alg / fus / 1e6 / HBM_PEAK_GBS, 4), "ms": round(fus, 4),
+        "encode_only_ms": round(enc, 4), "checksum_overhead": round(fus / enc - 1, 4),
+        "kernel": ecg.last_kernel()}
+    n = 1024
+    ms = time_kernel(ctx, lambda: ctx.csum_extents(ecg.HASH_CRC32, 32768, 1, 0, C, data.ptr, C, n, out.ptr), iters)
+    rows["crc32_32KiB_chunks_1GiB"] = {"alg_GBps": round(C * n / ms / 1e6, 1),
+                                       "roofline_frac": round(C * n / ms / 1e6 / HBM_PEAK_GBS, 4),
+                                       "ms": round(ms, 4), "kernel": ecg.last_kernel(),
+                                       "bound": "LDS lookups (1.25 ds_read_b32 per byte), DESIGN.md §11"}
+    data.free(); par.free(); out.free()
     return rows
 
 

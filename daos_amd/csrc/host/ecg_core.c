@@ -396,6 +396,19 @@ int ecg_recover(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
  * device, the fused path only saves the re-read of the outputs.
  * csums[row_slot[r]][s][chunk].
  */
+static int aligned16_ok(const void *src, const int64_t *soff, int k, int64_t sstride,
+			const void *dst, const int64_t *doff, int rows, int64_t dstride)
+{
+	uint64_t bits = (uint64_t)(uintptr_t)src | (uint64_t)(uintptr_t)dst | (uint64_t)sstride |
+			(uint64_t)dstride;
+
+	for (int j = 0; j < k; j++)
+		bits |= (uint64_t)soff[j];
+	for (int r = 0; r < rows; r++)
+		bits |= (uint64_t)doff[r];
+	return (bits & 15u) == 0;
+}
+
 static int matmul_csum(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, uint64_t C,
 		       uint32_t S, const void *src, const int64_t *soff, int64_t sstride, void *dst,
 		       const int64_t *doff, int64_t dstride, int type, uint64_t chunksize,
@@ -445,6 +458,15 @@ static int matmul_csum(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coe
 			q.row_slot[r] = row_slot[r];
 			for (j = 0; j < k; j++)
 				ecg_build_ptbl(coef[(size_t)r * k + j], &prm->tbl[r][j]);
+		}
+		/* the fused kernel XORs per-wave partials into the checksums */
+		if (aligned16_ok(src, soff, k, sstride, dst, doff, rows, dstride)) {
+			hipError_t he = hipMemsetAsync(csums, 0, (size_t)rows * S * q.nch * (size_t)cl, st);
+
+			if (he != hipSuccess) {
+				free(prm);
+				return ecg_hip_fail(he, "csum memset");
+			}
 		}
 		e = ecg_k_launch_matmul_csum(prm, &q, &ctx->cfg, (void *)st, &kid);
 		free(prm);

@@ -314,6 +314,9 @@ int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t
 		return 0;
 	if (rcs == 0 || rcs % ECG_MMCS_STRIDE || C % 16 || C % rec_size)
 		return 0;
+	/* the kernel XORs partials in with 32-bit (crc16/crc32) or 64-bit atomics */
+	if ((uintptr_t)csums % (type == ECG_HASH_CRC64 ? 8u : 4u))
+		return 0;
 	d = &g_defs[type];
 	rc = crc_tables(ctx, type, &q->tbl);
 	if (rc)

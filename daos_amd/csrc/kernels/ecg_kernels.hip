@@ -67,17 +67,13 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 // The uniform cell offsets are passed through an empty asm per item so LICM
 // cannot hoist k+rows 64-bit pointers out of the stripe loop (they land in
 // VGPRs and spill at EC_8P2/EC_16P2).
-template <int KM, int RM, bool ACC, bool DIFF, bool KEEP = false>
-__device__ __forceinline__ void mm_item(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
-					uint32_t s, uint64_t cbase, uint32_t lo, u32x4 *keep = nullptr)
+template <int KM, bool DIFF>
+__device__ __forceinline__ void mm_load(const ecg_mm_params_t &P, int k, uint32_t s, uint64_t cbase,
+					uint32_t lo, u32x4 *x)
 {
-	constexpr int T2V = (RM + 3) / 4;
-	constexpr int PER_J = RM + T2V;
 	const int64_t s_src = (int64_t)s * P.src_stripe_stride + (int64_t)cbase;
 	const int64_t s_src2 = DIFF ? (int64_t)s * P.src2_stripe_stride + (int64_t)cbase : 0;
-	const int64_t s_dst = (int64_t)s * P.dst_stripe_stride + (int64_t)cbase;
 
-	u32x4 x[KM];
 #pragma unroll
 	for (int j = 0; j < KM; j++) {
 		if (j < k) {
@@ -91,6 +87,33 @@ __device__ __forceinline__ void mm_item(const ecg_mm_params_t &P, const u32x4 *t
 			}
 		}
 	}
+}
+
+template <int KM, int RM, bool ACC, bool KEEP>
+__device__ __forceinline__ void mm_compute(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
+					   uint32_t s, uint64_t cbase, uint32_t lo, const u32x4 *x,
+					   u32x4 *keep);
+
+template <int KM, int RM, bool ACC, bool DIFF, bool KEEP = false>
+__device__ __forceinline__ void mm_item(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
+					uint32_t s, uint64_t cbase, uint32_t lo, u32x4 *keep = nullptr)
+{
+	u32x4 x[KM];
+
+	mm_load<KM, DIFF>(P, k, s, cbase, lo, x);
+	mm_compute<KM, RM, ACC, KEEP>(P, tb, k, rows, s, cbase, lo, x, keep);
+}
+
+// The product of one loaded column: x[j] = the lane's 16 bytes of cell j.
+template <int KM, int RM, bool ACC, bool KEEP>
+__device__ __forceinline__ void mm_compute(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
+					   uint32_t s, uint64_t cbase, uint32_t lo, const u32x4 *x,
+					   u32x4 *keep)
+{
+	constexpr int T2V = (RM + 3) / 4;
+	constexpr int PER_J = RM + T2V;
+	const int64_t s_dst = (int64_t)s * P.dst_stripe_stride + (int64_t)cbase;
+
 	u32x4 acc[RM];
 #pragma unroll
 	for (int r = 0; r < RM; r++) {
@@ -266,12 +289,12 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	constexpr int NB = W / 8;
 	constexpr int KM = K ? K : ECG_KMAX_K;
 	constexpr int RM = R ? R : ECG_KMAX_R;
+	constexpr bool PF = K != 0 && K <= 8;	// prefetch: 4*KM more VGPRs
 	constexpr int T2V = (RM + 3) / 4;
 	constexpr int PER_J = RM + T2V;
 	__shared__ u32x4 s_tbl[KM * PER_J];
 	__shared__ T s_sl[NB * 256];
 	__shared__ T s_sh[NB * 256];
-	__shared__ T s_red[BLOCK / 64][RM];
 	const int k = K ? K : (int)P.k;
 	const int rows = R ? R : (int)P.rows;
 	const uint64_t C = P.cell_bytes;
@@ -304,18 +327,36 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 #pragma unroll
 			for (int r = 0; r < RM; r++)
 				crc[r] = 0;
+			// column i+1's loads are issued before column i's product (PF):
+			// the workgroup walks its chunk sequentially, so this is what
+			// keeps HBM requests in flight across the columns
+			u32x4 xa[KM];
+			if (c0 + lo + 16 <= C)
+				mm_load<KM, false>(P, k, s, c0, lo, xa);
 			for (uint32_t i = 0; i < m; i++) {
 				const uint64_t cbase = c0 + (uint64_t)i * CHUNK_BYTES;
 				const bool have = cbase + lo + 16 <= C;	// C % 16 == 0
 				u32x4 outv[RM];
+				u32x4 xb[PF ? KM : 1];
 				uint32_t z = 0;
 
+				if constexpr (PF) {
+					if (i + 1 < m && cbase + CHUNK_BYTES + lo + 16 <= C)
+						mm_load<KM, false>(P, k, s, cbase + CHUNK_BYTES, lo, xb);
+				} else if (i > 0 && have) {
+					mm_load<KM, false>(P, k, s, cbase, lo, xa);
+				}
 				asm volatile("" : "+v"(z));
 				const u32x4 *tb = s_tbl + z;
 				if (cbase + CHUNK_BYTES <= C)
-					mm_item<KM, RM, false, false, true>(P, tb, k, rows, s, cbase, lo, outv);
+					mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, xa, outv);
 				else if (have)
-					mm_item<KM, RM, false, false, true>(P, tb, k, rows, s, cbase, lo, outv);
+					mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, xa, outv);
+				if constexpr (PF) {
+#pragma unroll
+					for (int j = 0; j < KM; j++)
+						xa[j] = xb[j];
+				}
 #pragma unroll
 				for (int r = 0; r < RM; r++) {
 					if (r < rows) {
@@ -332,32 +373,29 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 					}
 				}
 			}
+			// each wave XORs its partial straight into the (zeroed) output:
+			// no workgroup barrier, so the other waves keep their loads in
+			// flight while one finishes its chunk
 #pragma unroll
 			for (int r = 0; r < RM; r++) {
 				if (r < rows) {
 					T v = ecg_crc::mulmod<W, REFL>(kt, crc[r], poly);
 					v = ecg_crc::wave_xor(v);
-					if ((threadIdx.x & 63) == 0)
-						s_red[threadIdx.x >> 6][r] = v;
+					if ((threadIdx.x & 63) == 0) {
+						if (clen & (CHUNK_BYTES - 1))	// linear: per wave
+							v = ecg_crc::mulmod<W, REFL>((T)Q.tail_fix, v, poly);
+						if (threadIdx.x == 0)
+							v ^= (T)Q.xorout;
+						const uint64_t slot =
+							((uint64_t)Q.row_slot[r] * P.nstripes + s) * Q.nch + c;
+						if constexpr (W == 16)
+							atomicXor((uint32_t *)Q.out + slot / 2,
+								  (uint32_t)v << (16 * (slot & 1)));
+						else
+							atomicXor((T *)Q.out + slot, v);
+					}
 				}
 			}
-			__syncthreads();
-			if ((int)threadIdx.x < rows) {
-				const int r = threadIdx.x;
-				T v = 0;
-#pragma unroll
-				for (int w = 0; w < BLOCK / 64; w++)
-					v ^= s_red[w][r];
-				if (clen & (CHUNK_BYTES - 1))
-					v = ecg_crc::mulmod<W, REFL>((T)Q.tail_fix, v, poly);
-				v ^= (T)Q.xorout;
-				const uint64_t slot = ((uint64_t)Q.row_slot[r] * P.nstripes + s) * Q.nch + c;
-				if constexpr (W == 16)
-					((uint16_t *)Q.out)[slot] = (uint16_t)v;
-				else
-					((T *)Q.out)[slot] = v;
-			}
-			__syncthreads();
 		}
 	}
 }

@@ -258,3 +258,22 @@ def test_encode_csum_errors(ecglib, ctx):
                                  None) == -1003          # cell not a multiple of the record size
     finally:
         b.free()
+
+
+def test_encode_csum_misaligned_csums(oracle, ecglib, ctx):
+    """A checksum array that is only 2-byte aligned takes the two-pass path."""
+    k, p, C, S, cs = 4, 2, 1 << 18, 2, 32768
+    nch = C // cs
+    rng = np.random.default_rng(9)
+    data = rng.integers(0, 256, S * k * C, dtype=np.uint8)
+    d = ctx.to_device(data)
+    par = ctx.alloc(p * S * C)
+    out = ctx.alloc(p * S * nch * 2 + 16)
+    try:
+        ctx.encode_csum(k, p, C, S, d.ptr, k * C, par.ptr, S * C, C, 1, cs, 1, out.ptr + 2)
+        ctx.sync()
+        want_par = oracle.encode_batch(k, p, C, S, data, nthreads=8, simd=True).reshape(p, S, C)
+        got = out.download(p * S * nch * 2, offset=2).view(np.uint16).reshape(p, S, nch)
+        assert np.array_equal(got, _want_cell_csums(oracle, 1, cs, 1, want_par).reshape(p, S, nch))
+    finally:
+        d.free(); par.free(); out.free()
