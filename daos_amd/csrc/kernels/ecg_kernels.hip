@@ -317,84 +317,102 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	const T poly = (T)Q.poly;
 	__syncthreads();
 
+	// The workgroup's work is a stream of (chunk, column) steps: chunks
+	// blockIdx.x, blockIdx.x + gridDim.x, ... of stripe blockIdx.y (+ gridDim.y
+	// ...), each chunk's 4 KiB columns in order.  With PF the next step's
+	// loads are issued before this step's product and before a chunk's
+	// reduction, so HBM requests stay in flight across both.
 	for (uint32_t s = blockIdx.y; s < P.nstripes; s += gridDim.y) {
-		for (uint32_t c = blockIdx.x; c < Q.nch; c += gridDim.x) {
+		uint32_t c = blockIdx.x, i = 0;
+		bool first = true;
+		T crc[RM];
+		u32x4 xa[KM];
+
+		if (c >= Q.nch)
+			continue;
+#pragma unroll
+		for (int r = 0; r < RM; r++)
+			crc[r] = 0;
+		if ((uint64_t)c * Q.chunk_bytes + lo + 16 <= C)
+			mm_load<KM, false>(P, k, s, (uint64_t)c * Q.chunk_bytes, lo, xa);
+		for (;;) {
 			const uint64_t c0 = (uint64_t)c * Q.chunk_bytes;
 			const uint64_t clen = C - c0 < Q.chunk_bytes ? C - c0 : Q.chunk_bytes;
 			const uint32_t m = (uint32_t)((clen + CHUNK_BYTES - 1) / CHUNK_BYTES);
-			T crc[RM];
+			const uint64_t cbase = c0 + (uint64_t)i * CHUNK_BYTES;
+			const bool have = cbase + lo + 16 <= C;	// C % 16 == 0
+			const bool last = i + 1 == m;
+			const uint32_t nc = last ? c + gridDim.x : c, ni = last ? 0 : i + 1;
+			const bool more = nc < Q.nch;
+			const uint64_t nbase = (uint64_t)nc * Q.chunk_bytes + (uint64_t)ni * CHUNK_BYTES;
+			u32x4 outv[RM];
+			u32x4 xb[PF ? KM : 1];
+			uint32_t z = 0;
 
-#pragma unroll
-			for (int r = 0; r < RM; r++)
-				crc[r] = 0;
-			// column i+1's loads are issued before column i's product (PF):
-			// the workgroup walks its chunk sequentially, so this is what
-			// keeps HBM requests in flight across the columns
-			u32x4 xa[KM];
-			if (c0 + lo + 16 <= C)
-				mm_load<KM, false>(P, k, s, c0, lo, xa);
-			for (uint32_t i = 0; i < m; i++) {
-				const uint64_t cbase = c0 + (uint64_t)i * CHUNK_BYTES;
-				const bool have = cbase + lo + 16 <= C;	// C % 16 == 0
-				u32x4 outv[RM];
-				u32x4 xb[PF ? KM : 1];
-				uint32_t z = 0;
-
-				if constexpr (PF) {
-					if (i + 1 < m && cbase + CHUNK_BYTES + lo + 16 <= C)
-						mm_load<KM, false>(P, k, s, cbase + CHUNK_BYTES, lo, xb);
-				} else if (i > 0 && have) {
-					mm_load<KM, false>(P, k, s, cbase, lo, xa);
-				}
-				asm volatile("" : "+v"(z));
-				const u32x4 *tb = s_tbl + z;
+			if constexpr (PF) {
+				if (more && nbase + lo + 16 <= C)
+					mm_load<KM, false>(P, k, s, nbase, lo, xb);
+			} else if (!first) {
 				if (cbase + CHUNK_BYTES <= C)
-					mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, xa, outv);
+					mm_load<KM, false>(P, k, s, cbase, lo, xa);
 				else if (have)
-					mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, xa, outv);
-				if constexpr (PF) {
+					mm_load<KM, false>(P, k, s, cbase, lo, xa);
+			}
+			first = false;
+			asm volatile("" : "+v"(z));
+			const u32x4 *tb = s_tbl + z;
+			if (cbase + CHUNK_BYTES <= C)
+				mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, xa, outv);
+			else if (have)
+				mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, xa, outv);
 #pragma unroll
-					for (int j = 0; j < KM; j++)
-						xa[j] = xb[j];
+			for (int r = 0; r < RM; r++) {
+				if (r < rows) {
+					crc[r] = ecg_crc::lin_map<W>(crc[r], s_sh);
+					if (have) {
+						uint32_t d[4] = {outv[r][0], outv[r][1], outv[r][2], outv[r][3]};
+						if (i == 0 && threadIdx.x == 0) {	// initial register
+							d[0] ^= (uint32_t)Q.init;
+							if constexpr (W == 64)
+								d[1] ^= (uint32_t)(Q.init >> 32);
+						}
+						crc[r] ^= ecg_crc::piece_crc<W, REFL>(d, s_sl);
+					}
 				}
+			}
+			if (last) {
+				// each wave XORs its partial into the (zeroed) output: no
+				// workgroup barrier, other waves keep streaming
 #pragma unroll
 				for (int r = 0; r < RM; r++) {
 					if (r < rows) {
-						crc[r] = ecg_crc::lin_map<W>(crc[r], s_sh);
-						if (have) {
-							uint32_t d[4] = {outv[r][0], outv[r][1], outv[r][2], outv[r][3]};
-							if (i == 0 && threadIdx.x == 0) {	// initial register
-								d[0] ^= (uint32_t)Q.init;
-								if constexpr (W == 64)
-									d[1] ^= (uint32_t)(Q.init >> 32);
-							}
-							crc[r] ^= ecg_crc::piece_crc<W, REFL>(d, s_sl);
+						T v = ecg_crc::mulmod<W, REFL>(kt, crc[r], poly);
+						v = ecg_crc::wave_xor(v);
+						crc[r] = 0;
+						if ((threadIdx.x & 63) == 0) {
+							if (clen & (CHUNK_BYTES - 1))	// linear: per wave
+								v = ecg_crc::mulmod<W, REFL>((T)Q.tail_fix, v, poly);
+							if (threadIdx.x == 0)
+								v ^= (T)Q.xorout;
+							const uint64_t slot =
+								((uint64_t)Q.row_slot[r] * P.nstripes + s) * Q.nch + c;
+							if constexpr (W == 16)
+								atomicXor((uint32_t *)Q.out + slot / 2,
+									  (uint32_t)v << (16 * (slot & 1)));
+							else
+								atomicXor((T *)Q.out + slot, v);
 						}
 					}
 				}
 			}
-			// each wave XORs its partial straight into the (zeroed) output:
-			// no workgroup barrier, so the other waves keep their loads in
-			// flight while one finishes its chunk
+			if (!more)
+				break;
+			c = nc;
+			i = ni;
+			if constexpr (PF) {
 #pragma unroll
-			for (int r = 0; r < RM; r++) {
-				if (r < rows) {
-					T v = ecg_crc::mulmod<W, REFL>(kt, crc[r], poly);
-					v = ecg_crc::wave_xor(v);
-					if ((threadIdx.x & 63) == 0) {
-						if (clen & (CHUNK_BYTES - 1))	// linear: per wave
-							v = ecg_crc::mulmod<W, REFL>((T)Q.tail_fix, v, poly);
-						if (threadIdx.x == 0)
-							v ^= (T)Q.xorout;
-						const uint64_t slot =
-							((uint64_t)Q.row_slot[r] * P.nstripes + s) * Q.nch + c;
-						if constexpr (W == 16)
-							atomicXor((uint32_t *)Q.out + slot / 2,
-								  (uint32_t)v << (16 * (slot & 1)));
-						else
-							atomicXor((T *)Q.out + slot, v);
-					}
-				}
+				for (int j = 0; j < KM; j++)
+					xa[j] = xb[j];
 			}
 		}
 	}
@@ -676,8 +694,15 @@ extern "C" int ecg_k_launch_matmul_csum(const ecg_mm_params_t *p, const ecg_mmcs
 			}
 	if (id == N_CSKERNELS)
 		return (int)hipErrorInvalidValue;
-	uint32_t gx = cfg && cfg->grid_x ? cfg->grid_x : (q->nch < 65535 ? q->nch : 65535);
+	// default: ~16 KiB of columns per workgroup (tools/tune8.py,
+	// profiles/r01/tune8_fused_chunks.json: walking more columns per
+	// workgroup loses HBM parallelism, fewer pays a chunk reduction per
+	// column); chunks >= 16 KiB -> one chunk per workgroup
+	const uint64_t cpb = q->chunk_bytes >= 16384 ? 1 : 16384 / q->chunk_bytes;
+	uint32_t gx = cfg && cfg->grid_x ? cfg->grid_x : (uint32_t)((q->nch + cpb - 1) / cpb);
 	uint32_t gy = cfg && cfg->grid_y ? cfg->grid_y : (p->nstripes < 65535 ? p->nstripes : 65535);
+	if (gx > 65535)
+		gx = 65535;
 	hipLaunchKernelGGL(g_cskernels[id].fn, dim3(gx, gy), dim3(BLOCK), 0, (hipStream_t)stream, *p, *q);
 	if (kernel_id)
 		*kernel_id = KID_FUSED + id;

@@ -26,8 +26,13 @@ def main():
     out = ctx.alloc(p * S * (C // 4096) * 8)
     res = {"encode_ms": timed(lambda: ctx.encode(k, p, C, S, data.ptr, k * C, par.ptr, pitch, C))}
     for cs in (4096, 8192, 16384, 32768, 131072, 1 << 20):
-        res[f"fused_crc32_cs{cs >> 10}K_ms"] = timed(
-            lambda: ctx.encode_csum(k, p, C, S, data.ptr, k * C, par.ptr, pitch, C, 2, cs, 1, out.ptr))
+        nch = C // cs
+        for cpb in (1, 2, 4, 8):
+            gx = max(1, (nch + cpb - 1) // cpb)
+            ctx.set_launch(gx, 0, 0)
+            res[f"fused_crc32_cs{cs >> 10}K_cpb{cpb}_ms"] = timed(
+                lambda: ctx.encode_csum(k, p, C, S, data.ptr, k * C, par.ptr, pitch, C, 2, cs, 1, out.ptr))
+        ctx.set_launch(0, 0, 0)
     res = {kk: round(v, 4) for kk, v in res.items()}
     print(json.dumps(res, indent=0))
     json.dump(res, open(os.path.join(ROOT, "gpurun_out", "tune8.json"), "w"), indent=1)
