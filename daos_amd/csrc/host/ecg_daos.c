@@ -391,3 +391,40 @@ int ecg_obj_ec_singv_encode(uint32_t oc_id, uint64_t iod_size, const unsigned ch
 	free(cells);
 	return rc;
 }
+
+/* ---- stripe / index math, ref:src/object/obj_ec.h:271-350 ---- */
+uint64_t ecg_obj_ec_stripe_rec_nr(uint32_t k, uint64_t e_len)
+{
+	return (uint64_t)k * e_len;
+}
+
+uint64_t ecg_obj_ec_cell_bytes(uint64_t e_len, uint64_t iod_size)
+{
+	return e_len * iod_size;
+}
+
+uint32_t ecg_obj_ec_tgt_of_recx_idx(uint64_t idx, uint64_t stripe_rec_nr, uint64_t e_len)
+{
+	return (uint32_t)((idx % stripe_rec_nr) / e_len);
+}
+
+uint64_t ecg_obj_ec_idx_daos2vos(uint64_t idx, uint64_t stripe_rec_nr, uint64_t e_len)
+{
+	return (idx / stripe_rec_nr) * e_len + idx % e_len;
+}
+
+uint64_t ecg_obj_ec_idx_vos2daos(uint64_t vos_idx, uint64_t stripe_rec_nr, uint64_t e_len,
+				 uint32_t tgt_idx)
+{
+	return (vos_idx / e_len) * stripe_rec_nr + (uint64_t)tgt_idx * e_len + vos_idx % e_len;
+}
+
+uint64_t ecg_obj_ec_idx_parity2daos(uint64_t vos_off, uint64_t e_len, uint64_t stripe_rec_nr)
+{
+	return (vos_off / e_len) * stripe_rec_nr;
+}
+
+uint32_t ecg_obj_ec_shard_off_by_start(uint32_t tgt_idx, uint32_t tgt_nr, uint32_t start_tgt)
+{
+	return (tgt_idx + tgt_nr - start_tgt) % tgt_nr;
+}

@@ -102,6 +102,13 @@ _SIGS = [
     ("ecg_agg_recalc_parity", C.c_int, [vp, C.c_uint32, C.c_uint64, u8p, C.c_uint32, u8p, u8p, u8p]),
     ("ecg_obj_ec_singv_cell_bytes", C.c_uint64, [C.c_uint32, C.c_uint64]),
     ("ecg_obj_ec_singv_encode", C.c_int, [C.c_uint32, C.c_uint64, u8p, C.POINTER(u8p)]),
+    ("ecg_obj_ec_stripe_rec_nr", C.c_uint64, [C.c_uint32, C.c_uint64]),
+    ("ecg_obj_ec_cell_bytes", C.c_uint64, [C.c_uint64, C.c_uint64]),
+    ("ecg_obj_ec_tgt_of_recx_idx", C.c_uint32, [C.c_uint64, C.c_uint64, C.c_uint64]),
+    ("ecg_obj_ec_idx_daos2vos", C.c_uint64, [C.c_uint64, C.c_uint64, C.c_uint64]),
+    ("ecg_obj_ec_idx_vos2daos", C.c_uint64, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32]),
+    ("ecg_obj_ec_idx_parity2daos", C.c_uint64, [C.c_uint64, C.c_uint64, C.c_uint64]),
+    ("ecg_obj_ec_shard_off_by_start", C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32]),
     # chunked checksums (ecg_csum.h)
     ("ecg_csum_len", C.c_int, [C.c_int]),
     ("ecg_csum_record_chunksize", C.c_uint64, [C.c_uint64, C.c_uint64]),

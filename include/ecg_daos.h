@@ -143,6 +143,27 @@ uint64_t ecg_obj_ec_singv_cell_bytes(uint32_t oc_id, uint64_t iod_size);
 int ecg_obj_ec_singv_encode(uint32_t oc_id, uint64_t iod_size, const unsigned char *value,
 			    unsigned char *p_bufs[]);
 
+/* ---- stripe / index math (ref:src/object/obj_ec.h:271-350) -------------
+ * e_len = records per cell (oca->u.ec.e_len), stripe_rec_nr = k * e_len.
+ * Parity extents carry ECG_EC_PARITY_BIT in their VOS index
+ * (DAOS_EC_PARITY_BIT, ref:src/include/daos/object.h:19). */
+#define ECG_EC_PARITY_BIT	(1ULL << 63)
+
+uint64_t ecg_obj_ec_stripe_rec_nr(uint32_t k, uint64_t e_len);	/* obj_ec_stripe_rec_nr */
+uint64_t ecg_obj_ec_cell_bytes(uint64_t e_len, uint64_t iod_size);	/* obj_ec_cell_bytes */
+/* data target (0..k-1) holding daos record idx: obj_ec_tgt_of_recx_idx */
+uint32_t ecg_obj_ec_tgt_of_recx_idx(uint64_t idx, uint64_t stripe_rec_nr, uint64_t e_len);
+/* daos record idx -> VOS idx on its data target: obj_ec_idx_daos2vos */
+uint64_t ecg_obj_ec_idx_daos2vos(uint64_t idx, uint64_t stripe_rec_nr, uint64_t e_len);
+/* VOS idx on data target tgt_idx -> daos record idx: obj_ec_idx_vos2daos */
+uint64_t ecg_obj_ec_idx_vos2daos(uint64_t vos_idx, uint64_t stripe_rec_nr, uint64_t e_len,
+				 uint32_t tgt_idx);
+/* parity VOS offset -> daos idx of the stripe start: obj_ec_idx_parity2daos */
+uint64_t ecg_obj_ec_idx_parity2daos(uint64_t vos_off, uint64_t e_len, uint64_t stripe_rec_nr);
+/* physical target -> logical cell index given the group's start target:
+ * obj_ec_shard_off_by_start */
+uint32_t ecg_obj_ec_shard_off_by_start(uint32_t tgt_idx, uint32_t tgt_nr, uint32_t start_tgt);
+
 #ifdef __cplusplus
 }
 #endif
