@@ -140,6 +140,11 @@ int ecg_k_launch_copy(const void *src, void *dst, uint64_t bytes, int mode, void
  * launches nothing) when the operands are not 16-byte aligned. */
 int ecg_k_launch_matmul_csum(const ecg_mm_params_t *p, const ecg_mmcs_params_t *q,
 			     const ecg_launch_cfg_t *cfg, void *stream, uint32_t *kernel_id);
+/* Pointer-table product (kernels/ecg_kernels.hip): cells_dev[s*(k+rows)+j] =
+ * device address of input cell j / output cell j-k of stripe s.  aligned = all
+ * addresses 16-byte aligned (else the byte-granular kernel). */
+int ecg_k_launch_matmul_ptrs(const ecg_mm_params_t *p, const uint64_t *cells_dev, int aligned,
+			     const ecg_launch_cfg_t *cfg, void *stream, uint32_t *kernel_id);
 /* Chunked checksums (kernels/ecg_csum_kernels.hip). max_blocks 0 = default. */
 int ecg_k_launch_csum(const ecg_csum_params_t *p, void *stream, uint32_t max_blocks,
 		      uint32_t *kernel_id);

@@ -137,6 +137,7 @@ void ecg_ctx_destroy(ecg_ctx_t *ctx)
 	(void)hipSetDevice(ctx->device);
 	(void)hipStreamSynchronize(ctx->stream);
 	stage_free(ctx);
+	ecg_scratch_free(ctx);
 	ecg_csum_ctx_fini(ctx);
 	(void)hipStreamDestroy(ctx->stream);
 	pthread_mutex_destroy(&ctx->lock);

@@ -33,6 +33,17 @@ struct ecg_stage {
 	hipEvent_t done[ECG_NSLOT];
 };
 
+/* Pointer tables and gathered cells (ecg_ptrs.c), guarded by ctx->lock and
+ * the `done` event of the last launch that read them. */
+struct ecg_scratch {
+	void *pin;
+	size_t pin_bytes;
+	void *dev;
+	size_t dev_bytes;
+	hipEvent_t done;
+	int pending;
+};
+
 struct ecg_ctx {
 	int device;
 	hipStream_t stream;
@@ -44,6 +55,7 @@ struct ecg_ctx {
 #define ECG_NCSUM_TBL 4
 	void *csum_tbl[ECG_NCSUM_TBL];	/* device CRC tables by hash type (ecg_csum.c) */
 	uint32_t csum_blocks;		/* csum grid cap, 0 = kernel default */
+	struct ecg_scratch scratch;
 };
 
 /* errors (thread-local detail string) */
@@ -59,6 +71,9 @@ void ecg_build_ptbl(unsigned char c, ecg_ptbl_t *t);
 int ecg_recov_rows(int k, int p, const unsigned char *en_matrix,
 		   const uint32_t *err_list, int nerrs, unsigned char *rows,
 		   uint32_t *out_idx, uint32_t *dec_idx, int *reused_encode);
+
+/* pointer tables (ecg_ptrs.c) */
+void ecg_scratch_free(ecg_ctx_t *ctx);
 
 /* checksums (ecg_csum.c) */
 void ecg_csum_ctx_fini(ecg_ctx_t *ctx);

@@ -1,0 +1,303 @@
+/*
+ * ecg_ptrs.c -- pointer-table products and the scatter-gather encode of the
+ * DAOS client (include/ecg.h ecg_matmul_ptrs, include/ecg_daos.h
+ * ecg_obj_ec_recx_encode).
+ *
+ * ISA-L's interface takes one array of cell pointers per stripe
+ * (ec_encode_data(len, k, rows, tbls, data[], coding[])); the client's encode
+ * loop hands it cells that live wherever the user's scatter-gather list put
+ * them (ref:src/object/cli_ec.c:476-546, 593-663).  Here the per-stripe
+ * pointer arrays of a whole batch become one device table and one launch of
+ * ecg_mm_ptr_kernel.
+ *
+ * Scratch (per context, ctx->lock): pinned staging + device copy of the
+ * pointer table, and device space for cells gathered from several iovs.  The
+ * event `done` is recorded after every launch that reads the scratch; the
+ * next user waits for it before overwriting, whatever its stream.
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "ecg_internal.h"
+#include "../../../include/ecg_daos.h"
+
+static int scratch_reserve(ecg_ctx_t *ctx, size_t pin_bytes, size_t dev_bytes)
+{
+	struct ecg_scratch *sc = &ctx->scratch;
+	hipError_t e;
+
+	if (sc->done == NULL) {
+		e = hipEventCreateWithFlags(&sc->done, hipEventDisableTiming);
+		if (e != hipSuccess)
+			return ecg_hip_fail(e, "scratch event");
+	}
+	if (sc->pending) {		/* previous launch still reading the scratch? */
+		e = hipEventSynchronize(sc->done);
+		if (e != hipSuccess)
+			return ecg_hip_fail(e, "scratch wait");
+		sc->pending = 0;
+	}
+	if (pin_bytes > sc->pin_bytes) {
+		if (sc->pin)
+			(void)hipHostFree(sc->pin);
+		sc->pin = NULL;
+		sc->pin_bytes = 0;
+		e = hipHostMalloc(&sc->pin, pin_bytes, hipHostMallocDefault);
+		if (e != hipSuccess)
+			return ecg_hip_fail(e, "scratch pinned alloc");
+		sc->pin_bytes = pin_bytes;
+	}
+	if (dev_bytes > sc->dev_bytes) {
+		if (sc->dev)
+			(void)hipFree(sc->dev);
+		sc->dev = NULL;
+		sc->dev_bytes = 0;
+		e = hipMalloc(&sc->dev, dev_bytes);
+		if (e != hipSuccess)
+			return ecg_hip_fail(e, "scratch device alloc");
+		sc->dev_bytes = dev_bytes;
+	}
+	return 0;
+}
+
+void ecg_scratch_free(ecg_ctx_t *ctx)
+{
+	struct ecg_scratch *sc = &ctx->scratch;
+
+	if (sc->pending && sc->done)
+		(void)hipEventSynchronize(sc->done);
+	if (sc->pin)
+		(void)hipHostFree(sc->pin);
+	if (sc->dev)
+		(void)hipFree(sc->dev);
+	if (sc->done)
+		(void)hipEventDestroy(sc->done);
+	memset(sc, 0, sizeof(*sc));
+}
+
+/* table already in sc->pin (n entries); copy, launch, record (ctx->lock held) */
+static int launch_table(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, uint64_t C,
+			uint32_t S, int aligned, hipStream_t st)
+{
+	struct ecg_scratch *sc = &ctx->scratch;
+	const size_t tbytes = (size_t)S * (size_t)(k + rows) * sizeof(uint64_t);
+	ecg_mm_params_t *prm;
+	uint32_t kid = 0;
+	hipError_t e;
+	int r, j, ke;
+
+	e = hipMemcpyAsync(sc->dev, sc->pin, tbytes, hipMemcpyHostToDevice, st);
+	if (e != hipSuccess)
+		return ecg_hip_fail(e, "pointer table H2D");
+	prm = calloc(1, sizeof(*prm));
+	if (prm == NULL)
+		return ecg_fail(-ECG_DER_NOMEM, "matmul_ptrs: calloc");
+	ecg_gf_init();
+	prm->cell_bytes = C;
+	prm->nstripes = S;
+	prm->k = (uint32_t)k;
+	prm->rows = (uint32_t)rows;
+	for (r = 0; r < rows; r++)
+		for (j = 0; j < k; j++)
+			ecg_build_ptbl(coef[(size_t)r * k + j], &prm->tbl[r][j]);
+	ke = ecg_k_launch_matmul_ptrs(prm, (const uint64_t *)sc->dev, aligned, &ctx->cfg, (void *)st,
+				      &kid);
+	free(prm);
+	if (ke != 0)
+		return ecg_hip_fail((hipError_t)ke, "pointer-table kernel launch");
+	e = hipEventRecord(sc->done, st);
+	if (e != hipSuccess)
+		return ecg_hip_fail(e, "scratch event record");
+	sc->pending = 1;
+	ecg_set_last_kernel(ecg_k_kernel_name(kid));
+	return 0;
+}
+
+int ecg_matmul_ptrs(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, uint64_t cell_bytes,
+		    uint32_t nstripes, void *const *cells, void *stream)
+{
+	const size_t n = (size_t)nstripes * (size_t)(k + rows);
+	uint64_t bits = cell_bytes;
+	hipStream_t st;
+	int rc;
+
+	if (ctx == NULL || coef == NULL || (nstripes && cells == NULL))
+		return ecg_fail(-ECG_DER_INVAL, "matmul_ptrs: NULL argument");
+	if (k < 1 || k > ECG_KMAX_K || rows < 1 || rows > ECG_KMAX_R)
+		return ecg_fail(-ECG_DER_INVAL, "matmul_ptrs: k=%d rows=%d (max %d x %d)", k, rows,
+				ECG_KMAX_K, ECG_KMAX_R);
+	if (cell_bytes == 0 || nstripes == 0)
+		return 0;
+	for (size_t i = 0; i < n; i++) {
+		if (cells[i] == NULL)
+			return ecg_fail(-ECG_DER_INVAL, "matmul_ptrs: NULL cell %zu", i);
+		bits |= (uint64_t)(uintptr_t)cells[i];
+	}
+	rc = ecg_ctx_enter(ctx);
+	if (rc)
+		return rc;
+	st = ecg_pick_stream(ctx, stream);
+	pthread_mutex_lock(&ctx->lock);
+	rc = scratch_reserve(ctx, n * sizeof(uint64_t), n * sizeof(uint64_t));
+	if (rc == 0) {
+		memcpy(ctx->scratch.pin, cells, n * sizeof(uint64_t));
+		rc = launch_table(ctx, k, rows, coef, cell_bytes, nstripes, (bits & 15u) == 0, st);
+	}
+	pthread_mutex_unlock(&ctx->lock);
+	return rc;
+}
+
+/* ---- obj_ec_recx_encode over a device-resident sgl ---------------------- */
+
+struct sgl_cur {
+	const ecg_iov_t *iovs;
+	uint32_t nr, idx;
+	uint64_t off;
+};
+
+static uint64_t iov_left(const struct sgl_cur *c)
+{
+	return c->idx < c->nr ? c->iovs[c->idx].iov_buf_len - c->off : 0;
+}
+
+/* daos_sgl_move (ref:src/include/daos/common.h:419-433): landing exactly on
+ * an iov's end steps to the next iov.  Returns bytes actually moved. */
+static uint64_t sgl_move(struct sgl_cur *c, uint64_t dist)
+{
+	uint64_t moved = 0;
+
+	while (moved < dist && c->idx < c->nr) {
+		uint64_t left = iov_left(c), step = left < dist - moved ? left : dist - moved;
+
+		c->off += step;
+		moved += step;
+		if (iov_left(c) == 0) {
+			c->idx++;
+			c->off = 0;
+		}
+	}
+	return moved;
+}
+
+/* Walk the recxs over the sgl exactly as obj_ec_recx_encode /
+ * obj_ec_stripe_encode do (ref:src/object/cli_ec.c:493-541, 625-660): a data
+ * cell wholly inside the current iov is used in place, any other is gathered
+ * (D2D copies) into gbase.  tbl == NULL: dry run that only counts the
+ * gathered cells.  Fills tbl[n*(k+p) + c] with cell addresses. */
+static int sgl_walk(const ecg_iov_t *iovs, uint32_t iov_nr, const ecg_ec_recx_t *recxs,
+		    uint32_t recx_nr, int k, int p, uint64_t C, unsigned char *const *pbufs,
+		    uint64_t *tbl, unsigned char *gbase, hipStream_t st, uint64_t *ngather,
+		    uint64_t *bits)
+{
+	struct sgl_cur cur = {iovs, iov_nr, 0, 0};
+	uint64_t last_off = 0, n = 0;
+
+	*ngather = 0;
+	for (uint32_t i = 0; i < recx_nr; i++) {
+		sgl_move(&cur, recxs[i].byte_off - last_off);		/* :630-633 */
+		last_off = recxs[i].byte_off;
+		for (uint32_t j = 0; j < recxs[i].stripe_nr; j++, n++) {
+			uint64_t *row = tbl ? tbl + n * (uint64_t)(k + p) : NULL;
+
+			for (int c = 0; c < k; c++) {
+				if (iov_left(&cur) >= C) {
+					if (row)
+						row[c] = (uint64_t)(uintptr_t)iovs[cur.idx].iov_buf + cur.off;
+					sgl_move(&cur, C);
+					continue;
+				}
+				unsigned char *dst = gbase ? gbase + *ngather * C : NULL;
+				uint64_t copied = 0;
+
+				(*ngather)++;
+				if (row)
+					row[c] = (uint64_t)(uintptr_t)dst;
+				while (copied < C) {
+					uint64_t left, cp;
+
+					if (cur.idx >= cur.nr)
+						return ecg_fail(-ECG_DER_REC2BIG,
+								"recx_encode: sgl shorter than the recxs");
+					left = iov_left(&cur);
+					cp = left < C - copied ? left : C - copied;
+					if (cp == 0) {			/* empty iov: next */
+						cur.idx++;
+						cur.off = 0;
+						continue;
+					}
+					if (row) {
+						hipError_t e = hipMemcpyAsync(
+							dst + copied,
+							(unsigned char *)iovs[cur.idx].iov_buf + cur.off, cp,
+							hipMemcpyDeviceToDevice, st);
+						if (e != hipSuccess)
+							return ecg_hip_fail(e, "recx_encode gather");
+					}
+					copied += sgl_move(&cur, cp);
+				}
+			}
+			if (row) {
+				for (int m = 0; m < p; m++)		/* oer_pbufs[m] + n*C, :637-640 */
+					row[k + m] = (uint64_t)(uintptr_t)pbufs[m] + n * C;
+				for (int c = 0; c < k + p; c++)
+					*bits |= row[c];
+			}
+		}
+		last_off += (uint64_t)recxs[i].stripe_nr * (uint64_t)k * C;	/* :655-656 */
+	}
+	return 0;
+}
+
+int ecg_obj_ec_recx_encode(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_bytes,
+			   const ecg_iov_t *iovs, uint32_t iov_nr, const ecg_ec_recx_t *recxs,
+			   uint32_t recx_nr, unsigned char *const *pbufs, void *stream)
+{
+	const struct ecg_obj_ec_codec *codec;
+	uint64_t S = 0, ngather = 0, bits = cell_bytes, tbytes;
+	int k, p, rc;
+	uint32_t i;
+	hipStream_t st;
+
+	if (ctx == NULL || iovs == NULL || recxs == NULL || pbufs == NULL || cell_bytes == 0)
+		return ecg_fail(-ECG_DER_INVAL, "recx_encode: bad arguments");
+	rc = ecg_obj_ec_class_kp(oc_id, &k, &p);
+	if (rc)
+		return rc;
+	codec = ecg_obj_ec_codec_get(oc_id);
+	if (codec == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "recx_encode: no codec for oc_id 0x%x", oc_id);
+	if (k > ECG_KMAX_K)
+		return ecg_fail(-ECG_DER_INVAL, "recx_encode: k=%d > %d", k, ECG_KMAX_K);
+	for (i = 0; i < recx_nr; i++) {
+		S += recxs[i].stripe_nr;
+		if (i && recxs[i].byte_off < recxs[i - 1].byte_off +
+					     (uint64_t)recxs[i - 1].stripe_nr * (uint64_t)k * cell_bytes)
+			return ecg_fail(-ECG_DER_INVAL, "recx_encode: recxs overlap or out of order");
+	}
+	if (S == 0)
+		return 0;
+	rc = sgl_walk(iovs, iov_nr, recxs, recx_nr, k, p, cell_bytes, pbufs, NULL, NULL, NULL,
+		      &ngather, &bits);	/* dry run: validate + count gathered cells */
+	if (rc)
+		return rc;
+	rc = ecg_ctx_enter(ctx);
+	if (rc)
+		return rc;
+	st = ecg_pick_stream(ctx, stream);
+	tbytes = (S * (uint64_t)(k + p) * sizeof(uint64_t) + 255) & ~255ull;
+
+	pthread_mutex_lock(&ctx->lock);
+	rc = scratch_reserve(ctx, S * (uint64_t)(k + p) * sizeof(uint64_t),
+			     tbytes + ngather * cell_bytes);
+	if (rc == 0)
+		rc = sgl_walk(iovs, iov_nr, recxs, recx_nr, k, p, cell_bytes, pbufs,
+			      (uint64_t *)ctx->scratch.pin, (unsigned char *)ctx->scratch.dev + tbytes,
+			      st, &ngather, &bits);
+	if (rc == 0)	/* gathers are on `st`, ahead of the table copy and the kernel */
+		rc = launch_table(ctx, k, p, &codec->ec_en_matrix[k * k], cell_bytes, (uint32_t)S,
+				  (bits & 15u) == 0, st);
+	else if (hipEventRecord(ctx->scratch.done, st) == hipSuccess)
+		ctx->scratch.pending = 1;	/* queued copies may still read the scratch */
+	pthread_mutex_unlock(&ctx->lock);
+	return rc;
+}

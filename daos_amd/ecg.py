@@ -50,6 +50,7 @@ _SIGS = [
     ("ecg_recover", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, vp, C.c_int64, u32p, C.c_int, vp]),
     ("ecg_update", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, C.c_int, u32p, vp, vp, C.c_int64,
                              vp, C.c_int64, C.c_int64, vp]),
+    ("ecg_matmul_ptrs", C.c_int, [vp, C.c_int, C.c_int, u8p, C.c_uint64, C.c_uint32, C.POINTER(vp), vp]),
     ("ecg_matmul_host", C.c_int, [vp, C.c_int, C.c_int, C.c_int, u8p, C.POINTER(u8p), C.POINTER(u8p), C.c_uint]),
     ("ecg_encode_host", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, vp, vp, C.c_uint32]),
     ("ecg_recover_host", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, vp, u32p, C.c_int, C.c_uint32]),
@@ -102,6 +103,8 @@ _SIGS = [
     ("ecg_agg_recalc_parity", C.c_int, [vp, C.c_uint32, C.c_uint64, u8p, C.c_uint32, u8p, u8p, u8p]),
     ("ecg_obj_ec_singv_cell_bytes", C.c_uint64, [C.c_uint32, C.c_uint64]),
     ("ecg_obj_ec_singv_encode", C.c_int, [C.c_uint32, C.c_uint64, u8p, C.POINTER(u8p)]),
+    ("ecg_obj_ec_recx_encode", C.c_int, [vp, C.c_uint32, C.c_uint64, vp, C.c_uint32, vp, C.c_uint32,
+                                         C.POINTER(vp), vp]),
     ("ecg_obj_ec_stripe_rec_nr", C.c_uint64, [C.c_uint32, C.c_uint64]),
     ("ecg_obj_ec_cell_bytes", C.c_uint64, [C.c_uint64, C.c_uint64]),
     ("ecg_obj_ec_tgt_of_recx_idx", C.c_uint32, [C.c_uint64, C.c_uint64, C.c_uint64]),
@@ -125,6 +128,16 @@ _SIGS = [
 HASH_CRC16, HASH_CRC32, HASH_CRC64, HASH_ADLER32 = 1, 2, 3, 7
 
 EXPORTED = [n for n, _, _ in _SIGS]
+
+
+class Iov(C.Structure):
+    """ecg_iov_t (d_iov_t's iov_buf / iov_buf_len), device memory."""
+    _fields_ = [("iov_buf", vp), ("iov_buf_len", C.c_uint64)]
+
+
+class EcRecx(C.Structure):
+    """ecg_ec_recx_t (struct obj_ec_recx: oer_byte_off, oer_stripe_nr)."""
+    _fields_ = [("byte_off", C.c_uint64), ("stripe_nr", C.c_uint32), ("pad", C.c_uint32)]
 
 _lib = None
 
@@ -361,6 +374,13 @@ class Context:
                      err_list: Sequence[int], htype: int, chunksize: int, rec_size: int, csums: int, stream=None):
         _chk(lib().ecg_recover_csum(self.h, k, p, cell_bytes, nstripes, stripes, stripe_stride, _u32(err_list),
                                     len(err_list), htype, chunksize, rec_size, csums, stream), "recover_csum")
+
+    def matmul_ptrs(self, k: int, rows: int, coef: np.ndarray, cell_bytes: int, nstripes: int,
+                    cells: Sequence[int], stream=None):
+        """cells[s*(k+rows)+j]: device addresses (inputs then outputs) per stripe."""
+        co = np.ascontiguousarray(coef, dtype=np.uint8).reshape(-1)
+        arr = (vp * len(cells))(*cells)
+        _chk(lib().ecg_matmul_ptrs(self.h, k, rows, _u8(co), cell_bytes, nstripes, arr, stream), "matmul_ptrs")
 
     def encode_host(self, k: int, p: int, cell_bytes: int, nstripes: int, data: np.ndarray, parity: np.ndarray,
                     chunk: int = 0):

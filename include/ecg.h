@@ -213,6 +213,16 @@ int ecg_dev_copy_kernel(ecg_ctx_t *ctx, void *dst, const void *src, size_t bytes
  * variant: 0 auto, 1 runtime-shaped kernel, 2 byte kernel. */
 int ecg_set_launch(ecg_ctx_t *ctx, uint32_t grid_x, uint32_t grid_y, uint32_t variant);
 
+/* Pointer-table product: ISA-L's per-stripe pointer arrays
+ * (ec_encode_data(len, k, rows, tbls, data[], coding[])) batched over
+ * nstripes.  cells[s*(k+rows) + j] is the DEVICE address of input cell j
+ * (j < k) or output cell j-k of stripe s; the table itself is a host array
+ * (copied before return is not required: it is staged internally).  k <= 16,
+ * rows <= 8; any alignment (16-byte aligned cells take the vector kernel).
+ * Asynchronous on `stream`. */
+int ecg_matmul_ptrs(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef,
+		    uint64_t cell_bytes, uint32_t nstripes, void *const *cells, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

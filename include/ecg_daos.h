@@ -143,6 +143,31 @@ uint64_t ecg_obj_ec_singv_cell_bytes(uint32_t oc_id, uint64_t iod_size);
 int ecg_obj_ec_singv_encode(uint32_t oc_id, uint64_t iod_size, const unsigned char *value,
 			    unsigned char *p_bufs[]);
 
+/* ---- client full-stripe encode over a scatter-gather list --------------
+ * obj_ec_recx_encode + obj_ec_stripe_encode (ref:src/object/cli_ec.c:476-546,
+ * 593-663) for an array iod whose sgl and parity buffers are in device
+ * memory.  The sgl is walked exactly as the reference does (daos_sgl_move
+ * semantics, iov_buf_len): for recx i the cursor moves to byte_off, then
+ * stripe_nr full stripes of k cells are consumed; a cell wholly inside one
+ * iov is encoded in place, a cell spanning iovs is gathered on the device
+ * first.  Parity of the n-th stripe overall goes to pbufs[m] + n*cell_bytes
+ * (oer_pbufs).  One launch for all stripes.  -DER_REC2BIG when the sgl runs
+ * out (as the reference), -DER_INVAL for recxs out of order. */
+typedef struct ecg_iov {	/* d_iov_t: iov_buf, iov_buf_len (device memory) */
+	void *iov_buf;
+	uint64_t iov_buf_len;
+} ecg_iov_t;
+
+typedef struct ecg_ec_recx {	/* struct obj_ec_recx: oer_byte_off, oer_stripe_nr */
+	uint64_t byte_off;
+	uint32_t stripe_nr;
+	uint32_t pad;
+} ecg_ec_recx_t;
+
+int ecg_obj_ec_recx_encode(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_bytes,
+			   const ecg_iov_t *iovs, uint32_t iov_nr, const ecg_ec_recx_t *recxs,
+			   uint32_t recx_nr, unsigned char *const *pbufs, void *stream);
+
 /* ---- stripe / index math (ref:src/object/obj_ec.h:271-350) -------------
  * e_len = records per cell (oca->u.ec.e_len), stripe_rec_nr = k * e_len.
  * Parity extents carry ECG_EC_PARITY_BIT in their VOS index
