@@ -252,7 +252,7 @@ int ecg_obj_ec_recx_encode(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_bytes,
 			   const ecg_iov_t *iovs, uint32_t iov_nr, const ecg_ec_recx_t *recxs,
 			   uint32_t recx_nr, unsigned char *const *pbufs, void *stream)
 {
-	const struct ecg_obj_ec_codec *codec;
+	unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
 	uint64_t S = 0, ngather = 0, bits = cell_bytes, tbytes;
 	int k, p, rc;
 	uint32_t i;
@@ -263,9 +263,7 @@ int ecg_obj_ec_recx_encode(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_bytes,
 	rc = ecg_obj_ec_class_kp(oc_id, &k, &p);
 	if (rc)
 		return rc;
-	codec = ecg_obj_ec_codec_get(oc_id);
-	if (codec == NULL)
-		return ecg_fail(-ECG_DER_INVAL, "recx_encode: no codec for oc_id 0x%x", oc_id);
+	ecg_gen_cauchy1(k, p, en);	/* the codec's matrix, ref:src/object/obj_class.c:614 */
 	if (k > ECG_KMAX_K)
 		return ecg_fail(-ECG_DER_INVAL, "recx_encode: k=%d > %d", k, ECG_KMAX_K);
 	for (i = 0; i < recx_nr; i++) {
@@ -294,7 +292,7 @@ int ecg_obj_ec_recx_encode(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_bytes,
 			      (uint64_t *)ctx->scratch.pin, (unsigned char *)ctx->scratch.dev + tbytes,
 			      st, &ngather, &bits);
 	if (rc == 0)	/* gathers are on `st`, ahead of the table copy and the kernel */
-		rc = launch_table(ctx, k, p, &codec->ec_en_matrix[k * k], cell_bytes, (uint32_t)S,
+		rc = launch_table(ctx, k, p, &en[k * k], cell_bytes, (uint32_t)S,
 				  (bits & 15u) == 0, st);
 	else if (hipEventRecord(ctx->scratch.done, st) == hipSuccess)
 		ctx->scratch.pending = 1;	/* queued copies may still read the scratch */

@@ -57,7 +57,7 @@ def _split_sgl(rng, total, C, n_iov, zero_iovs):
 
 
 @pytest.mark.parametrize("k,p,C,recx_plan,n_iov,zeros", [
-    (4, 2, 8192, [(0, 3), (40960, 2)], 1, 0),              # one iov: every cell in place
+    (4, 2, 8192, [(0, 3), (131072, 2)], 1, 0),             # one iov: every cell in place
     (8, 2, 4096, [(0, 4), (4096 * 8 * 6, 3)], 7, 2),        # cells cut across iovs, empty iovs
     (2, 1, 1000, [(0, 5), (30000, 4), (60000, 1)], 23, 3),  # unaligned cells
     (16, 2, 16384, [(16384 * 16, 3)], 5, 1),                # leading gap
