@@ -33,15 +33,22 @@ struct ecg_stage {
 	hipEvent_t done[ECG_NSLOT];
 };
 
-/* Pointer tables and gathered cells (ecg_ptrs.c), guarded by ctx->lock and
- * the `done` event of the last launch that read them. */
-struct ecg_scratch {
+/* Pointer tables and gathered cells (ecg_ptrs.c): two slots used in turn,
+ * each guarded by ctx->lock and the `done` event of the last launch that read
+ * it, so a call only waits for the launch before last. */
+#define ECG_NSCRATCH 2
+struct ecg_scratch_slot {
 	void *pin;
 	size_t pin_bytes;
 	void *dev;
 	size_t dev_bytes;
 	hipEvent_t done;
 	int pending;
+};
+
+struct ecg_scratch {
+	struct ecg_scratch_slot slot[ECG_NSCRATCH];
+	unsigned next;
 };
 
 struct ecg_ctx {

@@ -21,17 +21,20 @@
 #include "ecg_internal.h"
 #include "../../../include/ecg_daos.h"
 
-static int scratch_reserve(ecg_ctx_t *ctx, size_t pin_bytes, size_t dev_bytes)
+/* Next scratch slot, grown to size and free of readers (ctx->lock held). */
+static int scratch_reserve(ecg_ctx_t *ctx, size_t pin_bytes, size_t dev_bytes,
+			   struct ecg_scratch_slot **out)
 {
-	struct ecg_scratch *sc = &ctx->scratch;
+	struct ecg_scratch_slot *sc = &ctx->scratch.slot[ctx->scratch.next];
 	hipError_t e;
 
+	ctx->scratch.next = (ctx->scratch.next + 1) % ECG_NSCRATCH;
 	if (sc->done == NULL) {
 		e = hipEventCreateWithFlags(&sc->done, hipEventDisableTiming);
 		if (e != hipSuccess)
 			return ecg_hip_fail(e, "scratch event");
 	}
-	if (sc->pending) {		/* previous launch still reading the scratch? */
+	if (sc->pending) {		/* the launch before last still reading it? */
 		e = hipEventSynchronize(sc->done);
 		if (e != hipSuccess)
 			return ecg_hip_fail(e, "scratch wait");
@@ -57,29 +60,31 @@ static int scratch_reserve(ecg_ctx_t *ctx, size_t pin_bytes, size_t dev_bytes)
 			return ecg_hip_fail(e, "scratch device alloc");
 		sc->dev_bytes = dev_bytes;
 	}
+	*out = sc;
 	return 0;
 }
 
 void ecg_scratch_free(ecg_ctx_t *ctx)
 {
-	struct ecg_scratch *sc = &ctx->scratch;
+	for (int i = 0; i < ECG_NSCRATCH; i++) {
+		struct ecg_scratch_slot *sc = &ctx->scratch.slot[i];
 
-	if (sc->pending && sc->done)
-		(void)hipEventSynchronize(sc->done);
-	if (sc->pin)
-		(void)hipHostFree(sc->pin);
-	if (sc->dev)
-		(void)hipFree(sc->dev);
-	if (sc->done)
-		(void)hipEventDestroy(sc->done);
-	memset(sc, 0, sizeof(*sc));
+		if (sc->pending && sc->done)
+			(void)hipEventSynchronize(sc->done);
+		if (sc->pin)
+			(void)hipHostFree(sc->pin);
+		if (sc->dev)
+			(void)hipFree(sc->dev);
+		if (sc->done)
+			(void)hipEventDestroy(sc->done);
+	}
+	memset(&ctx->scratch, 0, sizeof(ctx->scratch));
 }
 
 /* table already in sc->pin (n entries); copy, launch, record (ctx->lock held) */
-static int launch_table(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, uint64_t C,
-			uint32_t S, int aligned, hipStream_t st)
+static int launch_table(ecg_ctx_t *ctx, struct ecg_scratch_slot *sc, int k, int rows,
+			const unsigned char *coef, uint64_t C, uint32_t S, int aligned, hipStream_t st)
 {
-	struct ecg_scratch *sc = &ctx->scratch;
 	const size_t tbytes = (size_t)S * (size_t)(k + rows) * sizeof(uint64_t);
 	ecg_mm_params_t *prm;
 	uint32_t kid = 0;
@@ -117,6 +122,7 @@ int ecg_matmul_ptrs(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, 
 		    uint32_t nstripes, void *const *cells, void *stream)
 {
 	const size_t n = (size_t)nstripes * (size_t)(k + rows);
+	struct ecg_scratch_slot *sc = NULL;
 	uint64_t bits = cell_bytes;
 	hipStream_t st;
 	int rc;
@@ -138,10 +144,10 @@ int ecg_matmul_ptrs(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, 
 		return rc;
 	st = ecg_pick_stream(ctx, stream);
 	pthread_mutex_lock(&ctx->lock);
-	rc = scratch_reserve(ctx, n * sizeof(uint64_t), n * sizeof(uint64_t));
+	rc = scratch_reserve(ctx, n * sizeof(uint64_t), n * sizeof(uint64_t), &sc);
 	if (rc == 0) {
-		memcpy(ctx->scratch.pin, cells, n * sizeof(uint64_t));
-		rc = launch_table(ctx, k, rows, coef, cell_bytes, nstripes, (bits & 15u) == 0, st);
+		memcpy(sc->pin, cells, n * sizeof(uint64_t));
+		rc = launch_table(ctx, sc, k, rows, coef, cell_bytes, nstripes, (bits & 15u) == 0, st);
 	}
 	pthread_mutex_unlock(&ctx->lock);
 	return rc;
@@ -253,6 +259,7 @@ int ecg_obj_ec_recx_encode(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_bytes,
 			   uint32_t recx_nr, unsigned char *const *pbufs, void *stream)
 {
 	unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
+	struct ecg_scratch_slot *sc = NULL;
 	uint64_t S = 0, ngather = 0, bits = cell_bytes, tbytes;
 	int k, p, rc;
 	uint32_t i;
@@ -286,16 +293,17 @@ int ecg_obj_ec_recx_encode(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_bytes,
 
 	pthread_mutex_lock(&ctx->lock);
 	rc = scratch_reserve(ctx, S * (uint64_t)(k + p) * sizeof(uint64_t),
-			     tbytes + ngather * cell_bytes);
-	if (rc == 0)
+			     tbytes + ngather * cell_bytes, &sc);
+	if (rc == 0) {
 		rc = sgl_walk(iovs, iov_nr, recxs, recx_nr, k, p, cell_bytes, pbufs,
-			      (uint64_t *)ctx->scratch.pin, (unsigned char *)ctx->scratch.dev + tbytes,
-			      st, &ngather, &bits);
-	if (rc == 0)	/* gathers are on `st`, ahead of the table copy and the kernel */
-		rc = launch_table(ctx, k, p, &en[k * k], cell_bytes, (uint32_t)S,
-				  (bits & 15u) == 0, st);
-	else if (hipEventRecord(ctx->scratch.done, st) == hipSuccess)
-		ctx->scratch.pending = 1;	/* queued copies may still read the scratch */
+			      (uint64_t *)sc->pin, (unsigned char *)sc->dev + tbytes, st, &ngather,
+			      &bits);
+		if (rc == 0)	/* gathers are on `st`, ahead of the table copy and the kernel */
+			rc = launch_table(ctx, sc, k, p, &en[k * k], cell_bytes, (uint32_t)S,
+					  (bits & 15u) == 0, st);
+		else if (hipEventRecord(sc->done, st) == hipSuccess)
+			sc->pending = 1;	/* queued copies may still read the scratch */
+	}
 	pthread_mutex_unlock(&ctx->lock);
 	return rc;
 }

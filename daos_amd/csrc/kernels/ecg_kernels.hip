@@ -469,16 +469,23 @@ ecg_mm_ptr_kernel(const ecg_mm_params_t P, const uint64_t *__restrict__ cells)
 
 	for (uint32_t s = blockIdx.y; s < P.nstripes; s += gridDim.y) {
 		const uint64_t *pt = cells + (uint64_t)s * (uint32_t)(k + rows);
+		uint64_t base[KM + RM];
+
+		// the stripe's addresses: one dependent (scalar) load per stripe, not
+		// per column -- the workgroup then walks several columns
+#pragma unroll
+		for (int j = 0; j < KM + RM; j++)
+			if (j < k || (j >= KM && j - KM < rows))
+				base[j] = pt[j < KM ? j : k + (j - KM)];
 		for (uint32_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
 			const uint64_t cbase = (uint64_t)ch * CHUNK_BYTES;
 			uint64_t a[KM + RM];
 			uint32_t z = 0;
 
-			// the stripe's addresses, loaded in uniform control flow (SGPRs)
 #pragma unroll
 			for (int j = 0; j < KM + RM; j++) {
 				if (j < k || (j >= KM && j - KM < rows)) {
-					a[j] = pt[j < KM ? j : k + (j - KM)] + cbase;
+					a[j] = base[j] + cbase;
 					asm volatile("" : "+s"(a[j]));
 				}
 			}

@@ -85,6 +85,9 @@ for what in "$@"; do
 		make -C tests/c > /dev/null || exit 2
 		step ctest 300 ./build/ctest/test_ecg_c || exit $?
 		;;
+	tune9)
+		step tune9 600 python tools/tune9.py || exit $?
+		;;
 	tune8)
 		step tune8 600 python tools/tune8.py || exit $?
 		;;
