@@ -126,9 +126,29 @@ typedef struct ecg_mmcs_params {
 	uint32_t row_slot[ECG_KMAX_R];
 } ecg_mmcs_params_t;
 
+/*
+ * Batched byte-range copies (kernels/ecg_copy_kernels.hip): segment s copies
+ * len bytes from src to dst (device addresses, any alignment, no overlap)
+ * and owns the launch's 16 KiB destination tiles [tile0, tile0 +
+ * ecg_k_copy_tiles(dst, len)); segments are listed in tile0 order from 0.
+ */
+typedef struct ecg_copy_seg {
+	uint64_t dst;
+	uint64_t src;
+	uint64_t len;
+	uint64_t tile0;
+} ecg_copy_seg_t;
+
+#define ECG_KID_COPY_SEGS 900
+
 #ifdef __cplusplus
 extern "C" {
 #endif
+/* Tiles one segment occupies (0 when len == 0). */
+uint64_t ecg_k_copy_tiles(uint64_t dst, uint64_t len);
+/* One launch of ntiles workgroups over nseg segments (segs_dev in device memory). */
+int ecg_k_launch_copy_segs(const ecg_copy_seg_t *segs_dev, uint32_t nseg, uint64_t ntiles,
+			   void *stream, uint32_t *kernel_id);
 /* Implemented in kernels/ecg_kernels.hip.  Returns a hipError_t value. */
 int ecg_k_launch_matmul(const ecg_mm_params_t *p, const ecg_launch_cfg_t *cfg,
 			void *stream, uint32_t *kernel_id);

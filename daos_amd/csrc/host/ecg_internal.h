@@ -81,6 +81,22 @@ int ecg_recov_rows(int k, int p, const unsigned char *en_matrix,
 
 /* pointer tables (ecg_ptrs.c) */
 void ecg_scratch_free(ecg_ctx_t *ctx);
+/* next scratch slot with at least these sizes, free of readers (ctx->lock held) */
+int ecg_scratch_reserve(ecg_ctx_t *ctx, size_t pin_bytes, size_t dev_bytes,
+			struct ecg_scratch_slot **out);
+
+/* batched segment copies (ecg_sgl.c).  A fixed list (cap preset, fixed = 1)
+ * writes into caller memory and fails instead of growing. */
+struct ecg_segs {
+	ecg_copy_seg_t *seg;
+	size_t n, cap;
+	uint64_t tiles;
+	int fixed;
+};
+int ecg_segs_add(struct ecg_segs *v, uint64_t dst, uint64_t src, uint64_t len);
+void ecg_segs_fini(struct ecg_segs *v);
+/* launch over a device copy of v->seg already queued on st */
+int ecg_segs_launch(const struct ecg_segs *v, const void *segs_dev, hipStream_t st);
 
 /* checksums (ecg_csum.c) */
 void ecg_csum_ctx_fini(ecg_ctx_t *ctx);

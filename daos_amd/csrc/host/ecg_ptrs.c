@@ -22,7 +22,7 @@
 #include "../../../include/ecg_daos.h"
 
 /* Next scratch slot, grown to size and free of readers (ctx->lock held). */
-static int scratch_reserve(ecg_ctx_t *ctx, size_t pin_bytes, size_t dev_bytes,
+int ecg_scratch_reserve(ecg_ctx_t *ctx, size_t pin_bytes, size_t dev_bytes,
 			   struct ecg_scratch_slot **out)
 {
 	struct ecg_scratch_slot *sc = &ctx->scratch.slot[ctx->scratch.next];
@@ -81,19 +81,30 @@ void ecg_scratch_free(ecg_ctx_t *ctx)
 	memset(&ctx->scratch, 0, sizeof(ctx->scratch));
 }
 
-/* table already in sc->pin (n entries); copy, launch, record (ctx->lock held) */
+/* Table already in sc->pin (S x (k+rows) entries); copy, launch, record
+ * (ctx->lock held).  With `gather`, its segment table follows the pointer
+ * table at byte seg_off of the slot (pinned and device alike): both travel in
+ * one H2D and the gather copies run before the product. */
 static int launch_table(ecg_ctx_t *ctx, struct ecg_scratch_slot *sc, int k, int rows,
-			const unsigned char *coef, uint64_t C, uint32_t S, int aligned, hipStream_t st)
+			const unsigned char *coef, uint64_t C, uint32_t S, int aligned, hipStream_t st,
+			const struct ecg_segs *gather, size_t seg_off)
 {
-	const size_t tbytes = (size_t)S * (size_t)(k + rows) * sizeof(uint64_t);
+	size_t tbytes = (size_t)S * (size_t)(k + rows) * sizeof(uint64_t);
 	ecg_mm_params_t *prm;
 	uint32_t kid = 0;
 	hipError_t e;
 	int r, j, ke;
 
+	if (gather && gather->n)
+		tbytes = seg_off + gather->n * sizeof(ecg_copy_seg_t);
 	e = hipMemcpyAsync(sc->dev, sc->pin, tbytes, hipMemcpyHostToDevice, st);
 	if (e != hipSuccess)
 		return ecg_hip_fail(e, "pointer table H2D");
+	if (gather && gather->n) {
+		r = ecg_segs_launch(gather, (unsigned char *)sc->dev + seg_off, st);
+		if (r)
+			return r;
+	}
 	prm = calloc(1, sizeof(*prm));
 	if (prm == NULL)
 		return ecg_fail(-ECG_DER_NOMEM, "matmul_ptrs: calloc");
@@ -144,10 +155,10 @@ int ecg_matmul_ptrs(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, 
 		return rc;
 	st = ecg_pick_stream(ctx, stream);
 	pthread_mutex_lock(&ctx->lock);
-	rc = scratch_reserve(ctx, n * sizeof(uint64_t), n * sizeof(uint64_t), &sc);
+	rc = ecg_scratch_reserve(ctx, n * sizeof(uint64_t), n * sizeof(uint64_t), &sc);
 	if (rc == 0) {
 		memcpy(sc->pin, cells, n * sizeof(uint64_t));
-		rc = launch_table(ctx, sc, k, rows, coef, cell_bytes, nstripes, (bits & 15u) == 0, st);
+		rc = launch_table(ctx, sc, k, rows, coef, cell_bytes, nstripes, (bits & 15u) == 0, st, NULL, 0);
 	}
 	pthread_mutex_unlock(&ctx->lock);
 	return rc;
@@ -188,17 +199,19 @@ static uint64_t sgl_move(struct sgl_cur *c, uint64_t dist)
 /* Walk the recxs over the sgl exactly as obj_ec_recx_encode /
  * obj_ec_stripe_encode do (ref:src/object/cli_ec.c:493-541, 625-660): a data
  * cell wholly inside the current iov is used in place, any other is gathered
- * (D2D copies) into gbase.  tbl == NULL: dry run that only counts the
- * gathered cells.  Fills tbl[n*(k+p) + c] with cell addresses. */
+ * into gbase (one copy segment per piece, added to `segs`).  tbl == NULL: dry
+ * run that only counts the gathered cells and their pieces.  Fills
+ * tbl[n*(k+p) + c] with cell addresses. */
 static int sgl_walk(const ecg_iov_t *iovs, uint32_t iov_nr, const ecg_ec_recx_t *recxs,
 		    uint32_t recx_nr, int k, int p, uint64_t C, unsigned char *const *pbufs,
-		    uint64_t *tbl, unsigned char *gbase, hipStream_t st, uint64_t *ngather,
-		    uint64_t *bits)
+		    uint64_t *tbl, unsigned char *gbase, struct ecg_segs *segs, uint64_t *ngather,
+		    uint64_t *npieces, uint64_t *bits)
 {
 	struct sgl_cur cur = {iovs, iov_nr, 0, 0};
 	uint64_t last_off = 0, n = 0;
 
 	*ngather = 0;
+	*npieces = 0;
 	for (uint32_t i = 0; i < recx_nr; i++) {
 		sgl_move(&cur, recxs[i].byte_off - last_off);		/* :630-633 */
 		last_off = recxs[i].byte_off;
@@ -231,13 +244,13 @@ static int sgl_walk(const ecg_iov_t *iovs, uint32_t iov_nr, const ecg_ec_recx_t 
 						cur.off = 0;
 						continue;
 					}
+					(*npieces)++;
 					if (row) {
-						hipError_t e = hipMemcpyAsync(
-							dst + copied,
-							(unsigned char *)iovs[cur.idx].iov_buf + cur.off, cp,
-							hipMemcpyDeviceToDevice, st);
-						if (e != hipSuccess)
-							return ecg_hip_fail(e, "recx_encode gather");
+						int rc = ecg_segs_add(
+							segs, (uint64_t)(uintptr_t)(dst + copied),
+							(uint64_t)(uintptr_t)iovs[cur.idx].iov_buf + cur.off, cp);
+						if (rc)
+							return rc;
 					}
 					copied += sgl_move(&cur, cp);
 				}
@@ -260,7 +273,7 @@ int ecg_obj_ec_recx_encode(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_bytes,
 {
 	unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
 	struct ecg_scratch_slot *sc = NULL;
-	uint64_t S = 0, ngather = 0, bits = cell_bytes, tbytes;
+	uint64_t S = 0, ngather = 0, npieces = 0, bits = cell_bytes, tbytes, sbytes;
 	int k, p, rc;
 	uint32_t i;
 	hipStream_t st;
@@ -282,27 +295,27 @@ int ecg_obj_ec_recx_encode(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_bytes,
 	if (S == 0)
 		return 0;
 	rc = sgl_walk(iovs, iov_nr, recxs, recx_nr, k, p, cell_bytes, pbufs, NULL, NULL, NULL,
-		      &ngather, &bits);	/* dry run: validate + count gathered cells */
+		      &ngather, &npieces, &bits);	/* dry run: validate + count gathers */
 	if (rc)
 		return rc;
 	rc = ecg_ctx_enter(ctx);
 	if (rc)
 		return rc;
 	st = ecg_pick_stream(ctx, stream);
+	/* slot layout: [pointer table | gather segments | gathered cells (dev)] */
 	tbytes = (S * (uint64_t)(k + p) * sizeof(uint64_t) + 255) & ~255ull;
+	sbytes = (npieces * sizeof(ecg_copy_seg_t) + 255) & ~255ull;
 
 	pthread_mutex_lock(&ctx->lock);
-	rc = scratch_reserve(ctx, S * (uint64_t)(k + p) * sizeof(uint64_t),
-			     tbytes + ngather * cell_bytes, &sc);
+	rc = ecg_scratch_reserve(ctx, tbytes + sbytes, tbytes + sbytes + ngather * cell_bytes, &sc);
 	if (rc == 0) {
-		rc = sgl_walk(iovs, iov_nr, recxs, recx_nr, k, p, cell_bytes, pbufs,
-			      (uint64_t *)sc->pin, (unsigned char *)sc->dev + tbytes, st, &ngather,
-			      &bits);
-		if (rc == 0)	/* gathers are on `st`, ahead of the table copy and the kernel */
+		struct ecg_segs segs = {(ecg_copy_seg_t *)((unsigned char *)sc->pin + tbytes), 0, npieces, 0, 1};
+
+		rc = sgl_walk(iovs, iov_nr, recxs, recx_nr, k, p, cell_bytes, pbufs, (uint64_t *)sc->pin,
+			      (unsigned char *)sc->dev + tbytes + sbytes, &segs, &ngather, &npieces, &bits);
+		if (rc == 0)	/* one H2D of both tables, gather launch, product launch */
 			rc = launch_table(ctx, sc, k, p, &en[k * k], cell_bytes, (uint32_t)S,
-					  (bits & 15u) == 0, st);
-		else if (hipEventRecord(sc->done, st) == hipSuccess)
-			sc->pending = 1;	/* queued copies may still read the scratch */
+					  (bits & 15u) == 0, st, &segs, tbytes);
 	}
 	pthread_mutex_unlock(&ctx->lock);
 	return rc;

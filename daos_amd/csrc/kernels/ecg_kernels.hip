@@ -714,6 +714,8 @@ extern "C" const char *ecg_k_kernel_name(uint32_t id)
 		return g_pkernels[id - KID_PTR].name;
 	if (id == KID_PTR_BYTE)
 		return "ecg_mm_ptr_byte_kernel";
+	if (id == ECG_KID_COPY_SEGS)
+		return "ecg_copy_segs_kernel";
 
 	return "?";
 }

@@ -105,6 +105,9 @@ _SIGS = [
     ("ecg_obj_ec_singv_encode", C.c_int, [C.c_uint32, C.c_uint64, u8p, C.POINTER(u8p)]),
     ("ecg_obj_ec_recx_encode", C.c_int, [vp, C.c_uint32, C.c_uint64, vp, C.c_uint32, vp, C.c_uint32,
                                          C.POINTER(vp), vp]),
+    ("ecg_obj_ec_stripe_list_init", C.c_int, [C.c_uint64, vp, C.c_uint32, vp, C.c_uint32, u32p]),
+    ("ecg_obj_ec_recov_fill_back", C.c_int, [vp, C.c_uint64, C.c_int, vp, C.c_uint32, vp, vp, C.c_uint32, vp,
+                                             C.c_uint32, vp, C.c_uint64, C.c_uint64, vp]),
     ("ecg_obj_ec_stripe_rec_nr", C.c_uint64, [C.c_uint32, C.c_uint64]),
     ("ecg_obj_ec_cell_bytes", C.c_uint64, [C.c_uint64, C.c_uint64]),
     ("ecg_obj_ec_tgt_of_recx_idx", C.c_uint32, [C.c_uint64, C.c_uint64, C.c_uint64]),
@@ -131,13 +134,31 @@ EXPORTED = [n for n, _, _ in _SIGS]
 
 
 class Iov(C.Structure):
-    """ecg_iov_t (d_iov_t's iov_buf / iov_buf_len), device memory."""
-    _fields_ = [("iov_buf", vp), ("iov_buf_len", C.c_uint64)]
+    """ecg_iov_t (d_iov_t: iov_buf, iov_buf_len, iov_len), device memory."""
+    _fields_ = [("iov_buf", vp), ("iov_buf_len", C.c_uint64), ("iov_len", C.c_uint64)]
 
 
 class EcRecx(C.Structure):
     """ecg_ec_recx_t (struct obj_ec_recx: oer_byte_off, oer_stripe_nr)."""
     _fields_ = [("byte_off", C.c_uint64), ("stripe_nr", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class Recx(C.Structure):
+    """ecg_recx_t (daos_recx_t)."""
+    _fields_ = [("rx_idx", C.c_uint64), ("rx_nr", C.c_uint64)]
+
+
+class RecxEp(C.Structure):
+    """ecg_recx_ep_t (struct daos_recx_ep)."""
+    _fields_ = [("re_recx", Recx), ("re_ep", C.c_uint64), ("re_rec_size", C.c_uint32), ("re_type", C.c_uint8)]
+
+
+class Sgl(C.Structure):
+    """ecg_sgl_t (d_sg_list_t) over device iov buffers."""
+    _fields_ = [("sg_nr", C.c_uint32), ("sg_nr_out", C.c_uint32), ("sg_iovs", C.POINTER(Iov))]
+
+
+DRT_SHADOW = 2
 
 _lib = None
 

@@ -153,9 +153,10 @@ int ecg_obj_ec_singv_encode(uint32_t oc_id, uint64_t iod_size, const unsigned ch
  * first.  Parity of the n-th stripe overall goes to pbufs[m] + n*cell_bytes
  * (oer_pbufs).  One launch for all stripes.  -DER_REC2BIG when the sgl runs
  * out (as the reference), -DER_INVAL for recxs out of order. */
-typedef struct ecg_iov {	/* d_iov_t: iov_buf, iov_buf_len (device memory) */
+typedef struct ecg_iov {	/* d_iov_t (ref:src/include/gurt/types.h:93-100), device buffer */
 	void *iov_buf;
 	uint64_t iov_buf_len;
+	uint64_t iov_len;
 } ecg_iov_t;
 
 typedef struct ecg_ec_recx {	/* struct obj_ec_recx: oer_byte_off, oer_stripe_nr */
@@ -167,6 +168,63 @@ typedef struct ecg_ec_recx {	/* struct obj_ec_recx: oer_byte_off, oer_stripe_nr 
 int ecg_obj_ec_recx_encode(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_bytes,
 			   const ecg_iov_t *iovs, uint32_t iov_nr, const ecg_ec_recx_t *recxs,
 			   uint32_t recx_nr, unsigned char *const *pbufs, void *stream);
+
+/* ---- degraded read: stripe list and fill-back ---------------------------
+ * After a degraded fetch the client reads whole stripes of the records it
+ * could not get (the "stripe list", obj_ec_stripe_list_init/_add,
+ * ref:src/object/cli_ec.c:2252-2381) into one [stripes][k+p][C] buffer,
+ * regenerates the lost cells (ecg_recover / obj_ec_recov_stripe), then
+ * copies the records it was missing back into the user's sgl
+ * (obj_ec_recov_fill_back + obj_ec_sgl_copy, :2645-2812).  Types mirror
+ * daos_recx_t, struct daos_recx_ep (ref:src/include/daos/object.h:714-719)
+ * and d_sg_list_t (ref:src/include/gurt/types.h:127-132). */
+typedef struct ecg_recx {	/* daos_recx_t */
+	uint64_t rx_idx;
+	uint64_t rx_nr;
+} ecg_recx_t;
+
+#define ECG_DRT_SHADOW		2	/* DRT_SHADOW: a to-be-recovered recx */
+
+typedef struct ecg_recx_ep {	/* struct daos_recx_ep */
+	ecg_recx_t re_recx;
+	uint64_t re_ep;
+	uint32_t re_rec_size;
+	uint8_t re_type;
+} ecg_recx_ep_t;
+
+typedef struct ecg_sgl {	/* d_sg_list_t, iov buffers in device memory */
+	uint32_t sg_nr;
+	uint32_t sg_nr_out;
+	ecg_iov_t *sg_iovs;
+} ecg_sgl_t;
+
+/* obj_ec_stripe_list_init for one array iod: every DRT_SHADOW recx rounded
+ * out to whole stripes of stripe_rec_nr records, merged into stripes[] in
+ * the reference's order (overlapping entries merge whatever their epochs,
+ * keeping the higher; adjacent ones only with equal epochs).  *stripe_nr =
+ * entries written.  cap >= recx_nr always suffices; -ECG_DER_INVAL if cap
+ * is exceeded or stripe_rec_nr == 0. */
+int ecg_obj_ec_stripe_list_init(uint64_t stripe_rec_nr, const ecg_recx_ep_t *recx, uint32_t recx_nr,
+				ecg_recx_ep_t *stripes, uint32_t cap, uint32_t *stripe_nr);
+
+/* obj_ec_recov_fill_back for one iod: copy the recovered records of each
+ * recov recx from the stripe buffer (device, stripe n of the stripe list at
+ * stripe_buf + n * stripe_total_sz, its records from byte 0 in index order)
+ * to their place in the user sgl (offset = records of the iod recxs before
+ * it times iod_size), with the reference's sgl bookkeeping: iov_len grows
+ * over copied bytes, sg_nr_out is set by the last copy.  singv != 0: single
+ * value, iod_size bytes from stripe_buf[0] (recxs ignored).  All copies go
+ * to `stream` as one launch; the host structs are updated on return.
+ * -ECG_DER_INVAL where the reference asserts (a recov recx starting before
+ * the iod recx it overlaps, stripe recxs not whole stripes, a recov recx not
+ * covered by the stripe list).  Iovs of zero capacity are skipped (the
+ * reference asserts). */
+int ecg_obj_ec_recov_fill_back(ecg_ctx_t *ctx, uint64_t iod_size, int singv,
+			       const ecg_recx_t *iod_recxs, uint32_t iod_nr, ecg_sgl_t *sgl,
+			       const ecg_recx_ep_t *recov, uint32_t recov_nr,
+			       const ecg_recx_ep_t *stripes, uint32_t stripe_nr,
+			       const void *stripe_buf, uint64_t stripe_total_sz, uint64_t stripe_rec_nr,
+			       void *stream);
 
 /* ---- stripe / index math (ref:src/object/obj_ec.h:271-350) -------------
  * e_len = records per cell (oca->u.ec.e_len), stripe_rec_nr = k * e_len.
