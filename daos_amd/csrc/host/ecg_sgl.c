@@ -128,20 +128,44 @@ static uint64_t sgl_get_bytes(const ecg_sgl_t *sgl, struct sgl_idx *idx, uint64_
 	return n;
 }
 
+/* Where daos_sgl_processor leaves idx after skipping `off` > 0 bytes
+ * (ref:src/common/misc.c:359-385), found by binary search over the prefix
+ * sums of the iov capacities (cap[i] = pre[i+1] - pre[i]) instead of the
+ * reference's walk from iov 0 on every copy: the first iov whose end
+ * reaches `off`, or the one after it when `off` is exactly that end. */
+static struct sgl_idx sgl_skip(const ecg_sgl_t *sgl, const uint64_t *pre, uint64_t off)
+{
+	struct sgl_idx idx = {sgl->sg_nr, 0};
+	uint32_t lo = 0, hi = sgl->sg_nr;
+
+	if (off == 0)
+		return (struct sgl_idx){0, 0};
+	if (sgl->sg_nr == 0 || pre[sgl->sg_nr] < off)
+		return idx;				/* sgl exhausted */
+	while (lo < hi) {				/* smallest i: pre[i+1] >= off */
+		const uint32_t mid = lo + (hi - lo) / 2;
+
+		if (pre[mid + 1] >= off)
+			hi = mid;
+		else
+			lo = mid + 1;
+	}
+	if (pre[lo + 1] == off)
+		return (struct sgl_idx){lo + 1, 0};
+	return (struct sgl_idx){lo, off - pre[lo]};
+}
+
 /* obj_ec_sgl_copy (ref:src/object/cli_ec.c:2681-2707): skip `off` bytes of
  * the sgl, then copy `size` bytes from src into it; oes_copy's iov_len
  * updates (:2653-2679) and the final sg_nr_out.  Copies what fits when the
  * sgl is short, as the reference does. */
-static int sgl_copy(ecg_sgl_t *sgl, uint64_t off, uint64_t src, uint64_t size, struct ecg_segs *v)
+static int sgl_copy(ecg_sgl_t *sgl, const uint64_t *pre, uint64_t off, uint64_t src, uint64_t size,
+		    struct ecg_segs *v)
 {
-	struct sgl_idx idx = {0, 0};
-	uint64_t req = off, copied = 0, addr = 0, n;
+	struct sgl_idx idx = sgl_skip(sgl, pre, off);
+	uint64_t req, copied = 0, addr = 0, n;
 	int have, end = 0, rc;
 
-	while (req > 0 && !end) {
-		n = sgl_get_bytes(sgl, &idx, req, &addr, &have, &end);
-		req -= n;
-	}
 	req = size;
 	end = 0;
 	while (req > 0 && !end) {
@@ -180,7 +204,7 @@ static uint64_t min64(uint64_t a, uint64_t b)
 
 /* The reference's fill-back walk (ref:src/object/cli_ec.c:2731-2811). */
 static int fill_back_walk(uint64_t iod_size, const ecg_recx_t *iod_recxs, uint32_t iod_nr, ecg_sgl_t *sgl,
-			  const ecg_recx_ep_t *recov, uint32_t recov_nr, const ecg_recx_ep_t *stripes,
+			  const uint64_t *pre, const ecg_recx_ep_t *recov, uint32_t recov_nr, const ecg_recx_ep_t *stripes,
 			  uint32_t stripe_nr, uint64_t sbuf, uint64_t stripe_total_sz, uint64_t stripe_rec_nr,
 			  struct ecg_segs *v)
 {
@@ -230,7 +254,7 @@ static int fill_back_walk(uint64_t iod_size, const ecg_recx_t *iod_recxs, uint32
 									"fill_back: record %lu not in the stripe list",
 									(unsigned long)ovl.rx_idx);
 						cnt = min64(ovl.rx_idx + ovl.rx_nr, sr.rx_idx + sr.rx_nr) - ovl.rx_idx;
-						rc = sgl_copy(sgl, iod_off,
+						rc = sgl_copy(sgl, pre, iod_off,
 							      sbuf + soff + iod_size * (ovl.rx_idx - sr.rx_idx),
 							      cnt * iod_size, v);
 						if (rc)
@@ -266,24 +290,33 @@ int ecg_obj_ec_recov_fill_back(ecg_ctx_t *ctx, uint64_t iod_size, int singv, con
 {
 	const uint64_t sbuf = (uint64_t)(uintptr_t)stripe_buf;
 	struct ecg_segs v = {0};
+	uint64_t *pre;
 	hipStream_t st;
 	int rc;
 
 	if (ctx == NULL || sgl == NULL || stripe_buf == NULL || (sgl->sg_nr && sgl->sg_iovs == NULL))
 		return ecg_fail(-ECG_DER_INVAL, "fill_back: NULL argument");
+	pre = malloc(((size_t)sgl->sg_nr + 1) * sizeof(*pre));	/* iov capacity prefix sums */
+	if (pre == NULL)
+		return ecg_fail(-ECG_DER_NOMEM, "fill_back: malloc");
+	pre[0] = 0;
+	for (uint32_t i = 0; i < sgl->sg_nr; i++)
+		pre[i + 1] = pre[i] + sgl->sg_iovs[i].iov_buf_len;
 	if (singv) {
-		rc = sgl_copy(sgl, 0, sbuf, iod_size, &v);		/* :2725-2729 */
+		rc = sgl_copy(sgl, pre, 0, sbuf, iod_size, &v);		/* :2725-2729 */
 	} else {
+		rc = 0;
 		if ((iod_nr && iod_recxs == NULL) || (recov_nr && recov == NULL) ||
 		    (stripe_nr && stripes == NULL) || stripe_rec_nr == 0)
-			return ecg_fail(-ECG_DER_INVAL, "fill_back: bad recx lists");
-		for (uint32_t j = 0; j < stripe_nr; j++)
+			rc = ecg_fail(-ECG_DER_INVAL, "fill_back: bad recx lists");
+		for (uint32_t j = 0; rc == 0 && j < stripe_nr; j++)
 			if (stripes[j].re_recx.rx_nr % stripe_rec_nr)		/* :2767 */
-				return ecg_fail(-ECG_DER_INVAL, "fill_back: stripe recx %u is not whole stripes",
-						j);
-		rc = fill_back_walk(iod_size, iod_recxs, iod_nr, sgl, recov, recov_nr, stripes, stripe_nr, sbuf,
-				    stripe_total_sz, stripe_rec_nr, &v);
+				rc = ecg_fail(-ECG_DER_INVAL, "fill_back: stripe recx %u is not whole stripes", j);
+		if (rc == 0)
+			rc = fill_back_walk(iod_size, iod_recxs, iod_nr, sgl, pre, recov, recov_nr, stripes,
+					    stripe_nr, sbuf, stripe_total_sz, stripe_rec_nr, &v);
 	}
+	free(pre);
 	if (rc == 0 && v.n) {
 		rc = ecg_ctx_enter(ctx);
 		if (rc == 0) {

@@ -6,9 +6,9 @@
 // segments with arbitrary byte alignment: one launch copies all of them.
 //
 // Work unit: a 16 KiB tile of one segment's destination (256 lanes x 4 x
-// 16 B).  Segment s owns tiles [tile0[s], tile0[s+1]); a workgroup finds its
-// segment by binary search over the tile0 column (wave-uniform scalar
-// loads).  Inside a segment the destination is split into
+// 16 B).  Segment s owns tiles [tile0[s], tile0[s+1]); each wave finds its
+// segment by a 64-ary search over the tile0 column.  Inside a segment the
+// destination is split into
 //   head  -- bytes up to the first 16-byte aligned destination address,
 //   body  -- 16-byte aligned destination words,
 //   tail  -- the < 16 bytes after the last whole word.
@@ -66,14 +66,21 @@ __device__ __forceinline__ u32x4 shift_pair(u32x4 a, u32x4 b, uint32_t q, uint32
 __global__ void __launch_bounds__(CP_BLOCK)
 ecg_copy_segs_kernel(const ecg_copy_seg_t *__restrict__ segs, uint32_t nseg)
 {
-	// this tile's segment: the last s with segs[s].tile0 <= blockIdx.x
-	uint32_t lo = 0, hi = nseg;
-	while (hi - lo > 1) {
-		const uint32_t mid = (lo + hi) / 2;
-		if (segs[mid].tile0 <= blockIdx.x)
-			lo = mid;
-		else
-			hi = mid;
+	// This tile's segment: the last s with segs[s].tile0 <= blockIdx.x.  A
+	// 64-ary search per wave: each round the lanes probe 64 evenly spaced
+	// entries of the bracket and a ballot picks the sub-bracket, so a list
+	// of up to 4096 segments costs two dependent loads instead of a binary
+	// search's dozen.
+	const uint32_t lane = threadIdx.x & 63u;
+	uint32_t lo = 0, n = nseg;
+	while (n > 1) {
+		const uint32_t step = (n + 63u) / 64u;
+		const bool in = lane * step < n;
+		const bool le = in && segs[lo + lane * step].tile0 <= blockIdx.x;
+		const uint32_t c = (uint32_t)__popcll(__ballot(le));	// >= 1: segs[lo] qualifies
+
+		lo += (c - 1u) * step;
+		n = n - (c - 1u) * step < step ? n - (c - 1u) * step : step;
 	}
 	const ecg_copy_seg_t sg = segs[lo];
 	const uint64_t t = blockIdx.x - sg.tile0;
@@ -114,8 +121,11 @@ ecg_copy_segs_kernel(const ecg_copy_seg_t *__restrict__ segs, uint32_t nseg)
 				st16(bd + w * 16, v[q]);
 		}
 	} else {
-		// word w needs source bytes bsa + 16w + sh .. + 15: the aligned
-		// words at bsa + 16w and bsa + 16w + 16, both holding segment bytes
+		// Word w needs source bytes bsa + 16w + sh .. + 15: the aligned
+		// words at bsa + 16w and bsa + 16w + 16, both holding segment bytes.
+		// (Taking the second word from the next lane with a shuffle instead
+		// of a second load measured the same: the extra 16 B per lane hits
+		// L1, the cost of a misaligned source is the extra line per wave.)
 		const uint8_t *bsa = bs - sh;
 		const uint32_t dq = sh >> 2, r = sh & 3u;
 		u32x4 a[CP_WORDS], b[CP_WORDS];

@@ -94,6 +94,17 @@ for what in "$@"; do
 	csum)
 		step bench_csum 600 python tools/bench_csum.py || exit $?
 		;;
+	cpubase)
+		step cpu_baselines 600 python tools/cpu_baselines.py || exit $?
+		;;
+	fillback)
+		step bench_fillback 300 python tools/bench_fillback.py || exit $?
+		;;
+	fillback_prof)
+		rm -rf gpurun_out/prof_fb
+		step rocprof_fillback 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_fb -o run \
+			-- python3 tools/bench_fillback.py || exit $?
+		;;
 	tune3)
 		step tune3 600 python tools/tune3.py || exit $?
 		;;
