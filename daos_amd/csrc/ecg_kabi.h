@@ -77,13 +77,16 @@ typedef struct ecg_launch_cfg {
  *   k[64]        x^(8*16*(63-lane)) mod P, for the final per-lane shift
  *   sh4k[NB][256] shift by ECG_MMCS_STRIDE zero bytes (fused kernels)
  *   k256[256]    x^(8*16*(255-thread)) mod P (fused kernels)
+ *   p2[48]       x^(8*2^j) mod P (shift by any byte count: product over its bits)
  * with NB = W/8, T = uint32_t (W <= 32) or uint64_t (W = 64).
  */
 #define ECG_CSUM_STRIDE 1024	/* bytes a wave consumes per step (64 lanes x 16 B) */
 #define ECG_KID_CSUM 1000	/* kernel ids of the checksum kernels start here */
 
 #define ECG_MMCS_STRIDE 4096	/* fused kernels: 256 threads x 16 B per step */
-#define ECG_CSUM_TBL_ENTRIES(NB) (3 * (NB) * 256 + 64 + 256)
+#define ECG_CSUM_NP2 48
+#define ECG_CSUM_TBL_ENTRIES(NB) (3 * (NB) * 256 + 64 + 256 + ECG_CSUM_NP2)
+#define ECG_CSUM_OFF_P2(NB) (3 * (NB) * 256 + 64 + 256)
 #define ECG_CSUM_OFF_SH(NB) ((NB) * 256)
 #define ECG_CSUM_OFF_K64(NB) (2 * (NB) * 256)
 #define ECG_CSUM_OFF_SH4K(NB) (2 * (NB) * 256 + 64)
@@ -103,8 +106,16 @@ typedef struct ecg_csum_params {
 	uint32_t n_ext;
 	uint32_t nchunks;
 	uint32_t type;			/* DAOS hash type: 1 crc16, 2 crc32, 3 crc64, 7 adler32 */
-	uint32_t pad;
+	uint32_t variant;		/* CRC: 0 auto, 1 wave per chunk, 2 workgroup per chunk */
+	/* workgroup-per-chunk CRC: a chunk of m 1 KiB steps is cut into
+	 * ECG_CSUM_SPLIT_NW slices; split_sh[c][w] = x^(8 * bytes after slice w)
+	 * mod P for the chunk lengths' step counts split_m[c] (first, middle and
+	 * last chunk of an extent), filled by the host */
+	uint64_t split_m[3];
+	uint64_t split_sh[3][8];
 } ecg_csum_params_t;
+
+#define ECG_CSUM_SPLIT_NW 8
 
 /*
  * Fused product + checksum: a launch of the GF product (ecg_mm_params_t)

@@ -120,6 +120,48 @@ static uint64_t crc_unshift(const struct crc_def *d, uint64_t z)
 	return r;
 }
 
+/* x^(8n) mod P: "1" moved through n zero bytes, by square and multiply */
+static uint64_t crc_xpow8(const struct crc_def *d, uint64_t n)
+{
+	uint64_t r = crc_one(d), b = zero_byte(d, crc_one(d));
+
+	for (; n; n >>= 1) {
+		if (n & 1)
+			r = crc_mulmod(d, r, b);
+		b = crc_mulmod(d, b, b);
+	}
+	return r;
+}
+
+/* Workgroup-per-chunk CRC: shift of each wave's slice to the end of a chunk
+ * of m 1 KiB steps (ecg_kabi.h split_sh), cached per context by (type, m). */
+static void split_shifts(ecg_ctx_t *ctx, int type, uint64_t m, uint64_t *sh)
+{
+	const uint64_t ms = (m + ECG_CSUM_SPLIT_NW - 1) / ECG_CSUM_SPLIT_NW;
+	struct ecg_split_ent *e;
+
+	pthread_mutex_lock(&ctx->lock);
+	for (int i = 0; i < ECG_NSPLIT_CACHE; i++) {
+		e = &ctx->split_cache[i];
+		if (e->valid && e->type == type && e->m == m) {
+			memcpy(sh, e->sh, sizeof(e->sh));
+			pthread_mutex_unlock(&ctx->lock);
+			return;
+		}
+	}
+	e = &ctx->split_cache[ctx->split_next++ % ECG_NSPLIT_CACHE];
+	for (int w = 0; w < ECG_CSUM_SPLIT_NW; w++) {
+		const uint64_t i0 = w * ms < m ? w * ms : m, i1 = i0 + ms < m ? i0 + ms : m;
+
+		e->sh[w] = crc_xpow8(&g_defs[type], (m - i1) * ECG_CSUM_STRIDE);
+	}
+	e->type = type;
+	e->m = m;
+	e->valid = 1;
+	memcpy(sh, e->sh, sizeof(e->sh));
+	pthread_mutex_unlock(&ctx->lock);
+}
+
 /* linear map "shift by n zero bytes" as NB byte tables at t */
 static void build_shift(const struct crc_def *d, int n, uint64_t *t)
 {
@@ -177,6 +219,12 @@ static void *build_crc_tables(const struct crc_def *d, size_t *bytes)
 		t[ECG_CSUM_OFF_K256(nb) + l] = c;
 		for (int z = 0; z < 16; z++)
 			c = zero_byte(d, c);
+	}
+	/* p2[j] = x^(8*2^j) mod P */
+	c = zero_byte(d, crc_one(d));
+	for (int j = 0; j < ECG_CSUM_NP2; j++) {
+		t[ECG_CSUM_OFF_P2(nb) + j] = c;
+		c = crc_mulmod(d, c, c);
 	}
 	*bytes = n * (size_t)es;
 	if (es == 8)
@@ -282,6 +330,25 @@ int ecg_csum_extents(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_
 	prm.n_ext = n_ext;
 	prm.nchunks = ecg_csum_chunk_count(chunksize, rec_size, rx_idx, rx_nr);
 	prm.type = (uint32_t)type;
+	if (type != ECG_HASH_ADLER32) {
+		/* a workgroup per chunk when one wave per chunk would leave fewer
+		 * than 4 waves per SIMD and each wave still gets >= 2 KiB steps
+		 * (tools/bench_csum.py shape_* rows) */
+		const uint64_t total = (uint64_t)n_ext * prm.nchunks;
+		const uint64_t steps = (rcs / 16 + 63) / 64;
+		const int split = ctx->csum_variant == 2 ||
+				  (ctx->csum_variant == 0 && total < 4096 && steps >= 2 * ECG_CSUM_SPLIT_NW);
+		const uint64_t lens[3] = {
+			prm.first_bytes, rcs,
+			prm.nchunks >= 2 ? prm.ext_bytes - prm.first_bytes - (uint64_t)(prm.nchunks - 2) * rcs
+					 : prm.first_bytes};
+
+		prm.variant = split ? 2 : 1;
+		for (int c = 0; split && c < 3; c++) {
+			prm.split_m[c] = (lens[c] / 16 + 63) / 64;
+			split_shifts(ctx, type, prm.split_m[c], prm.split_sh[c]);
+		}
+	}
 	e = ecg_k_launch_csum(&prm, (void *)ecg_pick_stream(ctx, stream), ctx->csum_blocks, &kid);
 	if (e != 0)
 		return ecg_hip_fail((hipError_t)e, "csum kernel launch");
@@ -294,6 +361,14 @@ int ecg_set_csum_launch(ecg_ctx_t *ctx, uint32_t max_blocks)
 	if (ctx == NULL)
 		return ecg_fail(-ECG_DER_INVAL, "set_csum_launch: NULL context");
 	ctx->csum_blocks = max_blocks;
+	return 0;
+}
+
+int ecg_set_csum_variant(ecg_ctx_t *ctx, uint32_t variant)
+{
+	if (ctx == NULL || variant > 2)
+		return ecg_fail(-ECG_DER_INVAL, "set_csum_variant: bad arguments");
+	ctx->csum_variant = variant;
 	return 0;
 }
 

@@ -62,6 +62,14 @@ struct ecg_ctx {
 #define ECG_NCSUM_TBL 4
 	void *csum_tbl[ECG_NCSUM_TBL];	/* device CRC tables by hash type (ecg_csum.c) */
 	uint32_t csum_blocks;		/* csum grid cap, 0 = kernel default */
+	uint32_t csum_variant;		/* CRC kernel choice, 0 = by shape */
+#define ECG_NSPLIT_CACHE 8
+	struct ecg_split_ent {		/* workgroup-per-chunk CRC shifts (ecg_csum.c) */
+		int valid, type;
+		uint64_t m;
+		uint64_t sh[ECG_CSUM_SPLIT_NW];
+	} split_cache[ECG_NSPLIT_CACHE];
+	unsigned split_next;
 	struct ecg_scratch scratch;
 };
 

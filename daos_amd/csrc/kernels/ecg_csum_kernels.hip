@@ -137,6 +137,121 @@ __global__ __launch_bounds__(CS_BLOCK) void ecg_crc_kernel(ecg_csum_params_t p)
 	}
 }
 
+template <typename T>
+__device__ __forceinline__ T shfl_xor_t(T v, int s)
+{
+	if constexpr (sizeof(T) == 8)
+		return ((uint64_t)(uint32_t)__shfl_xor((uint32_t)(v >> 32), s) << 32) |
+		       (uint32_t)__shfl_xor((uint32_t)v, s);
+	else
+		return (T)__shfl_xor((uint32_t)v, s);
+}
+
+// Long chunks, few of them (e.g. 1024 chunks of 1 MiB = one wave per SIMD
+// with ecg_crc_kernel): one workgroup of NW waves per chunk.  The chunk's
+// 1 KiB steps are cut into NW contiguous slices; each wave computes the raw
+// CRC of its slice exactly as ecg_crc_kernel does a whole chunk, moves it to
+// the end of the chunk's aligned part by multiplying with x^(8 * bytes after
+// the slice) mod P -- that power is the product of the p2[j] = x^(8*2^j)
+// table entries of its set bits, one bit per lane, multiplied down the wave
+// in 6 butterfly steps -- and the waves' values are XORed through LDS (CRC
+// is linear: crc(A || B) = crc(A) * x^(8|B|) ^ crc(B) for zero registers).
+template <int W, bool REFL, int NW>
+__global__ __launch_bounds__(64 * NW) void ecg_crc_split_kernel(ecg_csum_params_t p)
+{
+	using T = typename reg<W>::T;
+	constexpr int NB = W / 8;
+	__shared__ T sl[NB * 256];
+	__shared__ T sh[NB * 256];
+	__shared__ T part[NW];
+	const T *gt = (const T *)p.tbl;
+
+	for (int i = threadIdx.x; i < NB * 256; i += 64 * NW) {
+		sl[i] = gt[i];
+		sh[i] = gt[NB * 256 + i];
+	}
+	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+	const T klane = gt[2 * NB * 256 + lane];
+	const T one = REFL ? (T)((T)1 << (W - 1)) : (T)1;
+	const T p2 = lane < ECG_CSUM_NP2 ? gt[ECG_CSUM_OFF_P2(NB) + lane] : one;
+	const T poly = (T)p.poly, init = (T)p.init, xorout = (T)p.xorout;
+	__syncthreads();
+
+	const uint64_t total = (uint64_t)p.n_ext * p.nchunks;
+	for (uint64_t g = blockIdx.x; g < total; g += gridDim.x) {
+		uint64_t off, len;
+		const uint8_t *base;
+
+		chunk_geom(p, g, off, len, base);
+		const int64_t nq = (int64_t)(len / 16);
+		const int64_t m = (nq + 63) / 64;
+		const int64_t z = m * 64 - nq;
+		const int64_t ms = (m + NW - 1) / NW;
+		const int64_t i0 = wv * ms < m ? wv * ms : m;
+		const int64_t i1 = i0 + ms < m ? i0 + ms : m;
+		T acc = 0;
+
+		for (int64_t i = i0; i < i1; i += CS_UNROLL) {
+			uint32_t d[CS_UNROLL][4];
+#pragma unroll
+			for (int u = 0; u < CS_UNROLL; u++) {
+				const int64_t q = (i + u) * 64 + lane - z;
+				if (i + u < i1 && q >= 0) {
+					load16<true>(base + 16 * q, d[u]);
+					if (q == 0) {	// fold the initial register into the first bytes
+						d[u][0] ^= (uint32_t)init;
+						if constexpr (W == 64)
+							d[u][1] ^= (uint32_t)((uint64_t)init >> 32);
+					}
+				} else {
+					d[u][0] = d[u][1] = d[u][2] = d[u][3] = 0;
+				}
+			}
+#pragma unroll
+			for (int u = 0; u < CS_UNROLL; u++) {
+				if (i + u < i1)
+					acc = lin_map<W>(acc, sh) ^ piece_crc<W, REFL>(d[u], sl);
+			}
+		}
+		acc = mulmod<W, REFL>(klane, acc, poly);
+		acc = wave_xor(acc);
+		// x^(8 * (m - i1) KiB): the host's constant for this chunk length,
+		// else the product of p2[j] over the set bits j (one bit per lane)
+		T f;
+		if (m == (int64_t)p.split_m[0] || m == (int64_t)p.split_m[1] || m == (int64_t)p.split_m[2]) {
+			const int c = m == (int64_t)p.split_m[0] ? 0 : m == (int64_t)p.split_m[1] ? 1 : 2;
+			f = (T)p.split_sh[c][wv];
+		} else {
+			const uint64_t after = (uint64_t)(m - i1) * ECG_CSUM_STRIDE;
+			f = lane < ECG_CSUM_NP2 && ((after >> lane) & 1) ? p2 : one;
+#pragma unroll
+			for (int s = 32; s >= 1; s >>= 1)
+				f = mulmod<W, REFL>(f, shfl_xor_t(f, s), poly);
+		}
+		acc = mulmod<W, REFL>(f, acc, poly);
+		if (lane == 0)
+			part[wv] = acc;
+		__syncthreads();
+		if (threadIdx.x == 0) {
+			T crc = 0;
+
+#pragma unroll
+			for (int w = 0; w < NW; w++)
+				crc ^= part[w];
+			if (nq == 0)
+				crc = init;
+			for (uint64_t b = (uint64_t)nq * 16; b < len; b++)
+				crc = byte_step<W, REFL>(crc, base[b], sl);
+			crc ^= xorout;
+			if constexpr (W == 16)
+				((uint16_t *)p.out)[g] = (uint16_t)crc;
+			else
+				((T *)p.out)[g] = crc;
+		}
+		__syncthreads();
+	}
+}
+
 // adler32 with A = B = 0 at each chunk start (isal_adler32(0, ...)): lanes sum
 // bytes and position-weighted bytes of their pieces (v_dot4_u32_u8), the wave
 // reduces, A = sum mod 65521, B = L*sum - sum(pos*byte) mod 65521.
@@ -214,11 +329,23 @@ const csum_entry g_csum[] = {
 };
 constexpr uint32_t N_CSUM = sizeof(g_csum) / sizeof(g_csum[0]);
 
+constexpr int SPLIT_NW = ECG_CSUM_SPLIT_NW;	// waves per chunk in the split kernel
+const csum_entry g_split[] = {
+	{1, true, ecg_crc_split_kernel<16, false, SPLIT_NW>, "ecg_crc_split_kernel<crc16>"},
+	{2, true, ecg_crc_split_kernel<32, true, SPLIT_NW>, "ecg_crc_split_kernel<crc32>"},
+	{3, true, ecg_crc_split_kernel<64, true, SPLIT_NW>, "ecg_crc_split_kernel<crc64>"},
+};
+constexpr uint32_t N_SPLIT = sizeof(g_split) / sizeof(g_split[0]);
+
 } // namespace
 
 extern "C" const char *ecg_k_csum_kernel_name(uint32_t id)
 {
-	return id >= ECG_KID_CSUM && id < ECG_KID_CSUM + N_CSUM ? g_csum[id - ECG_KID_CSUM].name : "?";
+	if (id >= ECG_KID_CSUM && id < ECG_KID_CSUM + N_CSUM)
+		return g_csum[id - ECG_KID_CSUM].name;
+	if (id >= ECG_KID_CSUM + N_CSUM && id < ECG_KID_CSUM + N_CSUM + N_SPLIT)
+		return g_split[id - ECG_KID_CSUM - N_CSUM].name;
+	return "?";
 }
 
 extern "C" int ecg_k_launch_csum(const ecg_csum_params_t *p, void *stream, uint32_t max_blocks,
@@ -231,6 +358,28 @@ extern "C" int ecg_k_launch_csum(const ecg_csum_params_t *p, void *stream, uint3
 
 	if (total == 0)
 		return (int)hipSuccess;
+	if (p->type != 7 && aligned) {
+		// a workgroup per chunk when one wave per chunk would leave fewer
+		// than 4 waves per SIMD and every wave still gets >= 2 steps
+		const uint64_t steps = (p->chunk_bytes / 16 + 63) / 64;
+		const bool split = p->variant == 2 ||
+				   (p->variant == 0 && total < 4096 && steps >= 2 * SPLIT_NW);
+
+		for (uint32_t i = 0; split && i < N_SPLIT; i++) {
+			if (g_split[i].type != p->type)
+				continue;
+			uint64_t nb = total;
+			const uint64_t cap = max_blocks ? max_blocks : 256 * 8;
+
+			if (nb > cap)
+				nb = cap;
+			hipLaunchKernelGGL(g_split[i].fn, dim3((uint32_t)nb), dim3(64 * SPLIT_NW), 0,
+					   (hipStream_t)stream, *p);
+			if (kernel_id)
+				*kernel_id = ECG_KID_CSUM + N_CSUM + i;
+			return (int)hipGetLastError();
+		}
+	}
 	if (max_blocks == 0)
 		max_blocks = 256 * 16;	// 16 blocks per CU, grid-stride beyond
 	if (blocks > max_blocks)

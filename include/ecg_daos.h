@@ -28,6 +28,12 @@
  *                                      ref:src/object/srv_ec_aggregate.c:1110-1138
  *   ecg_obj_ec_singv_cell_bytes /   <- obj_ec_singv_cell_bytes, obj_ec_singv_encode
  *   ecg_obj_ec_singv_encode            ref:src/object/obj_ec.h:421-434, cli_ec.c:1447-1465
+ *   ecg_obj_ec_recx_encode          <- obj_ec_recx_encode + obj_ec_stripe_encode over an sgl
+ *                                      ref:src/object/cli_ec.c:476-546, 593-663
+ *   ecg_obj_ec_stripe_list_init     <- obj_ec_stripe_list_init / _add
+ *                                      ref:src/object/cli_ec.c:2252-2381
+ *   ecg_obj_ec_recov_fill_back      <- obj_ec_recov_fill_back + obj_ec_sgl_copy
+ *                                      ref:src/object/cli_ec.c:2645-2812
  */
 #ifndef ECG_DAOS_H
 #define ECG_DAOS_H

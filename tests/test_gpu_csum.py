@@ -64,6 +64,29 @@ def test_csum_parity(oracle, ecglib, ctx, htype, geom):
     assert np.array_equal(got, want), np.argwhere(got != want)[:5]
 
 
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("htype", (1, 2, 3))
+@pytest.mark.parametrize("geom", GEOMS + [(1 << 20, 1, 0, 3 << 20), ((1 << 20) + 4096, 1, 5, 2 << 20),
+                                          (65536, 16, 0, 70001), (2048, 1, 0, 100000)])
+def test_crc_kernel_shapes(oracle, ecglib, ctx, variant, htype, geom):
+    """Both CRC kernel shapes on every geometry: a wave per chunk (1) and a
+    workgroup per chunk whose waves' slice CRCs are shifted and combined (2);
+    chunks shorter than the workgroup's slices leave waves idle."""
+    cs, rb, idx, nr = geom
+    L = ecglib.lib()
+    rng = np.random.default_rng((hash(geom) + htype) & 0xFFFFFFFF)
+    host = rng.integers(0, 256, rb * nr, dtype=np.uint8)
+    assert L.ecg_set_csum_variant(ctx.h, variant) == 0
+    try:
+        got = _dev_csum(ecglib, ctx, htype, cs, rb, idx, nr, host)
+        kern = L.ecg_last_kernel().decode()
+    finally:
+        L.ecg_set_csum_variant(ctx.h, 0)
+    if "bytes" not in kern:
+        assert ("split" in kern) == (variant == 2), kern
+    assert np.array_equal(got, oracle.csum_extents(htype, cs, rb, idx, nr, host))
+
+
 @pytest.mark.parametrize("htype", TYPES)
 @pytest.mark.parametrize("offset", [1, 3, 8, 15])
 def test_csum_unaligned_base(oracle, ecglib, ctx, htype, offset):
