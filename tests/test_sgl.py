@@ -99,3 +99,14 @@ def test_fill_back_oracle_singv():
     sgl_py.recov_fill_back(37, [], sgl, [], [], img, 64, 8, singv=True)   # 37-byte value (ref :657)
     assert np.array_equal(np.concatenate(sgl.bufs)[:37], img[:37])
     assert sgl.iov_len == [5, 0, 32] and sgl.nr_out == 3
+
+
+def test_struct_layouts_match_daos(ecglib):
+    """ecg_iov_t / ecg_recx_ep_t / ecg_sgl_t are field-for-field d_iov_t,
+    struct daos_recx_ep and d_sg_list_t (ref:src/include/gurt/types.h:93-132,
+    ref:src/include/daos/object.h:714-719), so DAOS glue casts pointers."""
+    assert ct.sizeof(ecglib.Iov) == 24 and ecglib.Iov.iov_len.offset == 16
+    assert ct.sizeof(ecglib.Recx) == 16
+    assert ct.sizeof(ecglib.RecxEp) == 32 and ecglib.RecxEp.re_ep.offset == 16
+    assert ecglib.RecxEp.re_rec_size.offset == 24 and ecglib.RecxEp.re_type.offset == 28
+    assert ct.sizeof(ecglib.Sgl) == 16 and ecglib.Sgl.sg_iovs.offset == 8
