@@ -218,7 +218,9 @@ def mix_ceiling(ceil, read_frac):
 def detail_rows(ctx, ceil, iters=7):
     """Extra device-resident rows (per GPU): the north-star EC_8P2 encode,
     EC_8P2 2-erasure decode, EC_16P2 128 KiB encode, EC_2P1 128 KiB encode.
-    Median kernel time over `iters` launches."""
+    Encodes use the client write layout (data [S][k][C], parity [p][S][C] at
+    the padded row pitch, as the headline); decodes the recovery layout
+    [S][k+p][C].  Median kernel time over `iters` launches."""
     from daos_amd import ecg
 
     rows = {}
@@ -230,10 +232,14 @@ def detail_rows(ctx, ceil, iters=7):
         buf = ctx.alloc(S * st)
         fill_device(ctx, buf, S * st, 7)
         if mode == "enc":
-            fn = (lambda buf=buf, k=k, p=p, C=C, S=S, st=st:
-                  ctx.encode(k, p, C, S, buf.ptr, st, buf.ptr + k * C, C, st))
+            pitch = S * C + PARITY_ROW_PAD          # data [S][k][C] in buf, parity rows in buf2
+            buf2 = ctx.alloc(p * pitch)
+            par = buf2.ptr
+            fn = (lambda buf=buf, k=k, p=p, C=C, S=S, par=par, pitch=pitch:
+                  ctx.encode(k, p, C, S, buf.ptr, k * C, par, pitch, C))
             rd, wr = k, p
         else:
+            buf2 = None
             ctx.encode(k, p, C, S, buf.ptr, st, buf.ptr + k * C, C, st)
             fn = (lambda buf=buf, k=k, p=p, C=C, S=S, st=st:
                   ctx.recover(k, p, C, S, buf.ptr, st, [0, 1]))
@@ -245,8 +251,11 @@ def detail_rows(ctx, ceil, iters=7):
         rows[name] = {"GiBps_user": round(k * C * S / (ms / 1e3) / GIB, 1), "alg_GBps": round(gbs, 1),
                       "roofline_frac": round(gbs / HBM_PEAK_GBS, 4),
                       "measured_mix_ceiling_GBps": round(mix, 1), "frac_of_measured_mix": round(gbs / mix, 4),
-                      "kernel": ecg.last_kernel(), "ms": round(ms, 4)}
+                      "kernel": ecg.last_kernel(), "ms": round(ms, 4),
+                      "layout": "client [S][k][C] -> [p][S][C]" if mode == "enc" else "recovery [S][k+p][C]"}
         buf.free()
+        if buf2 is not None:
+            buf2.free()
     # checksums of regenerated cells (include/ecg_csum.h): EC_8P2 encode with
     # crc32 over 32 KiB chunks of the parity, fused vs the product alone, and
     # the standalone checksum kernel over 1 GiB of 1 MiB cells
