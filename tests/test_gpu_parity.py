@@ -367,6 +367,41 @@ def test_config2_ec4p2_1mib_full_size(ctx, oracle):
     stripes.free()
 
 
+def test_config4_ec16p2_full_size_sharded(ctx, oracle):
+    """BASELINE configs[3]: EC_16P2, 128 KiB cells, 8192 stripes (16 GiB of
+    data) sharded over 8 ranks by contiguous stripe ranges.  The 8 shard
+    launches (what 8 GPUs each run, bench.py --workload enc_16p2_strong) must
+    write exactly the parity of one launch over all stripes -- stripes are
+    independent -- and sampled stripes must match the oracle."""
+    from tools.datagen import stripe_bytes
+
+    k, p, C_, S, G = 16, 2, 128 << 10, 8192, 8
+    blk = stripe_bytes(256 << 20, 4)
+    data = ctx.alloc(S * k * C_)
+    for i, off in enumerate(range(0, S * k * C_, blk.size)):
+        data.upload(np.roll(blk, i * 4099), offset=off)      # no two 256 MiB tiles alike
+    full = ctx.alloc(p * S * C_)
+    shard = ctx.alloc(p * S * C_)
+    try:
+        ctx.encode(k, p, C_, S, data.ptr, k * C_, full.ptr, S * C_, C_)
+        per = S // G
+        for g in range(G):
+            ctx.encode(k, p, C_, per, data.ptr + g * per * k * C_, k * C_, shard.ptr + g * per * C_, S * C_, C_)
+        ctx.sync()
+        a, b = full.download(), shard.download()
+        assert np.array_equal(a, b)
+        par = a.reshape(p, S, C_)
+        en = oracle.cauchy1(k, p)
+        for s in np.random.default_rng(4).choice(S, 8, replace=False):
+            cells = data.download(k * C_, offset=int(s) * k * C_).reshape(k, C_)
+            want = oracle.encode_data(en[k:], cells)
+            assert np.array_equal(par[:, s], want), s
+    finally:
+        data.free()
+        full.free()
+        shard.free()
+
+
 def test_config3_ec8p2_1mib_degraded_decode(ctx, oracle):
     """BASELINE configs[2]: EC_8P2, 1 MiB cells, 512 stripes, cells {d0,d1}
     missing; recovered bytes must equal the original data."""
