@@ -410,10 +410,10 @@ static int aligned16_ok(const void *src, const int64_t *soff, int k, int64_t sst
 	return (bits & 15u) == 0;
 }
 
-static int matmul_csum(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, uint64_t C,
-		       uint32_t S, const void *src, const int64_t *soff, int64_t sstride, void *dst,
-		       const int64_t *doff, int64_t dstride, int type, uint64_t chunksize,
-		       uint64_t rec_size, void *csums, const uint32_t *row_slot, void *stream)
+int ecg_matmul_csum(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, uint64_t C,
+		    uint32_t S, const void *src, const int64_t *soff, int64_t sstride, void *dst,
+		    const int64_t *doff, int64_t dstride, int type, uint64_t chunksize,
+		    uint64_t rec_size, void *csums, const uint32_t *row_slot, void *stream)
 {
 	const int cl = ecg_csum_len(type);
 	ecg_mmcs_params_t q;
@@ -517,7 +517,7 @@ int ecg_encode_csum(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S, const 
 		doff[i] = (int64_t)i * parity_cell_stride;
 		slot[i] = (uint32_t)i;
 	}
-	return matmul_csum(ctx, k, p, &en[k * k], C, S, data, soff, data_stripe_stride, parity, doff,
+	return ecg_matmul_csum(ctx, k, p, &en[k * k], C, S, data, soff, data_stripe_stride, parity, doff,
 			   parity_stripe_stride, type, chunksize, rec_size, csums, slot, stream);
 }
 
@@ -551,7 +551,7 @@ int ecg_recover_csum(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S, void 
 			if (err_list[j] == ent.out_idx[i])
 				slot[i] = (uint32_t)j;
 	}
-	return matmul_csum(ctx, ent.k, ent.nerrs, ent.rows, C, S, stripes, soff, stripe_stride,
+	return ecg_matmul_csum(ctx, ent.k, ent.nerrs, ent.rows, C, S, stripes, soff, stripe_stride,
 			   stripes, doff, stripe_stride, type, chunksize, rec_size, csums, slot,
 			   stream);
 }

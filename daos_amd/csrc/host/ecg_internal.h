@@ -111,6 +111,13 @@ void ecg_csum_ctx_fini(ecg_ctx_t *ctx);
 int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_size,
 			  uint64_t C, void *csums, ecg_mmcs_params_t *q);
 
+/* product + chunk checksums of every output cell, cells as extents from
+ * record index 0; csums[row_slot[r]][s][chunk] (ecg_core.c) */
+int ecg_matmul_csum(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, uint64_t C,
+		    uint32_t S, const void *src, const int64_t *soff, int64_t sstride, void *dst,
+		    const int64_t *doff, int64_t dstride, int type, uint64_t chunksize,
+		    uint64_t rec_size, void *csums, const uint32_t *row_slot, void *stream);
+
 /* context helpers (ecg_core.c) */
 int ecg_ctx_enter(ecg_ctx_t *ctx);
 hipStream_t ecg_pick_stream(ecg_ctx_t *ctx, void *stream);

@@ -108,6 +108,11 @@ _SIGS = [
     ("ecg_obj_ec_stripe_list_init", C.c_int, [C.c_uint64, vp, C.c_uint32, vp, C.c_uint32, u32p]),
     ("ecg_obj_ec_recov_fill_back", C.c_int, [vp, C.c_uint64, C.c_int, vp, C.c_uint32, vp, vp, C.c_uint32, vp,
                                              C.c_uint32, vp, C.c_uint64, C.c_uint64, vp]),
+    ("ecg_migrate_plan_size", C.c_int, [C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int,
+                                        C.c_int, C.c_uint64, u32p, u32p, C.POINTER(C.c_uint64)]),
+    ("ecg_migrate_update_parity", C.c_int, [vp, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, vp, C.c_uint64,
+                                            C.c_uint64, C.c_int, C.c_int, C.c_uint64, vp, vp, vp, C.c_uint32,
+                                            u32p, vp]),
     ("ecg_obj_ec_stripe_rec_nr", C.c_uint64, [C.c_uint32, C.c_uint64]),
     ("ecg_obj_ec_cell_bytes", C.c_uint64, [C.c_uint64, C.c_uint64]),
     ("ecg_obj_ec_tgt_of_recx_idx", C.c_uint32, [C.c_uint64, C.c_uint64, C.c_uint64]),
@@ -157,6 +162,12 @@ class RecxEp(C.Structure):
 class Sgl(C.Structure):
     """ecg_sgl_t (d_sg_list_t) over device iov buffers."""
     _fields_ = [("sg_nr", C.c_uint32), ("sg_nr_out", C.c_uint32), ("sg_iovs", C.POINTER(Iov))]
+
+
+class MigratePiece(C.Structure):
+    """ecg_migrate_piece_t: one piece of migrate_update_parity's walk."""
+    _fields_ = [("recx", Recx), ("buf_off", C.c_uint64), ("buf_len", C.c_uint64), ("csum_off", C.c_uint64),
+                ("nr_csums", C.c_uint32), ("parity", C.c_uint32)]
 
 
 DRT_SHADOW = 2

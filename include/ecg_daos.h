@@ -232,6 +232,42 @@ int ecg_obj_ec_recov_fill_back(ecg_ctx_t *ctx, uint64_t iod_size, int singv,
 			       const void *stripe_buf, uint64_t stripe_total_sz, uint64_t stripe_rec_nr,
 			       void *stream);
 
+/* ---- rebuild of a parity shard ------------------------------------------
+ * migrate_update_parity (ref:src/object/srv_obj_migrate.c:1096-1181) over a
+ * fetched range of records [offset, offset + size) of iod_size bytes, held in
+ * `buffer` (device) in record order.  The range is cut exactly as the
+ * reference cuts it (at stripe boundaries when `encode`, else at cell
+ * boundaries); every full stripe becomes a parity piece -- this shard's
+ * parity cell, VOS index obj_ec_idx_daos2vos(offset) | ECG_EC_PARITY_BIT,
+ * e_len records -- and every other piece is written as replicated records.
+ * All parity cells come from one product launch with a single output row
+ * into parity_out ([nparity][e_len * iod_size], device); with csum_type (an
+ * ECG_HASH_* of ecg_csum.h, 0 = none) every piece's chunk checksums
+ * (daos_csummer_calc_iods, :1156) go to csums_out (device) at the piece's
+ * csum_off.  `shard` is the logical cell index of the shard being rebuilt
+ * (k .. k+p-1, obj_ec_shard_off_by_layout_ver in the caller).  The caller
+ * then hands each piece to vos_obj_update as the reference does.
+ * -ECG_DER_REC2BIG when pieces_cap is too small (ecg_migrate_plan_size gives
+ * the counts), -ECG_DER_INVAL for a shard that is not a parity shard. */
+typedef struct ecg_migrate_piece {
+	ecg_recx_t recx;	/* the recx for vos_obj_update */
+	uint64_t buf_off;	/* bytes into parity_out (parity pieces) or buffer */
+	uint64_t buf_len;
+	uint64_t csum_off;	/* bytes into csums_out: nr_csums checksums */
+	uint32_t nr_csums;
+	uint32_t parity;	/* 1: this shard's parity cell of a full stripe */
+} ecg_migrate_piece_t;
+
+/* Sizing for ecg_migrate_update_parity: pieces, parity cells, checksum bytes. */
+int ecg_migrate_plan_size(uint32_t oc_id, uint64_t e_len, uint64_t iod_size, uint64_t offset, uint64_t size,
+			  int encode, int csum_type, uint64_t chunksize, uint32_t *npieces, uint32_t *nparity,
+			  uint64_t *csum_bytes);
+
+int ecg_migrate_update_parity(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t e_len, uint64_t iod_size,
+			      uint32_t shard, const void *buffer, uint64_t offset, uint64_t size, int encode,
+			      int csum_type, uint64_t chunksize, void *parity_out, void *csums_out,
+			      ecg_migrate_piece_t *pieces, uint32_t pieces_cap, uint32_t *npieces, void *stream);
+
 /* ---- stripe / index math (ref:src/object/obj_ec.h:271-350) -------------
  * e_len = records per cell (oca->u.ec.e_len), stripe_rec_nr = k * e_len.
  * Parity extents carry ECG_EC_PARITY_BIT in their VOS index

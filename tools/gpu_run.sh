@@ -105,6 +105,9 @@ for what in "$@"; do
 		step rocprof_fillback 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_fb -o run \
 			-- python3 tools/bench_fillback.py || exit $?
 		;;
+	rebuild)
+		step bench_rebuild 300 python tools/bench_rebuild.py || exit $?
+		;;
 	tune10)
 		step tune10 600 python tools/tune10.py || exit $?
 		;;
