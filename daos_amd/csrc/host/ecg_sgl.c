@@ -330,6 +330,71 @@ int ecg_obj_ec_recov_fill_back(ecg_ctx_t *ctx, uint64_t iod_size, int singv, con
 	return rc;
 }
 
+/* obj_ec_singv_one_tgt (ref:src/object/obj_ec.h:409-419): a single value of at
+ * most OBJ_EC_SINGV_EVENDIST_SZ bytes lives on one target, unencoded. */
+static int singv_one_tgt(uint64_t iod_size, const ecg_sgl_t *sgl, int k)
+{
+	const uint64_t evendist = ((uint64_t)k / 8 + 1) * 4096;	/* OBJ_EC_SINGV_EVENDIST_SZ */
+	uint64_t buf = 0;
+
+	if (iod_size != 0 && iod_size <= evendist)
+		return 1;
+	if (sgl == NULL)
+		return 0;
+	for (uint32_t i = 0; i < sgl->sg_nr; i++)
+		buf += sgl->sg_iovs[i].iov_buf_len;
+	return buf <= evendist;
+}
+
+int ecg_obj_ec_recov_data_dev(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t e_len,
+			      const struct ecg_obj_ec_recov_codec *recov, ecg_recov_iod_t *iods, uint32_t iod_nr,
+			      void *stream)
+{
+	int k, p, rc;
+
+	if (ctx == NULL || recov == NULL || (iod_nr && iods == NULL))
+		return ecg_fail(-ECG_DER_INVAL, "recov_data_dev: NULL argument");
+	rc = ecg_obj_ec_class_kp(oc_id, &k, &p);
+	if (rc)
+		return rc;
+	if (recov->k != k || recov->p != p || e_len == 0)
+		return ecg_fail(-ECG_DER_INVAL, "recov_data_dev: codec %d+%d for class %d+%d, e_len %lu",
+				recov->k, recov->p, k, p, (unsigned long)e_len);
+	for (uint32_t i = 0; i < iod_nr; i++) {		/* ref:src/object/cli_ec.c:2839-2884 */
+		ecg_recov_iod_t *io = &iods[i];
+		const uint64_t srn = (uint64_t)k * e_len;
+		uint64_t cell, nst = 0;
+
+		if (!io->singv && (io->recov_nr == 0 || io->stripe_nr == 0))
+			continue;
+		cell = io->singv ? ecg_obj_ec_singv_cell_bytes(oc_id, io->iod_size) : e_len * io->iod_size;
+		if (io->singv) {
+			nst = singv_one_tgt(io->iod_size, io->sgl, k) ? 0 : 1;
+		} else {
+			for (uint32_t j = 0; j < io->stripe_nr; j++) {
+				if (io->stripes[j].re_recx.rx_nr % srn)
+					return ecg_fail(-ECG_DER_INVAL, "recov_data_dev: stripe recx %u of iod %u", j,
+							i);
+				nst += io->stripes[j].re_recx.rx_nr / srn;
+			}
+		}
+		if (nst > UINT32_MAX)
+			return ecg_fail(-ECG_DER_INVAL, "recov_data_dev: %lu stripes", (unsigned long)nst);
+		if (nst) {
+			rc = ecg_recover(ctx, k, p, cell, (uint32_t)nst, io->stripe_buf, (int64_t)(cell * (k + p)),
+					 recov->er_err_list, (int)recov->er_nerrs, stream);
+			if (rc)
+				return rc;
+		}
+		rc = ecg_obj_ec_recov_fill_back(ctx, io->iod_size, (int)io->singv, io->iod_recxs, io->iod_nr, io->sgl,
+						io->recov, io->recov_nr, io->stripes, io->stripe_nr, io->stripe_buf,
+						cell * (uint64_t)(k + p), srn, stream);
+		if (rc)
+			return rc;
+	}
+	return 0;
+}
+
 /* ---- stripe list (obj_ec_stripe_list_init / _add) ----------------------- */
 
 /* obj_ec_stripe_list_add (ref:src/object/cli_ec.c:2252-2310) */

@@ -108,6 +108,7 @@ _SIGS = [
     ("ecg_obj_ec_stripe_list_init", C.c_int, [C.c_uint64, vp, C.c_uint32, vp, C.c_uint32, u32p]),
     ("ecg_obj_ec_recov_fill_back", C.c_int, [vp, C.c_uint64, C.c_int, vp, C.c_uint32, vp, vp, C.c_uint32, vp,
                                              C.c_uint32, vp, C.c_uint64, C.c_uint64, vp]),
+    ("ecg_obj_ec_recov_data_dev", C.c_int, [vp, C.c_uint32, C.c_uint64, vp, vp, C.c_uint32, vp]),
     ("ecg_migrate_plan_size", C.c_int, [C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int,
                                         C.c_int, C.c_uint64, u32p, u32p, C.POINTER(C.c_uint64)]),
     ("ecg_migrate_update_parity", C.c_int, [vp, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, vp, C.c_uint64,
@@ -162,6 +163,14 @@ class RecxEp(C.Structure):
 class Sgl(C.Structure):
     """ecg_sgl_t (d_sg_list_t) over device iov buffers."""
     _fields_ = [("sg_nr", C.c_uint32), ("sg_nr_out", C.c_uint32), ("sg_iovs", C.POINTER(Iov))]
+
+
+class RecovIod(C.Structure):
+    """ecg_recov_iod_t: one iod of obj_ec_recov_data (device buffers)."""
+    _fields_ = [("iod_size", C.c_uint64), ("singv", C.c_uint32), ("iod_nr", C.c_uint32),
+                ("iod_recxs", C.POINTER(Recx)), ("sgl", C.POINTER(Sgl)), ("recov", C.POINTER(RecxEp)),
+                ("recov_nr", C.c_uint32), ("stripe_nr", C.c_uint32), ("stripes", C.POINTER(RecxEp)),
+                ("stripe_buf", vp)]
 
 
 class MigratePiece(C.Structure):

@@ -232,6 +232,31 @@ int ecg_obj_ec_recov_fill_back(ecg_ctx_t *ctx, uint64_t iod_size, int singv,
 			       const void *stripe_buf, uint64_t stripe_total_sz, uint64_t stripe_rec_nr,
 			       void *stream);
 
+/* obj_ec_recov_data (ref:src/object/cli_ec.c:2814-2885) on device buffers:
+ * for every iod, regenerate the erased cells (recov->er_err_list) of all
+ * stripes of its stripe list in one launch -- the cell size is e_len *
+ * iod_size, or obj_ec_singv_cell_bytes for a single value (one stripe,
+ * skipped when the value lives on one target, obj_ec_singv_one_tgt) -- then
+ * fill the recovered records back into its sgl (ecg_obj_ec_recov_fill_back).
+ * Array iods with an empty recov or stripe list are skipped, as in the
+ * reference.  Asynchronous on `stream`; sgl bookkeeping done on return. */
+typedef struct ecg_recov_iod {
+	uint64_t iod_size;
+	uint32_t singv;			/* DAOS_IOD_SINGLE */
+	uint32_t iod_nr;		/* iod recxs */
+	const ecg_recx_t *iod_recxs;
+	ecg_sgl_t *sgl;			/* the user's sgl (device buffers) */
+	const ecg_recx_ep_t *recov;	/* efi_recx_lists[i] */
+	uint32_t recov_nr;
+	uint32_t stripe_nr;
+	const ecg_recx_ep_t *stripes;	/* efi_stripe_lists[i] */
+	void *stripe_buf;		/* efi_stripe_sgls[i]: [n][k+p][cell] (device) */
+} ecg_recov_iod_t;
+
+int ecg_obj_ec_recov_data_dev(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t e_len,
+			      const struct ecg_obj_ec_recov_codec *recov, ecg_recov_iod_t *iods, uint32_t iod_nr,
+			      void *stream);
+
 /* ---- rebuild of a parity shard ------------------------------------------
  * migrate_update_parity (ref:src/object/srv_obj_migrate.c:1096-1181) over a
  * fetched range of records [offset, offset + size) of iod_size bytes, held in

@@ -143,3 +143,61 @@ def test_fill_back_errors(ecglib, ctx):
         ctx.sync()
     finally:
         buf.free()
+
+
+def test_recov_data_dev_iods(oracle, ecglib, ctx):
+    """obj_ec_recov_data over three iods in one call: an array iod (stripe
+    list, fill-back into a scattered sgl), an evenly distributed single
+    value (one stripe of obj_ec_singv_cell_bytes cells), and a short single
+    value stored on one target (no recovery, only the copy)."""
+    L = ecglib.lib()
+    k, p = 4, 2
+    oc = (35 << 24) | 1
+    case = make_case(11, k, 256, 2, 6, 3, 7, 5, 1, 3)
+    isz, srn = case["iod_size"], case["srn"]
+    C = case["e_len"] * isz
+    lost = [1, k]
+    en = oracle.cauchy1(k, p)
+    rng = np.random.default_rng(11)
+    stripes = c_stripe_list(ecglib, srn, case["recov"])
+    img = stripe_image(case, stripes, p, parity_fn=lambda d: oracle.encode_data(en[k:], d))
+    nst = img.size // ((k + p) * C)
+    broken = img.reshape(nst, k + p, C).copy()
+    broken[:, lost] = 0
+    # evenly distributed single value: 100 000 bytes -> 4 cells of 25 000 (last one padded)
+    sv = rng.integers(0, 256, 100000, dtype=np.uint8)
+    scell = L.ecg_obj_ec_singv_cell_bytes(oc, sv.size)
+    cells = np.zeros(k * scell, np.uint8)
+    cells[:sv.size] = sv
+    simg = np.concatenate([cells, oracle.encode_data(en[k:], cells.reshape(k, scell)).reshape(-1)])
+    sbroken = simg.reshape(k + p, scell).copy()
+    sbroken[lost] = 0
+    # short single value: lives on one target, the buffer already holds it
+    small = rng.integers(0, 256, 1000, dtype=np.uint8)
+    codec = L.ecg_obj_ec_recov_codec_alloc()
+    dimg, dsv, dsmall = ctx.to_device(broken), ctx.to_device(sbroken), ctx.to_device(small)
+    b1, offs1, iovs1, sgl1 = device_sgl(ctx, ecglib, rng, case["lens"])
+    b2, offs2, iovs2, sgl2 = device_sgl(ctx, ecglib, rng, [60000, 50000], fill=0)
+    b3, offs3, iovs3, sgl3 = device_sgl(ctx, ecglib, rng, [4096], fill=0)
+    try:
+        assert L.ecg_obj_ec_recov_codec_init(oc, ecglib._u32(lost), len(lost), codec) == 0
+        iod, rec, st = recx_arrays(ecglib, case, stripes)
+        io = (ecglib.RecovIod * 3)()
+        io[0] = ecglib.RecovIod(isz, 0, len(case["iod"]), iod, ct.pointer(sgl1), rec, len(case["recov"]),
+                                len(stripes), st, dimg.ptr)
+        io[1] = ecglib.RecovIod(sv.size, 1, 0, None, ct.pointer(sgl2), None, 0, 0, None, dsv.ptr)
+        io[2] = ecglib.RecovIod(small.size, 1, 0, None, ct.pointer(sgl3), None, 0, 0, None, dsmall.ptr)
+        assert L.ecg_obj_ec_recov_data_dev(ctx.h, oc, case["e_len"], codec, io, 3, None) == 0, L.ecg_strerror()
+        ctx.sync()
+        got1, _ = read_sgl(b1, offs1, case["lens"])
+        assert np.array_equal(np.concatenate(got1), expected_user_bytes(case))
+        got2, _ = read_sgl(b2, offs2, [60000, 50000])
+        assert np.array_equal(np.concatenate(got2)[:sv.size], sv)
+        assert np.array_equal(dsv.download().reshape(k + p, scell), simg.reshape(k + p, scell))
+        got3, _ = read_sgl(b3, offs3, [4096])
+        assert np.array_equal(got3[0][:small.size], small)
+        assert sgl2.sg_nr_out == 2 and iovs2[1].iov_len == sv.size - 60000
+    finally:
+        L.ecg_obj_ec_recov_codec_free(codec)
+        for b in (dimg, dsv, dsmall, b1, b2, b3):
+            b.free()
