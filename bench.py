@@ -274,6 +274,23 @@ def detail_rows(ctx, ceil, iters=7):
         "roofline_frac": round(alg / fus / 1e6 / HBM_PEAK_GBS, 4), "ms": round(fus, 4),
         "encode_only_ms": round(enc, 4), "checksum_overhead": round(fus / enc - 1, 4),
         "kernel": ecg.last_kernel()}
+    # rebuild of parity shard p1 over the same 512 fetched stripes (migrate_update_parity,
+    # include/ecg_daos.h): one output row + its crc32 chunks, (k + 1) cells of traffic per stripe
+    import ctypes
+    pieces = (ecg.MigratePiece * S)()
+    npc = ctypes.c_uint32()
+
+    def shard():
+        ecg._chk(ecg.lib().ecg_migrate_update_parity(ctx.h, (37 << 24) | 1, C, 1, k + p - 1, data.ptr, 0, S * k * C,
+                                                     1, ecg.HASH_CRC32, 32768, par.ptr, out.ptr, pieces, S,
+                                                     ctypes.byref(npc), None), "migrate_update_parity")
+
+    ms = time_kernel(ctx, shard, iters)
+    alg = (k + 1) * C * S
+    rows["EC_8P2_1MiB_rebuild_parity_shard_crc32"] = {
+        "GiBps_user": round(k * C * S / (ms / 1e3) / GIB, 1), "alg_GBps": round(alg / ms / 1e6, 1),
+        "roofline_frac": round(alg / ms / 1e6 / HBM_PEAK_GBS, 4), "ms": round(ms, 4),
+        "kernel": ecg.last_kernel()}
     n = 1024
     ms = time_kernel(ctx, lambda: ctx.csum_extents(ecg.HASH_CRC32, 32768, 1, 0, C, data.ptr, C, n, out.ptr), iters)
     rows["crc32_32KiB_chunks_1GiB"] = {"alg_GBps": round(C * n / ms / 1e6, 1),
