@@ -27,6 +27,11 @@ struct tstage {
 static pthread_key_t g_key;
 static pthread_once_t g_key_once = PTHREAD_ONCE_INIT;
 
+/* Staging bytes up to which a call skips the DMA copies and lets the kernel
+ * work on the pinned staging in place (env ECG_ZERO_COPY_MAX overrides;
+ * measured in tools/bench_pcie.py). */
+static size_t g_zero_copy_max = 4u << 20;
+
 static void tstage_release(struct tstage *t)
 {
 	if (t->st) {
@@ -51,7 +56,11 @@ static void tstage_dtor(void *p)
 
 static void key_init(void)
 {
+	const char *env = getenv("ECG_ZERO_COPY_MAX");
+
 	pthread_key_create(&g_key, tstage_dtor);
+	if (env)
+		g_zero_copy_max = (size_t)strtoull(env, NULL, 0);
 }
 
 static int tstage_get(ecg_ctx_t *ctx, size_t bytes, struct tstage **out)
@@ -141,10 +150,21 @@ int ecg_matmul_host(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned cha
 			memcpy(h + (k + r) * pitch, dst[r], (size_t)len);
 		doff[r] = (int64_t)((k + r) * pitch);
 	}
-	e = hipMemcpyAsync(d, h, (flags & ECG_F_ACCUMULATE) ? bytes : pitch * k,
-			   hipMemcpyHostToDevice, t->st);
-	if (e != hipSuccess)
-		return ecg_hip_fail(e, "matmul_host H2D");
+	if (bytes <= g_zero_copy_max) {
+		/* small call: the kernel reads and writes the pinned staging over
+		 * PCIe directly -- one launch instead of H2D + launch + D2H */
+		void *hd = NULL;
+
+		e = hipHostGetDevicePointer(&hd, h, 0);
+		if (e != hipSuccess)
+			return ecg_hip_fail(e, "matmul_host device view of staging");
+		d = hd;
+	} else {
+		e = hipMemcpyAsync(d, h, (flags & ECG_F_ACCUMULATE) ? bytes : pitch * k,
+				   hipMemcpyHostToDevice, t->st);
+		if (e != hipSuccess)
+			return ecg_hip_fail(e, "matmul_host H2D");
+	}
 	if (k <= ECG_MAX_K) {
 		rc = ecg_matmul(ctx, k, rows, coef, (uint64_t)len, 1, d, soff, 0, d, doff, 0,
 				flags, t->st);
@@ -165,10 +185,15 @@ int ecg_matmul_host(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned cha
 	}
 	if (rc)
 		return rc;
-	e = hipMemcpyAsync(h + k * pitch, d + k * pitch, pitch * rows, hipMemcpyDeviceToHost,
-			   t->st);
+	e = hipSuccess;
+	if (d == (unsigned char *)t->dev)
+		e = hipMemcpyAsync(h + k * pitch, d + k * pitch, pitch * rows, hipMemcpyDeviceToHost,
+				   t->st);
+	/* the caller is synchronous (ISA-L convention): poll rather than let the
+	 * runtime put the thread to sleep and pay its wake-up */
 	if (e == hipSuccess)
-		e = hipStreamSynchronize(t->st);
+		while ((e = hipStreamQuery(t->st)) == hipErrorNotReady)
+			;
 	if (e != hipSuccess)
 		return ecg_hip_fail(e, "matmul_host D2H");
 	for (r = 0; r < rows; r++)

@@ -1,0 +1,42 @@
+"""Latency of the synchronous ISA-L drop-in (ec_encode_data, one EC_8P2
+stripe per call, host buffers) by cell size -- what an unbatched DAOS caller
+linked against libecg sees.  Run once per staging mode (env
+ECG_ZERO_COPY_MAX: 0 = always DMA copies, large = kernel on the pinned
+staging in place); appends one JSON line to gpurun_out/bench_dropin.jsonl.
+Bench infrastructure (no oracle)."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+from daos_amd import ecg  # noqa: E402
+
+
+def main():
+    k, p = 8, 2
+    tbls = ecg.isal_init_tables(ecg.cauchy1(k, p)[k:])
+    rng = np.random.default_rng(5)
+    res = {"zero_copy_max": os.environ.get("ECG_ZERO_COPY_MAX", "default")}
+    for C in (4096, 16384, 32768, 65536, 131072, 262144, 1 << 20):
+        cells = [rng.integers(0, 256, C, dtype=np.uint8) for _ in range(k)]
+        coding = [np.zeros(C, dtype=np.uint8) for _ in range(p)]
+        for _ in range(5):
+            ecg.isal_encode_data(tbls, k, p, cells, coding)
+        it = 200 if C <= 65536 else 40
+        t0 = time.perf_counter()
+        for _ in range(it):
+            ecg.isal_encode_data(tbls, k, p, cells, coding)
+        us = (time.perf_counter() - t0) / it * 1e6
+        res[f"{C >> 10}KiB_us"] = round(us, 1)
+        res[f"{C >> 10}KiB_GiBps"] = round(k * C / (us / 1e6) / (1 << 30), 2)
+    print(json.dumps(res), flush=True)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "bench_dropin.jsonl"), "a") as f:
+        f.write(json.dumps(res) + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -105,6 +105,12 @@ for what in "$@"; do
 		step rocprof_fillback 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_fb -o run \
 			-- python3 tools/bench_fillback.py || exit $?
 		;;
+	dropin)
+		rm -f gpurun_out/bench_dropin.jsonl
+		for zc in 0 1048576 1073741824; do
+			ECG_ZERO_COPY_MAX=$zc step dropin_$zc 300 python tools/bench_dropin.py || exit $?
+		done
+		;;
 	rebuild)
 		step bench_rebuild 300 python tools/bench_rebuild.py || exit $?
 		;;
