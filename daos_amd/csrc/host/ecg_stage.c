@@ -29,7 +29,7 @@ static pthread_once_t g_key_once = PTHREAD_ONCE_INIT;
 
 /* Staging bytes up to which a call skips the DMA copies and lets the kernel
  * work on the pinned staging in place (env ECG_ZERO_COPY_MAX overrides;
- * measured in tools/bench_pcie.py). */
+ * tools/bench_dropin.py, profiles/r01/bench_dropin.jsonl). */
 static size_t g_zero_copy_max = 4u << 20;
 
 static void tstage_release(struct tstage *t)
