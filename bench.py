@@ -50,7 +50,7 @@ WORKLOADS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="enc_dec_4p2", choices=sorted(WORKLOADS),
                     help="enc_dec_4p2 = BASELINE configs[1] (+ its decode); dec_8p2 = configs[2]; "
@@ -380,9 +380,9 @@ def main():
         wl.step(timed=True)
     ctx.sync()
     torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0      # this rank's K steps, from the common start barrier
     barrier(world)
-    elapsed = time.perf_counter() - t0
-    elapsed = max_over_ranks(world, elapsed)
+    elapsed = max_over_ranks(world, elapsed)    # the job took as long as its slowest rank
 
     if args.profile_only:
         wl.free()
