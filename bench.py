@@ -44,7 +44,10 @@ WORKLOADS = {
     "enc_dec_4p2": (4, 2, 1 << 20, 1024, ("enc", "dec"), False),
     "dec_8p2": (8, 2, 1 << 20, 512, ("dec",), False),
     "enc_16p2_strong": (16, 2, 128 << 10, 8192, ("enc",), True),
+    # configs[4]: stripes in pinned host memory, PCIe-inclusive (never the headline)
+    "rebuild_stream_8p2": (8, 2, 1 << 20, 64, ("enc_host", "dec_host"), False),
 }
+HOST_CHUNK = 16         # stripes per staging chunk (profiles/r01/pcie.json chunk sweep)
 
 
 def parse():
@@ -54,7 +57,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="enc_dec_4p2", choices=sorted(WORKLOADS),
                     help="enc_dec_4p2 = BASELINE configs[1] (+ its decode); dec_8p2 = configs[2]; "
-                         "enc_16p2_strong = configs[3] (8192 stripes split across ranks)")
+                         "enc_16p2_strong = configs[3] (8192 stripes split across ranks); "
+                         "rebuild_stream_8p2 = configs[4] (host-resident, PCIe-inclusive)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
     ap.add_argument("--no-detail", action="store_true", help="skip the extra per-config rows")
     ap.add_argument("--no-cpu", action="store_true")
@@ -174,6 +178,95 @@ class Workload:
     def free(self):
         for b in (self.data, self.parity, self.stripes):
             b.free()
+
+
+class HostWorkload:
+    """BASELINE configs[4], the rebuild stream: one rank's stripes live in
+    pinned host memory (engine-side bio/NIC buffers); a step is one encode
+    batch (data [S][k][C] -> parity [p][S][C]) and one 2-erasure recovery
+    batch (in place in [S][k+p][C]), each streamed through device staging by
+    ecg_encode_host / ecg_recover_host (H2D || kernel || D2H on 3 streams).
+    PCIe-bound by construction."""
+
+    def __init__(self, ctx, k, p, C, S, ops=("enc_host", "dec_host"), err=(0, 1), config_id=9):
+        from tools.datagen import stripe_bytes
+
+        self.ctx, self.k, self.p, self.C, self.S, self.err = ctx, k, p, C, S, list(err)
+        self.ops = tuple(ops)
+        self.data = ctx.host_alloc(S * k * C)
+        self.parity = ctx.host_alloc(S * p * C)
+        self.stripes = ctx.host_alloc(S * (k + p) * C)
+        blk = stripe_bytes(min(256 << 20, S * k * C), config_id)
+        a = self.data.array
+        for off in range(0, a.size, blk.size):
+            n = min(blk.size, a.size - off)
+            a[off:off + n] = blk[:n]
+        ctx.encode_host(k, p, C, S, a, self.parity.array, chunk=HOST_CHUNK)
+        img = self.stripes.array.reshape(S, k + p, C)
+        img[:, :k] = a.reshape(S, k, C)
+        img[:, k:] = self.parity.array.reshape(p, S, C).transpose(1, 0, 2)
+        self.events = []
+
+    def step(self, timed=False):
+        c, k, p, C, S = self.ctx, self.k, self.p, self.C, self.S
+        if "enc_host" in self.ops:
+            c.encode_host(k, p, C, S, self.data.array, self.parity.array, chunk=HOST_CHUNK)
+        if "dec_host" in self.ops:
+            c.recover_host(k, p, C, S, self.stripes.array, self.err, chunk=HOST_CHUNK)
+
+    def kernel_ms(self):
+        return {}
+
+    def user_bytes_per_step(self):
+        return len(self.ops) * self.k * self.C * self.S
+
+    def h2d_bytes_per_step(self):
+        # encode: k cells in; recovery: the k survivors in
+        return len(self.ops) * self.k * self.C * self.S
+
+    def d2h_bytes_per_step(self):
+        n = 0
+        if "enc_host" in self.ops:
+            n += self.p * self.C * self.S
+        if "dec_host" in self.ops:
+            n += len(self.err) * self.C * self.S
+        return n
+
+    def verify(self):
+        """Recovered cells must equal the original data (the stripes were
+        encoded from it); parity must be stable across steps."""
+        import numpy as np
+
+        img = self.stripes.array.reshape(self.S, self.k + self.p, self.C)
+        return bool(np.array_equal(img[:, :self.k], self.data.array.reshape(self.S, self.k, self.C)))
+
+    def free(self):
+        for b in (self.data, self.parity, self.stripes):
+            b.free()
+
+
+def pinned_copy_rates(ctx, n=1 << 30):
+    """Raw pinned hipMemcpy H2D / D2H GB/s on this rank's device."""
+    h = ctx.host_alloc(n)
+    d = ctx.alloc(n)
+    h.array[:] = 7
+    from daos_amd import ecg
+
+    out = {}
+    for kind, name in ((0, "h2d"), (1, "d2h")):
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            if kind == 0:
+                ecg._chk(ecg.lib().ecg_memcpy(ctx.h, d.ptr, h.ptr, n, 0, None), "h2d")
+            else:
+                ecg._chk(ecg.lib().ecg_memcpy(ctx.h, h.ptr, d.ptr, n, 1, None), "d2h")
+            ctx.sync()
+            ts.append(time.perf_counter() - t0)
+        out[name] = round(n / sorted(ts)[1] / 1e9, 2)
+    h.free()
+    d.free()
+    return out
 
 
 def time_kernel(ctx, fn, iters):
@@ -350,6 +443,54 @@ def pmc_traffic():
     return None
 
 
+def host_report(args, ctx, wl, world, rank, value, elapsed):
+    """JSON line of the PCIe-inclusive rebuild stream (configs[4]).  The
+    device kernels are not the bound here, the host links are: `roofline`
+    is null and `pcie` sets the achieved H2D rate against this box's raw
+    pinned copy rate (measured on rank 0 at N=1)."""
+    k, p, C, S = wl.k, wl.p, wl.C, wl.S
+    ok = wl.verify()
+    h2d = wl.h2d_bytes_per_step() * args.steps * world / elapsed / 1e9
+    d2h = wl.d2h_bytes_per_step() * args.steps * world / elapsed / 1e9
+    out = {
+        "metric": "EC rebuild stream GiB/s (host-resident stripes, PCIe-inclusive)",
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: xoshiro256** stripes in pinned host memory",
+        "config": {"workload": f"EC_{k}P{p} {C >> 10} KiB cells: per step one encode batch of {S} stripes "
+                               f"+ one {{d0,d1}} recovery batch of {S} stripes per GPU, host<->device copies "
+                               f"included ({HOST_CHUNK}-stripe staging chunks)",
+                   "name": args.workload, "k": k, "p": p, "cell_bytes": C, "stripes_per_gpu": S,
+                   "erasures": wl.err, "parallelism": f"stripe-sharded x{world}, no collective"},
+        "roofline": None,
+        "pcie": {"bound": "pcie", "h2d_GBps_all_ranks": round(h2d, 2), "d2h_GBps_all_ranks": round(d2h, 2)},
+        "recovered_bytes_ok": ok,
+        "cpu_baseline": None,
+    }
+    wl.free()
+    if rank == 0 and world == 1 and not args.no_detail:
+        raw = pinned_copy_rates(ctx)
+        out["pcie"]["measured_pinned_GBps"] = raw
+        out["pcie"]["frac_of_h2d"] = round(h2d / raw["h2d"], 4)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+    if not ok:
+        raise SystemExit("bench.py: recovered cells differ from the original data")
+
+
 def main():
     args = parse()
     world, rank, local = dist_init()
@@ -366,7 +507,8 @@ def main():
     k, p, C, S, ops, strong = WORKLOADS[args.workload]
     if strong:                      # configs[3]: a fixed stripe total split across ranks
         S = S // world + (1 if rank < S % world else 0)
-    wl = Workload(ctx, k, p, C, S, ops=ops)
+    host = ops[0].endswith("_host")
+    wl = (HostWorkload if host else Workload)(ctx, k, p, C, S, ops=ops)
 
     for _ in range(args.warmup):
         wl.step()
@@ -394,6 +536,9 @@ def main():
     else:           # every rank processed the same batch
         user = wl.user_bytes_per_step() * args.steps * world
     value = user / elapsed / GIB
+    if host:
+        host_report(args, ctx, wl, world, rank, value, elapsed)
+        return
     kms = wl.kernel_ms()
     launches = [(op, ms) for op in ops for ms in kms[op]]
     mean_launch_ms = sum(ms for _, ms in launches) / len(launches)

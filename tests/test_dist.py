@@ -62,5 +62,20 @@ def test_weak_scaling_accounting():
     assert wl.alg_bytes("enc") == wl.alg_bytes("dec") == 6 * (1 << 20) * 1024
     wl.k, wl.p, wl.ops = 16, 2, ("enc",)
     assert wl.user_bytes_per_step() == 16 * (1 << 20) * 1024
-    assert set(bench.WORKLOADS) == {"enc_dec_4p2", "dec_8p2", "enc_16p2_strong"}
+    assert set(bench.WORKLOADS) == {"enc_dec_4p2", "dec_8p2", "enc_16p2_strong", "rebuild_stream_8p2"}
     assert bench.WORKLOADS["enc_dec_4p2"][:4] == (4, 2, 1 << 20, 1024)      # BASELINE configs[1]
+
+
+def test_host_stream_accounting():
+    """configs[4] (rebuild stream): user bytes = k cells per stripe per batch,
+    H2D = the k inputs (encode) / k survivors (recovery), D2H = p parity cells
+    + the erased cells."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    wl = bench.HostWorkload.__new__(bench.HostWorkload)
+    wl.k, wl.p, wl.C, wl.S, wl.err, wl.ops = 8, 2, 1 << 20, 64, [0, 1], ("enc_host", "dec_host")
+    assert wl.user_bytes_per_step() == 2 * 8 * (1 << 20) * 64
+    assert wl.h2d_bytes_per_step() == 2 * 8 * (1 << 20) * 64
+    assert wl.d2h_bytes_per_step() == (2 + 2) * (1 << 20) * 64
+    assert bench.WORKLOADS["rebuild_stream_8p2"][:2] == (8, 2)
