@@ -544,6 +544,7 @@ def main():
     mean_launch_ms = sum(ms for _, ms in launches) / len(launches)
     alg_per_launch = sum(wl.alg_bytes(op) for op, _ in launches) / len(launches)
     achieved = alg_per_launch / (mean_launch_ms / 1e3) / 1e9
+    read_GBps = k * C * S / (mean_launch_ms / 1e3) / 1e9
     kernel_name = f"ecg_mm_kernel<{k},{p},0,0>"
     traffic = None
     pmc = pmc_traffic()
@@ -570,6 +571,8 @@ def main():
                    "parallelism": f"stripe-sharded x{world}, no collective"},
         "roofline": {"bound": "hbm", "kernel": kernel_name, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     # north star's "fraction of HBM-read peak": the k input cells read per launch
+                     "read_GBps": round(read_GBps, 1), "read_frac": round(read_GBps / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "alg_bytes_per_launch": int(alg_per_launch),
                      "mean_launch_ms": round(mean_launch_ms, 4),
                      **{f"{op}_ms_median": round(sorted(kms[op])[len(kms[op]) // 2], 4) for op in ops}},

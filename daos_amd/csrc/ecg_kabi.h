@@ -76,7 +76,7 @@ typedef struct ecg_launch_cfg {
  *   sh[NB][256]  "shift by ECG_CSUM_STRIDE zero bytes" as a byte-wise linear map
  *   k[64]        x^(8*16*(63-lane)) mod P, for the final per-lane shift
  *   sh4k[NB][256] shift by ECG_MMCS_STRIDE zero bytes (fused kernels)
- *   k256[256]    x^(8*16*(255-thread)) mod P (fused kernels)
+ *   k256[256]    x^(8*16*(255-thread)) mod P (host builds the fused kh rows from it)
  *   p2[48]       x^(8*2^j) mod P (shift by any byte count: product over its bits)
  * with NB = W/8, T = uint32_t (W <= 32) or uint64_t (W = 64).
  */
@@ -123,17 +123,30 @@ typedef struct ecg_csum_params {
  * bytes are still in registers.  Each output cell starts on a chunk boundary;
  * chunk_bytes is a multiple of ECG_MMCS_STRIDE; cell_bytes a multiple of 16.
  * out[(row_slot[r] * nstripes + s) * nch + c] = checksum of chunk c of output
- * row r of stripe s.  tail_fix = x^(-8Z) mod P undoes the Z zero bytes that
- * pad the last chunk of a cell to a whole number of 4 KiB steps.
+ * row r of stripe s (zeroed by the host: workgroups XOR their partials in).
+ *
+ * Work items: chunk c (m 4 KiB columns; m_last for the last chunk of a cell)
+ * is cut into sub-chunks of ncols columns, item = (c, h) with h < nh (nh_last
+ * for the last chunk), numbered c * nh + h; nitems = (nch - 1) * nh + nh_last.
+ * A workgroup Horner-accumulates its sub-chunk's columns per thread and then
+ * multiplies thread t's value by kh[(row0 + h) * 256 + t] (row0 = 0, or nh for
+ * the last chunk) = x^(8 * (16 * (255 - t) + 4096 * (columns after the
+ * sub-chunk))) mod P, times x^(-8Z) in the last chunk's rows, Z being the zero
+ * bytes that pad the cell to whole columns.  CRC is linear, so the
+ * workgroups' values XOR to the chunk's CRC.
  */
 typedef struct ecg_mmcs_params {
 	const void *tbl;
 	uint8_t *out;
+	const void *kh;			/* (nh + nh_last) x 256 entries, T as tbl */
 	uint64_t chunk_bytes;
 	uint64_t init, xorout, poly;
-	uint64_t tail_fix;
 	uint32_t nch;
 	uint32_t type;
+	uint32_t m, m_last;		/* 4 KiB columns per chunk / in the last chunk */
+	uint32_t ncols;			/* columns per item */
+	uint32_t nh, nh_last;		/* items per chunk / in the last chunk */
+	uint32_t nitems;
 	uint32_t row_slot[ECG_KMAX_R];
 } ecg_mmcs_params_t;
 

@@ -279,6 +279,117 @@ void ecg_csum_ctx_fini(ecg_ctx_t *ctx)
 			(void)hipFree(ctx->csum_tbl[i]);
 			ctx->csum_tbl[i] = NULL;
 		}
+	for (int i = 0; i < ECG_NKH_CACHE; i++)
+		if (ctx->kh_cache[i].dev) {
+			(void)hipFree(ctx->kh_cache[i].dev);
+			memset(&ctx->kh_cache[i], 0, sizeof(ctx->kh_cache[i]));
+		}
+}
+
+/* Columns per fused-kernel work item: a whole chunk up to 4 columns (8 for
+ * crc64, whose 64-step reduction costs twice crc32's), else 4 / 8
+ * (tools/tune11.py, profiles/r01/tune11_fused_cols.jsonl: EC_8P2 1 MiB cells,
+ * crc32 32 KiB chunks 1.00 -> 0.89 ms vs a whole chunk per workgroup, crc64
+ * best at 8); ECG_FUSED_COLS overrides (tuning). */
+static uint32_t fused_cols(uint64_t m, int type)
+{
+	const uint64_t dflt = type == ECG_HASH_CRC64 ? 8 : 4;
+	static int env = -1;
+
+	if (env < 0) {
+		const char *e = getenv("ECG_FUSED_COLS");
+
+		env = e ? atoi(e) : 0;
+		if (env < 0)
+			env = 0;
+	}
+	if (env > 0)
+		return (uint32_t)((uint64_t)env < m ? (uint64_t)env : m);
+	return (uint32_t)(m < dflt ? m : dflt);
+}
+
+/* Device table of the fused kernel's per-(item row, thread) multipliers
+ * (ecg_kabi.h ecg_mmcs_params kh): row h < nh of a full chunk of m columns,
+ * rows nh + h of the last chunk (m_last columns, z padding bytes):
+ *   kh[row][t] = x^(8*(16*(255-t) + 4096*(columns after item h))) * x^(-8z)
+ * Cached per context by (type, chunk bytes, columns per item, last length). */
+static int fused_kh(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, uint32_t ncols,
+		    uint32_t nh, uint32_t nh_last, const void **out)
+{
+	const struct crc_def *d = &g_defs[type];
+	const uint64_t m = rcs / ECG_MMCS_STRIDE;
+	const uint64_t m_last = (last + ECG_MMCS_STRIDE - 1) / ECG_MMCS_STRIDE;
+	const uint64_t z = m_last * ECG_MMCS_STRIDE - last;
+	const size_t es = d->width == 64 ? 8 : 4, nrow = (size_t)nh + nh_last;
+	struct ecg_kh_ent *e;
+	uint64_t k256[256];
+	unsigned char *img;
+	void *dev = NULL;
+	hipError_t he;
+	int rc = 0;
+
+	pthread_mutex_lock(&ctx->lock);
+	for (int i = 0; i < ECG_NKH_CACHE; i++) {
+		e = &ctx->kh_cache[i];
+		if (e->valid && e->type == type && e->rcs == rcs && e->last == last && e->ncols == ncols) {
+			*out = e->dev;
+			pthread_mutex_unlock(&ctx->lock);
+			return 0;
+		}
+	}
+	img = malloc(nrow * 256 * es);
+	if (img == NULL) {
+		pthread_mutex_unlock(&ctx->lock);
+		return ecg_fail(-ECG_DER_NOMEM, "fused csum multipliers");
+	}
+	k256[255] = crc_one(d);
+	for (int t = 254; t >= 0; t--)
+		k256[t] = crc_mulmod(d, k256[t + 1], crc_xpow8(d, 16));
+	for (size_t row = 0; row < nrow; row++) {
+		const int lastc = row >= nh;
+		const uint64_t h = lastc ? row - nh : row, mc = lastc ? m_last : m;
+		const uint64_t end = (h + 1) * ncols < mc ? (h + 1) * ncols : mc;
+		uint64_t sh = crc_xpow8(d, (mc - end) * ECG_MMCS_STRIDE);
+
+		if (lastc)
+			sh = crc_mulmod(d, sh, crc_unshift(d, z));
+		for (int t = 0; t < 256; t++) {
+			const uint64_t v = crc_mulmod(d, k256[t], sh);
+
+			if (es == 8) {
+				memcpy(img + (row * 256 + t) * 8, &v, 8);
+			} else {
+				const uint32_t w = (uint32_t)v;
+
+				memcpy(img + (row * 256 + t) * 4, &w, 4);
+			}
+		}
+	}
+	he = hipMalloc(&dev, nrow * 256 * es);
+	if (he == hipSuccess)
+		he = hipMemcpy(dev, img, nrow * 256 * es, hipMemcpyHostToDevice);
+	free(img);
+	if (he != hipSuccess) {
+		if (dev)
+			(void)hipFree(dev);
+		pthread_mutex_unlock(&ctx->lock);
+		return ecg_hip_fail(he, "fused csum multipliers");
+	}
+	e = &ctx->kh_cache[ctx->kh_next++ % ECG_NKH_CACHE];
+	if (e->dev) {
+		/* launches queued on any stream may still read the evicted table */
+		(void)hipDeviceSynchronize();
+		(void)hipFree(e->dev);
+	}
+	e->valid = 1;
+	e->type = type;
+	e->rcs = rcs;
+	e->last = last;
+	e->ncols = ncols;
+	e->dev = dev;
+	*out = dev;
+	pthread_mutex_unlock(&ctx->lock);
+	return rc;
 }
 
 int ecg_csum_extents(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_size,
@@ -381,7 +492,7 @@ int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t
 {
 	const uint64_t rcs = ecg_csum_record_chunksize(chunksize, rec_size);
 	const struct crc_def *d;
-	uint64_t last, z;
+	uint64_t last, m;
 	int rc;
 
 	memset(q, 0, sizeof(*q));
@@ -404,7 +515,17 @@ int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t
 	q->poly = d->poly;
 	q->type = (uint32_t)type;
 	last = C - (uint64_t)(q->nch - 1) * rcs;
-	z = (last + ECG_MMCS_STRIDE - 1) / ECG_MMCS_STRIDE * ECG_MMCS_STRIDE - last;
-	q->tail_fix = crc_unshift(d, z);
+	m = rcs / ECG_MMCS_STRIDE;
+	q->m = (uint32_t)m;
+	q->m_last = (uint32_t)((last + ECG_MMCS_STRIDE - 1) / ECG_MMCS_STRIDE);
+	q->ncols = fused_cols(m, type);
+	q->nh = (uint32_t)((m + q->ncols - 1) / q->ncols);
+	q->nh_last = (q->m_last + q->ncols - 1) / q->ncols;
+	if ((uint64_t)(q->nch - 1) * q->nh + q->nh_last > UINT32_MAX)
+		return 0;
+	q->nitems = (q->nch - 1) * q->nh + q->nh_last;
+	rc = fused_kh(ctx, type, rcs, last, q->ncols, q->nh, q->nh_last, &q->kh);
+	if (rc)
+		return rc;
 	return 1;
 }

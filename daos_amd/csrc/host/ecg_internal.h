@@ -70,6 +70,14 @@ struct ecg_ctx {
 		uint64_t sh[ECG_CSUM_SPLIT_NW];
 	} split_cache[ECG_NSPLIT_CACHE];
 	unsigned split_next;
+#define ECG_NKH_CACHE 8
+	struct ecg_kh_ent {		/* fused-kernel item multipliers (ecg_csum.c) */
+		int valid, type;
+		uint64_t rcs, last;
+		uint32_t ncols;
+		void *dev;
+	} kh_cache[ECG_NKH_CACHE];
+	unsigned kh_next;
 	struct ecg_scratch scratch;
 };
 

@@ -274,25 +274,43 @@ ecg_mm_kernel(const ecg_mm_params_t P)
 	}
 }
 
+// Work item `it` of the fused kernel -> chunk c, sub-chunk h, its columns
+// [col0, col1) and the row of Q.kh its threads multiply by (ecg_kabi.h).
+__device__ __forceinline__ void mmcs_item(const ecg_mmcs_params_t &Q, uint32_t it, uint32_t &c, uint32_t &col0,
+					  uint32_t &col1, uint32_t &khrow)
+{
+	c = it / Q.nh;
+	const uint32_t h = it - c * Q.nh;
+	const bool lastc = c + 1 == Q.nch;
+	const uint32_t m = lastc ? Q.m_last : Q.m;
+
+	col0 = h * Q.ncols;
+	col1 = col0 + Q.ncols < m ? col0 + Q.ncols : m;
+	khrow = (lastc ? Q.nh : 0) + h;
+}
+
 // Fused product + checksum of every output cell (ecg_kabi.h, ecg_mmcs_params).
-// Block = one (stripe, checksum chunk) item; it walks the chunk's 4 KiB
-// columns, computing and storing the outputs exactly as ecg_mm_kernel does,
-// and folds each thread's 16-byte output piece into a per-row Horner CRC
-// (acc = shift_4KiB(acc) ^ crc(piece)).  At the end of the chunk every
-// thread multiplies by x^(8*16*(255-t)) mod P, the block XOR-reduces, a
-// ragged last chunk is corrected by tail_fix, and the checksum is stored.
+// Block = a stream of (stripe, sub-chunk) items of a few 4 KiB columns each;
+// it walks the columns, computing and storing the outputs exactly as
+// ecg_mm_kernel does, and folds each thread's 16-byte output piece into a
+// per-row Horner CRC (acc = shift_4KiB(acc) ^ crc(piece)).  At the end of an
+// item every thread multiplies by its kh entry (moves its pieces to the end
+// of the chunk, undoes a ragged last chunk's zero padding), the waves
+// XOR-reduce and XOR their values into the zeroed checksum.  Cutting a
+// chunk into several items keeps one workgroup from walking a whole 32 KiB+
+// chunk serially (tools/tune8.py: ~4 columns per workgroup is best).
 // The outputs are never re-read from HBM: the checksum costs LDS lookups on
 // p/(k+p) of the traffic instead of a second pass over the regenerated
 // cells (ref:src/object/srv_obj_migrate.c:1156 checksums them after encode).
 template <int K, int R, int W, bool REFL>
-__global__ void __launch_bounds__(BLOCK)
+__global__ void __launch_bounds__(BLOCK, 4)	// >= 4 waves per SIMD: <= 128 VGPRs
 ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 {
 	using T = typename ecg_crc::reg<W>::T;
 	constexpr int NB = W / 8;
 	constexpr int KM = K ? K : ECG_KMAX_K;
 	constexpr int RM = R ? R : ECG_KMAX_R;
-	constexpr bool PF = K != 0 && K <= 8;	// prefetch: 4*KM more VGPRs
+	constexpr bool PF = K != 0 && K <= 8 && W != 64;	// prefetch: 4*KM more VGPRs (crc64 spills)
 	constexpr int T2V = (RM + 3) / 4;
 	constexpr int PER_J = RM + T2V;
 	__shared__ u32x4 s_tbl[KM * PER_J];
@@ -316,106 +334,88 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 		s_sl[i] = gt[i];
 		s_sh[i] = gt[ECG_CSUM_OFF_SH4K(NB) + i];
 	}
-	const T kt = gt[ECG_CSUM_OFF_K256(NB) + threadIdx.x];
+	const T *kh = (const T *)Q.kh;
 	const T poly = (T)Q.poly;
 	__syncthreads();
 
-	// The workgroup's work is a stream of (chunk, column) steps: chunks
-	// blockIdx.x, blockIdx.x + gridDim.x, ... of stripe blockIdx.y (+ gridDim.y
-	// ...), each chunk's 4 KiB columns in order.  With PF the next step's
-	// loads are issued before this step's product and before a chunk's
-	// reduction, so HBM requests stay in flight across both.
+	// The workgroup's work: items blockIdx.x, blockIdx.x + gridDim.x, ... of
+	// stripe blockIdx.y (+ gridDim.y ...), each item's 4 KiB columns in
+	// order.  With PF the next column's loads are issued before this
+	// column's product, so HBM requests stay in flight across it.  Live state
+	// is kept small on purpose: the crc64 instantiations ran out of SGPRs.
 	for (uint32_t s = blockIdx.y; s < P.nstripes; s += gridDim.y) {
-		uint32_t c = blockIdx.x, i = 0;
-		bool first = true;
-		T crc[RM];
-		u32x4 xa[KM];
+		for (uint32_t it = blockIdx.x; it < Q.nitems; it += gridDim.x) {
+			uint32_t c, i, col1, khrow;
+			T crc[RM];
+			u32x4 xa[KM];
 
-		if (c >= Q.nch)
-			continue;
-#pragma unroll
-		for (int r = 0; r < RM; r++)
-			crc[r] = 0;
-		if ((uint64_t)c * Q.chunk_bytes + lo + 16 <= C)
-			mm_load<KM, false>(P, k, s, (uint64_t)c * Q.chunk_bytes, lo, xa);
-		for (;;) {
+			mmcs_item(Q, it, c, i, col1, khrow);
 			const uint64_t c0 = (uint64_t)c * Q.chunk_bytes;
-			const uint64_t clen = C - c0 < Q.chunk_bytes ? C - c0 : Q.chunk_bytes;
-			const uint32_t m = (uint32_t)((clen + CHUNK_BYTES - 1) / CHUNK_BYTES);
-			const uint64_t cbase = c0 + (uint64_t)i * CHUNK_BYTES;
-			const bool have = cbase + lo + 16 <= C;	// C % 16 == 0
-			const bool last = i + 1 == m;
-			const uint32_t nc = last ? c + gridDim.x : c, ni = last ? 0 : i + 1;
-			const bool more = nc < Q.nch;
-			const uint64_t nbase = (uint64_t)nc * Q.chunk_bytes + (uint64_t)ni * CHUNK_BYTES;
-			u32x4 outv[RM];
-			u32x4 xb[PF ? KM : 1];
-			uint32_t z = 0;
-
-			if constexpr (PF) {
-				if (more && nbase + lo + 16 <= C)
-					mm_load<KM, false>(P, k, s, nbase, lo, xb);
-			} else if (!first) {
-				if (cbase + CHUNK_BYTES <= C)
-					mm_load<KM, false>(P, k, s, cbase, lo, xa);
-				else if (have)
-					mm_load<KM, false>(P, k, s, cbase, lo, xa);
-			}
-			first = false;
-			asm volatile("" : "+v"(z));
-			const u32x4 *tb = s_tbl + z;
-			if (cbase + CHUNK_BYTES <= C)
-				mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, xa, outv);
-			else if (have)
-				mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, xa, outv);
 #pragma unroll
-			for (int r = 0; r < RM; r++) {
-				if (r < rows) {
-					crc[r] = ecg_crc::lin_map<W>(crc[r], s_sh);
-					if (have) {
-						uint32_t d[4] = {outv[r][0], outv[r][1], outv[r][2], outv[r][3]};
-						if (i == 0 && threadIdx.x == 0) {	// initial register
-							d[0] ^= (uint32_t)Q.init;
-							if constexpr (W == 64)
-								d[1] ^= (uint32_t)(Q.init >> 32);
-						}
-						crc[r] ^= ecg_crc::piece_crc<W, REFL>(d, s_sl);
-					}
-				}
+			for (int r = 0; r < RM; r++)
+				crc[r] = 0;
+			if constexpr (PF) {
+				if (c0 + (uint64_t)i * CHUNK_BYTES + lo + 16 <= C)
+					mm_load<KM, false>(P, k, s, c0 + (uint64_t)i * CHUNK_BYTES, lo, xa);
 			}
-			if (last) {
-				// each wave XORs its partial into the (zeroed) output: no
-				// workgroup barrier, other waves keep streaming
+			for (; i < col1; i++) {
+				const uint64_t cbase = c0 + (uint64_t)i * CHUNK_BYTES;
+				const bool have = cbase + lo + 16 <= C;	// C % 16 == 0
+				u32x4 outv[RM];
+				u32x4 xb[PF ? KM : 1];
+				uint32_t z = 0;
+
+				if constexpr (PF) {
+					if (i + 1 < col1 && cbase + CHUNK_BYTES + lo + 16 <= C)
+						mm_load<KM, false>(P, k, s, cbase + CHUNK_BYTES, lo, xb);
+				} else if (have) {
+					mm_load<KM, false>(P, k, s, cbase, lo, xa);
+				}
+				asm volatile("" : "+v"(z));
+				const u32x4 *tb = s_tbl + z;
+				if (cbase + CHUNK_BYTES <= C)
+					mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, xa, outv);
+				else if (have)
+					mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, xa, outv);
 #pragma unroll
 				for (int r = 0; r < RM; r++) {
 					if (r < rows) {
-						T v = ecg_crc::mulmod<W, REFL>(kt, crc[r], poly);
-						v = ecg_crc::wave_xor(v);
-						crc[r] = 0;
-						if ((threadIdx.x & 63) == 0) {
-							if (clen & (CHUNK_BYTES - 1))	// linear: per wave
-								v = ecg_crc::mulmod<W, REFL>((T)Q.tail_fix, v, poly);
-							if (threadIdx.x == 0)
-								v ^= (T)Q.xorout;
-							const uint64_t slot =
-								((uint64_t)Q.row_slot[r] * P.nstripes + s) * Q.nch + c;
-							if constexpr (W == 16)
-								atomicXor((uint32_t *)Q.out + slot / 2,
-									  (uint32_t)v << (16 * (slot & 1)));
-							else
-								atomicXor((T *)Q.out + slot, v);
+						crc[r] = ecg_crc::lin_map<W>(crc[r], s_sh);
+						if (have) {
+							uint32_t d[4] = {outv[r][0], outv[r][1], outv[r][2], outv[r][3]};
+							if (i == 0 && threadIdx.x == 0) {	// initial register
+								d[0] ^= (uint32_t)Q.init;
+								if constexpr (W == 64)
+									d[1] ^= (uint32_t)(Q.init >> 32);
+							}
+							crc[r] ^= ecg_crc::piece_crc<W, REFL>(d, s_sl);
 						}
 					}
 				}
-			}
-			if (!more)
-				break;
-			c = nc;
-			i = ni;
-			if constexpr (PF) {
+				if constexpr (PF) {
 #pragma unroll
-				for (int j = 0; j < KM; j++)
-					xa[j] = xb[j];
+					for (int j = 0; j < KM; j++)
+						xa[j] = xb[j];
+				}
+			}
+			// each wave XORs its partial into the (zeroed) output: no
+			// workgroup barrier, other waves keep streaming
+			const T kcur = kh[khrow * 256 + threadIdx.x];
+#pragma unroll
+			for (int r = 0; r < RM; r++) {
+				if (r < rows) {
+					T v = ecg_crc::mulmod<W, REFL>(kcur, crc[r], poly);
+					v = ecg_crc::wave_xor(v);
+					if ((threadIdx.x & 63) == 0) {
+						if (threadIdx.x == 0 && khrow == (c + 1 == Q.nch ? Q.nh : 0))
+							v ^= (T)Q.xorout;	// once per chunk
+						const uint64_t slot = ((uint64_t)Q.row_slot[r] * P.nstripes + s) * Q.nch + c;
+						if constexpr (W == 16)
+							atomicXor((uint32_t *)Q.out + slot / 2, (uint32_t)v << (16 * (slot & 1)));
+						else
+							atomicXor((T *)Q.out + slot, v);
+					}
+				}
 			}
 		}
 	}
@@ -825,12 +825,15 @@ extern "C" int ecg_k_launch_matmul_csum(const ecg_mm_params_t *p, const ecg_mmcs
 			}
 	if (id == N_CSKERNELS)
 		return (int)hipErrorInvalidValue;
+	if (q->nitems == 0 || q->ncols == 0 || q->kh == nullptr)
+		return (int)hipErrorInvalidValue;
 	// default: ~16 KiB of columns per workgroup (tools/tune8.py,
 	// profiles/r01/tune8_fused_chunks.json: walking more columns per
-	// workgroup loses HBM parallelism, fewer pays a chunk reduction per
-	// column); chunks >= 16 KiB -> one chunk per workgroup
-	const uint64_t cpb = q->chunk_bytes >= 16384 ? 1 : 16384 / q->chunk_bytes;
-	uint32_t gx = cfg && cfg->grid_x ? cfg->grid_x : (uint32_t)((q->nch + cpb - 1) / cpb);
+	// workgroup loses HBM parallelism, fewer pays a reduction per column);
+	// one-column items (4 KiB chunks) 8 per workgroup, two-column items 2,
+	// longer items one per workgroup
+	const uint64_t ipb = q->ncols == 1 ? 8 : q->ncols == 2 ? 2 : 1;
+	uint32_t gx = cfg && cfg->grid_x ? cfg->grid_x : (uint32_t)((q->nitems + ipb - 1) / ipb);
 	uint32_t gy = cfg && cfg->grid_y ? cfg->grid_y : (p->nstripes < 65535 ? p->nstripes : 65535);
 	if (gx > 65535)
 		gx = 65535;
