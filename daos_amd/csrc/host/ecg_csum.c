@@ -459,6 +459,8 @@ int ecg_csum_extents(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_
 			prm.split_m[c] = (lens[c] / 16 + 63) / 64;
 			split_shifts(ctx, type, prm.split_m[c], prm.split_sh[c]);
 		}
+	} else {
+		prm.variant = ctx->csum_variant;	/* adler32: the kernel picks by shape when 0 */
 	}
 	e = ecg_k_launch_csum(&prm, (void *)ecg_pick_stream(ctx, stream), ctx->csum_blocks, &kid);
 	if (e != 0)

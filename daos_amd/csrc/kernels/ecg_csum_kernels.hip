@@ -309,6 +309,77 @@ __global__ __launch_bounds__(CS_BLOCK) void ecg_adler_kernel(ecg_csum_params_t p
 	}
 }
 
+// adler32 of long chunks that are few (one wave per chunk would leave the
+// CUs idle, e.g. 1024 chunks of 1 MiB): a workgroup of NW waves per chunk.
+// The sums use absolute positions within the chunk, so the threads' partial
+// sums simply add: thread t takes the 16-byte pieces t, t + 64*NW, ... (every
+// load instruction of a wave still reads 1 KiB contiguous), the waves reduce
+// with shuffles and combine through LDS.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void ecg_adler_split_kernel(ecg_csum_params_t p)
+{
+	__shared__ uint64_t ps[NW], pw[NW];
+	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+	const uint64_t total = (uint64_t)p.n_ext * p.nchunks;
+
+	for (uint64_t g = blockIdx.x; g < total; g += gridDim.x) {
+		uint64_t off, len;
+		const uint8_t *base;
+
+		chunk_geom(p, g, off, len, base);
+		const uint64_t nq = len / 16;
+		uint64_t s = 0, w = 0;
+
+		for (uint64_t q = threadIdx.x, it = 0; q < nq; q += 64 * NW, it++) {
+			uint32_t d[4];
+			uint32_t s16 = 0, w16 = 0;
+
+			load16<true>(base + 16 * q, d);
+#pragma unroll
+			for (int j = 0; j < 4; j++) {
+				s16 = __builtin_amdgcn_udot4(d[j], 0x01010101u, s16, false);
+				w16 = __builtin_amdgcn_udot4(d[j], 0x03020100u + 0x04040404u * j, w16, false);
+			}
+			s += s16;
+			w += 16 * q * (uint64_t)s16 + w16;
+			if ((it & 255) == 255) {
+				s %= ADLER_MOD;
+				w %= ADLER_MOD;
+			}
+		}
+		s %= ADLER_MOD;
+		w %= ADLER_MOD;
+#pragma unroll
+		for (int sft = 32; sft >= 1; sft >>= 1) {
+			s += __shfl_xor(s, sft);
+			w += __shfl_xor(w, sft);
+		}
+		if (lane == 0) {
+			ps[wv] = s;
+			pw[wv] = w;
+		}
+		__syncthreads();
+		if (threadIdx.x == 0) {
+			s = 0;
+			w = 0;
+#pragma unroll
+			for (int i = 0; i < NW; i++) {
+				s += ps[i];
+				w += pw[i];
+			}
+			for (uint64_t b = nq * 16; b < len; b++) {
+				s += base[b];
+				w += b * (uint64_t)base[b];
+			}
+			const uint64_t A = s % ADLER_MOD;
+			const uint64_t Bp = ((len % ADLER_MOD) * A) % ADLER_MOD;
+			const uint64_t B = (Bp + ADLER_MOD - w % ADLER_MOD) % ADLER_MOD;
+			((uint32_t *)p.out)[g] = (uint32_t)((B << 16) | A);
+		}
+		__syncthreads();
+	}
+}
+
 typedef void (*csum_fn_t)(ecg_csum_params_t);
 struct csum_entry {
 	uint32_t type;
@@ -334,6 +405,7 @@ const csum_entry g_split[] = {
 	{1, true, ecg_crc_split_kernel<16, false, SPLIT_NW>, "ecg_crc_split_kernel<crc16>"},
 	{2, true, ecg_crc_split_kernel<32, true, SPLIT_NW>, "ecg_crc_split_kernel<crc32>"},
 	{3, true, ecg_crc_split_kernel<64, true, SPLIT_NW>, "ecg_crc_split_kernel<crc64>"},
+	{7, true, ecg_adler_split_kernel<SPLIT_NW>, "ecg_adler_split_kernel"},
 };
 constexpr uint32_t N_SPLIT = sizeof(g_split) / sizeof(g_split[0]);
 
@@ -358,9 +430,10 @@ extern "C" int ecg_k_launch_csum(const ecg_csum_params_t *p, void *stream, uint3
 
 	if (total == 0)
 		return (int)hipSuccess;
-	if (p->type != 7 && aligned) {
+	if (aligned) {
 		// a workgroup per chunk when one wave per chunk would leave fewer
 		// than 4 waves per SIMD and every wave still gets >= 2 steps
+		// (adler32 too: profiles/r01/bench_csum.json adler32_cs1024K rows)
 		const uint64_t steps = (p->chunk_bytes / 16 + 63) / 64;
 		const bool split = p->variant == 2 ||
 				   (p->variant == 0 && total < 4096 && steps >= 2 * SPLIT_NW);

@@ -65,13 +65,14 @@ def test_csum_parity(oracle, ecglib, ctx, htype, geom):
 
 
 @pytest.mark.parametrize("variant", [1, 2])
-@pytest.mark.parametrize("htype", (1, 2, 3))
+@pytest.mark.parametrize("htype", (1, 2, 3, 7))
 @pytest.mark.parametrize("geom", GEOMS + [(1 << 20, 1, 0, 3 << 20), ((1 << 20) + 4096, 1, 5, 2 << 20),
                                           (65536, 16, 0, 70001), (2048, 1, 0, 100000)])
 def test_crc_kernel_shapes(oracle, ecglib, ctx, variant, htype, geom):
-    """Both CRC kernel shapes on every geometry: a wave per chunk (1) and a
-    workgroup per chunk whose waves' slice CRCs are shifted and combined (2);
-    chunks shorter than the workgroup's slices leave waves idle."""
+    """Both kernel shapes on every geometry: a wave per chunk (1) and a
+    workgroup per chunk (2) -- CRC: the waves' slice CRCs shifted and
+    combined; adler32: the threads' position-weighted sums added; chunks
+    shorter than the workgroup's slices leave waves idle."""
     cs, rb, idx, nr = geom
     L = ecglib.lib()
     rng = np.random.default_rng((hash(geom) + htype) & 0xFFFFFFFF)
