@@ -291,18 +291,23 @@ void ecg_csum_ctx_fini(ecg_ctx_t *ctx)
  * (tools/tune11.py, profiles/r01/tune11_fused_cols.jsonl: EC_8P2 1 MiB cells,
  * crc32 32 KiB chunks 1.00 -> 0.89 ms vs a whole chunk per workgroup, crc64
  * best at 8); ECG_FUSED_COLS overrides (tuning). */
+static int g_fused_cols_env;
+static pthread_once_t g_fused_cols_once = PTHREAD_ONCE_INIT;
+
+static void fused_cols_init(void)
+{
+	const char *e = getenv("ECG_FUSED_COLS");
+
+	g_fused_cols_env = e ? atoi(e) : 0;
+	if (g_fused_cols_env < 0)
+		g_fused_cols_env = 0;
+}
+
 static uint32_t fused_cols(uint64_t m, int type)
 {
 	const uint64_t dflt = type == ECG_HASH_CRC64 ? 8 : 4;
-	static int env = -1;
+	const int env = (pthread_once(&g_fused_cols_once, fused_cols_init), g_fused_cols_env);
 
-	if (env < 0) {
-		const char *e = getenv("ECG_FUSED_COLS");
-
-		env = e ? atoi(e) : 0;
-		if (env < 0)
-			env = 0;
-	}
 	if (env > 0)
 		return (uint32_t)((uint64_t)env < m ? (uint64_t)env : m);
 	return (uint32_t)(m < dflt ? m : dflt);
