@@ -78,6 +78,7 @@ typedef struct ecg_launch_cfg {
  *   sh4k[NB][256] shift by ECG_MMCS_STRIDE zero bytes (fused kernels)
  *   k256[256]    x^(8*16*(255-thread)) mod P (host builds the fused kh rows from it)
  *   p2[48]       x^(8*2^j) mod P (shift by any byte count: product over its bits)
+ *   sh256[NB][256] shift by ECG_CSUM_GSTRIDE zero bytes (lane-group kernel)
  * with NB = W/8, T = uint32_t (W <= 32) or uint64_t (W = 64).
  */
 #define ECG_CSUM_STRIDE 1024	/* bytes a wave consumes per step (64 lanes x 16 B) */
@@ -85,8 +86,11 @@ typedef struct ecg_launch_cfg {
 
 #define ECG_MMCS_STRIDE 4096	/* fused kernels: 256 threads x 16 B per step */
 #define ECG_CSUM_NP2 48
-#define ECG_CSUM_TBL_ENTRIES(NB) (3 * (NB) * 256 + 64 + 256 + ECG_CSUM_NP2)
+#define ECG_CSUM_TBL_ENTRIES(NB) (4 * (NB) * 256 + 64 + 256 + ECG_CSUM_NP2)
 #define ECG_CSUM_OFF_P2(NB) (3 * (NB) * 256 + 64 + 256)
+#define ECG_CSUM_OFF_SH256(NB) (3 * (NB) * 256 + 64 + 256 + ECG_CSUM_NP2)
+#define ECG_CSUM_GLANES 16	/* lanes per chunk in the lane-group CRC kernel */
+#define ECG_CSUM_GSTRIDE (16 * ECG_CSUM_GLANES)	/* bytes a lane group consumes per step */
 #define ECG_CSUM_OFF_SH(NB) ((NB) * 256)
 #define ECG_CSUM_OFF_K64(NB) (2 * (NB) * 256)
 #define ECG_CSUM_OFF_SH4K(NB) (2 * (NB) * 256 + 64)
@@ -106,7 +110,8 @@ typedef struct ecg_csum_params {
 	uint32_t n_ext;
 	uint32_t nchunks;
 	uint32_t type;			/* DAOS hash type: 1 crc16, 2 crc32, 3 crc64, 7 adler32 */
-	uint32_t variant;		/* CRC: 0 auto, 1 wave per chunk, 2 workgroup per chunk */
+	uint32_t variant;		/* CRC: 0 auto, 1 wave per chunk, 2 workgroup per chunk,
+					 * 3 a 16-lane group per chunk */
 	/* workgroup-per-chunk CRC: a chunk of m 1 KiB steps is cut into
 	 * ECG_CSUM_SPLIT_NW slices; split_sh[c][w] = x^(8 * bytes after slice w)
 	 * mod P for the chunk lengths' step counts split_m[c] (first, middle and

@@ -210,6 +210,7 @@ static void *build_crc_tables(const struct crc_def *d, size_t *bytes)
 	}
 	build_shift(d, ECG_CSUM_STRIDE, t + ECG_CSUM_OFF_SH(nb));
 	build_shift(d, ECG_MMCS_STRIDE, t + ECG_CSUM_OFF_SH4K(nb));
+	build_shift(d, ECG_CSUM_GSTRIDE, t + ECG_CSUM_OFF_SH256(nb));
 	/* k64[lane] = x^(8*16*(63-lane)), k256[t] = x^(8*16*(255-t)) mod P:
 	 * "1" moved through that many zero bytes, walking down from the last */
 	c = crc_one(d);
@@ -459,7 +460,11 @@ int ecg_csum_extents(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_
 			prm.nchunks >= 2 ? prm.ext_bytes - prm.first_bytes - (uint64_t)(prm.nchunks - 2) * rcs
 					 : prm.first_bytes};
 
-		prm.variant = split ? 2 : 1;
+		/* short chunks (<= 8 KiB): a 16-lane group each, so the per-lane
+		 * final multiply is paid once per >= 8 pieces instead of per 1-2 */
+		const int group = ctx->csum_variant == 3 || (ctx->csum_variant == 0 && !split && steps <= 8);
+
+		prm.variant = split ? 2 : group ? 3 : 1;
 		for (int c = 0; split && c < 3; c++) {
 			prm.split_m[c] = (lens[c] / 16 + 63) / 64;
 			split_shifts(ctx, type, prm.split_m[c], prm.split_sh[c]);
@@ -484,7 +489,7 @@ int ecg_set_csum_launch(ecg_ctx_t *ctx, uint32_t max_blocks)
 
 int ecg_set_csum_variant(ecg_ctx_t *ctx, uint32_t variant)
 {
-	if (ctx == NULL || variant > 2)
+	if (ctx == NULL || variant > 3)
 		return ecg_fail(-ECG_DER_INVAL, "set_csum_variant: bad arguments");
 	ctx->csum_variant = variant;
 	return 0;

@@ -147,6 +147,92 @@ __device__ __forceinline__ T shfl_xor_t(T v, int s)
 		return (T)__shfl_xor((uint32_t)v, s);
 }
 
+// Short chunks (<= 8 KiB): with a wave per chunk each lane holds only 1-8
+// pieces and the per-lane final multiply (W GF(2) steps) dominates.  Here a
+// group of G = ECG_CSUM_GLANES lanes takes a chunk (4 chunks per wave): lane
+// l of the group takes pieces q = G*i + l - z, so each load instruction still
+// reads 4 x 256 B contiguous, Horner-steps by G*16 bytes (sh256 table), and
+// the group reduces with shuffles after multiplying by x^(8*16*(G-1-l)) =
+// k64[64 - G + l].  Otherwise as ecg_crc_kernel.
+template <int W, bool REFL>
+__global__ __launch_bounds__(CS_BLOCK) void ecg_crc_group_kernel(ecg_csum_params_t p)
+{
+	using T = typename reg<W>::T;
+	constexpr int NB = W / 8;
+	constexpr int G = ECG_CSUM_GLANES;
+	constexpr int GPW = 64 / G;		// chunks per wave
+	__shared__ T sl[NB * 256];
+	__shared__ T sh[NB * 256];
+	const T *gt = (const T *)p.tbl;
+
+	for (int i = threadIdx.x; i < NB * 256; i += CS_BLOCK) {
+		sl[i] = gt[i];
+		sh[i] = gt[ECG_CSUM_OFF_SH256(NB) + i];
+	}
+	const int lane = threadIdx.x & 63, gl = lane % G;
+	const T klane = gt[ECG_CSUM_OFF_K64(NB) + 64 - G + gl];
+	const T poly = (T)p.poly, init = (T)p.init, xorout = (T)p.xorout;
+	__syncthreads();
+
+	const uint64_t total = (uint64_t)p.n_ext * p.nchunks;
+	const uint64_t waves = (uint64_t)gridDim.x * CS_WAVES;
+	// every lane runs the same number of outer iterations (shuffles below
+	// need the whole wave): the wave's first chunk decides, idle groups mask
+	for (uint64_t g0 = ((uint64_t)blockIdx.x * CS_WAVES + (threadIdx.x >> 6)) * GPW; g0 < total;
+	     g0 += waves * GPW) {
+		const uint64_t g = g0 + lane / G;
+		const bool live = g < total;
+		uint64_t off = 0, len = 0;
+		const uint8_t *base = p.src;
+
+		if (live)
+			chunk_geom(p, g, off, len, base);
+		const int64_t nq = (int64_t)(len / 16);
+		const int64_t m = (nq + G - 1) / G;
+		const int64_t z = m * G - nq;
+		T acc = 0;
+
+		for (int64_t i = 0; i < m; i += CS_UNROLL) {
+			uint32_t d[CS_UNROLL][4];
+#pragma unroll
+			for (int u = 0; u < CS_UNROLL; u++) {
+				const int64_t q = (i + u) * G + gl - z;
+				if (i + u < m && q >= 0) {
+					load16<true>(base + 16 * q, d[u]);
+					if (q == 0) {
+						d[u][0] ^= (uint32_t)init;
+						if constexpr (W == 64)
+							d[u][1] ^= (uint32_t)((uint64_t)init >> 32);
+					}
+				} else {
+					d[u][0] = d[u][1] = d[u][2] = d[u][3] = 0;
+				}
+			}
+#pragma unroll
+			for (int u = 0; u < CS_UNROLL; u++) {
+				if (i + u < m)
+					acc = lin_map<W>(acc, sh) ^ piece_crc<W, REFL>(d[u], sl);
+			}
+		}
+		acc = mulmod<W, REFL>(klane, acc, poly);
+#pragma unroll
+		for (int s = G / 2; s >= 1; s >>= 1)
+			acc ^= shfl_xor_t(acc, s);
+		if (live && gl == 0) {
+			T crc = nq == 0 ? init : acc;
+
+			for (uint64_t b = (uint64_t)nq * 16; b < len; b++)
+				crc = byte_step<W, REFL>(crc, base[b], sl);
+			crc ^= xorout;
+			if constexpr (W == 16)
+				((uint16_t *)p.out)[g] = (uint16_t)crc;
+			else
+				((T *)p.out)[g] = crc;
+		}
+	}
+}
+
+
 // Long chunks, few of them (e.g. 1024 chunks of 1 MiB = one wave per SIMD
 // with ecg_crc_kernel): one workgroup of NW waves per chunk.  The chunk's
 // 1 KiB steps are cut into NW contiguous slices; each wave computes the raw
@@ -409,6 +495,13 @@ const csum_entry g_split[] = {
 };
 constexpr uint32_t N_SPLIT = sizeof(g_split) / sizeof(g_split[0]);
 
+const csum_entry g_group[] = {
+	{1, true, ecg_crc_group_kernel<16, false>, "ecg_crc_group_kernel<crc16>"},
+	{2, true, ecg_crc_group_kernel<32, true>, "ecg_crc_group_kernel<crc32>"},
+	{3, true, ecg_crc_group_kernel<64, true>, "ecg_crc_group_kernel<crc64>"},
+};
+constexpr uint32_t N_GROUP = sizeof(g_group) / sizeof(g_group[0]);
+
 } // namespace
 
 extern "C" const char *ecg_k_csum_kernel_name(uint32_t id)
@@ -417,6 +510,8 @@ extern "C" const char *ecg_k_csum_kernel_name(uint32_t id)
 		return g_csum[id - ECG_KID_CSUM].name;
 	if (id >= ECG_KID_CSUM + N_CSUM && id < ECG_KID_CSUM + N_CSUM + N_SPLIT)
 		return g_split[id - ECG_KID_CSUM - N_CSUM].name;
+	if (id >= ECG_KID_CSUM + N_CSUM + N_SPLIT && id < ECG_KID_CSUM + N_CSUM + N_SPLIT + N_GROUP)
+		return g_group[id - ECG_KID_CSUM - N_CSUM - N_SPLIT].name;
 	return "?";
 }
 
@@ -455,6 +550,22 @@ extern "C" int ecg_k_launch_csum(const ecg_csum_params_t *p, void *stream, uint3
 	}
 	if (max_blocks == 0)
 		max_blocks = 256 * 16;	// 16 blocks per CU, grid-stride beyond
+	if (p->type != 7 && aligned && p->variant == 3) {
+		const uint32_t per_block = CS_WAVES * (64 / ECG_CSUM_GLANES);
+		uint64_t nb = (total + per_block - 1) / per_block;
+
+		if (nb > max_blocks)
+			nb = max_blocks;
+		for (uint32_t i = 0; i < N_GROUP; i++) {
+			if (g_group[i].type != p->type)
+				continue;
+			hipLaunchKernelGGL(g_group[i].fn, dim3((uint32_t)nb), dim3(CS_BLOCK), 0,
+					   (hipStream_t)stream, *p);
+			if (kernel_id)
+				*kernel_id = ECG_KID_CSUM + N_CSUM + N_SPLIT + i;
+			return (int)hipGetLastError();
+		}
+	}
 	if (blocks > max_blocks)
 		blocks = max_blocks;
 	for (uint32_t i = 0; i < N_CSUM; i++) {

@@ -92,8 +92,10 @@ int ecg_recover_csum(ecg_ctx_t *ctx, int k, int p, uint64_t cell_bytes, uint32_t
 int ecg_set_csum_launch(ecg_ctx_t *ctx, uint32_t max_blocks);
 
 /* Launch tuning: CRC kernel shape for 16-byte aligned extents -- 0 by shape
- * (default: a workgroup per chunk when chunks are long and few), 1 one wave
- * per chunk, 2 one workgroup per chunk.  Same results either way. */
+ * (default: a workgroup per chunk when chunks are long and few, a 16-lane
+ * group per chunk when chunks are <= 8 KiB), 1 one wave per chunk, 2 one
+ * workgroup per chunk, 3 one 16-lane group per chunk.  Same results either
+ * way. */
 int ecg_set_csum_variant(ecg_ctx_t *ctx, uint32_t variant);
 
 #ifdef __cplusplus

@@ -64,15 +64,18 @@ def test_csum_parity(oracle, ecglib, ctx, htype, geom):
     assert np.array_equal(got, want), np.argwhere(got != want)[:5]
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 @pytest.mark.parametrize("htype", (1, 2, 3, 7))
 @pytest.mark.parametrize("geom", GEOMS + [(1 << 20, 1, 0, 3 << 20), ((1 << 20) + 4096, 1, 5, 2 << 20),
-                                          (65536, 16, 0, 70001), (2048, 1, 0, 100000)])
+                                          (65536, 16, 0, 70001), (2048, 1, 0, 100000),
+                                          (4096, 1, 0, 4096 * 7 + 16 * 5), (8192, 8, 0, 3001)])
 def test_crc_kernel_shapes(oracle, ecglib, ctx, variant, htype, geom):
-    """Both kernel shapes on every geometry: a wave per chunk (1) and a
+    """Every kernel shape on every geometry: a wave per chunk (1), a
     workgroup per chunk (2) -- CRC: the waves' slice CRCs shifted and
     combined; adler32: the threads' position-weighted sums added; chunks
-    shorter than the workgroup's slices leave waves idle."""
+    shorter than the workgroup's slices leave waves idle -- and, for CRC, a
+    16-lane group per chunk (3; 4 chunks per wave, the wave's last groups
+    idle past the final chunk)."""
     cs, rb, idx, nr = geom
     L = ecglib.lib()
     rng = np.random.default_rng((hash(geom) + htype) & 0xFFFFFFFF)
@@ -85,6 +88,7 @@ def test_crc_kernel_shapes(oracle, ecglib, ctx, variant, htype, geom):
         L.ecg_set_csum_variant(ctx.h, 0)
     if "bytes" not in kern:
         assert ("split" in kern) == (variant == 2), kern
+        assert ("group" in kern) == (variant == 3 and htype != 7), kern
     assert np.array_equal(got, oracle.csum_extents(htype, cs, rb, idx, nr, host))
 
 
