@@ -606,6 +606,24 @@ static int stage_reserve(ecg_ctx_t *ctx, size_t bytes)
 	return 0;
 }
 
+/* H2D copies per encode_host chunk: 1 = one contiguous copy, else one strided
+ * copy per cell column (ECG_ENC_H2D_PARTS; tools/bench_pcie.py) */
+static int g_enc_h2d_parts;
+static pthread_once_t g_enc_h2d_once = PTHREAD_ONCE_INIT;
+
+static void enc_h2d_init(void)
+{
+	const char *e = getenv("ECG_ENC_H2D_PARTS");
+
+	g_enc_h2d_parts = e ? atoi(e) : 0;
+}
+
+static int enc_h2d_parts(void)
+{
+	pthread_once(&g_enc_h2d_once, enc_h2d_init);
+	return g_enc_h2d_parts;
+}
+
 int ecg_encode_host(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 		    const void *data, void *parity, uint32_t chunk)
 {
@@ -636,9 +654,17 @@ int ecg_encode_host(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 		hipError_t e;
 
 		e = hipEventSynchronize(ctx->stage.done[slot]);
-		if (e == hipSuccess)
+		if (e == hipSuccess && enc_h2d_parts() == 1) {
 			e = hipMemcpyAsync(dd, hd + (size_t)s0 * k * C, (size_t)cs * k * C,
 					   hipMemcpyHostToDevice, st);
+		} else {
+			/* one strided copy per cell column, as recover_host does: the
+			 * runtime spreads them over its copy engines */
+			for (r = 0; e == hipSuccess && r < k; r++)
+				e = hipMemcpy2DAsync(dd + (size_t)r * C, (size_t)k * C,
+						     hd + (size_t)s0 * k * C + (size_t)r * C, (size_t)k * C, C, cs,
+						     hipMemcpyHostToDevice, st);
+		}
 		if (e != hipSuccess) {
 			rc = ecg_hip_fail(e, "encode_host H2D");
 			break;
