@@ -606,8 +606,30 @@ static int stage_reserve(ecg_ctx_t *ctx, size_t bytes)
 	return 0;
 }
 
-/* H2D copies per encode_host chunk: 1 = one contiguous copy, else one strided
- * copy per cell column (ECG_ENC_H2D_PARTS; tools/bench_pcie.py) */
+hipError_t ecg_stage_copy(void *dst, const void *src, size_t bytes, size_t row, hipMemcpyKind kind,
+			  hipStream_t st)
+{
+	hipError_t e = hipSuccess;
+	size_t h;
+
+	/* both sides are contiguous, so any row length works: whole rows up to
+	 * 1 MiB (short rows made the queue's 32 KiB-cell copies slower) */
+	if (row && row < (1u << 20))
+		row *= (1u << 20) / row;
+	h = row ? bytes / row : 0;
+
+	if (h == 0)
+		return bytes ? hipMemcpyAsync(dst, src, bytes, kind, st) : hipSuccess;
+	e = hipMemcpy2DAsync(dst, row, src, row, row, h, kind, st);
+	if (e == hipSuccess && bytes > h * row)
+		e = hipMemcpyAsync((char *)dst + h * row, (const char *)src + h * row, bytes - h * row,
+				   kind, st);
+	return e;
+}
+
+/* H2D copy of an encode_host chunk: 0 (default) one 2D copy of cell rows
+ * (ecg_stage_copy), 1 one 1D copy, 3 one strided 2D copy per cell column
+ * (ECG_ENC_H2D_PARTS; tools/bench_pcie.py: 52.1 / 45.0 / 50.5 GiB/s EC_8P2) */
 static int g_enc_h2d_parts;
 static pthread_once_t g_enc_h2d_once = PTHREAD_ONCE_INIT;
 
@@ -629,6 +651,7 @@ int ecg_encode_host(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 {
 	const unsigned char *hd = data;
 	unsigned char *hp = parity;
+	const int h2d_mode = enc_h2d_parts();
 	uint32_t s0, slot = 0;
 	int rc, r;
 
@@ -654,16 +677,17 @@ int ecg_encode_host(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 		hipError_t e;
 
 		e = hipEventSynchronize(ctx->stage.done[slot]);
-		if (e == hipSuccess && enc_h2d_parts() == 1) {
+		if (e == hipSuccess && h2d_mode == 1) {
 			e = hipMemcpyAsync(dd, hd + (size_t)s0 * k * C, (size_t)cs * k * C,
 					   hipMemcpyHostToDevice, st);
-		} else {
-			/* one strided copy per cell column, as recover_host does: the
-			 * runtime spreads them over its copy engines */
+		} else if (e == hipSuccess && h2d_mode == 3) {
 			for (r = 0; e == hipSuccess && r < k; r++)
 				e = hipMemcpy2DAsync(dd + (size_t)r * C, (size_t)k * C,
 						     hd + (size_t)s0 * k * C + (size_t)r * C, (size_t)k * C, C, cs,
 						     hipMemcpyHostToDevice, st);
+		} else if (e == hipSuccess) {
+			e = ecg_stage_copy(dd, hd + (size_t)s0 * k * C, (size_t)cs * k * C, C,
+					   hipMemcpyHostToDevice, st);
 		}
 		if (e != hipSuccess) {
 			rc = ecg_hip_fail(e, "encode_host H2D");
@@ -672,8 +696,8 @@ int ecg_encode_host(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 		rc = ecg_encode(ctx, k, p, C, cs, dd, (int64_t)k * C, dp, (int64_t)cs * C,
 				(int64_t)C, st);
 		for (r = 0; rc == 0 && r < p; r++) {
-			e = hipMemcpyAsync(hp + ((size_t)r * S + s0) * C, dp + (size_t)r * cs * C,
-					   (size_t)cs * C, hipMemcpyDeviceToHost, st);
+			e = ecg_stage_copy(hp + ((size_t)r * S + s0) * C, dp + (size_t)r * cs * C,
+					   (size_t)cs * C, C, hipMemcpyDeviceToHost, st);
 			if (e != hipSuccess)
 				rc = ecg_hip_fail(e, "encode_host D2H");
 		}

@@ -84,6 +84,14 @@ struct ecg_ctx {
 /* errors (thread-local detail string) */
 int ecg_fail(int rc, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 int ecg_hip_fail(hipError_t e, const char *what);
+/* Pinned-host <-> device staging copy of a contiguous range issued as a 2D
+ * copy of rows of a multiple of `row` bytes up to 1 MiB (the remainder, if
+ * any, as a 1D copy).  Measured under concurrent traffic
+ * in the other direction, the 2D path sustains ~97 % of the raw pinned H2D
+ * rate where one 1D copy reaches ~84 % (tools/bench_pcie.py,
+ * profiles/r01/pcie.json). */
+hipError_t ecg_stage_copy(void *dst, const void *src, size_t bytes, size_t row, hipMemcpyKind kind,
+			  hipStream_t st);
 void ecg_set_last_kernel(const char *name);
 
 /* GF(2^8) tables (ecg_gf.c) */

@@ -189,14 +189,15 @@ static void launch_slot(struct ecg_queue *q, struct qslot *s)
 		soff[j] = (int64_t)(j * s->pitch);
 	for (j = 0; j < s->rows; j++)
 		doff[j] = (int64_t)(j * s->pitch);
-	e = hipMemcpyAsync(s->dev, s->host, (size_t)in_stride * n, hipMemcpyHostToDevice, s->st);
+	e = ecg_stage_copy(s->dev, s->host, (size_t)in_stride * n, (size_t)s->pitch, hipMemcpyHostToDevice,
+			   s->st);
 	rc = e == hipSuccess ? 0 : ecg_hip_fail(e, "queue H2D");
 	if (rc == 0)
 		rc = ecg_matmul(q->ctx, s->k, s->rows, s->coef, s->C, n, s->dev, soff, (int64_t)in_stride,
 				dout, doff, (int64_t)out_stride, 0, s->st);
 	if (rc == 0) {
-		e = hipMemcpyAsync(s->host + (size_t)in_stride * s->cap, dout, (size_t)out_stride * n,
-				   hipMemcpyDeviceToHost, s->st);
+		e = ecg_stage_copy(s->host + (size_t)in_stride * s->cap, dout, (size_t)out_stride * n,
+				   (size_t)s->pitch, hipMemcpyDeviceToHost, s->st);
 		if (e == hipSuccess)
 			e = hipEventRecord(s->done, s->st);
 		if (e != hipSuccess)

@@ -160,6 +160,9 @@ int ecg_matmul_host(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned cha
 			return ecg_hip_fail(e, "matmul_host device view of staging");
 		d = hd;
 	} else {
+		/* 1D: a lone synchronous call is latency-bound and the 2D copy
+		 * path costs more per call (tools/bench_dropin.py: 1 MiB cells
+		 * 435 -> 584 us with 2D) */
 		e = hipMemcpyAsync(d, h, (flags & ECG_F_ACCUMULATE) ? bytes : pitch * k,
 				   hipMemcpyHostToDevice, t->st);
 		if (e != hipSuccess)
