@@ -433,7 +433,7 @@ int ecg_matmul_csum(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, 
 	ecg_gf_init();
 	st = ecg_pick_stream(ctx, stream);
 	if (k <= ECG_KMAX_K && rows <= ECG_KMAX_R) {
-		fused = ecg_csum_fused_params(ctx, type, chunksize, rec_size, C, csums, &q);
+		fused = ecg_csum_fused_params(ctx, type, chunksize, rec_size, C, rows, csums, &q);
 		if (fused < 0)
 			return fused;
 	}

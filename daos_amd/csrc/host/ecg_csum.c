@@ -287,11 +287,11 @@ void ecg_csum_ctx_fini(ecg_ctx_t *ctx)
 		}
 }
 
-/* Columns per fused-kernel work item: a whole chunk up to 4 columns (8 for
- * crc64, whose 64-step reduction costs twice crc32's), else 4 / 8
- * (tools/tune11.py, profiles/r01/tune11_fused_cols.jsonl: EC_8P2 1 MiB cells,
- * crc32 32 KiB chunks 1.00 -> 0.89 ms vs a whole chunk per workgroup, crc64
- * best at 8); ECG_FUSED_COLS overrides (tuning). */
+/* Columns per fused-kernel work item: 4 for one output row of crc16/crc32
+ * (parity-shard rebuild), else 8 (every reduction multiplies `rows` values;
+ * crc64's costs twice crc32's); a whole chunk when shorter.  Measured A/B in
+ * one process on random data (tools/tune12.py, profiles/r01/tune12.json);
+ * ecg_set_fused_cols / ECG_FUSED_COLS override. */
 static int g_fused_cols_env;
 static pthread_once_t g_fused_cols_once = PTHREAD_ONCE_INIT;
 
@@ -304,10 +304,11 @@ static void fused_cols_init(void)
 		g_fused_cols_env = 0;
 }
 
-static uint32_t fused_cols(uint64_t m, int type)
+static uint32_t fused_cols(const ecg_ctx_t *ctx, uint64_t m, int type, int rows)
 {
-	const uint64_t dflt = type == ECG_HASH_CRC64 ? 8 : 4;
-	const int env = (pthread_once(&g_fused_cols_once, fused_cols_init), g_fused_cols_env);
+	const uint64_t dflt = type == ECG_HASH_CRC64 || rows > 1 ? 8 : 4;
+	const int env = ctx->fused_cols ? (int)ctx->fused_cols
+					: (pthread_once(&g_fused_cols_once, fused_cols_init), g_fused_cols_env);
 
 	if (env > 0)
 		return (uint32_t)((uint64_t)env < m ? (uint64_t)env : m);
@@ -487,6 +488,14 @@ int ecg_set_csum_launch(ecg_ctx_t *ctx, uint32_t max_blocks)
 	return 0;
 }
 
+int ecg_set_fused_cols(ecg_ctx_t *ctx, uint32_t ncols)
+{
+	if (ctx == NULL || ncols > 4096)
+		return ecg_fail(-ECG_DER_INVAL, "set_fused_cols: bad arguments");
+	ctx->fused_cols = ncols;
+	return 0;
+}
+
 int ecg_set_csum_variant(ecg_ctx_t *ctx, uint32_t variant)
 {
 	if (ctx == NULL || variant > 3)
@@ -500,7 +509,7 @@ int ecg_set_csum_variant(ecg_ctx_t *ctx, uint32_t variant)
  * can take the request, 0 when the caller must run the product and
  * ecg_csum_extents separately, < 0 on error. */
 int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_size,
-			  uint64_t C, void *csums, ecg_mmcs_params_t *q)
+			  uint64_t C, int rows, void *csums, ecg_mmcs_params_t *q)
 {
 	const uint64_t rcs = ecg_csum_record_chunksize(chunksize, rec_size);
 	const struct crc_def *d;
@@ -530,7 +539,7 @@ int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t
 	m = rcs / ECG_MMCS_STRIDE;
 	q->m = (uint32_t)m;
 	q->m_last = (uint32_t)((last + ECG_MMCS_STRIDE - 1) / ECG_MMCS_STRIDE);
-	q->ncols = fused_cols(m, type);
+	q->ncols = fused_cols(ctx, m, type, rows);
 	q->nh = (uint32_t)((m + q->ncols - 1) / q->ncols);
 	q->nh_last = (q->m_last + q->ncols - 1) / q->ncols;
 	if ((uint64_t)(q->nch - 1) * q->nh + q->nh_last > UINT32_MAX)

@@ -63,6 +63,7 @@ struct ecg_ctx {
 	void *csum_tbl[ECG_NCSUM_TBL];	/* device CRC tables by hash type (ecg_csum.c) */
 	uint32_t csum_blocks;		/* csum grid cap, 0 = kernel default */
 	uint32_t csum_variant;		/* CRC kernel choice, 0 = by shape */
+	uint32_t fused_cols;		/* fused kernel columns per item, 0 = default */
 #define ECG_NSPLIT_CACHE 8
 	struct ecg_split_ent {		/* workgroup-per-chunk CRC shifts (ecg_csum.c) */
 		int valid, type;
@@ -125,7 +126,7 @@ int ecg_segs_launch(const struct ecg_segs *v, const void *segs_dev, hipStream_t 
 /* checksums (ecg_csum.c) */
 void ecg_csum_ctx_fini(ecg_ctx_t *ctx);
 int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_size,
-			  uint64_t C, void *csums, ecg_mmcs_params_t *q);
+			  uint64_t C, int rows, void *csums, ecg_mmcs_params_t *q);
 
 /* product + chunk checksums of every output cell, cells as extents from
  * record index 0; csums[row_slot[r]][s][chunk] (ecg_core.c) */

@@ -129,6 +129,7 @@ _SIGS = [
                                    C.c_uint32, vp, vp]),
     ("ecg_set_csum_launch", C.c_int, [vp, C.c_uint32]),
     ("ecg_set_csum_variant", C.c_int, [vp, C.c_uint32]),
+    ("ecg_set_fused_cols", C.c_int, [vp, C.c_uint32]),
     ("ecg_encode_csum", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, vp, C.c_int64, vp, C.c_int64,
                                   C.c_int64, C.c_int, C.c_uint64, C.c_uint64, vp, vp]),
     ("ecg_recover_csum", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, vp, C.c_int64, u32p, C.c_int,

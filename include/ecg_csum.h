@@ -98,6 +98,11 @@ int ecg_set_csum_launch(ecg_ctx_t *ctx, uint32_t max_blocks);
  * way. */
 int ecg_set_csum_variant(ecg_ctx_t *ctx, uint32_t variant);
 
+/* Launch tuning: 4 KiB columns per work item of the fused product +
+ * checksum kernels (ecg_encode_csum / ecg_recover_csum); 0 restores the
+ * default (env ECG_FUSED_COLS, else by hash type).  Same results either way. */
+int ecg_set_fused_cols(ecg_ctx_t *ctx, uint32_t ncols);
+
 #ifdef __cplusplus
 }
 #endif

@@ -61,7 +61,8 @@ def main():
         data = ctx.alloc(S * k * C2)
         par = ctx.alloc(p * S * C2 + 4096)
         cs_out = ctx.alloc(p * S * (C2 // 32768) * 8)
-        data.upload(blk[: min(blk.size, S * k * C2)])
+        for off in range(0, S * k * C2, blk.size):      # random bytes everywhere: CRC lookups are data-dependent
+            data.upload(blk[: min(blk.size, S * k * C2 - off)], offset=off)
         pitch = S * C2 + 4096
         enc = timed(lambda: ctx.encode(k, p, C2, S, data.ptr, k * C2, par.ptr, pitch, C2))
         for htype in ((1, 2, 3) if tag == "8p2_1M" else (2,)):
@@ -79,7 +80,8 @@ def main():
                 "fused_overhead_vs_encode": round(fus / enc - 1, 4), "fused_kernel": L.ecg_last_kernel().decode()}
         if tag == "8p2_1M":
             st = ctx.alloc(S * (k + p) * C2)
-            st.fill(0x11)
+            for off in range(0, S * (k + p) * C2, blk.size):
+                st.upload(blk[: min(blk.size, S * (k + p) * C2 - off)], offset=off)
             rec = timed(lambda: ctx.recover(k, p, C2, S, st.ptr, (k + p) * C2, [0, 1]))
             recf = timed(lambda: ctx.recover_csum(k, p, C2, S, st.ptr, (k + p) * C2, [0, 1], 2, 32768, 1,
                                                   cs_out.ptr))

@@ -32,7 +32,9 @@ def main():
     C = 1 << 20
     for k, p, S in ((8, 2, 512), (4, 2, 1024)):
         data = ctx.alloc(S * k * C)
-        data.upload(stripe_bytes(256 << 20, 5))
+        blk = stripe_bytes(256 << 20, 5)
+        for off in range(0, S * k * C, blk.size):      # random everywhere: CRC lookups are data-dependent
+            data.upload(blk[: min(blk.size, S * k * C - off)], offset=off)
         pitch = S * C + 4096
         par = ctx.alloc(p * pitch)
         out = ctx.alloc(p * S * (C // 4096) * 8)
