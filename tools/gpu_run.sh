@@ -2,7 +2,7 @@
 # GPU-box driver for one gpurun call.  Every GPU step has its own time limit;
 # any fault / abort / segfault / timeout ends the call (no retries).  Test
 # failures (pytest exit 1) are not faults and do not stop later steps.
-#   tools/gpu_run.sh [smoke] [tests] [bench] [prof] [pmc] [fulltests]
+#   tools/gpu_run.sh [smoke] [tests] [bench] [prof] [pmc] [fulltests] [csumtests] [hoststream] [tune12] ...
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -119,6 +119,20 @@ for what in "$@"; do
 		;;
 	tune3)
 		step tune3 600 python tools/tune3.py || exit $?
+		;;
+	tune12)
+		step tune12 500 python tools/tune12.py || exit $?
+		;;
+	hoststream)
+		step hoststream_n1 300 python bench.py --workload rebuild_stream_8p2 --steps 5 --warmup 1 || exit $?
+		step hoststream_2rank 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+			--master-addr 127.0.0.1 --master-port 29541 bench.py --workload rebuild_stream_8p2 --gpus 2 \
+			--steps 5 --warmup 1 || exit $?
+		;;
+	csumtests)
+		step csum_tests 300 python -m pytest tests/test_gpu_csum.py tests/test_migrate.py tests/test_gpu_graph.py \
+			-q -x -p no:cacheprovider
+		rc=$?; [ $rc -eq 0 ] || exit $rc
 		;;
 	*)
 		echo "unknown step $what"; exit 2
