@@ -540,6 +540,10 @@ int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t
 	q->m = (uint32_t)m;
 	q->m_last = (uint32_t)((last + ECG_MMCS_STRIDE - 1) / ECG_MMCS_STRIDE);
 	q->ncols = fused_cols(ctx, m, type, rows);
+	/* bound the multiplier table (nh + nh_last rows of 256 entries) for
+	 * very long chunks: at most 2048 items per chunk */
+	if ((m + q->ncols - 1) / q->ncols > 2048)
+		q->ncols = (uint32_t)((m + 2047) / 2048);
 	q->nh = (uint32_t)((m + q->ncols - 1) / q->ncols);
 	q->nh_last = (q->m_last + q->ncols - 1) / q->ncols;
 	if ((uint64_t)(q->nch - 1) * q->nh + q->nh_last > UINT32_MAX)
