@@ -212,6 +212,45 @@ def test_encode_csum_fused(oracle, ecglib, ctx, case):
         d.free(); par.free(); out.free()
 
 
+ITEM_CASES = [
+    # (k, p, C, S, chunksize, htype): chunks cut into work items of `cols` columns, ragged last chunks
+    (8, 2, 3 * 65536 + 4096 * 3 + 48, 3, 65536, 2),      # last chunk 3 columns + 48 B
+    (4, 1, (1 << 20) + 48, 2, 1 << 20, 1),                 # 256-column chunks, last chunk 48 B
+    (8, 3, 5 * 32768, 2, 32768, 3),
+    (16, 2, 131072 + 16, 2, 40960, 2),                     # 10-column chunks
+]
+
+
+@pytest.mark.parametrize("cols", [1, 2, 3, 5, 0])
+@pytest.mark.parametrize("case", ITEM_CASES)
+def test_encode_csum_fused_items(oracle, ecglib, ctx, case, cols):
+    """Every split of a chunk into work items (ecg_set_fused_cols; 0 = the
+    default) yields the same checksums: per-item multipliers, the last
+    chunk's own rows (zero padding removed), xorout once per chunk."""
+    k, p, C, S, cs, htype = case
+    L = ecglib.lib()
+    nch = L.ecg_csum_chunk_count(cs, 1, 0, C)
+    cl = L.ecg_csum_len(htype)
+    rng = np.random.default_rng(sum(case) + cols)
+    data = rng.integers(0, 256, S * k * C, dtype=np.uint8)
+    d = ctx.to_device(data)
+    par = ctx.alloc(p * S * C)
+    out = ctx.alloc(p * S * nch * cl)
+    assert L.ecg_set_fused_cols(ctx.h, cols) == 0
+    try:
+        ctx.encode_csum(k, p, C, S, d.ptr, k * C, par.ptr, S * C, C, htype, cs, 1, out.ptr)
+        ctx.sync()
+        assert "ecg_mm_csum_kernel" in L.ecg_last_kernel().decode(), L.ecg_last_kernel()
+        want_par = oracle.encode_batch(k, p, C, S, data, nthreads=8, simd=True).reshape(p, S, C)
+        assert np.array_equal(par.download().reshape(p, S, C), want_par)
+        got = out.download().view(DT[cl]).reshape(p, S, nch)
+        want = _want_cell_csums(oracle, htype, cs, 1, want_par).reshape(p, S, nch)
+        assert np.array_equal(got, want), np.argwhere(got != want)[:5]
+    finally:
+        L.ecg_set_fused_cols(ctx.h, 0)
+        d.free(); par.free(); out.free()
+
+
 @pytest.mark.parametrize("errs", [[3, 9], [9, 3], [8, 9], [0], [0, 1], [5]])
 @pytest.mark.parametrize("htype", (2, 3))
 def test_recover_csum_fused(oracle, ecglib, ctx, errs, htype):
