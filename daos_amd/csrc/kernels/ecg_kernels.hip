@@ -380,7 +380,9 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 #pragma unroll
 				for (int r = 0; r < RM; r++) {
 					if (r < rows) {
+#ifndef ECG_EXP_NO_CRC
 						crc[r] = ecg_crc::lin_map<W>(crc[r], s_sh);
+#endif
 						if (have) {
 							uint32_t d[4] = {outv[r][0], outv[r][1], outv[r][2], outv[r][3]};
 							if (i == 0 && threadIdx.x == 0) {	// initial register
@@ -388,7 +390,11 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 								if constexpr (W == 64)
 									d[1] ^= (uint32_t)(Q.init >> 32);
 							}
+#ifndef ECG_EXP_NO_CRC
 							crc[r] ^= ecg_crc::piece_crc<W, REFL>(d, s_sl);
+#else
+							crc[r] ^= (T)(d[0] ^ d[1] ^ d[2] ^ d[3]);
+#endif
 						}
 					}
 				}
@@ -404,7 +410,11 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 #pragma unroll
 			for (int r = 0; r < RM; r++) {
 				if (r < rows) {
+#ifndef ECG_EXP_NO_MULMOD
 					T v = ecg_crc::mulmod<W, REFL>(kcur, crc[r], poly);
+#else
+					T v = kcur ^ crc[r];
+#endif
 					v = ecg_crc::wave_xor(v);
 					if ((threadIdx.x & 63) == 0) {
 						if (threadIdx.x == 0 && khrow == (c + 1 == Q.nch ? Q.nh : 0))

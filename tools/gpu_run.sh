@@ -134,6 +134,19 @@ for what in "$@"; do
 			-q -x -p no:cacheprovider
 		rc=$?; [ $rc -eq 0 ] || exit $rc
 		;;
+	fusedcost)
+		for lib in daos_amd/lib/libecg.so build/exp/libecg_NO_MULMOD.so build/exp/libecg_NO_CRC.so \
+			   daos_amd/lib/libecg.so; do
+			step fusedcost 300 python tools/fused_cost.py $lib || exit $?
+			grep '^{' gpurun_out/fusedcost.log >> gpurun_out/fusedcost.jsonl
+		done
+		;;
+	fusedstruct)
+		for lib in build/exp/libecg_NONE.so daos_amd/lib/libecg.so; do
+			FUSED_COST_COLS=1,2,4,8 step fusedcost 400 python tools/fused_cost.py $lib || exit $?
+			grep '^{' gpurun_out/fusedcost.log >> gpurun_out/fusedcost.jsonl
+		done
+		;;
 	*)
 		echo "unknown step $what"; exit 2
 		;;
