@@ -147,6 +147,9 @@ for what in "$@"; do
 			grep '^{' gpurun_out/fusedcost.log >> gpurun_out/fusedcost.jsonl
 		done
 		;;
+	tune13)
+		step tune13 500 python tools/tune13.py || exit $?
+		;;
 	*)
 		echo "unknown step $what"; exit 2
 		;;
