@@ -150,6 +150,16 @@ for what in "$@"; do
 	tune13)
 		step tune13 500 python tools/tune13.py || exit $?
 		;;
+	csumbench)
+		step bench_csum 300 python tools/bench_csum.py || exit $?
+		python - <<'PY'
+import json
+d = json.load(open("gpurun_out/bench_csum.json"))
+for k, v in d.items():
+    if k.startswith(("crc32", "shape_crc32", "enc_8p2")):
+        print(k, v)
+PY
+		;;
 	*)
 		echo "unknown step $what"; exit 2
 		;;
