@@ -160,6 +160,10 @@ for k, v in d.items():
         print(k, v)
 PY
 		;;
+	dist4)
+		step dist4 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+			--master-port 29537 bench.py --gpus 4 --steps 20 --warmup 3 || exit $?
+		;;
 	*)
 		echo "unknown step $what"; exit 2
 		;;
