@@ -748,22 +748,34 @@ int ecg_recover_host(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 		hipStream_t st = ctx->stage.st[slot];
 		hipError_t e = hipEventSynchronize(ctx->stage.done[slot]);
 
-		/* survivors the decode reads: k strided cells per stripe */
-		for (i = 0; e == hipSuccess && i < k; i++)
+		/* survivors the decode reads: k cells per stripe, one strided 2D
+		 * copy per run of consecutive cells */
+		for (i = 0; e == hipSuccess && i < k;) {
+			int n = 1;
+
+			while (i + n < k && ent.dec_idx[i + n] == ent.dec_idx[i] + (uint32_t)n)
+				n++;
 			e = hipMemcpy2DAsync(dd + (size_t)ent.dec_idx[i] * C, sstride,
 					     hs + (size_t)s0 * sstride + (size_t)ent.dec_idx[i] * C,
-					     sstride, C, cs, hipMemcpyHostToDevice, st);
+					     sstride, (size_t)n * C, cs, hipMemcpyHostToDevice, st);
+			i += n;
+		}
 		if (e != hipSuccess) {
 			rc = ecg_hip_fail(e, "recover_host H2D");
 			break;
 		}
 		rc = recover_with(ctx, &ent, C, cs, dd, (int64_t)sstride, st);
-		for (i = 0; rc == 0 && i < nerrs; i++) {
+		for (i = 0; rc == 0 && i < nerrs;) {
+			int n = 1;	/* runs of consecutive erased cells in err_list order */
+
+			while (i + n < nerrs && err_list[i + n] == err_list[i] + (uint32_t)n)
+				n++;
 			e = hipMemcpy2DAsync(hs + (size_t)s0 * sstride + (size_t)err_list[i] * C,
-					     sstride, dd + (size_t)err_list[i] * C, sstride, C, cs,
+					     sstride, dd + (size_t)err_list[i] * C, sstride, (size_t)n * C, cs,
 					     hipMemcpyDeviceToHost, st);
 			if (e != hipSuccess)
 				rc = ecg_hip_fail(e, "recover_host D2H");
+			i += n;
 		}
 		if (rc == 0) {
 			e = hipEventRecord(ctx->stage.done[slot], st);

@@ -327,6 +327,21 @@ def test_host_pipeline(ctx, oracle):
     assert np.array_equal(broken, stripes)
 
 
+@pytest.mark.parametrize("errs", [[0, 1], [8, 9], [1, 2], [9, 8], [3], [7, 8]])
+def test_recover_host_erasure_runs(ctx, oracle, errs):
+    """Host-resident recovery moves survivors and regenerated cells in runs
+    of consecutive cells (one strided copy per run): every erasure shape,
+    including runs that straddle the data/parity boundary."""
+    k, p, C_, S = 8, 2, 8192 + 64, 11
+    data = rand((S, k, C_), 95 + sum(errs))
+    want = oracle_parity(oracle, k, p, data)
+    stripes = np.concatenate([data, want.transpose(1, 0, 2)], axis=1).copy()
+    broken = stripes.copy()
+    broken[:, errs] = 0x5A
+    ctx.recover_host(k, p, C_, S, broken, errs, chunk=4)
+    assert np.array_equal(broken, stripes)
+
+
 # --------------------------------------------------------------- BASELINE sizes
 def _sample_check(oracle, k, p, data_host, par_host, S, stripes):
     en = oracle.cauchy1(k, p)
