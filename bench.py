@@ -343,6 +343,7 @@ def detail_rows(ctx, ceil, iters=7):
         mix = mix_ceiling(ceil, rd / (rd + wr))
         rows[name] = {"GiBps_user": round(k * C * S / (ms / 1e3) / GIB, 1), "alg_GBps": round(gbs, 1),
                       "roofline_frac": round(gbs / HBM_PEAK_GBS, 4),
+                      "read_frac": round(k * C * S / ms / 1e6 / HBM_PEAK_GBS, 4),
                       "measured_mix_ceiling_GBps": round(mix, 1), "frac_of_measured_mix": round(gbs / mix, 4),
                       "kernel": ecg.last_kernel(), "ms": round(ms, 4),
                       "layout": "client [S][k][C] -> [p][S][C]" if mode == "enc" else "recovery [S][k+p][C]"}
