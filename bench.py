@@ -11,23 +11,36 @@ stripes --
 value = user bytes through the codec (k*C*S per encode + k*C*S per decode,
 summed over ranks) / wall time of K steps, GiB/s.
 
-Stripes are independent: each rank owns its own batch (weak scaling), no
-data-path collective.  torch.distributed (gloo) only provides the barrier and
-the max-over-ranks of the elapsed time.
+Multi-GPU: stripes are independent, so each GPU owns its own
+batch (weak scaling; `enc_16p2_strong` splits a fixed 8192-stripe total) and
+there is no data-path collective.
+  * `--gpus N` with no WORLD_SIZE in the environment spawns N rank processes
+    itself (one per device, before anything touches the GPU); under
+    torch.distributed.run the launcher's ranks are used.  torch.distributed
+    (gloo) only provides the barrier and the max-over-ranks of the elapsed
+    time.  Ranks must land on distinct devices (--allow-shared-device to
+    rehearse on fewer); n_gpus counts distinct PCI devices.
+  * `--sharder lib` runs the N shards in ONE process through the library's
+    own multi-device sharder (include/ecg_multi.h): one host thread +
+    context per device.
 
 roofline: the dominant kernel (ecg_mm_kernel<4,2>, which serves both the
 encode and the 2-erasure decode) -- algorithmic bytes per launch
 (k+rows)*C*S / mean launch duration from HIP events on its stream, against
-the 8 TB/s HBM spec peak; `traffic` from the committed rocprofv3 PMC pass
-(profiles/<round>/pmc_traffic.json) when present.
-cpu_baseline: the oracle's SIMD ISA-L-equivalent restatement (AVX2/GFNI +
-OpenMP) on a bounded sample, rank 0 at N=1 only.
+the 8 TB/s HBM spec peak; `traffic` is copied from the committed rocprofv3
+PMC pass of this command (`traffic_source` names the file), not measured in
+the run.
+cpu_baseline: the oracle's SIMD ISA-L-equivalent restatement (GFNI/AVX-512
++ OpenMP) on a bounded sample with a >= 1 GiB working set, rank 0 at N=1
+only, all of the box's CPU share and 1 core.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -37,49 +50,93 @@ sys.path.insert(0, ROOT)
 GIB = float(1 << 30)
 PARITY_ROW_PAD = 4096
 HBM_PEAK_GBS = 8000.0          # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
-ROUND = "r01"
+ROUND = "r02"
 
 # name -> (k, p, cell bytes, stripes, ops, strong scaling?)
 WORKLOADS = {
     "enc_dec_4p2": (4, 2, 1 << 20, 1024, ("enc", "dec"), False),
     "dec_8p2": (8, 2, 1 << 20, 512, ("dec",), False),
+    "enc_8p2": (8, 2, 1 << 20, 512, ("enc",), False),
     "enc_16p2_strong": (16, 2, 128 << 10, 8192, ("enc",), True),
     # configs[4]: stripes in pinned host memory, PCIe-inclusive (never the headline)
     "rebuild_stream_8p2": (8, 2, 1 << 20, 64, ("enc_host", "dec_host"), False),
 }
 HOST_CHUNK = 16         # stripes per staging chunk (profiles/r01/pcie.json chunk sweep)
+MARKER = 0x5A           # erased cells are overwritten with this before any decode runs
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="enc_dec_4p2", choices=sorted(WORKLOADS),
                     help="enc_dec_4p2 = BASELINE configs[1] (+ its decode); dec_8p2 = configs[2]; "
-                         "enc_16p2_strong = configs[3] (8192 stripes split across ranks); "
+                         "enc_8p2 = the north-star EC_8P2 encode; "
+                         "enc_16p2_strong = configs[3] (8192 stripes split across GPUs); "
                          "rebuild_stream_8p2 = configs[4] (host-resident, PCIe-inclusive)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
+    ap.add_argument("--sharder", default="procs", choices=("procs", "lib"),
+                    help="procs: one process per GPU; lib: one process, the library's ecg_multi sharder")
+    ap.add_argument("--allow-shared-device", action="store_true",
+                    help="permit more ranks/shards than visible devices (rehearsal on a small box)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--no-detail", action="store_true", help="skip the extra per-config rows")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-only", action="store_true", help="just the timed loop (for rocprofv3)")
-    return ap.parse_args()
+    ap.add_argument("--rehearse", action="store_true",
+                    help="CPU-only rehearsal of launcher, barrier and aggregation: no GPU work, the "
+                         "line carries rehearsal=true and its value is not a measurement")
+    return ap.parse_args(argv)
 
 
-def describe(name, k, p, C, S, ops):
+def describe(name, k, p, C, S, ops, n_shards=1):
     parts = []
     if "enc" in ops:
         parts.append("encode (data [S][k][C] -> parity [p][S][C], row pitch S*C+4KiB)")
     if "dec" in ops:
         parts.append("degraded decode of cells d0,d1 in [S][k+p][C]")
-    per = "per GPU" if not WORKLOADS[name][5] else "on this rank (8192 total, split)"
+    per = "per GPU" if not WORKLOADS[name][5] else f"per GPU ({WORKLOADS[name][3]} total, split {n_shards} ways)"
     return f"EC_{k}P{p} {C >> 10} KiB cells x {S} stripes {per}: " + " + ".join(parts)
+
+
+# ------------------------------------------------------------------ launcher
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """`--gpus N` without a launcher: start N rank processes (RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* set) and wait.  This parent process
+    never touches the GPU; rank 0 prints the JSON line.  If one rank fails the
+    others are stopped (their exact PIDs), so nobody hangs in a barrier."""
+    port = free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r if r > 0 else 128 - r
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
 
 
 def dist_init():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
     if world > 1:
         import torch.distributed as dist
 
@@ -106,9 +163,28 @@ def max_over_ranks(world, x: float) -> float:
     return float(t.item())
 
 
+def gather(world, obj):
+    if world == 1:
+        return [obj]
+    import torch.distributed as dist
+
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def finish_dist(world):
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------ workloads
 def fill_device(ctx, buf, nbytes, config_id, chunk=256 << 20):
     """Seeded random bytes; one generated chunk tiled over the buffer (the
-    codec's cost does not depend on cross-chunk uniqueness)."""
+    codec's cost does not depend on cross-chunk uniqueness).  Returns the
+    chunk, from which the expected byte at any offset o is blk[o % blk.size]."""
     from tools.datagen import stripe_bytes
 
     blk = stripe_bytes(min(chunk, nbytes), config_id)
@@ -117,10 +193,22 @@ def fill_device(ctx, buf, nbytes, config_id, chunk=256 << 20):
         n = min(blk.size, nbytes - off)
         buf.upload(blk[:n], offset=off)
         off += n
+    return blk
+
+
+def tiled(blk, off, n):
+    """Bytes [off, off + n) of blk tiled without end."""
+    import numpy as np
+
+    idx = (np.arange(n, dtype=np.int64) + off) % blk.size
+    return blk[idx]
 
 
 class Workload:
-    """One rank's EC batch: encode (client layout) + decode (recovery layout)."""
+    """One shard's EC batch on one device: encode (client layout) + decode
+    (recovery layout).  The erased cells of the recovery image hold a marker
+    until the first decode regenerates them, so verify() fails for a decode
+    that wrote nothing."""
 
     def __init__(self, ctx, k, p, C, S, ops=("enc", "dec"), err=(0, 1), config_id=2):
         self.ctx, self.k, self.p, self.C, self.S, self.err = ctx, k, p, C, S, list(err)
@@ -129,16 +217,29 @@ class Workload:
         # of two apart alias in HBM and cost EC_8P2 encode ~10 %
         # (profiles/r01/tune5_parity_row_aliasing.json, tune6_pitch.json).
         self.prow = S * C + PARITY_ROW_PAD
-        self.data = ctx.alloc(S * k * C)
+        self.data = ctx.alloc(max(1, S * k * C))
         self.parity = ctx.alloc(p * self.prow)
-        self.stripes = ctx.alloc(S * (k + p) * C)
+        self.stripes = ctx.alloc(max(1, S * (k + p) * C))
+        self.events = []        # per timed step: (start, stop) per op
+        if S == 0:
+            return
         fill_device(ctx, self.data, S * k * C, config_id)
         # recovery buffer: a consistent [S][k+p][C] image (encode in place)
-        fill_device(ctx, self.stripes, S * (k + p) * C, config_id + 1)
+        self.img_blk = fill_device(ctx, self.stripes, S * (k + p) * C, config_id + 1)
         st = (k + p) * C
         ctx.encode(k, p, C, S, self.stripes.ptr, st, self.stripes.ptr + k * C, C, st)
         ctx.sync()
-        self.events = []        # per timed step: 4 events bracketing the two launches
+        if "dec" in self.ops:
+            from daos_amd import ecg
+
+            for s in range(S):
+                for e in self.err:
+                    ecg._chk(ecg.lib().ecg_memset(ctx.h, self.stripes.ptr + s * st + e * C, MARKER, C, None),
+                             "memset")
+            ctx.sync()
+
+    def enc_call(self):
+        return (self.data.ptr, self.parity.ptr)
 
     def step(self, timed=False):
         c, k, p, C, S = self.ctx, self.k, self.p, self.C, self.S
@@ -166,6 +267,43 @@ class Workload:
                 self.ctx.destroy_event(a)
                 self.ctx.destroy_event(b)
         self.events = []
+        return out
+
+    def verify(self, nsample=3):
+        """After the timed steps, on sampled stripes: the decode regenerated
+        the erased cells (they held MARKER before) with the original bytes, and
+        the timed encode's parity, put in a fresh stripe with d0/d1 erased,
+        decodes back to its data.  The oracle checks live in tests/; this is
+        the run's own consistency check."""
+        import numpy as np
+
+        if self.S == 0:
+            return {}
+        k, p, C, S = self.k, self.p, self.C, self.S
+        st = (k + p) * C
+        samples = sorted({0, S // 2, S - 1})[:nsample]
+        out = {}
+        if "dec" in self.ops:
+            ok = True
+            for s in samples:
+                for e in self.err:
+                    got = self.stripes.download(C, offset=s * st + e * C)
+                    ok &= bool(np.array_equal(got, tiled(self.img_blk, s * st + e * C, C)))
+            out["decode_regenerated_erased_cells"] = ok
+        if "enc" in self.ops:
+            ok = True
+            probe = self.ctx.alloc(st)
+            for s in samples:
+                cells = self.data.download(k * C, offset=s * k * C)
+                par = np.stack([self.parity.download(C, offset=r * self.prow + s * C) for r in range(p)])
+                img = np.concatenate([cells.reshape(k, C), par]).copy()
+                img[self.err] = MARKER
+                probe.upload(img)
+                self.ctx.recover(k, p, C, 1, probe.ptr, st, self.err)
+                self.ctx.sync()
+                ok &= bool(np.array_equal(probe.download()[:k * C], cells))
+            probe.free()
+            out["encode_parity_decodes_to_data"] = ok
         return out
 
     def user_bytes_per_step(self):
@@ -205,6 +343,8 @@ class HostWorkload:
         img = self.stripes.array.reshape(S, k + p, C)
         img[:, :k] = a.reshape(S, k, C)
         img[:, k:] = self.parity.array.reshape(p, S, C).transpose(1, 0, 2)
+        img[:, self.err] = MARKER           # the first recovery must regenerate them
+        self.parity.array[:] = 0            # the first timed-region encode must write them
         self.events = []
 
     def step(self, timed=False):
@@ -233,18 +373,90 @@ class HostWorkload:
         return n
 
     def verify(self):
-        """Recovered cells must equal the original data (the stripes were
-        encoded from it); parity must be stable across steps."""
+        """Recovered cells (MARKER before the first step) equal the original
+        data; and the timed encode's parity, copied into the image with d0/d1
+        erased again, decodes back to the data."""
         import numpy as np
 
-        img = self.stripes.array.reshape(self.S, self.k + self.p, self.C)
-        return bool(np.array_equal(img[:, :self.k], self.data.array.reshape(self.S, self.k, self.C)))
+        S, k, p, C = self.S, self.k, self.p, self.C
+        img = self.stripes.array.reshape(S, k + p, C)
+        data = self.data.array.reshape(S, k, C)
+        out = {"decode_regenerated_erased_cells": bool(np.array_equal(img[:, :k], data))}
+        img[:, k:] = self.parity.array.reshape(p, S, C).transpose(1, 0, 2)
+        img[:, self.err] = MARKER
+        self.ctx.recover_host(k, p, C, S, self.stripes.array, self.err, chunk=HOST_CHUNK)
+        out["encode_parity_decodes_to_data"] = bool(np.array_equal(img[:, :k], data))
+        return out
 
     def free(self):
         for b in (self.data, self.parity, self.stripes):
             b.free()
 
 
+class MultiWorkload:
+    """`--sharder lib`: N shards in one process through ecg_multi (one host
+    thread + context per device).  Each shard is a Workload on its own
+    context; a step is one ecg_multi_encode + one ecg_multi_recover over all
+    shards (asynchronous), the timed region ends with ecg_multi_sync."""
+
+    def __init__(self, m, k, p, C, S_total, ops, strong):
+        self.m, self.k, self.p, self.C = m, k, p, C
+        self.ops = tuple(ops)
+        self.shards = []
+        for i, c in enumerate(m.ctxs):
+            S = m.range(S_total, i)[1] if strong else S_total
+            self.shards.append(Workload(c, k, p, C, S, ops=ops, config_id=2))
+        self.err = self.shards[0].err
+        self.S = self.shards[0].S
+
+    def step(self, timed=False):
+        from daos_amd import ecg
+
+        k, p, C = self.k, self.p, self.C
+        w0 = self.shards[0]
+        ns = [w.S for w in self.shards]
+        evs = []
+        for op in self.ops:
+            ev = (w0.ctx.event(), w0.ctx.event()) if timed else None
+            if timed:
+                w0.ctx.record(ev[0])
+            if op == "enc":
+                self.m.encode(k, p, C, ns, [w.data.ptr for w in self.shards], k * C,
+                              [w.parity.ptr for w in self.shards], w0.prow, C, flags=ecg.MULTI_ASYNC)
+            else:
+                self.m.recover(k, p, C, ns, [w.stripes.ptr for w in self.shards], (k + p) * C, self.err,
+                               flags=ecg.MULTI_ASYNC)
+            if timed:
+                w0.ctx.record(ev[1])
+                evs.append(ev)
+        if timed:
+            w0.events.append(evs)
+
+    def sync(self):
+        self.m.sync()
+
+    def kernel_ms(self):
+        return self.shards[0].kernel_ms()
+
+    def verify(self):
+        out = {}
+        for w in self.shards:
+            for key, v in w.verify().items():
+                out[key] = out.get(key, True) and v
+        return out
+
+    def user_bytes_per_step(self):
+        return sum(w.user_bytes_per_step() for w in self.shards)
+
+    def alg_bytes(self, op):
+        return self.shards[0].alg_bytes(op)
+
+    def free(self):
+        for w in self.shards:
+            w.free()
+
+
+# ------------------------------------------------------------------ measurements
 def pinned_copy_rates(ctx, n=1 << 30):
     """Raw pinned hipMemcpy H2D / D2H GB/s on this rank's device."""
     h = ctx.host_alloc(n)
@@ -358,16 +570,17 @@ def detail_rows(ctx, ceil, iters=7):
     fill_device(ctx, data, S * k * C, 8)
     pitch = S * C + PARITY_ROW_PAD
     par = ctx.alloc(p * pitch)
-    out = ctx.alloc(p * S * (C // 32768) * 4)
+    out = ctx.alloc(p * S * (C // 32768) * 8)
     enc = time_kernel(ctx, lambda: ctx.encode(k, p, C, S, data.ptr, k * C, par.ptr, pitch, C), iters)
-    fus = time_kernel(ctx, lambda: ctx.encode_csum(k, p, C, S, data.ptr, k * C, par.ptr, pitch, C,
-                                                   ecg.HASH_CRC32, 32768, 1, out.ptr), iters)
-    alg = (k + p) * C * S
-    rows["EC_8P2_1MiB_encode_crc32_32KiB_fused"] = {
-        "GiBps_user": round(k * C * S / (fus / 1e3) / GIB, 1), "alg_GBps": round(alg / fus / 1e6, 1),
-        "roofline_frac": round(alg / fus / 1e6 / HBM_PEAK_GBS, 4), "ms": round(fus, 4),
-        "encode_only_ms": round(enc, 4), "checksum_overhead": round(fus / enc - 1, 4),
-        "kernel": ecg.last_kernel()}
+    for hname, htype in (("crc32", ecg.HASH_CRC32), ("crc64", ecg.HASH_CRC64)):
+        fus = time_kernel(ctx, lambda: ctx.encode_csum(k, p, C, S, data.ptr, k * C, par.ptr, pitch, C,
+                                                       htype, 32768, 1, out.ptr), iters)
+        alg = (k + p) * C * S
+        rows[f"EC_8P2_1MiB_encode_{hname}_32KiB_fused"] = {
+            "GiBps_user": round(k * C * S / (fus / 1e3) / GIB, 1), "alg_GBps": round(alg / fus / 1e6, 1),
+            "roofline_frac": round(alg / fus / 1e6 / HBM_PEAK_GBS, 4), "ms": round(fus, 4),
+            "encode_only_ms": round(enc, 4), "checksum_overhead": round(fus / enc - 1, 4),
+            "kernel": ecg.last_kernel()}
     # rebuild of parity shard p1 over the same 512 fetched stripes (migrate_update_parity,
     # include/ecg_daos.h): one output row + its crc32 chunks, (k + 1) cells of traffic per stripe
     import ctypes
@@ -386,19 +599,31 @@ def detail_rows(ctx, ceil, iters=7):
         "roofline_frac": round(alg / ms / 1e6 / HBM_PEAK_GBS, 4), "ms": round(ms, 4),
         "kernel": ecg.last_kernel()}
     n = 1024
-    ms = time_kernel(ctx, lambda: ctx.csum_extents(ecg.HASH_CRC32, 32768, 1, 0, C, data.ptr, C, n, out.ptr), iters)
-    rows["crc32_32KiB_chunks_1GiB"] = {"alg_GBps": round(C * n / ms / 1e6, 1),
-                                       "roofline_frac": round(C * n / ms / 1e6 / HBM_PEAK_GBS, 4),
-                                       "ms": round(ms, 4), "kernel": ecg.last_kernel(),
-                                       "bound": "LDS lookups (1.25 ds_read_b32 per byte), DESIGN.md §11"}
+    for hname, htype in (("crc32", ecg.HASH_CRC32), ("crc64", ecg.HASH_CRC64)):
+        ms = time_kernel(ctx, lambda: ctx.csum_extents(htype, 32768, 1, 0, C, data.ptr, C, n, out.ptr), iters)
+        rows[f"{hname}_32KiB_chunks_1GiB"] = {"alg_GBps": round(C * n / ms / 1e6, 1),
+                                              "roofline_frac": round(C * n / ms / 1e6 / HBM_PEAK_GBS, 4),
+                                              "ms": round(ms, 4), "kernel": ecg.last_kernel()}
     data.free(); par.free(); out.free()
     return rows
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(k, p, C, budget_s, ops=("enc", "dec")):
     """Oracle SIMD restatement (ISA-L-equivalent), OpenMP over stripes, on a
-    bounded sample: 32 stripes of the same workload (same ops), repeated until
-    ~budget_s of CPU time."""
+    bounded sample of the same workload (same ops): a working set of >= 1 GiB
+    of user data (so the 256 MiB L3 of the box's EPYC cannot hold it),
+    repeated for ~60 % of the budget on the box's CPU share, then ~40 % on one
+    core."""
     import numpy as np
 
     from oracle import ref
@@ -409,55 +634,75 @@ def cpu_baseline(k, p, C, budget_s, ops=("enc", "dec")):
     except AttributeError:
         cores = os.cpu_count() or 1
     cores = max(1, min(cores, 16))      # the GPU box's CPU share is 16
-    S = 32
-    data = stripe_bytes(S * k * C, 2)
-    stripes = np.zeros(S * (k + p) * C, dtype=np.uint8)
+    S = max(32, -(-(1 << 30) // (k * C)))
+    blk = stripe_bytes(min(256 << 20, S * k * C), 2)
+    data = np.resize(blk, S * k * C)
+    stripes = np.empty(S * (k + p) * C, dtype=np.uint8)
     sv = stripes.reshape(S, k + p, C)
     sv[:, :k] = data.reshape(S, k, C)
-    par = ref.encode_batch(k, p, C, S, data, nthreads=cores, simd=True).reshape(p, S, C)
-    sv[:, k:] = par.transpose(1, 0, 2)
+    pout = np.empty(p * S * C, dtype=np.uint8)     # reused: no page faults in the timed loop
+    ref.encode_batch(k, p, C, S, data, nthreads=cores, simd=True, out=pout)
+    sv[:, k:] = pout.reshape(p, S, C).transpose(1, 0, 2)
     rc, de, dec, el, gt, reused = ref.recov_codec(k, p, [0, 1])
     assert rc == 0
-    pout = np.empty(p * S * C, dtype=np.uint8)     # reused: no page faults in the timed loop
-    user = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < budget_s:
-        if "enc" in ops:
-            ref.encode_batch(k, p, C, S, data, nthreads=cores, simd=True, out=pout)
-        if "dec" in ops:
-            ref.recov_batch(k, 2, gt, dec, el, C, (k + p) * C, S, stripes, nthreads=cores, simd=True)
-        user += len(ops) * k * C * S
-    dt = time.perf_counter() - t0
+
+    def run(threads, secs):
+        user, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < secs:
+            if "enc" in ops:
+                ref.encode_batch(k, p, C, S, data, nthreads=threads, simd=True, out=pout)
+            if "dec" in ops:
+                ref.recov_batch(k, 2, gt, dec, el, C, (k + p) * C, S, stripes, nthreads=threads, simd=True)
+            user += len(ops) * k * C * S
+        dt = time.perf_counter() - t0
+        return round(user / dt / GIB, 3), round(dt, 1)
+
+    many, t_many = run(cores, 0.6 * budget_s)
+    one, t_one = run(1, 0.4 * budget_s)
     variant = {0: "scalar", 1: "avx2-vpshufb", 2: "gfni-avx512"}[ref.simd_variant()]
-    return {"value": round(user / dt / GIB, 3), "unit": "GiB/s", "cores": cores, "kind": "port",
-            "sample": f"EC_{k}P{p} {C >> 10} KiB cells, {S} stripes, {' + '.join(ops)}, repeated "
-                      f"{dt:.1f} s; ISA-L-equivalent restatement ({variant}, OpenMP)"}
+    ws = S * (k + (k + p) + p) * C
+    return {"value": many, "unit": "GiB/s", "cores": cores, "kind": "port",
+            "one_core": {"value": one, "unit": "GiB/s", "cores": 1, "seconds": t_one},
+            "cpu_model": cpu_model(), "working_set_bytes": ws,
+            "sample": f"EC_{k}P{p} {C >> 10} KiB cells, {S} stripes ({S * k * C / GIB:.2f} GiB of data, "
+                      f"{ws / GIB:.2f} GiB touched), {' + '.join(ops)}, repeated {t_many} s; "
+                      f"ISA-L-equivalent restatement ({variant}, OpenMP)",
+            "note": "r01 reported 129 GiB/s here (32-stripe, 192 MiB sample that partly fits the EPYC's "
+                    "256 MB L3) and 170 GiB/s in DESIGN (tools/cpu_baselines.py, encode-only rows); this "
+                    "line uses a >= 1 GiB working set, so memory bandwidth, not L3, feeds the cores"}
 
 
 def pmc_traffic():
     path = os.path.join(ROOT, "profiles", ROUND, "pmc_traffic.json")
+    if not os.path.exists(path):
+        path = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
     if os.path.exists(path):
         try:
-            return json.load(open(path))
+            d = json.load(open(path))
+            d["_path"] = os.path.relpath(path, ROOT)
+            return d
         except (OSError, ValueError):
             return None
     return None
 
 
-def host_report(args, ctx, wl, world, rank, value, elapsed):
+# ------------------------------------------------------------------ reporting
+def host_report(args, ctx, wl, world, rank, value, elapsed, ranks):
     """JSON line of the PCIe-inclusive rebuild stream (configs[4]).  The
     device kernels are not the bound here, the host links are: `roofline`
     is null and `pcie` sets the achieved H2D rate against this box's raw
     pinned copy rate (measured on rank 0 at N=1)."""
     k, p, C, S = wl.k, wl.p, wl.C, wl.S
-    ok = wl.verify()
+    ver = wl.verify()
+    allver = gather(world, ver)
+    ok = all(all(v.values()) for v in allver)
     h2d = wl.h2d_bytes_per_step() * args.steps * world / elapsed / 1e9
     d2h = wl.d2h_bytes_per_step() * args.steps * world / elapsed / 1e9
     out = {
         "metric": "EC rebuild stream GiB/s (host-resident stripes, PCIe-inclusive)",
         "value": round(value, 2),
         "unit": "GiB/s",
-        "n_gpus": world,
+        "n_gpus": len({r["pci"] for r in ranks}),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -473,7 +718,8 @@ def host_report(args, ctx, wl, world, rank, value, elapsed):
                    "erasures": wl.err, "parallelism": f"stripe-sharded x{world}, no collective"},
         "roofline": None,
         "pcie": {"bound": "pcie", "h2d_GBps_all_ranks": round(h2d, 2), "d2h_GBps_all_ranks": round(d2h, 2)},
-        "recovered_bytes_ok": ok,
+        "verified": ver,
+        "ranks": ranks,
         "cpu_baseline": None,
     }
     wl.free()
@@ -483,18 +729,40 @@ def host_report(args, ctx, wl, world, rank, value, elapsed):
         out["pcie"]["frac_of_h2d"] = round(h2d / raw["h2d"], 4)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    ctx.close()
-    if world > 1:
-        import torch.distributed as dist
+    return ok
 
-        dist.destroy_process_group()
-    if not ok:
-        raise SystemExit("bench.py: recovered cells differ from the original data")
+
+def rehearse(args, world, rank, local):
+    """CPU-only rehearsal of the N-rank plumbing (launcher, env, barrier,
+    max-over-ranks, gather): each rank 'steps' by sleeping 1 ms per step."""
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.001 * (1 + rank))
+    elapsed = max_over_ranks(world, time.perf_counter() - t0)
+    ranks = gather(world, {"rank": rank, "local_rank": local, "pid": os.getpid()})
+    if rank == 0:
+        print(json.dumps({"metric": "rehearsal (no GPU work)", "rehearsal": True, "value": None, "n_ranks": world,
+                          "steps": args.steps, "ms_per_step": round(elapsed / max(1, args.steps) * 1e3, 3),
+                          "ranks": ranks}), flush=True)
+    finish_dist(world)
 
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1 and args.sharder == "procs":
+        sys.exit(launch_ranks(args))          # parent: no GPU calls before or after
     world, rank, local = dist_init()
+    if "WORLD_SIZE" in os.environ and args.sharder == "procs" and world != args.gpus:
+        raise SystemExit(f"bench.py: launched as {world} ranks but --gpus {args.gpus}")
+    if args.sharder == "lib" and world > 1:
+        raise SystemExit("bench.py: --sharder lib runs in one process (no WORLD_SIZE > 1)")
+    if args.rehearse:
+        rehearse(args, world, rank, local)
+        return
+
     import torch  # noqa: F401  (shares libamdhip64 with libecg; sync per contract)
 
     from daos_amd import ecg
@@ -502,17 +770,39 @@ def main():
     ndev = ecg.device_count()
     if ndev < 1:
         raise SystemExit("bench.py: no gfx950 device visible")
-    dev = local % ndev          # > 1 rank per GPU only when rehearsing on a 1-GPU box
-    torch.cuda.set_device(dev)
-    ctx = ecg.Context(dev)
     k, p, C, S, ops, strong = WORKLOADS[args.workload]
-    if strong:                      # configs[3]: a fixed stripe total split across ranks
-        S = S // world + (1 if rank < S % world else 0)
     host = ops[0].endswith("_host")
-    wl = (HostWorkload if host else Workload)(ctx, k, p, C, S, ops=ops)
+    nshard = args.gpus if args.sharder == "lib" else world
+    if args.sharder == "lib":
+        devices = list(range(args.gpus)) if args.gpus <= ndev else [i % ndev for i in range(args.gpus)]
+        if args.gpus > ndev and not args.allow_shared_device:
+            raise SystemExit(f"bench.py: {args.gpus} shards but {ndev} devices (--allow-shared-device to rehearse)")
+        if host:
+            raise SystemExit("bench.py: --sharder lib covers the device-resident workloads")
+        m = ecg.Multi(devices)
+        ctx = m.ctxs[0]
+        dev = devices[0]
+        torch.cuda.set_device(dev)
+        wl = MultiWorkload(m, k, p, C, S, ops, strong)
+        rank_devs = [{"shard": i, "device": d, "pci": ecg.pci_bus_id(d)} for i, d in enumerate(devices)]
+        S = wl.S
+    else:
+        if local >= ndev and not args.allow_shared_device:
+            raise SystemExit(f"bench.py: local rank {local} but {ndev} visible devices "
+                             "(--allow-shared-device to rehearse several ranks on one GPU)")
+        dev = local % ndev
+        torch.cuda.set_device(dev)
+        ctx = ecg.Context(dev)
+        m = None
+        if strong:                      # configs[3]: a fixed stripe total split across ranks
+            S = S // world + (1 if rank < S % world else 0)
+        wl = (HostWorkload if host else Workload)(ctx, k, p, C, S, ops=ops)
+        rank_devs = None
 
     for _ in range(args.warmup):
         wl.step()
+    if m is not None:
+        wl.sync()
     ctx.sync()
 
     barrier(world)
@@ -521,24 +811,38 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         wl.step(timed=True)
+    if m is not None:
+        wl.sync()
     ctx.sync()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0      # this rank's K steps, from the common start barrier
+    mine = time.perf_counter() - t0       # this rank's K steps, from the common start barrier
     barrier(world)
-    elapsed = max_over_ranks(world, elapsed)    # the job took as long as its slowest rank
+    elapsed = max_over_ranks(world, mine)  # the job took as long as its slowest rank
 
     if args.profile_only:
         wl.free()
-        ctx.close()
+        if m is not None:
+            m.close()
+        else:
+            ctx.close()
+        finish_dist(world)
         return
 
+    if rank_devs is None:
+        rank_devs = gather(world, {"rank": rank, "device": dev, "pci": ecg.pci_bus_id(dev),
+                                   "ms_per_step": round(mine / args.steps * 1e3, 3)})
+    n_gpus = len({r["pci"] for r in rank_devs})
     if strong:      # the fixed total, however it was split
         user = WORKLOADS[args.workload][3] * k * C * len(ops) * args.steps
     else:           # every rank processed the same batch
         user = wl.user_bytes_per_step() * args.steps * world
     value = user / elapsed / GIB
     if host:
-        host_report(args, ctx, wl, world, rank, value, elapsed)
+        ok = host_report(args, ctx, wl, world, rank, value, elapsed, rank_devs)
+        ctx.close()
+        finish_dist(world)
+        if not ok:
+            raise SystemExit("bench.py: verification failed (see `verified`)")
         return
     kms = wl.kernel_ms()
     launches = [(op, ms) for op in ops for ms in kms[op]]
@@ -547,17 +851,24 @@ def main():
     achieved = alg_per_launch / (mean_launch_ms / 1e3) / 1e9
     read_GBps = k * C * S / (mean_launch_ms / 1e3) / 1e9
     kernel_name = f"ecg_mm_kernel<{k},{p},0,0>"
-    traffic = None
+    traffic, traffic_src = None, None
     pmc = pmc_traffic()
     if pmc and pmc.get("kernel", "").replace(" ", "") == f"ecg_mm_kernel<{k},{p}" and \
             pmc.get("alg_bytes_per_launch") == int(alg_per_launch):
         traffic = pmc.get("hbm_bytes_per_launch")
+        traffic_src = (f"{pmc['_path']} (rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes of this "
+                       "workload, FETCH x2 per the gfx950 correction; copied, not measured in this run)")
+    ver = wl.verify()
+    allver = gather(world, ver)
+    ok = all(all(v.values()) for v in allver)
 
+    par = (f"stripe-sharded x{nshard} in one process (ecg_multi), no collective" if m is not None
+           else f"stripe-sharded x{world} (one process per GPU), no collective")
     out = {
         "metric": "EC encode+decode GiB/s (device-resident stripes)",
         "value": round(value, 2),
         "unit": "GiB/s",
-        "n_gpus": world,
+        "n_gpus": n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -566,17 +877,20 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic: xoshiro256** stripes seeded 0xDA05EC00+id (BASELINE.md §3), device-resident",
-        "config": {"workload": describe(args.workload, k, p, C, S, ops),
+        "config": {"workload": describe(args.workload, k, p, C, S, ops, nshard),
                    "name": args.workload, "k": k, "p": p, "cell_bytes": C, "stripes_per_gpu": S,
                    "erasures": wl.err if "dec" in ops else [],
-                   "parallelism": f"stripe-sharded x{world}, no collective"},
+                   "parallelism": par},
         "roofline": {"bound": "hbm", "kernel": kernel_name, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      # north star's "fraction of HBM-read peak": the k input cells read per launch
                      "read_GBps": round(read_GBps, 1), "read_frac": round(read_GBps / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "alg_bytes_per_launch": int(alg_per_launch),
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "alg_bytes_per_launch": int(alg_per_launch),
                      "mean_launch_ms": round(mean_launch_ms, 4),
                      **{f"{op}_ms_median": round(sorted(kms[op])[len(kms[op]) // 2], 4) for op in ops}},
+        "verified": ver,
+        "ranks": rank_devs,
         "cpu_baseline": None,
     }
     wl.free()
@@ -586,16 +900,28 @@ def main():
         out["roofline"]["measured_stream_GBps"] = ceil
         out["roofline"]["measured_mix_ceiling_GBps"] = round(mix, 1)
         out["roofline"]["frac_of_measured_mix"] = round(achieved / mix, 4)
-        out["detail"] = detail_rows(ctx, ceil)
-    if rank == 0 and world == 1 and not args.no_cpu:
+        det = detail_rows(ctx, ceil)
+        out["detail"] = det
+        e8 = det["EC_8P2_1MiB_encode"]
+        out["roofline"]["north_star"] = {
+            "target": ">= 70 % of per-GPU HBM-read roofline on EC_8P2 encode at 1 MiB cells, device-resident",
+            "EC_8P2_1MiB_encode_frac": e8["roofline_frac"],
+            "EC_8P2_1MiB_encode_read_frac": e8["read_frac"],
+            "reading": "frac = (k+p)*C*S bytes (reads + writes) / t / 8 TB/s, the SURVEY §8(d) roofline; "
+                       "read_frac = the k input cells alone / t / 8 TB/s.  The same launch must also write "
+                       "p/k as many bytes, and this box's HBM streams 6.7-7.0 TB/s read-only, so read_frac "
+                       "cannot reach 0.70 while parity is written (DESIGN.md §6)"}
+    if rank == 0 and world == 1 and not args.no_cpu and m is None:
         out["cpu_baseline"] = cpu_baseline(k, p, C, args.cpu_seconds, ops)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    ctx.close()
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.destroy_process_group()
+    if m is not None:
+        m.close()
+    else:
+        ctx.close()
+    finish_dist(world)
+    if not ok:
+        raise SystemExit("bench.py: verification failed (see `verified`)")
 
 
 if __name__ == "__main__":

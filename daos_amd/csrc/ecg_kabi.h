@@ -181,6 +181,11 @@ int ecg_k_launch_copy_segs(const ecg_copy_seg_t *segs_dev, uint32_t nseg, uint64
 /* Implemented in kernels/ecg_kernels.hip.  Returns a hipError_t value. */
 int ecg_k_launch_matmul(const ecg_mm_params_t *p, const ecg_launch_cfg_t *cfg,
 			void *stream, uint32_t *kernel_id);
+/* One-cell product with a per-stripe coefficient column (p->k == 1):
+ * dst[s][r] = tbl[r][sel_dev[s]] * src[s]; tables for columns < ncols <= 16.
+ * 16-byte aligned operands only (hipErrorInvalidValue otherwise). */
+int ecg_k_launch_matmul_sel(const ecg_mm_params_t *p, const uint8_t *sel_dev, uint32_t ncols,
+			    void *stream, uint32_t *kernel_id);
 /* Streaming kernels used only to measure the box's achievable HBM rates:
  * mode 0 copy, 1 read-only, 2 write-only. */
 int ecg_k_launch_copy(const void *src, void *dst, uint64_t bytes, int mode, void *stream,

@@ -149,6 +149,18 @@ int ecg_ctx_device(const ecg_ctx_t *ctx)
 	return ctx ? ctx->device : -1;
 }
 
+int ecg_device_pci_bus_id(int device, char *buf, int len)
+{
+	hipError_t e;
+
+	if (buf == NULL || len < 13)
+		return ecg_fail(-ECG_DER_INVAL, "pci_bus_id: buffer too small");
+	e = hipDeviceGetPCIBusId(buf, len, device);
+	if (e != hipSuccess)
+		return ecg_hip_fail(e, "hipDeviceGetPCIBusId");
+	return 0;
+}
+
 void *ecg_ctx_stream(ecg_ctx_t *ctx)
 {
 	return ctx ? (void *)ctx->stream : NULL;
@@ -187,8 +199,11 @@ int ecg_set_launch(ecg_ctx_t *ctx, uint32_t grid_x, uint32_t grid_y, uint32_t va
 static int launch(ecg_ctx_t *ctx, const ecg_mm_params_t *prm, hipStream_t st)
 {
 	uint32_t kid = 0;
-	int e = ecg_k_launch_matmul(prm, &ctx->cfg, (void *)st, &kid);
+	int e;
 
+	ecg_trace_push("ecg:launch");
+	e = ecg_k_launch_matmul(prm, &ctx->cfg, (void *)st, &kid);
+	ecg_trace_pop();
 	if (e != 0)
 		return ecg_hip_fail((hipError_t)e, "kernel launch");
 	ecg_set_last_kernel(ecg_k_kernel_name(kid));
@@ -279,6 +294,47 @@ int ecg_matmul(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef,
 		       flags, stream);
 }
 
+int ecg_matmul_sel(ecg_ctx_t *ctx, int ncols, int rows, const unsigned char *coef, uint64_t C, uint32_t S,
+		   const void *src, int64_t sstride, const uint8_t *sel_dev, void *dst, const int64_t *doff,
+		   int64_t dstride, void *stream)
+{
+	ecg_mm_params_t *prm;
+	uint32_t kid = 0;
+	int rc, r, j, e;
+
+	if (ncols < 1 || ncols > ECG_KMAX_K || rows < 1 || rows > ECG_KMAX_R || coef == NULL ||
+	    src == NULL || sel_dev == NULL || dst == NULL || doff == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "matmul_sel: bad arguments");
+	if (C == 0 || S == 0)
+		return 0;
+	rc = ecg_ctx_enter(ctx);
+	if (rc)
+		return rc;
+	ecg_gf_init();
+	prm = calloc(1, sizeof(*prm));
+	if (prm == NULL)
+		return ecg_fail(-ECG_DER_NOMEM, "matmul_sel: calloc");
+	prm->src = src;
+	prm->dst = dst;
+	prm->src_stripe_stride = sstride;
+	prm->dst_stripe_stride = dstride;
+	prm->cell_bytes = C;
+	prm->nstripes = S;
+	prm->k = 1;
+	prm->rows = (uint32_t)rows;
+	for (r = 0; r < rows; r++) {
+		prm->dst_cell_off[r] = doff[r];
+		for (j = 0; j < ncols; j++)
+			ecg_build_ptbl(coef[r * ncols + j], &prm->tbl[r][j]);
+	}
+	e = ecg_k_launch_matmul_sel(prm, sel_dev, (uint32_t)ncols, (void *)ecg_pick_stream(ctx, stream), &kid);
+	free(prm);
+	if (e)
+		return ecg_hip_fail((hipError_t)e, "matmul_sel launch");
+	ecg_set_last_kernel(ecg_k_kernel_name(kid));
+	return 0;
+}
+
 static int check_kp(int k, int p)
 {
 	/* DAOS class limits, ref:src/object/obj_class.c:587-601 */
@@ -304,8 +360,11 @@ int ecg_encode(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 		soff[i] = (int64_t)i * (int64_t)C;
 	for (i = 0; i < p; i++)
 		doff[i] = (int64_t)i * parity_cell_stride;
-	return ecg_matmul(ctx, k, p, &en[k * k], C, S, data, soff, data_stripe_stride,
-			  parity, doff, parity_stripe_stride, 0, stream);
+	ecg_trace_push("ecg:encode");
+	rc = ecg_matmul(ctx, k, p, &en[k * k], C, S, data, soff, data_stripe_stride,
+			parity, doff, parity_stripe_stride, 0, stream);
+	ecg_trace_pop();
+	return rc;
 }
 
 /* Recovery rows through the per-context cache (the reference caches its
@@ -383,10 +442,12 @@ int ecg_recover(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 		return ecg_fail(-ECG_DER_DATA_LOSS, "recover: %d erasures > p=%d", nerrs, p);
 	if (nerrs <= 0)
 		return 0;
+	ecg_trace_push("ecg:recover");
 	rc = recov_lookup(ctx, k, p, err_list, nerrs, &ent);
-	if (rc)
-		return rc;
-	return recover_with(ctx, &ent, C, S, stripes, stripe_stride, stream);
+	if (rc == 0)
+		rc = recover_with(ctx, &ent, C, S, stripes, stripe_stride, stream);
+	ecg_trace_pop();
+	return rc;
 }
 
 /*
@@ -582,9 +643,12 @@ int ecg_update(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 	}
 	for (r = 0; r < p; r++)
 		doff[r] = (int64_t)r * parity_cell_stride;
-	return matmul2(ctx, nupd, p, coef, C, S, old_cells, soff, upd_stripe_stride,
-		       new_cells, soff, upd_stripe_stride, parity, doff, parity_stripe_stride,
-		       ECG_F_ACCUMULATE, stream);
+	ecg_trace_push("ecg:update");
+	rc = matmul2(ctx, nupd, p, coef, C, S, old_cells, soff, upd_stripe_stride,
+		     new_cells, soff, upd_stripe_stride, parity, doff, parity_stripe_stride,
+		     ECG_F_ACCUMULATE, stream);
+	ecg_trace_pop();
+	return rc;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -646,8 +710,10 @@ static int enc_h2d_parts(void)
 	return g_enc_h2d_parts;
 }
 
-int ecg_encode_host(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
-		    const void *data, void *parity, uint32_t chunk)
+/* parity row r of stripe s at parity + r*prow + s*C (prow = S*C for the
+ * [p][S][C] layout; a shard of a larger batch passes the batch's row pitch) */
+int ecg_encode_host_rows(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S, const void *data,
+			 void *parity, size_t prow, uint32_t chunk)
 {
 	const unsigned char *hd = data;
 	unsigned char *hp = parity;
@@ -658,6 +724,8 @@ int ecg_encode_host(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 	rc = check_kp(k, p);
 	if (rc)
 		return rc;
+	if (data == NULL || parity == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "encode_host: NULL buffer");
 	rc = ecg_ctx_enter(ctx);
 	if (rc)
 		return rc;
@@ -668,6 +736,7 @@ int ecg_encode_host(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 	if (chunk > S)
 		chunk = S;
 	pthread_mutex_lock(&ctx->lock);
+	ecg_trace_push("ecg:encode_host");
 	rc = stage_reserve(ctx, (size_t)chunk * (k + p) * C);
 	for (s0 = 0; rc == 0 && s0 < S; s0 += chunk, slot = (slot + 1) % ECG_NSLOT) {
 		uint32_t cs = S - s0 < chunk ? S - s0 : chunk;
@@ -676,7 +745,9 @@ int ecg_encode_host(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 		hipStream_t st = ctx->stage.st[slot];
 		hipError_t e;
 
+		ecg_trace_push("ecg:stage_wait");
 		e = hipEventSynchronize(ctx->stage.done[slot]);
+		ecg_trace_pop();
 		if (e == hipSuccess && h2d_mode == 1) {
 			e = hipMemcpyAsync(dd, hd + (size_t)s0 * k * C, (size_t)cs * k * C,
 					   hipMemcpyHostToDevice, st);
@@ -696,7 +767,7 @@ int ecg_encode_host(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 		rc = ecg_encode(ctx, k, p, C, cs, dd, (int64_t)k * C, dp, (int64_t)cs * C,
 				(int64_t)C, st);
 		for (r = 0; rc == 0 && r < p; r++) {
-			e = ecg_stage_copy(hp + ((size_t)r * S + s0) * C, dp + (size_t)r * cs * C,
+			e = ecg_stage_copy(hp + (size_t)r * prow + (size_t)s0 * C, dp + (size_t)r * cs * C,
 					   (size_t)cs * C, C, hipMemcpyDeviceToHost, st);
 			if (e != hipSuccess)
 				rc = ecg_hip_fail(e, "encode_host D2H");
@@ -710,8 +781,15 @@ int ecg_encode_host(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 	for (r = 0; r < ECG_NSLOT; r++)
 		if (ctx->stage.st[r])
 			(void)hipStreamSynchronize(ctx->stage.st[r]);
+	ecg_trace_pop();
 	pthread_mutex_unlock(&ctx->lock);
 	return rc;
+}
+
+int ecg_encode_host(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
+		    const void *data, void *parity, uint32_t chunk)
+{
+	return ecg_encode_host_rows(ctx, k, p, C, S, data, parity, (size_t)S * C, chunk);
 }
 
 int ecg_recover_host(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
@@ -726,6 +804,8 @@ int ecg_recover_host(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 	rc = check_kp(k, p);
 	if (rc)
 		return rc;
+	if (err_list == NULL || stripes == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "recover_host: NULL argument");
 	if (nerrs > p)
 		return ecg_fail(-ECG_DER_DATA_LOSS, "recover_host: %d erasures > p=%d", nerrs, p);
 	if (nerrs <= 0 || S == 0 || C == 0)
@@ -741,12 +821,17 @@ int ecg_recover_host(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 	if (chunk > S)
 		chunk = S;
 	pthread_mutex_lock(&ctx->lock);
+	ecg_trace_push("ecg:recover_host");
 	rc = stage_reserve(ctx, (size_t)chunk * sstride);
 	for (s0 = 0; rc == 0 && s0 < S; s0 += chunk, slot = (slot + 1) % ECG_NSLOT) {
 		uint32_t cs = S - s0 < chunk ? S - s0 : chunk;
 		unsigned char *dd = ctx->stage.dev[slot];
 		hipStream_t st = ctx->stage.st[slot];
-		hipError_t e = hipEventSynchronize(ctx->stage.done[slot]);
+		hipError_t e;
+
+		ecg_trace_push("ecg:stage_wait");
+		e = hipEventSynchronize(ctx->stage.done[slot]);
+		ecg_trace_pop();
 
 		/* survivors the decode reads: k cells per stripe, one strided 2D
 		 * copy per run of consecutive cells */
@@ -786,6 +871,7 @@ int ecg_recover_host(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 	for (i = 0; i < ECG_NSLOT; i++)
 		if (ctx->stage.st[i])
 			(void)hipStreamSynchronize(ctx->stage.st[i]);
+	ecg_trace_pop();
 	pthread_mutex_unlock(&ctx->lock);
 	return rc;
 }

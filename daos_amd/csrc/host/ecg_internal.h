@@ -135,6 +135,23 @@ int ecg_matmul_csum(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, 
 		    const int64_t *doff, int64_t dstride, int type, uint64_t chunksize,
 		    uint64_t rec_size, void *csums, const uint32_t *row_slot, void *stream);
 
+/* one-cell product, per-stripe coefficient column sel_dev[s] < ncols
+ * (coef rows x ncols), 16-byte aligned operands (ecg_core.c) */
+int ecg_matmul_sel(ecg_ctx_t *ctx, int ncols, int rows, const unsigned char *coef, uint64_t C, uint32_t S,
+		   const void *src, int64_t sstride, const uint8_t *sel_dev, void *dst, const int64_t *doff,
+		   int64_t dstride, void *stream);
+/* host pipeline with an explicit parity row pitch (ecg_core.c) */
+int ecg_encode_host_rows(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S, const void *data,
+			 void *parity, size_t prow, uint32_t chunk);
+/* "0,1,2" / "all" / NULL -> device list (ecg_multi.c); count or -ECG_DER_INVAL */
+int ecg_parse_devices(const char *spec, int *dev, int max);
+
+/* roctx ranges (ecg_trace.c): no-ops without the roctx library or with
+ * ECG_ROCTX=0 */
+void ecg_trace_push(const char *name);
+void ecg_trace_pop(void);
+int ecg_trace_active(void);
+
 /* context helpers (ecg_core.c) */
 int ecg_ctx_enter(ecg_ctx_t *ctx);
 hipStream_t ecg_pick_stream(ecg_ctx_t *ctx, void *stream);

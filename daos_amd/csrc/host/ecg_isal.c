@@ -15,16 +15,38 @@
 int ecg_matmul_host(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
 		    unsigned char *const *src, unsigned char *const *dst, unsigned flags);
 
-static ecg_ctx_t *g_ctx;
+/* One context per device of $ECG_DEVICES ("0,1,2,3" / "all"; default
+ * $ECG_DEVICE, else device 0).  Calling threads are spread over them
+ * round-robin on their first call, so an engine's xstreams calling the
+ * synchronous ISA-L API use every listed GPU. */
+#define ISAL_MAXDEV 64
+static ecg_ctx_t *g_ctx[ISAL_MAXDEV];
+static int g_nctx;
 static int g_ctx_rc;
+static unsigned g_next;
 static pthread_once_t g_ctx_once = PTHREAD_ONCE_INIT;
+static __thread ecg_ctx_t *t_ctx;
 
 static void default_ctx_init(void)
 {
-	const char *env = getenv("ECG_DEVICE");
-	int dev = env ? atoi(env) : 0;
+	const char *list = getenv("ECG_DEVICES");
+	const char *one = getenv("ECG_DEVICE");
+	int dev[ISAL_MAXDEV], n, i;
 
-	g_ctx_rc = ecg_ctx_create(dev, &g_ctx);
+	if (list) {
+		n = ecg_parse_devices(list, dev, ISAL_MAXDEV);
+	} else {
+		dev[0] = one ? atoi(one) : 0;
+		n = 1;
+	}
+	if (n <= 0) {
+		g_ctx_rc = n < 0 ? ecg_fail(-ECG_DER_INVAL, "bad ECG_DEVICES '%s'", list)
+				 : ecg_fail(-ECG_DER_NOSYS, "ECG_DEVICES: no device");
+		return;
+	}
+	for (i = 0; i < n && g_ctx_rc == 0; i++)
+		g_ctx_rc = ecg_ctx_create(dev[i], &g_ctx[i]);
+	g_nctx = i;
 }
 
 /* The ISA-L data-plane ABI is `void`: a failure cannot be returned, and
@@ -40,7 +62,9 @@ static ecg_ctx_t *default_ctx(const char *fn)
 	pthread_once(&g_ctx_once, default_ctx_init);
 	if (g_ctx_rc)
 		die(fn, g_ctx_rc);
-	return g_ctx;
+	if (t_ctx == NULL)
+		t_ctx = g_ctx[__atomic_fetch_add(&g_next, 1u, __ATOMIC_RELAXED) % (unsigned)g_nctx];
+	return t_ctx;
 }
 
 void gf_vect_mul_init(unsigned char c, unsigned char *tbl)
@@ -62,12 +86,31 @@ void ec_init_tables(int k, int rows, unsigned char *a, unsigned char *gftbls)
 		gf_vect_mul_init(a[i], gftbls + 32 * i);
 }
 
-static void coef_from_tables(int k, int rows, const unsigned char *gftbls, unsigned char *coef)
+/* The coefficient of each 32-byte table is its byte 1 (c * 1).  The tables
+ * must be ec_init_tables' base/AVX2 layout [c*0..c*15 | c*0x00..c*0xF0]; a
+ * libisal ec_init_tables resolved first in the process may emit its GFNI
+ * layout instead, and reading that as coefficients would
+ * silently corrupt parity -- so check and die instead. */
+static unsigned char table_coef(const char *fn, const unsigned char *t)
+{
+	const unsigned char c = t[1];
+
+	if (t[0] != 0 || t[16] != 0 || t[2] != ecg_gf_mul(c, 2) || t[15] != ecg_gf_mul(c, 15) ||
+	    t[17] != ecg_gf_mul(c, 0x10) || t[31] != ecg_gf_mul(c, 0xF0)) {
+		fprintf(stderr, "ecg: %s: gftbls are not ec_init_tables' 32-byte layout "
+			"(tables from another ISA-L build?)\n", fn);
+		abort();
+	}
+	return c;
+}
+
+static void coef_from_tables(const char *fn, int k, int rows, const unsigned char *gftbls,
+			     unsigned char *coef)
 {
 	int i;
 
 	for (i = 0; i < k * rows; i++)
-		coef[i] = gftbls[32 * i + 1];
+		coef[i] = table_coef(fn, gftbls + 32 * i);
 }
 
 void ec_encode_data(int len, int k, int rows, unsigned char *gftbls, unsigned char **data,
@@ -80,7 +123,7 @@ void ec_encode_data(int len, int k, int rows, unsigned char *gftbls, unsigned ch
 		return;
 	if (k > ECG_MAX_K || rows > 256)
 		die("ec_encode_data (k/rows out of range)", -ECG_DER_INVAL);
-	coef_from_tables(k, rows, gftbls, coef);
+	coef_from_tables("ec_encode_data", k, rows, gftbls, coef);
 	rc = ecg_matmul_host(default_ctx("ec_encode_data"), len, k, rows, coef, data, coding, 0);
 	if (rc)
 		die("ec_encode_data", rc);
@@ -98,7 +141,7 @@ void ec_encode_data_update(int len, int k, int rows, int vec_i, unsigned char *g
 	if (rows > 256 || vec_i < 0 || vec_i >= k)
 		die("ec_encode_data_update (bad arguments)", -ECG_DER_INVAL);
 	for (r = 0; r < rows; r++)
-		coef[r] = gftbls[32 * (r * k + vec_i) + 1];
+		coef[r] = table_coef("ec_encode_data_update", gftbls + 32 * (r * k + vec_i));
 	src[0] = data;
 	rc = ecg_matmul_host(default_ctx("ec_encode_data_update"), len, 1, rows, coef, src, coding,
 			     ECG_F_ACCUMULATE);

@@ -8,7 +8,7 @@
  * launch- and PCIe-latency bound.  The queue turns N concurrent
  * one-stripe calls into one device product over N stripes.
  *
- * Structure: NSLOT pinned staging slots, each owned by one request class
+ * Structure: nslot pinned staging slots, each owned by one request class
  * (op, k, p, cell size, erasure set) while it fills:
  *   FREE -> FILLING -> READY -> INFLIGHT -> DONE -> FREE
  * A submitter reserves a stripe index in a FILLING slot of its class (or
@@ -23,16 +23,31 @@
  * and another's D2H run.  Staging layout per slot: inputs [n][k][pitch], outputs
  * [n][rows][pitch] (pitch = cell size rounded to 64 B), so only inputs
  * cross H2D and only outputs cross D2H.
+ *
+ * Aggregation updates (ecg_queue_update: agg_update_parity's xor_gen +
+ * ec_encode_data_update per cell, ref:src/object/srv_ec_aggregate.c:
+ * 1086-1102) are a third class per (k, p, cell size): the submitter writes
+ * diff = old ^ new into the staging (the xor_gen), the device computes the p
+ * parity deltas coef[r][vec_i] * diff with the stripe's own column vec_i
+ * (ecg_mm_sel_kernel), and the completion threads XOR the deltas into the
+ * caller's parity cells -- parity never crosses PCIe in either direction.
+ *
+ * Slots are spread round-robin over the contexts of an ecg_multi_t
+ * (ecg_queue_create_multi): each slot's staging, stream and launches live on
+ * its own device.
  */
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
 
+#include "../../../include/ecg_multi.h"
 #include "ecg_internal.h"
 
 #define OP_ENCODE 0
 #define OP_RECOVER 1
-#define NSLOT 4
+#define OP_UPDATE 2
+#define NSLOT_MIN 4	/* staging slots for one device; 2 per device beyond */
+#define NSLOT_MAX 32
 #define NFIN 4		/* completion threads: output scatter + callbacks */
 
 enum slot_state { S_FREE, S_FILLING, S_READY, S_INFLIGHT, S_DONE };
@@ -40,12 +55,13 @@ enum slot_state { S_FREE, S_FILLING, S_READY, S_INFLIGHT, S_DONE };
 struct qreq {
 	int op, k, p, nerrs;
 	uint64_t C;
-	unsigned char *dst[ECG_MAX_P];	/* where each output row goes */
+	unsigned char *dst[ECG_MAX_P];	/* where each output row goes (XORed in for updates) */
 	ecg_done_cb_t cb;
 	void *arg;
 };
 
 struct qslot {
+	ecg_ctx_t *ctx;			/* device this slot's staging and launches live on */
 	enum slot_state state;
 	/* class */
 	int op, k, p, nerrs, rows;
@@ -53,13 +69,16 @@ struct qslot {
 	uint32_t err[ECG_MAX_P];
 	unsigned char coef[ECG_MAX_P * ECG_MAX_K];
 	uint32_t dec_idx[ECG_MAX_K], out_idx[ECG_MAX_P];
+	int nin;			/* input cells staged per request (k, or 1 for updates) */
 	/* fill state */
 	uint32_t cap, reserved, filled;
 	uint32_t fin_next, fin_done;	/* completion progress (S_DONE) */
 	uint64_t t_open_ns;
 	struct qreq *reqs;		/* cap entries */
 	/* staging */
-	unsigned char *host;		/* pinned: inputs then outputs */
+	unsigned char *host;		/* pinned: inputs [cap][k][pitch], (updates: vec_i [cap]),
+					 * outputs [cap][rows][pitch] at out_off */
+	size_t out_off;
 	unsigned char *dev;
 	size_t bytes;
 	hipStream_t st;
@@ -76,7 +95,9 @@ struct ecg_queue {
 	pthread_cond_t cv_slot;		/* a slot became FREE or gained room */
 	pthread_cond_t cv_done;		/* completions (flush) */
 	pthread_cond_t cv_fin;		/* a slot reached S_DONE */
-	struct qslot slot[NSLOT];
+	int nslot;
+	uint32_t open_next;		/* where the next FREE-slot search starts */
+	struct qslot slot[NSLOT_MAX];
 	uint64_t submitted, completed, batches, flush_target;
 	int stop, worker_exited;
 	pthread_t worker;
@@ -132,7 +153,7 @@ static int slot_open(struct ecg_queue *q, struct qslot *s, int op, int k, int p,
 	s->pitch = pitch_of(C);
 	s->nerrs = nerrs;
 	ecg_gen_cauchy1(k, p, en);
-	if (op == OP_ENCODE) {
+	if (op == OP_ENCODE || op == OP_UPDATE) {
 		s->rows = p;
 		memcpy(s->coef, &en[k * k], (size_t)p * k);
 		for (j = 0; j < k; j++)
@@ -146,13 +167,18 @@ static int slot_open(struct ecg_queue *q, struct qslot *s, int op, int k, int p,
 			return rc;
 		s->rows = nerrs;
 	}
-	per = s->pitch * (uint64_t)(k + s->rows);
-	s->cap = (uint32_t)(q->slot_bytes / per);
+	s->nin = op == OP_UPDATE ? 1 : k;	/* staged input cells per request */
+	/* an update request also stages its vec_i byte (+64 B of alignment slack) */
+	per = s->pitch * (uint64_t)(s->nin + s->rows) + (op == OP_UPDATE ? 1 : 0);
+	s->cap = (uint32_t)((q->slot_bytes - 64) / per);
 	if (s->cap > q->attr.max_batch)
 		s->cap = q->attr.max_batch;
 	if (s->cap == 0)
 		return ecg_fail(-ECG_DER_REC2BIG, "queue: one stripe (%llu B) exceeds a slot",
 				(unsigned long long)per);
+	s->out_off = (size_t)s->pitch * s->nin * s->cap;
+	if (op == OP_UPDATE)
+		s->out_off += ((size_t)s->cap + 63) & ~(size_t)63;
 	s->reserved = 0;
 	s->filled = 0;
 	s->rc = 0;
@@ -163,7 +189,7 @@ static int slot_open(struct ecg_queue *q, struct qslot *s, int op, int k, int p,
 
 static void close_due_slots(struct ecg_queue *q, uint64_t t, int force)
 {
-	for (int i = 0; i < NSLOT; i++) {
+	for (int i = 0; i < q->nslot; i++) {
 		struct qslot *s = &q->slot[i];
 
 		if (s->state == S_FILLING && s->reserved > 0 &&
@@ -178,25 +204,35 @@ static void close_due_slots(struct ecg_queue *q, uint64_t t, int force)
 static void launch_slot(struct ecg_queue *q, struct qslot *s)
 {
 	const uint32_t n = s->reserved;
-	const uint64_t in_stride = s->pitch * (uint64_t)s->k;
+	const uint64_t in_stride = s->pitch * (uint64_t)s->nin;
 	const uint64_t out_stride = s->pitch * (uint64_t)s->rows;
-	unsigned char *dout = s->dev + (size_t)in_stride * s->cap;
+	const size_t sel_off = (size_t)in_stride * s->cap;	/* updates: vec_i bytes */
+	unsigned char *dout = s->dev + s->out_off;
 	int64_t soff[ECG_MAX_K], doff[ECG_MAX_P];
 	hipError_t e;
 	int j, rc;
 
+	(void)q;
+	ecg_trace_push("ecg:queue_batch");
+	e = hipSetDevice(s->ctx->device);
 	for (j = 0; j < s->k; j++)
 		soff[j] = (int64_t)(j * s->pitch);
 	for (j = 0; j < s->rows; j++)
 		doff[j] = (int64_t)(j * s->pitch);
-	e = ecg_stage_copy(s->dev, s->host, (size_t)in_stride * n, (size_t)s->pitch, hipMemcpyHostToDevice,
-			   s->st);
+	if (e == hipSuccess)
+		e = ecg_stage_copy(s->dev, s->host, (size_t)in_stride * n, (size_t)s->pitch,
+				   hipMemcpyHostToDevice, s->st);
+	if (e == hipSuccess && s->op == OP_UPDATE)
+		e = hipMemcpyAsync(s->dev + sel_off, s->host + sel_off, n, hipMemcpyHostToDevice, s->st);
 	rc = e == hipSuccess ? 0 : ecg_hip_fail(e, "queue H2D");
-	if (rc == 0)
-		rc = ecg_matmul(q->ctx, s->k, s->rows, s->coef, s->C, n, s->dev, soff, (int64_t)in_stride,
+	if (rc == 0 && s->op == OP_UPDATE)
+		rc = ecg_matmul_sel(s->ctx, s->k, s->rows, s->coef, s->C, n, s->dev, (int64_t)in_stride,
+				    s->dev + sel_off, dout, doff, (int64_t)out_stride, s->st);
+	else if (rc == 0)
+		rc = ecg_matmul(s->ctx, s->k, s->rows, s->coef, s->C, n, s->dev, soff, (int64_t)in_stride,
 				dout, doff, (int64_t)out_stride, 0, s->st);
 	if (rc == 0) {
-		e = ecg_stage_copy(s->host + (size_t)in_stride * s->cap, dout, (size_t)out_stride * n,
+		e = ecg_stage_copy(s->host + s->out_off, dout, (size_t)out_stride * n,
 				   (size_t)s->pitch, hipMemcpyDeviceToHost, s->st);
 		if (e == hipSuccess)
 			e = hipEventRecord(s->done, s->st);
@@ -206,20 +242,42 @@ static void launch_slot(struct ecg_queue *q, struct qslot *s)
 	s->rc = rc;
 	s->state = S_INFLIGHT;
 	q->batches++;
+	ecg_trace_pop();
 }
 
 /* One request's outputs back to its buffers, then its callback (lock NOT
  * held). */
+/* dst ^= src (n bytes, any alignment) */
+static void xor_into(unsigned char *dst, const unsigned char *a, const unsigned char *b, uint64_t n)
+{
+	uint64_t i = 0;
+
+	for (; i + 8 <= n; i += 8) {
+		uint64_t x, y;
+
+		memcpy(&x, a + i, 8);
+		memcpy(&y, b + i, 8);
+		x ^= y;
+		memcpy(dst + i, &x, 8);
+	}
+	for (; i < n; i++)
+		dst[i] = a[i] ^ b[i];
+}
+
 static void finish_req(struct qslot *s, uint32_t i)
 {
-	const uint64_t in_stride = s->pitch * (uint64_t)s->k;
 	const uint64_t out_stride = s->pitch * (uint64_t)s->rows;
-	const unsigned char *out = s->host + (size_t)in_stride * s->cap + i * out_stride;
+	const unsigned char *out = s->host + s->out_off + i * out_stride;
 	struct qreq *r = &s->reqs[i];
 
-	if (s->rc == 0)
+	ecg_trace_push("ecg:queue_complete");
+	if (s->rc == 0 && s->op == OP_UPDATE)	/* parity ^= coef[r][vec_i] * diff */
+		for (int j = 0; j < s->rows; j++)
+			xor_into(r->dst[j], r->dst[j], out + j * s->pitch, s->C);
+	else if (s->rc == 0)
 		for (int j = 0; j < s->rows; j++)
 			memcpy(r->dst[j], out + j * s->pitch, s->C);
+	ecg_trace_pop();
 	if (r->cb)
 		r->cb(r->arg, s->rc);
 }
@@ -236,7 +294,7 @@ static void *fin_main(void *argp)
 		struct qslot *s = NULL;
 		uint32_t i;
 
-		for (int j = 0; j < NSLOT && s == NULL; j++)
+		for (int j = 0; j < q->nslot && s == NULL; j++)
 			if (q->slot[j].state == S_DONE && q->slot[j].fin_next < q->slot[j].reserved)
 				s = &q->slot[j];
 		if (s == NULL) {
@@ -265,14 +323,13 @@ static void *worker_main(void *argp)
 {
 	struct ecg_queue *q = argp;
 
-	(void)hipSetDevice(q->ctx->device);
 	pthread_mutex_lock(&q->lock);
 	for (;;) {
 		int busy = 0, idle = 1;
 		uint64_t t = now_ns(), next = UINT64_MAX;
 
 		close_due_slots(q, t, q->stop || q->completed < q->flush_target);
-		for (int i = 0; i < NSLOT; i++) {
+		for (int i = 0; i < q->nslot; i++) {
 			struct qslot *s = &q->slot[i];
 
 			if (s->state == S_READY && s->filled == s->reserved) {
@@ -280,7 +337,7 @@ static void *worker_main(void *argp)
 				idle = 0;
 			}
 		}
-		for (int i = 0; i < NSLOT; i++) {
+		for (int i = 0; i < q->nslot; i++) {
 			struct qslot *s = &q->slot[i];
 
 			if (s->state == S_INFLIGHT) {
@@ -311,7 +368,7 @@ static void *worker_main(void *argp)
 		if (q->stop) {
 			int live = 0;
 
-			for (int i = 0; i < NSLOT; i++)
+			for (int i = 0; i < q->nslot; i++)
 				live += q->slot[i].state != S_FREE;
 			if (!live)
 				break;
@@ -334,21 +391,38 @@ static void *worker_main(void *argp)
 	return NULL;
 }
 
-int ecg_queue_create(ecg_ctx_t *ctx, const ecg_queue_attr_t *attr, ecg_queue_t **out)
+static void slot_free(struct qslot *s)
+{
+	if (s->ctx)
+		(void)hipSetDevice(s->ctx->device);
+	if (s->host)
+		(void)hipHostFree(s->host);
+	if (s->dev)
+		(void)hipFree(s->dev);
+	if (s->st)
+		(void)hipStreamDestroy(s->st);
+	if (s->done)
+		(void)hipEventDestroy(s->done);
+	free(s->reqs);
+}
+
+/* Slots round-robin over ctxs[nctx] (one context = one device). */
+static int queue_create(ecg_ctx_t *const *ctxs, int nctx, const ecg_queue_attr_t *attr,
+			ecg_queue_t **out)
 {
 	struct ecg_queue *q;
 	hipError_t e = hipSuccess;
-	int rc, i;
+	int i;
 
-	if (ctx == NULL || out == NULL)
-		return ecg_fail(-ECG_DER_INVAL, "queue_create: NULL argument");
-	rc = ecg_ctx_enter(ctx);
-	if (rc)
-		return rc;
 	q = calloc(1, sizeof(*q));
 	if (q == NULL)
 		return ecg_fail(-ECG_DER_NOMEM, "queue_create: calloc");
-	q->ctx = ctx;
+	q->ctx = ctxs[0];
+	q->nslot = nctx == 1 ? NSLOT_MIN : 2 * nctx;
+	if (q->nslot < NSLOT_MIN)
+		q->nslot = NSLOT_MIN;
+	if (q->nslot > NSLOT_MAX)
+		q->nslot = NSLOT_MAX;
 	if (attr)
 		q->attr = *attr;
 	if (q->attr.max_batch == 0)
@@ -362,23 +436,26 @@ int ecg_queue_create(ecg_ctx_t *ctx, const ecg_queue_attr_t *attr, ecg_queue_t *
 	q->slot_bytes = (size_t)pitch_of(q->attr.max_cell_bytes) * 10u * q->attr.max_batch;
 	if (q->slot_bytes > (128u << 20))
 		q->slot_bytes = 128u << 20;
-	if (q->slot_bytes < (size_t)pitch_of(q->attr.max_cell_bytes) * (ECG_MAX_K + ECG_MAX_P))
-		q->slot_bytes = (size_t)pitch_of(q->attr.max_cell_bytes) * (ECG_MAX_K + ECG_MAX_P);
+	if (q->slot_bytes < (size_t)pitch_of(q->attr.max_cell_bytes) * (ECG_MAX_K + ECG_MAX_P) + 64)
+		q->slot_bytes = (size_t)pitch_of(q->attr.max_cell_bytes) * (ECG_MAX_K + ECG_MAX_P) + 64;
 	pthread_mutex_init(&q->lock, NULL);
 	pthread_cond_init(&q->cv_work, NULL);
 	pthread_cond_init(&q->cv_slot, NULL);
 	pthread_cond_init(&q->cv_done, NULL);
 	pthread_cond_init(&q->cv_fin, NULL);
-	for (i = 0; i < NSLOT && e == hipSuccess; i++) {
+	for (i = 0; i < q->nslot && e == hipSuccess; i++) {
 		struct qslot *s = &q->slot[i];
 
+		s->ctx = ctxs[i % nctx];
 		s->reqs = calloc(q->attr.max_batch, sizeof(*s->reqs));
 		if (s->reqs == NULL) {
 			e = hipErrorOutOfMemory;
 			break;
 		}
 		s->bytes = q->slot_bytes;
-		e = hipHostMalloc((void **)&s->host, s->bytes, hipHostMallocDefault);
+		e = hipSetDevice(s->ctx->device);
+		if (e == hipSuccess)
+			e = hipHostMalloc((void **)&s->host, s->bytes, hipHostMallocDefault);
 		if (e == hipSuccess)
 			e = hipMalloc((void **)&s->dev, s->bytes);
 		if (e == hipSuccess)
@@ -403,24 +480,37 @@ int ecg_queue_create(ecg_ctx_t *ctx, const ecg_queue_attr_t *attr, ecg_queue_t *
 			pthread_join(q->fin[i], NULL);
 	}
 	if (e != hipSuccess) {
-		for (i = 0; i < NSLOT; i++) {
-			struct qslot *s = &q->slot[i];
-
-			if (s->host)
-				(void)hipHostFree(s->host);
-			if (s->dev)
-				(void)hipFree(s->dev);
-			if (s->st)
-				(void)hipStreamDestroy(s->st);
-			if (s->done)
-				(void)hipEventDestroy(s->done);
-			free(s->reqs);
-		}
+		for (i = 0; i < q->nslot; i++)
+			slot_free(&q->slot[i]);
 		free(q);
 		return ecg_hip_fail(e, "queue_create");
 	}
 	*out = q;
 	return 0;
+}
+
+int ecg_queue_create(ecg_ctx_t *ctx, const ecg_queue_attr_t *attr, ecg_queue_t **out)
+{
+	int rc;
+
+	if (ctx == NULL || out == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "queue_create: NULL argument");
+	rc = ecg_ctx_enter(ctx);
+	if (rc)
+		return rc;
+	return queue_create(&ctx, 1, attr, out);
+}
+
+int ecg_queue_create_multi(ecg_multi_t *m, const ecg_queue_attr_t *attr, ecg_queue_t **out)
+{
+	ecg_ctx_t *ctxs[ECG_MULTI_MAX];
+	int i, n = ecg_multi_count(m);
+
+	if (m == NULL || out == NULL || n < 1)
+		return ecg_fail(-ECG_DER_INVAL, "queue_create_multi: bad argument");
+	for (i = 0; i < n; i++)
+		ctxs[i] = ecg_multi_ctx(m, i);
+	return queue_create(ctxs, n, attr, out);
 }
 
 void ecg_queue_destroy(ecg_queue_t *q)
@@ -435,16 +525,8 @@ void ecg_queue_destroy(ecg_queue_t *q)
 	pthread_join(q->worker, NULL);
 	for (int i = 0; i < q->nfin; i++)
 		pthread_join(q->fin[i], NULL);
-	(void)hipSetDevice(q->ctx->device);
-	for (int i = 0; i < NSLOT; i++) {
-		struct qslot *s = &q->slot[i];
-
-		(void)hipHostFree(s->host);
-		(void)hipFree(s->dev);
-		(void)hipStreamDestroy(s->st);
-		(void)hipEventDestroy(s->done);
-		free(s->reqs);
-	}
+	for (int i = 0; i < q->nslot; i++)
+		slot_free(&q->slot[i]);
 	pthread_cond_destroy(&q->cv_work);
 	pthread_cond_destroy(&q->cv_slot);
 	pthread_cond_destroy(&q->cv_done);
@@ -457,7 +539,7 @@ void ecg_queue_destroy(ecg_queue_t *q)
  * copy the inputs in without the lock, then publish. */
 static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const uint32_t *err,
 		  int nerrs, unsigned char *const *src, unsigned char *stripe,
-		  unsigned char *const *dst, ecg_done_cb_t cb, void *arg)
+		  unsigned char *const *dst, int vec_i, ecg_done_cb_t cb, void *arg)
 {
 	struct qslot *s = NULL;
 	uint32_t idx;
@@ -469,18 +551,23 @@ static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const u
 			pthread_mutex_unlock(&q->lock);
 			return ecg_fail(-ECG_DER_INVAL, "queue is being destroyed");
 		}
-		for (i = 0; i < NSLOT && s == NULL; i++)
+		for (i = 0; i < q->nslot && s == NULL; i++)
 			if (slot_matches(&q->slot[i], op, k, p, C, err, nerrs))
 				s = &q->slot[i];
-		for (i = 0; i < NSLOT && s == NULL; i++) {
-			if (q->slot[i].state == S_FREE) {
-				rc = slot_open(q, &q->slot[i], op, k, p, C, err, nerrs);
+		/* open FREE slots from a rotating start: batches spread over the
+		 * devices of a multi-device queue */
+		for (i = 0; i < q->nslot && s == NULL; i++) {
+			struct qslot *f = &q->slot[(q->open_next + (uint32_t)i) % (uint32_t)q->nslot];
+
+			if (f->state == S_FREE) {
+				rc = slot_open(q, f, op, k, p, C, err, nerrs);
 				if (rc) {
-					q->slot[i].state = S_FREE;
+					f->state = S_FREE;
 					pthread_mutex_unlock(&q->lock);
 					return rc;
 				}
-				s = &q->slot[i];
+				s = f;
+				q->open_next = (uint32_t)(s - q->slot) + 1;
 			}
 		}
 		if (s == NULL) {
@@ -496,7 +583,7 @@ static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const u
 
 	{
 		struct qreq *r = &s->reqs[idx];
-		unsigned char *in = s->host + (size_t)idx * s->pitch * (uint64_t)k;
+		unsigned char *in = s->host + (size_t)idx * s->pitch * (uint64_t)s->nin;
 
 		r->op = op;
 		r->k = k;
@@ -505,14 +592,18 @@ static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const u
 		r->nerrs = nerrs;
 		r->cb = cb;
 		r->arg = arg;
-		for (i = 0; i < k; i++) {
+		if (op == OP_UPDATE) {		/* the xor_gen: diff = old ^ new */
+			xor_into(in, src[0], src[1], C);
+			s->host[(size_t)s->pitch * s->nin * s->cap + idx] = (unsigned char)vec_i;
+		}
+		for (i = 0; op != OP_UPDATE && i < k; i++) {
 			const unsigned char *from = op == OP_ENCODE ? src[i]
 					: stripe + (uint64_t)s->dec_idx[i] * C;
 
 			memcpy(in + (uint64_t)i * s->pitch, from, C);
 		}
 		for (i = 0; i < s->rows; i++)
-			r->dst[i] = op == OP_ENCODE ? dst[i] : stripe + (uint64_t)s->out_idx[i] * C;
+			r->dst[i] = op != OP_RECOVER ? dst[i] : stripe + (uint64_t)s->out_idx[i] * C;
 	}
 
 	pthread_mutex_lock(&q->lock);
@@ -528,7 +619,7 @@ int ecg_queue_encode(ecg_queue_t *q, int k, int p, uint64_t C, unsigned char *co
 	if (q == NULL || data == NULL || parity == NULL || k < 1 || k > ECG_MAX_K || p < 1 ||
 	    p > ECG_MAX_P || C == 0)
 		return ecg_fail(-ECG_DER_INVAL, "queue_encode: bad arguments");
-	return submit(q, OP_ENCODE, k, p, C, NULL, 0, data, NULL, parity, cb, arg);
+	return submit(q, OP_ENCODE, k, p, C, NULL, 0, data, NULL, parity, 0, cb, arg);
 }
 
 int ecg_queue_recover(ecg_queue_t *q, int k, int p, uint64_t C, unsigned char *stripe,
@@ -549,7 +640,22 @@ int ecg_queue_recover(ecg_queue_t *q, int k, int p, uint64_t C, unsigned char *s
 				return ecg_fail(-ECG_DER_INVAL, "queue_recover: duplicate cell %u",
 						err_list[i]);
 	}
-	return submit(q, OP_RECOVER, k, p, C, err_list, nerrs, NULL, stripe, NULL, cb, arg);
+	return submit(q, OP_RECOVER, k, p, C, err_list, nerrs, NULL, stripe, NULL, 0, cb, arg);
+}
+
+int ecg_queue_update(ecg_queue_t *q, int k, int p, uint64_t C, int vec_i, const unsigned char *old_cell,
+		     const unsigned char *new_cell, unsigned char *const *parity, ecg_done_cb_t cb,
+		     void *arg)
+{
+	unsigned char *src[2];
+
+	/* one launch stages the tables of every column: k <= ECG_KMAX_K */
+	if (q == NULL || old_cell == NULL || new_cell == NULL || parity == NULL || k < 1 ||
+	    k > ECG_KMAX_K || p < 1 || p > ECG_MAX_P || C == 0 || vec_i < 0 || vec_i >= k)
+		return ecg_fail(-ECG_DER_INVAL, "queue_update: bad arguments");
+	src[0] = (unsigned char *)old_cell;
+	src[1] = (unsigned char *)new_cell;
+	return submit(q, OP_UPDATE, k, p, C, NULL, 0, src, NULL, parity, vec_i, cb, arg);
 }
 
 int ecg_queue_flush(ecg_queue_t *q)

@@ -274,6 +274,58 @@ ecg_mm_kernel(const ecg_mm_params_t P)
 	}
 }
 
+// One-cell product with a per-stripe coefficient column (the batching
+// facade's aggregation updates: ec_encode_data_update with vec_i differing
+// from stripe to stripe, ref:src/object/srv_ec_aggregate.c:1099-1101):
+//   dst[s][r] = coef[r][sel[s]] * src[s]        r < rows, sel[s] < ncols
+// The tables of every (row, column) pair are staged in LDS once per block;
+// the stripe's column picks the table base (a wave-uniform scalar load), so
+// the arithmetic and memory shape are exactly ecg_mm_kernel's with k = 1.
+template <int R>
+__global__ void __launch_bounds__(BLOCK)
+ecg_mm_sel_kernel(const ecg_mm_params_t P, const uint8_t *__restrict__ sel, uint32_t ncols)
+{
+	constexpr int RM = R ? R : ECG_KMAX_R;
+	constexpr int T2V = (RM + 3) / 4;
+	constexpr int PER_J = RM + T2V;
+	__shared__ u32x4 s_tbl[ECG_KMAX_K * PER_J];
+	const int rows = R ? R : (int)P.rows;
+	const uint64_t C = P.cell_bytes;
+	const uint32_t nchunk = (uint32_t)((C + CHUNK_BYTES - 1) / CHUNK_BYTES);
+	const uint32_t lo = threadIdx.x * 16u;
+
+	for (int i = threadIdx.x; i < ECG_KMAX_K * RM; i += BLOCK) {
+		const int j = i / RM, r = i % RM;
+		if (j < (int)ncols && r < rows) {
+			const ecg_ptbl_t &t = P.tbl[r][j];
+			s_tbl[j * PER_J + r] = (u32x4){t.t0lo, t.t0hi, t.t1lo, t.t1hi};
+			reinterpret_cast<uint32_t *>(&s_tbl[j * PER_J + RM])[r] = t.t2;
+		}
+	}
+	__syncthreads();
+
+	for (uint32_t s = blockIdx.y; s < P.nstripes; s += gridDim.y) {
+		const uint32_t j = sel[s];
+
+		if (j >= ncols)		// host-validated; never index past the tables
+			continue;
+		for (uint32_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
+			const uint64_t cbase = (uint64_t)ch * CHUNK_BYTES;
+			uint32_t z = 0;
+
+			asm volatile("" : "+v"(z));
+			const u32x4 *tb = s_tbl + j * PER_J + z;
+
+			if (cbase + CHUNK_BYTES <= C)
+				mm_item<1, RM, false, false>(P, tb, 1, rows, s, cbase, lo);
+			else if (cbase + lo + 16 <= C)
+				mm_item<1, RM, false, false>(P, tb, 1, rows, s, cbase, lo);
+			else if (cbase + lo < C)
+				mm_tail<RM, false, false>(P, tb, 1, rows, s, cbase + lo, (int)(C - cbase - lo));
+		}
+	}
+}
+
 // Work item `it` of the fused kernel -> chunk c, sub-chunk h, its columns
 // [col0, col1) and the row of Q.kh its threads multiply by (ecg_kabi.h).
 __device__ __forceinline__ void mmcs_item(const ecg_mmcs_params_t &Q, uint32_t it, uint32_t &c, uint32_t &col0,
@@ -683,6 +735,8 @@ static const pentry g_pkernels[] = {
 #define KID_PTR 600u		/* pointer-table kernel ids: KID_PTR + index */
 #define KID_PTR_BYTE (KID_PTR + N_PKERNELS)
 
+#define KID_SEL 700u		/* per-stripe column kernels: <1>, <2>, <0> */
+
 #define KID_BYTE N_KERNELS
 #define KID_COPY (N_KERNELS + 1)
 #define KID_READ (N_KERNELS + 2)
@@ -726,6 +780,12 @@ extern "C" const char *ecg_k_kernel_name(uint32_t id)
 		return "ecg_mm_ptr_byte_kernel";
 	if (id == ECG_KID_COPY_SEGS)
 		return "ecg_copy_segs_kernel";
+	if (id == KID_SEL)
+		return "ecg_mm_sel_kernel<1>";
+	if (id == KID_SEL + 1)
+		return "ecg_mm_sel_kernel<2>";
+	if (id == KID_SEL + 2)
+		return "ecg_mm_sel_kernel<0>";
 
 	return "?";
 }
@@ -850,6 +910,34 @@ extern "C" int ecg_k_launch_matmul_csum(const ecg_mm_params_t *p, const ecg_mmcs
 	hipLaunchKernelGGL(g_cskernels[id].fn, dim3(gx, gy), dim3(BLOCK), 0, (hipStream_t)stream, *p, *q);
 	if (kernel_id)
 		*kernel_id = KID_FUSED + id;
+	return (int)hipGetLastError();
+}
+
+extern "C" int ecg_k_launch_matmul_sel(const ecg_mm_params_t *p, const uint8_t *sel_dev, uint32_t ncols,
+				      void *stream, uint32_t *kernel_id)
+{
+	const uint64_t nchunk = (p->cell_bytes + CHUNK_BYTES - 1) / CHUNK_BYTES;
+
+	if (p->nstripes == 0 || p->cell_bytes == 0 || p->rows == 0)
+		return (int)hipSuccess;
+	if (!aligned16(p) || p->k != 1 || p->accumulate || p->diff || ncols == 0 || ncols > ECG_KMAX_K ||
+	    p->rows > ECG_KMAX_R)
+		return (int)hipErrorInvalidValue;
+	uint32_t gx = (uint32_t)(nchunk < 65535 ? nchunk : 65535);
+	uint32_t gy = p->nstripes < 65535 ? p->nstripes : 65535;
+	// the DAOS classes' p = 1, 2 specialised; 3..8 parity rows runtime-shaped
+	const uint32_t v = p->rows == 1 ? 0 : p->rows == 2 ? 1 : 2;
+	if (v == 0)
+		hipLaunchKernelGGL(ecg_mm_sel_kernel<1>, dim3(gx, gy), dim3(BLOCK), 0, (hipStream_t)stream, *p,
+				   sel_dev, ncols);
+	else if (v == 1)
+		hipLaunchKernelGGL(ecg_mm_sel_kernel<2>, dim3(gx, gy), dim3(BLOCK), 0, (hipStream_t)stream, *p,
+				   sel_dev, ncols);
+	else
+		hipLaunchKernelGGL(ecg_mm_sel_kernel<0>, dim3(gx, gy), dim3(BLOCK), 0, (hipStream_t)stream, *p,
+				   sel_dev, ncols);
+	if (kernel_id)
+		*kernel_id = KID_SEL + v;
 	return (int)hipGetLastError();
 }
 

@@ -36,6 +36,7 @@ _SIGS = [
     ("ecg_ctx_destroy", None, [vp]),
     ("ecg_ctx_device", C.c_int, [vp]),
     ("ecg_ctx_stream", vp, [vp]),
+    ("ecg_device_pci_bus_id", C.c_int, [C.c_int, C.c_char_p, C.c_int]),
     ("ecg_strerror", C.c_char_p, []),
     ("ecg_last_kernel", C.c_char_p, []),
     ("ecg_gf_mul", C.c_ubyte, [C.c_ubyte, C.c_ubyte]),
@@ -58,6 +59,8 @@ _SIGS = [
     ("ecg_queue_destroy", None, [vp]),
     ("ecg_queue_encode", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.POINTER(u8p), C.POINTER(u8p), vp, vp]),
     ("ecg_queue_recover", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, u8p, u32p, C.c_int, vp, vp]),
+    ("ecg_queue_update", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_int, u8p, u8p, C.POINTER(u8p), vp, vp]),
+    ("ecg_queue_create_multi", C.c_int, [vp, vp, C.POINTER(vp)]),
     ("ecg_queue_flush", C.c_int, [vp]),
     ("ecg_queue_stats", C.c_int, [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("ecg_dev_alloc", C.c_int, [vp, C.c_size_t, C.POINTER(vp)]),
@@ -76,6 +79,20 @@ _SIGS = [
     ("ecg_device_sync", C.c_int, [vp]),
     ("ecg_dev_copy_kernel", C.c_int, [vp, vp, vp, C.c_size_t, C.c_int, vp]),
     ("ecg_set_launch", C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_uint32]),
+    # multi-device sharder (ecg_multi.h)
+    ("ecg_multi_create", C.c_int, [C.POINTER(C.c_int), C.c_int, C.POINTER(vp)]),
+    ("ecg_multi_destroy", None, [vp]),
+    ("ecg_multi_count", C.c_int, [vp]),
+    ("ecg_multi_ctx", vp, [vp, C.c_int]),
+    ("ecg_multi_range", C.c_int, [vp, C.c_uint32, C.c_int, u32p, u32p]),
+    ("ecg_multi_encode", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, u32p, C.POINTER(vp), C.c_int64,
+                                   C.POINTER(vp), C.c_int64, C.c_int64, C.c_uint]),
+    ("ecg_multi_recover", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, u32p, C.POINTER(vp), C.c_int64, u32p,
+                                    C.c_int, C.c_uint]),
+    ("ecg_multi_sync", C.c_int, [vp]),
+    ("ecg_multi_encode_host", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, vp, vp, C.c_uint32]),
+    ("ecg_multi_recover_host", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, vp, u32p, C.c_int,
+                                         C.c_uint32]),
     # ISA-L drop-in (ecg_isal.h)
     ("ec_init_tables", None, [C.c_int, C.c_int, u8p, u8p]),
     ("ec_encode_data", None, [C.c_int, C.c_int, C.c_int, u8p, C.POINTER(u8p), C.POINTER(u8p)]),
@@ -137,6 +154,7 @@ _SIGS = [
 ]
 
 HASH_CRC16, HASH_CRC32, HASH_CRC64, HASH_ADLER32 = 1, 2, 3, 7
+MULTI_ASYNC = 1
 
 EXPORTED = [n for n, _, _ in _SIGS]
 
@@ -231,6 +249,25 @@ def last_kernel() -> str:
     return lib().ecg_last_kernel().decode()
 
 
+def pci_bus_id(device: int) -> str:
+    buf = C.create_string_buffer(64)
+    _chk(lib().ecg_device_pci_bus_id(device, buf, 64), "pci_bus_id")
+    return buf.value.decode()
+
+
+def _host_array(a: np.ndarray, nbytes: int, what: str, write: bool = True) -> int:
+    """Address of a host array the C side reads (or writes) `nbytes` of:
+    uint8, C-contiguous, writeable when written, large enough -- anything
+    else raises instead of letting native code run past it."""
+    if not isinstance(a, np.ndarray) or a.dtype != np.uint8:
+        raise ValueError(f"{what}: need a numpy uint8 array")
+    if not a.flags["C_CONTIGUOUS"] or (write and not a.flags["WRITEABLE"]):
+        raise ValueError(f"{what}: array must be C-contiguous" + (" and writeable" if write else ""))
+    if a.nbytes < nbytes:
+        raise ValueError(f"{what}: {a.nbytes} bytes < {nbytes} required")
+    return a.ctypes.data
+
+
 # ---------------------------------------------------------------- host math
 def gf_mul(a: int, b: int) -> int:
     return lib().ecg_gf_mul(a, b)
@@ -317,16 +354,20 @@ class HostBuffer:
 class Context:
     """One per device; mirrors ecg_ctx_t."""
 
-    def __init__(self, device: int = 0):
-        h = vp()
-        _chk(lib().ecg_ctx_create(device, C.byref(h)), f"ctx_create(device={device})")
-        self.h = h.value
-        self.device = device
+    def __init__(self, device: int = 0, _handle: int | None = None):
+        self.owned = _handle is None
+        if _handle is None:
+            h = vp()
+            _chk(lib().ecg_ctx_create(device, C.byref(h)), f"ctx_create(device={device})")
+            self.h = h.value
+        else:
+            self.h = _handle
+        self.device = lib().ecg_ctx_device(self.h)
 
     def close(self):
-        if self.h:
+        if self.h and self.owned:
             lib().ecg_ctx_destroy(self.h)
-            self.h = None
+        self.h = None
 
     # plumbing
     def alloc(self, nbytes: int) -> DeviceBuffer:
@@ -427,13 +468,15 @@ class Context:
 
     def encode_host(self, k: int, p: int, cell_bytes: int, nstripes: int, data: np.ndarray, parity: np.ndarray,
                     chunk: int = 0):
-        _chk(lib().ecg_encode_host(self.h, k, p, cell_bytes, nstripes, data.ctypes.data, parity.ctypes.data,
-                                   chunk), "encode_host")
+        dp = _host_array(data, nstripes * k * cell_bytes, "encode_host data", write=False)
+        pp = _host_array(parity, nstripes * p * cell_bytes, "encode_host parity")
+        _chk(lib().ecg_encode_host(self.h, k, p, cell_bytes, nstripes, dp, pp, chunk), "encode_host")
 
     def recover_host(self, k: int, p: int, cell_bytes: int, nstripes: int, stripes: np.ndarray,
                      err_list: Sequence[int], chunk: int = 0):
-        _chk(lib().ecg_recover_host(self.h, k, p, cell_bytes, nstripes, stripes.ctypes.data, _u32(err_list),
-                                    len(err_list), chunk), "recover_host")
+        sp = _host_array(stripes, nstripes * (k + p) * cell_bytes, "recover_host stripes")
+        _chk(lib().ecg_recover_host(self.h, k, p, cell_bytes, nstripes, sp, _u32(err_list), len(err_list), chunk),
+             "recover_host")
 
     def matmul_host(self, coef: np.ndarray, src: Sequence[np.ndarray], dst: Sequence[np.ndarray], flags: int = 0):
         coef = np.ascontiguousarray(coef, dtype=np.uint8)
@@ -442,6 +485,61 @@ class Context:
         sp = (u8p * k)(*[_u8(s) for s in src])
         dp = (u8p * rows)(*[_u8(d) for d in dst])
         _chk(lib().ecg_matmul_host(self.h, n, k, rows, _u8(coef), sp, dp, flags), "matmul_host")
+
+
+class Multi:
+    """ecg_multi_t: stripe ranges sharded over devices in one process, one
+    host thread + context per shard (include/ecg_multi.h).  devices may
+    repeat a device; None = $ECG_DEVICES or every device."""
+
+    def __init__(self, devices: Sequence[int] | None = None):
+        h = vp()
+        arr = (C.c_int * len(devices))(*devices) if devices else None
+        _chk(lib().ecg_multi_create(arr, len(devices) if devices else 0, C.byref(h)), "multi_create")
+        self.h = h.value
+        self.n = lib().ecg_multi_count(self.h)
+        self.ctxs = [Context(_handle=lib().ecg_multi_ctx(self.h, i)) for i in range(self.n)]
+
+    def range(self, nstripes: int, i: int):
+        f, c = C.c_uint32(), C.c_uint32()
+        _chk(lib().ecg_multi_range(self.h, nstripes, i, C.byref(f), C.byref(c)), "multi_range")
+        return f.value, c.value
+
+    def encode(self, k: int, p: int, cell_bytes: int, nstripes: Sequence[int], data: Sequence[int],
+               data_stripe_stride: int, parity: Sequence[int], parity_cell_stride: int, parity_stripe_stride: int,
+               flags: int = 0):
+        n = self.n
+        _chk(lib().ecg_multi_encode(self.h, k, p, cell_bytes, _u32(nstripes), (vp * n)(*data), data_stripe_stride,
+                                    (vp * n)(*parity), parity_cell_stride, parity_stripe_stride, flags),
+             "multi_encode")
+
+    def recover(self, k: int, p: int, cell_bytes: int, nstripes: Sequence[int], stripes: Sequence[int],
+                stripe_stride: int, err_list: Sequence[int], flags: int = 0):
+        n = self.n
+        _chk(lib().ecg_multi_recover(self.h, k, p, cell_bytes, _u32(nstripes), (vp * n)(*stripes), stripe_stride,
+                                     _u32(err_list), len(err_list), flags), "multi_recover")
+
+    def sync(self):
+        _chk(lib().ecg_multi_sync(self.h), "multi_sync")
+
+    def encode_host(self, k: int, p: int, cell_bytes: int, nstripes: int, data: np.ndarray, parity: np.ndarray,
+                    chunk: int = 0):
+        dp = _host_array(data, nstripes * k * cell_bytes, "multi_encode_host data", write=False)
+        pp = _host_array(parity, nstripes * p * cell_bytes, "multi_encode_host parity")
+        _chk(lib().ecg_multi_encode_host(self.h, k, p, cell_bytes, nstripes, dp, pp, chunk), "multi_encode_host")
+
+    def recover_host(self, k: int, p: int, cell_bytes: int, nstripes: int, stripes: np.ndarray,
+                     err_list: Sequence[int], chunk: int = 0):
+        sp = _host_array(stripes, nstripes * (k + p) * cell_bytes, "multi_recover_host stripes")
+        _chk(lib().ecg_multi_recover_host(self.h, k, p, cell_bytes, nstripes, sp, _u32(err_list), len(err_list),
+                                          chunk), "multi_recover_host")
+
+    def close(self):
+        if self.h:
+            for c in self.ctxs:
+                c.close()
+            lib().ecg_multi_destroy(self.h)
+            self.h = None
 
 
 class QueueAttr(C.Structure):
@@ -456,11 +554,15 @@ class Queue:
     Completion is reported through a C callback; this wrapper records rc per
     request id (callbacks run on the queue's worker thread)."""
 
-    def __init__(self, ctx: Context, max_batch: int = 0, max_wait_us: int = 0, max_cell_bytes: int = 0):
+    def __init__(self, ctx, max_batch: int = 0, max_wait_us: int = 0, max_cell_bytes: int = 0):
+        """ctx: a Context, or a Multi (slots spread over its devices)."""
         self.ctx = ctx
         h = vp()
         attr = QueueAttr(max_batch, max_wait_us, max_cell_bytes)
-        _chk(lib().ecg_queue_create(ctx.h, C.byref(attr), C.byref(h)), "queue_create")
+        if isinstance(ctx, Multi):
+            _chk(lib().ecg_queue_create_multi(ctx.h, C.byref(attr), C.byref(h)), "queue_create_multi")
+        else:
+            _chk(lib().ecg_queue_create(ctx.h, C.byref(attr), C.byref(h)), "queue_create")
         self.h = h.value
         self.done = {}
         self._keep = {}
@@ -483,6 +585,14 @@ class Queue:
         _chk(lib().ecg_queue_recover(self.h, k, p, C_, _u8(stripe), _u32(err_list), len(err_list), self._cb,
                                      rid + 1),
              "queue_recover")
+
+    def update(self, rid: int, k: int, p: int, vec_i: int, old: np.ndarray, new: np.ndarray, parity):
+        """parity[r] ^= coef[r][vec_i] * (old ^ new), in place at completion."""
+        C_ = old.shape[0]
+        dp = (u8p * p)(*[_u8(d) for d in parity])
+        self._keep[rid] = (old, new, parity)
+        _chk(lib().ecg_queue_update(self.h, k, p, C_, vec_i, _u8(old), _u8(new), dp, self._cb, rid + 1),
+             "queue_update")
 
     def flush(self):
         _chk(lib().ecg_queue_flush(self.h), "queue_flush")

@@ -55,6 +55,9 @@ int ecg_device_count(void);
 int ecg_ctx_create(int device, ecg_ctx_t **ctx);
 void ecg_ctx_destroy(ecg_ctx_t *ctx);
 int ecg_ctx_device(const ecg_ctx_t *ctx);
+/* PCI bus id ("0000:c1:00.0") of a visible device: tells ranks or shards
+ * that landed on the same physical GPU apart. */
+int ecg_device_pci_bus_id(int device, char *buf, int len);
 /* The context's default stream (used when a call passes stream == NULL). */
 void *ecg_ctx_stream(ecg_ctx_t *ctx);
 const char *ecg_strerror(void);
@@ -181,6 +184,15 @@ int ecg_queue_encode(ecg_queue_t *q, int k, int p, uint64_t cell_bytes,
  * logical cell order; err_list holds the erased logical cells. */
 int ecg_queue_recover(ecg_queue_t *q, int k, int p, uint64_t cell_bytes, unsigned char *stripe,
 		      const uint32_t *err_list, int nerrs, ecg_done_cb_t cb, void *arg);
+/* Aggregation delta update of one stripe's parity (agg_update_parity:
+ * xor_gen(old, new -> diff) then ec_encode_data_update(vec_i), ref:src/object/
+ * srv_ec_aggregate.c:1086-1102):  parity[r] ^= coef[r][vec_i] * (old ^ new)
+ * for the p parity cells (host memory, updated in place when the callback
+ * runs).  Requests of one (k, p, cell size) batch together whatever their
+ * vec_i.  k <= 16. */
+int ecg_queue_update(ecg_queue_t *q, int k, int p, uint64_t cell_bytes, int vec_i,
+		     const unsigned char *old_cell, const unsigned char *new_cell,
+		     unsigned char *const *parity, ecg_done_cb_t cb, void *arg);
 /* Block until every request submitted before the call has completed. */
 int ecg_queue_flush(ecg_queue_t *q);
 /* Counters: requests completed, device batches launched. */

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
-HEADERS = ["include/ecg.h", "include/ecg_isal.h", "include/ecg_daos.h", "include/ecg_csum.h"]
+HEADERS = ["include/ecg.h", "include/ecg_isal.h", "include/ecg_daos.h", "include/ecg_csum.h", "include/ecg_multi.h"]
 
 
 def declared_functions():
@@ -163,3 +163,33 @@ def test_daos_codec_table(ecglib, oracle):
     assert not L.ecg_obj_ec_codec_get((1 << 24) | 1)       # replicated class: not EC
     L.ecg_obj_ec_codec_fini()
     assert not L.ecg_obj_ec_codec_get((37 << 24) | 1)
+
+
+def test_isal_rejects_foreign_table_layout(ecglib):
+    """ec_encode_data reads coefficients out of ec_init_tables' 32-byte
+    layout; tables in any other layout (a libisal GFNI build's, SURVEY
+    App. A.4) must abort loudly before touching a device, never produce
+    silently wrong parity."""
+    import sys
+
+    code = (
+        "import sys, numpy as np; sys.path.insert(0, %r)\n"
+        "from daos_amd import ecg\n"
+        "k, p, C = 4, 2, 64\n"
+        "tb = np.random.default_rng(1).integers(1, 256, k * p * 32, dtype=np.uint8)\n"
+        "d = [np.zeros(C, np.uint8) for _ in range(k)]; o = [np.zeros(C, np.uint8) for _ in range(p)]\n"
+        "ecg.isal_encode_data(tb, k, p, d, o)\n" % ROOT)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "32-byte layout" in r.stderr
+
+
+def test_host_array_checks(ecglib):
+    a = np.zeros(100, dtype=np.uint8)
+    assert ecglib._host_array(a, 100, "x") == a.ctypes.data
+    with pytest.raises(ValueError):
+        ecglib._host_array(a, 101, "x")
+    with pytest.raises(ValueError):
+        ecglib._host_array(np.zeros(100, dtype=np.uint16), 10, "x")
+    with pytest.raises(ValueError):
+        ecglib._host_array(np.zeros((10, 10), dtype=np.uint8).T, 10, "x")

@@ -62,7 +62,7 @@ def test_weak_scaling_accounting():
     assert wl.alg_bytes("enc") == wl.alg_bytes("dec") == 6 * (1 << 20) * 1024
     wl.k, wl.p, wl.ops = 16, 2, ("enc",)
     assert wl.user_bytes_per_step() == 16 * (1 << 20) * 1024
-    assert set(bench.WORKLOADS) == {"enc_dec_4p2", "dec_8p2", "enc_16p2_strong", "rebuild_stream_8p2"}
+    assert set(bench.WORKLOADS) == {"enc_dec_4p2", "dec_8p2", "enc_8p2", "enc_16p2_strong", "rebuild_stream_8p2"}
     assert bench.WORKLOADS["enc_dec_4p2"][:4] == (4, 2, 1 << 20, 1024)      # BASELINE configs[1]
 
 
@@ -79,3 +79,39 @@ def test_host_stream_accounting():
     assert wl.h2d_bytes_per_step() == 2 * 8 * (1 << 20) * 64
     assert wl.d2h_bytes_per_step() == (2 + 2) * (1 << 20) * 64
     assert bench.WORKLOADS["rebuild_stream_8p2"][:2] == (8, 2)
+
+
+def _bench_env():
+    env = dict(os.environ)
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(v, None)
+    return env
+
+
+def test_bench_gpus_n_spawns_ranks():
+    """`bench.py --gpus 2` with no launcher in the environment starts two
+    rank processes itself (gloo rendezvous on 127.0.0.1) and rank 0 prints
+    ONE aggregated line: max-over-ranks time (rank 1 sleeps twice as long)
+    and both ranks listed.  --rehearse replaces the GPU work with sleeps."""
+    import json
+
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20",
+                        "--rehearse"], env=_bench_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["rehearsal"] is True and d["value"] is None
+    assert d["n_ranks"] == 2
+    assert sorted(x["rank"] for x in d["ranks"]) == [0, 1]
+    assert len({x["pid"] for x in d["ranks"]}) == 2
+    assert d["ms_per_step"] >= 2.0          # the slower rank (2 ms steps) sets the time
+
+
+def test_bench_world_mismatch_refused():
+    """Under an external launcher, --gpus must equal WORLD_SIZE (a driver
+    that launches N ranks reports N, never silently 1)."""
+    env = dict(_bench_env(), WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rehearse"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "--gpus 2" in (r.stderr + r.stdout)

@@ -1,0 +1,195 @@
+"""Multi-device sharding inside the library (include/ecg_multi.h) and the
+batching facade's aggregation updates, on the GPU box.
+
+A one-GPU box runs every shard on device 0 (the device list {0,0,0,0}): each
+shard still has its own host thread, context, streams and staging, so the
+sharding, range split and completion logic are exercised exactly as on 8
+GPUs; results must be identical to one launch over all stripes and to the
+oracle.  Stripes are independent at every reference call site
+(ref:src/object/cli_ec.c:627-659, ref:src/object/srv_obj_migrate.c:1116-1177).
+"""
+import os
+import subprocess
+import sys
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+
+
+def rand(shape, seed):
+    return np.random.default_rng(seed).integers(0, 256, shape, dtype=np.uint8)
+
+
+@pytest.fixture
+def multi4(ecglib):
+    m = ecglib.Multi([0, 0, 0, 0])
+    yield m
+    m.close()
+
+
+def test_multi_ranges_cover_batch(multi4):
+    for S in (0, 1, 3, 4, 37, 1024):
+        spans = [multi4.range(S, i) for i in range(4)]
+        assert spans[0][0] == 0
+        for (f0, c0), (f1, _) in zip(spans, spans[1:]):
+            assert f0 + c0 == f1
+        assert sum(c for _, c in spans) == S
+        assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
+
+
+def test_multi_device_resident_matches_one_launch(ecglib, ctx, oracle, multi4):
+    """Each shard's stripes on its own device buffers; parity and recovered
+    cells identical to a single launch over the whole batch and to the
+    oracle."""
+    k, p, C_, S = 8, 2, 16384 + 4096, 37
+    data = rand((S, k, C_), 1)
+    en = oracle.cauchy1(k, p)
+    want = np.stack([oracle.encode_data(en[k:], data[s]) for s in range(S)])      # [S][p][C]
+    stride = (k + p) * C_
+    bufs, ns = [], []
+    for i, c in enumerate(multi4.ctxs):
+        f, n = multi4.range(S, i)
+        img = np.zeros((max(n, 1), k + p, C_), dtype=np.uint8)
+        img[:n, :k] = data[f:f + n]
+        bufs.append(c.to_device(img))
+        ns.append(n)
+    ptrs = [b.ptr for b in bufs]
+    multi4.encode(k, p, C_, ns, ptrs, stride, [x + k * C_ for x in ptrs], C_, stride)
+    for i, b in enumerate(bufs):
+        f, n = multi4.range(S, i)
+        got = b.download().reshape(-1, k + p, C_)[:n]
+        assert np.array_equal(got[:, k:], want[f:f + n]), i
+    # one launch over everything, on the test context
+    one = ctx.to_device(np.concatenate([data, np.zeros((S, p, C_), np.uint8)], axis=1))
+    ctx.encode(k, p, C_, S, one.ptr, stride, one.ptr + k * C_, C_, stride)
+    ctx.sync()
+    ref_img = one.download().reshape(S, k + p, C_)
+    one.free()
+    # erase d1 + p0 everywhere, recover asynchronously, then sync
+    for b, n in zip(bufs, ns):
+        img = b.download().reshape(-1, k + p, C_)
+        img[:n, [1, k]] = 0x5A
+        b.upload(img)
+    multi4.recover(k, p, C_, ns, ptrs, stride, [1, k], flags=ecglib.MULTI_ASYNC)
+    multi4.sync()
+    for i, b in enumerate(bufs):
+        f, n = multi4.range(S, i)
+        assert np.array_equal(b.download().reshape(-1, k + p, C_)[:n], ref_img[f:f + n]), i
+        b.free()
+
+
+def test_multi_host_pipeline(ecglib, oracle, multi4):
+    """One host batch split over the shards: parity rows keep the batch's
+    [p][S][C] pitch, recovery works in place over [S][k+p][C]."""
+    k, p, C_, S = 4, 2, 65536, 29
+    data = rand((S, k, C_), 2)
+    par = np.full((p, S, C_), 0xA5, dtype=np.uint8)
+    multi4.encode_host(k, p, C_, S, data, par, chunk=3)
+    en = oracle.cauchy1(k, p)
+    want = np.stack([oracle.encode_data(en[k:], data[s]) for s in range(S)], axis=1)
+    assert np.array_equal(par, want)
+    stripes = np.concatenate([data, want.transpose(1, 0, 2)], axis=1).copy()
+    broken = stripes.copy()
+    broken[:, [0, 5]] = 0x5A
+    multi4.recover_host(k, p, C_, S, broken, [0, 5], chunk=2)
+    assert np.array_equal(broken, stripes)
+
+
+def test_multi_errors(ecglib, multi4):
+    with pytest.raises(ecglib.EcgError) as ei:
+        multi4.recover(4, 2, 4096, [1, 1, 1, 1], [0, 0, 0, 0], 6 * 4096, [0, 1, 2])
+    assert ei.value.rc == -ecglib.DER_DATA_LOSS
+    with pytest.raises(ecglib.EcgError):
+        ecglib.Multi([0, 99])
+
+
+def test_queue_multi_updates_concurrent(ecglib, oracle):
+    """8 threads x 24 one-cell aggregation updates (agg_update_parity's
+    xor_gen + ec_encode_data_update, ref:src/object/srv_ec_aggregate.c:
+    1086-1102) through a queue whose slots span 2 shards; every vec_i mixes in
+    one batch; parity bit-exact with the oracle's ec_encode_data_update."""
+    m = ecglib.Multi([0, 0])
+    q = ecglib.Queue(m, max_batch=32, max_wait_us=2000, max_cell_bytes=32768)
+    k, p, C_ = 8, 2, 32768 + 48
+    coef = oracle.cauchy1(k, p)[k:]
+    jobs = {}
+    for t in range(8):
+        for i in range(24):
+            rid = t * 100 + i
+            jobs[rid] = ((rid * 7) % k, rand(C_, rid), rand(C_, rid + 5000),
+                         [rand(C_, rid + 9000 + r) for r in range(p)])
+    want = {rid: oracle.encode_data_update(coef, vi, o ^ n, np.stack(par))
+            for rid, (vi, o, n, par) in jobs.items()}
+
+    def worker(t):
+        for i in range(24):
+            rid = t * 100 + i
+            vi, o, n, par = jobs[rid]
+            q.update(rid, k, p, vi, o, n, par)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    q.flush()
+    nreq, nbatch = q.stats()
+    assert nreq == 192 and all(rc == 0 for rc in q.done.values())
+    assert nbatch < nreq / 4
+    for rid, (vi, o, n, par) in jobs.items():
+        assert np.array_equal(np.stack(par), want[rid]), rid
+    q.close()
+    m.close()
+
+
+def test_queue_update_same_stripe_accumulates(ecglib, ctx, oracle):
+    """Two updates of different cells of the same stripe, submitted back to
+    back (the reference calls ec_encode_data_update once per updated cell on
+    the same parity buffers): both deltas land."""
+    q = ecglib.Queue(ctx, max_batch=8, max_wait_us=100)
+    k, p, C_ = 4, 2, 8192
+    data = rand((k, C_), 31)
+    en = oracle.cauchy1(k, p)
+    par = [r.copy() for r in oracle.encode_data(en[k:], data)]
+    new1, new3 = rand(C_, 32), rand(C_, 33)
+    q.update(0, k, p, 1, data[1], new1, par)
+    q.flush()
+    q.update(1, k, p, 3, data[3], new3, par)
+    q.flush()
+    d2 = data.copy()
+    d2[1], d2[3] = new1, new3
+    assert np.array_equal(np.stack(par), oracle.encode_data(en[k:], d2))
+    q.close()
+
+
+def test_isal_dropin_over_device_list(oracle):
+    """ECG_DEVICES=0,0,0 gives the synchronous ISA-L drop-in three contexts;
+    threads are spread over them and every call stays bit-exact."""
+    code = r'''
+import sys, threading, numpy as np
+sys.path.insert(0, %r)
+from daos_amd import ecg
+from oracle import ref
+k, p, C = 8, 2, 32768
+en = ref.cauchy1(k, p)
+tb = ecg.isal_init_tables(en[k:])
+bad = []
+def work(t):
+    for i in range(6):
+        d = np.random.default_rng(t * 10 + i).integers(0, 256, (k, C), dtype=np.uint8)
+        out = [np.zeros(C, np.uint8) for _ in range(p)]
+        ecg.isal_encode_data(tb, k, p, [d[j] for j in range(k)], out)
+        if not np.array_equal(np.stack(out), ref.encode_data(en[k:], d)):
+            bad.append((t, i))
+th = [threading.Thread(target=work, args=(t,)) for t in range(6)]
+[x.start() for x in th]; [x.join() for x in th]
+print("bad", bad)
+sys.exit(1 if bad else 0)
+''' % ROOT
+    env = dict(os.environ, ECG_DEVICES="0,0,0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr

@@ -160,6 +160,24 @@ for k, v in d.items():
         print(k, v)
 PY
 		;;
+	newtests)
+		step pytest_new 600 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_multi.py -v -x \
+			-p no:cacheprovider --timeout 300 --timeout-method thread
+		rc=$?; [ $rc -le 1 ] || exit $rc
+		;;
+	alltests)
+		step pytest_all 1000 python -u -m pytest tests -q -m gpu -p no:cacheprovider --timeout 300 \
+			--timeout-method thread
+		rc=$?; [ $rc -le 1 ] || exit $rc
+		;;
+	spawn2)
+		step bench_spawn2 300 python bench.py --gpus 2 --allow-shared-device --steps 10 --warmup 2 \
+			--no-detail --no-cpu || exit $?
+		;;
+	lib4)
+		step bench_lib4 300 python bench.py --gpus 4 --sharder lib --allow-shared-device --steps 10 \
+			--warmup 2 --no-detail || exit $?
+		;;
 	dist4)
 		step dist4 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
 			--master-port 29537 bench.py --gpus 4 --steps 20 --warmup 3 || exit $?
