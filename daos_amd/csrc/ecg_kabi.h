@@ -53,7 +53,7 @@ typedef struct ecg_mm_params {
 	uint32_t rows;
 	uint32_t accumulate;		/* dst ^= product instead of dst = product */
 	uint32_t diff;			/* source cell j = src[j] ^ src2[j] */
-	uint32_t pad;
+	uint32_t order;			/* block -> (stripe, column) map, 0 = 2D grid (ecg_kernels.hip) */
 	ecg_ptbl_t tbl[ECG_KMAX_R][ECG_KMAX_K];
 } ecg_mm_params_t;
 
@@ -62,7 +62,7 @@ typedef struct ecg_launch_cfg {
 	uint32_t grid_x;	/* chunks per stripe handled in parallel */
 	uint32_t grid_y;	/* stripes handled in parallel */
 	uint32_t variant;	/* 0 auto, 1 force generic, 2 force byte kernel */
-	uint32_t pad;
+	uint32_t order;		/* 0 = 2D grid x columns / y stripes; 1-3 1D orders (ecg_kernels.hip) */
 } ecg_launch_cfg_t;
 
 /*
@@ -86,7 +86,27 @@ typedef struct ecg_launch_cfg {
 
 #define ECG_MMCS_STRIDE 4096	/* fused kernels: 256 threads x 16 B per step */
 #define ECG_CSUM_NP2 48
-#define ECG_CSUM_TBL_ENTRIES(NB) (4 * (NB) * 256 + 64 + 256 + ECG_CSUM_NP2)
+/*
+ * 5-bit tables (conflict-free LDS lookups: a 32-entry table of 4-byte words
+ * covers the 32 banks ds_read_b32 sees, one of 8-byte words the 64 banks of
+ * ds_read_b64, so lanes never collide -- the byte tables above run ~3x
+ * conflicted on random data).  A 16-byte piece is 4 dwords x 7 fields (bits
+ * 5i..5i+4, the 7th field bits 30-31):
+ *   p5[28][32]   p5[7j + i][v] = raw CRC of the piece whose dword j is v << 5i
+ *   a5*[NA][32]  a register shifted by 1 KiB / 256 B / 4 KiB of zero bytes,
+ *                fields of each 32-bit half of the register (NA = 7 per half;
+ *                4 for crc16: bits 0-19)
+ */
+#define ECG_CSUM_NF5 28
+#define ECG_CSUM_NA5(NB) ((NB) == 2 ? 4 : 7 * (NB) / 4)
+#define ECG_CSUM_OFF_P5(NB) (4 * (NB) * 256 + 64 + 256 + ECG_CSUM_NP2)
+#define ECG_CSUM_OFF_A5_1K(NB) (ECG_CSUM_OFF_P5(NB) + ECG_CSUM_NF5 * 32)
+#define ECG_CSUM_OFF_A5_256(NB) (ECG_CSUM_OFF_A5_1K(NB) + ECG_CSUM_NA5(NB) * 32)
+#define ECG_CSUM_OFF_A5_4K(NB) (ECG_CSUM_OFF_A5_256(NB) + ECG_CSUM_NA5(NB) * 32)
+/* s16[16][256]: register after byte v and then j zero bytes, j < 16 (the
+ * raw CRC of a 16-byte piece is 16 independent lookups, no serial fold) */
+#define ECG_CSUM_OFF_S16(NB) (ECG_CSUM_OFF_A5_4K(NB) + ECG_CSUM_NA5(NB) * 32)
+#define ECG_CSUM_TBL_ENTRIES(NB) (ECG_CSUM_OFF_S16(NB) + 16 * 256)
 #define ECG_CSUM_OFF_P2(NB) (3 * (NB) * 256 + 64 + 256)
 #define ECG_CSUM_OFF_SH256(NB) (3 * (NB) * 256 + 64 + 256 + ECG_CSUM_NP2)
 #define ECG_CSUM_GLANES 16	/* lanes per chunk in the lane-group CRC kernel */
@@ -112,6 +132,8 @@ typedef struct ecg_csum_params {
 	uint32_t type;			/* DAOS hash type: 1 crc16, 2 crc32, 3 crc64, 7 adler32 */
 	uint32_t variant;		/* CRC: 0 auto, 1 wave per chunk, 2 workgroup per chunk,
 					 * 3 a 16-lane group per chunk */
+	uint32_t byte_tables;		/* CRC lookups: 0 = 5-bit tables, 1 = byte tables */
+	uint32_t pad2;
 	/* workgroup-per-chunk CRC: a chunk of m 1 KiB steps is cut into
 	 * ECG_CSUM_SPLIT_NW slices; split_sh[c][w] = x^(8 * bytes after slice w)
 	 * mod P for the chunk lengths' step counts split_m[c] (first, middle and
@@ -152,6 +174,7 @@ typedef struct ecg_mmcs_params {
 	uint32_t ncols;			/* columns per item */
 	uint32_t nh, nh_last;		/* items per chunk / in the last chunk */
 	uint32_t nitems;
+	uint32_t byte_tables;		/* 0 = 5-bit tables, 1 = byte tables (A/B) */
 	uint32_t row_slot[ECG_KMAX_R];
 } ecg_mmcs_params_t;
 

@@ -193,6 +193,14 @@ int ecg_set_launch(ecg_ctx_t *ctx, uint32_t grid_x, uint32_t grid_y, uint32_t va
 	return 0;
 }
 
+int ecg_set_launch_order(ecg_ctx_t *ctx, uint32_t order)
+{
+	if (ctx == NULL || order > 3)
+		return ecg_fail(-ECG_DER_INVAL, "set_launch_order: bad argument");
+	ctx->cfg.order = order;
+	return 0;
+}
+
 /* ------------------------------------------------------------------------ */
 /* batched GF matrix x cells                                                 */
 /* ------------------------------------------------------------------------ */

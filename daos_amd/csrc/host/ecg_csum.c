@@ -24,6 +24,20 @@ static const struct crc_def g_defs[4] = {
 	[ECG_HASH_CRC64] = {64, 1, 0xC96C5795D7870F42ull, ~0ull, ~0ull},
 };
 
+/* CRC table kind (tools/crc_ab.py, profiles/r02/crc_ab.json): the 5-bit
+ * conflict-free tables for crc16 / crc32 (crc32 over 32 KiB chunks 3.9 ->
+ * 5.1 TB/s), the byte tables for crc64, where 41 eight-byte lookups per 16 B
+ * lose to 24 conflicted ones.  csum_variant bit 4 forces the byte tables,
+ * bit 5 the 5-bit tables (A/B runs). */
+static uint32_t use_byte_tables(const ecg_ctx_t *ctx, int type)
+{
+	if (ctx->csum_variant & 16u)
+		return 1;
+	if (ctx->csum_variant & 32u)
+		return 0;
+	return type == ECG_HASH_CRC64;
+}
+
 int ecg_csum_len(int type)
 {
 	switch (type) {
@@ -186,8 +200,71 @@ static void build_shift(const struct crc_def *d, int n, uint64_t *t)
 		}
 }
 
+/* raw CRC (zero register) of len bytes */
+static uint64_t crc_raw(const struct crc_def *d, const unsigned char *buf, int len)
+{
+	const uint64_t mask = d->width == 64 ? ~0ull : (1ull << d->width) - 1;
+	uint64_t c = 0;
+
+	for (int i = 0; i < len; i++) {
+		c ^= d->refl ? (uint64_t)buf[i] : (uint64_t)buf[i] << (d->width - 8);
+		c = zero_byte(d, c) & mask;
+	}
+	return c;
+}
+
+/* 5-bit field tables (ecg_kabi.h p5 / a5): field (dword j, field i) covers
+ * bits 32j + 5i .. +4 of the piece or register; entry v = XOR of the basis
+ * images of v's set bits.  a5 for a shift of n zero bytes. */
+static void build_p5(const struct crc_def *d, uint64_t *p5)
+{
+	uint64_t basis[128];
+	unsigned char piece[16];
+
+	for (int k = 0; k < 128; k++) {
+		memset(piece, 0, sizeof(piece));
+		piece[k / 8] = (unsigned char)(1u << (k % 8));
+		basis[k] = crc_raw(d, piece, 16);
+	}
+	for (int f = 0; f < ECG_CSUM_NF5; f++) {
+		const int j = f / 7, i = f % 7;
+
+		for (int v = 0; v < 32; v++) {
+			uint64_t c = 0;
+
+			for (int t = 0; t < 5; t++)
+				if ((v >> t) & 1 && 5 * i + t < 32)
+					c ^= basis[32 * j + 5 * i + t];
+			p5[(size_t)f * 32 + v] = c;
+		}
+	}
+}
+
+static void build_a5(const struct crc_def *d, uint64_t n, uint64_t *a5)
+{
+	const uint64_t sh = crc_xpow8(d, n);
+	const int na = d->width == 16 ? 4 : 7 * d->width / 32;
+
+	for (int f = 0; f < na; f++) {
+		const int h = d->width == 16 ? 0 : f / 7, i = d->width == 16 ? f : f % 7;
+
+		for (int v = 0; v < 32; v++) {
+			uint64_t c = 0;
+
+			for (int t = 0; t < 5; t++) {
+				const int bit = 32 * h + 5 * i + t;
+
+				if ((v >> t) & 1 && 5 * i + t < 32 && bit < d->width)
+					c ^= crc_mulmod(d, 1ull << bit, sh);
+			}
+			a5[(size_t)f * 32 + v] = c;
+		}
+	}
+}
+
 /* Device table image (layout in ecg_kabi.h): sl, sh (1 KiB), k64, sh4k,
- * k256; entries of 4 (W <= 32) or 8 (W = 64) bytes. */
+ * k256, p2, sh256, p5, a5 (1 KiB, 256 B, 4 KiB); entries of 4 (W <= 32) or
+ * 8 (W = 64) bytes. */
 static void *build_crc_tables(const struct crc_def *d, size_t *bytes)
 {
 	const int nb = d->width / 8, es = d->width == 64 ? 8 : 4;
@@ -198,13 +275,16 @@ static void *build_crc_tables(const struct crc_def *d, size_t *bytes)
 
 	if (t == NULL)
 		return NULL;
-	/* sl[j][v]: register after byte v (from zero) and then j zero bytes */
+	/* sl[j][v] (j < NB) and s16[j][v] (j < 16): register after byte v (from
+	 * zero) and then j zero bytes */
 	for (int v = 0; v < 256; v++) {
 		uint64_t c = d->refl ? (uint64_t)v : (uint64_t)v << (d->width - 8);
 
 		c = zero_byte(d, c);
-		for (int j = 0; j < nb; j++) {
-			t[(size_t)j * 256 + v] = c;
+		for (int j = 0; j < 16; j++) {
+			if (j < nb)
+				t[(size_t)j * 256 + v] = c;
+			t[ECG_CSUM_OFF_S16(nb) + (size_t)j * 256 + v] = c;
 			c = zero_byte(d, c);
 		}
 	}
@@ -227,6 +307,11 @@ static void *build_crc_tables(const struct crc_def *d, size_t *bytes)
 		t[ECG_CSUM_OFF_P2(nb) + j] = c;
 		c = crc_mulmod(d, c, c);
 	}
+	build_p5(d, t + ECG_CSUM_OFF_P5(nb));
+	build_a5(d, ECG_CSUM_STRIDE, t + ECG_CSUM_OFF_A5_1K(nb));
+	build_a5(d, ECG_CSUM_GSTRIDE, t + ECG_CSUM_OFF_A5_256(nb));
+	build_a5(d, ECG_MMCS_STRIDE, t + ECG_CSUM_OFF_A5_4K(nb));
+
 	*bytes = n * (size_t)es;
 	if (es == 8)
 		return t;
@@ -454,8 +539,9 @@ int ecg_csum_extents(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_
 		 * (tools/bench_csum.py shape_* rows) */
 		const uint64_t total = (uint64_t)n_ext * prm.nchunks;
 		const uint64_t steps = (rcs / 16 + 63) / 64;
-		const int split = ctx->csum_variant == 2 ||
-				  (ctx->csum_variant == 0 && total < 4096 && steps >= 2 * ECG_CSUM_SPLIT_NW);
+		const uint32_t shape = ctx->csum_variant & 15u;
+		const int split = shape == 2 ||
+				  (shape == 0 && total < 4096 && steps >= 2 * ECG_CSUM_SPLIT_NW);
 		const uint64_t lens[3] = {
 			prm.first_bytes, rcs,
 			prm.nchunks >= 2 ? prm.ext_bytes - prm.first_bytes - (uint64_t)(prm.nchunks - 2) * rcs
@@ -463,15 +549,16 @@ int ecg_csum_extents(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_
 
 		/* short chunks (<= 8 KiB): a 16-lane group each, so the per-lane
 		 * final multiply is paid once per >= 8 pieces instead of per 1-2 */
-		const int group = ctx->csum_variant == 3 || (ctx->csum_variant == 0 && !split && steps <= 8);
+		const int group = shape == 3 || (shape == 0 && !split && steps <= 8);
 
 		prm.variant = split ? 2 : group ? 3 : 1;
+		prm.byte_tables = use_byte_tables(ctx, type);
 		for (int c = 0; split && c < 3; c++) {
 			prm.split_m[c] = (lens[c] / 16 + 63) / 64;
 			split_shifts(ctx, type, prm.split_m[c], prm.split_sh[c]);
 		}
 	} else {
-		prm.variant = ctx->csum_variant;	/* adler32: the kernel picks by shape when 0 */
+		prm.variant = ctx->csum_variant & 15u;	/* adler32: the kernel picks by shape when 0 */
 	}
 	e = ecg_k_launch_csum(&prm, (void *)ecg_pick_stream(ctx, stream), ctx->csum_blocks, &kid);
 	if (e != 0)
@@ -498,7 +585,7 @@ int ecg_set_fused_cols(ecg_ctx_t *ctx, uint32_t ncols)
 
 int ecg_set_csum_variant(ecg_ctx_t *ctx, uint32_t variant)
 {
-	if (ctx == NULL || variant > 3)
+	if (ctx == NULL || (variant & 15u) > 3 || variant > 127 || (variant & 48u) == 48u)
 		return ecg_fail(-ECG_DER_INVAL, "set_csum_variant: bad arguments");
 	ctx->csum_variant = variant;
 	return 0;
@@ -549,6 +636,9 @@ int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t
 	if ((uint64_t)(q->nch - 1) * q->nh + q->nh_last > UINT32_MAX)
 		return 0;
 	q->nitems = (q->nch - 1) * q->nh + q->nh_last;
+	/* fused kernels: table kind TB (ecg_kernels.hip); bit 6 of csum_variant
+	 * selects the s16 tables (A/B) */
+	q->byte_tables = (ctx->csum_variant & 64u) ? 2 : use_byte_tables(ctx, type);
 	rc = fused_kh(ctx, type, rcs, last, q->ncols, q->nh, q->nh_last, &q->kh);
 	if (rc)
 		return rc;

@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../ecg_kabi.h"
+
 namespace ecg_crc {
 
 template <int W> struct reg { using T = uint32_t; };
@@ -58,6 +60,79 @@ __device__ __forceinline__ T piece_crc(const uint32_t d[4], const T *sl)
 		}
 	}
 	return c;
+}
+
+// raw CRC (zero register) of one 16-byte piece from the s16 tables: 16
+// independent lookups (no serial fold through the register)
+template <int W, typename T>
+__device__ __forceinline__ T piece_crc16(const uint32_t d[4], const T *s16)
+{
+	T c = 0;
+#pragma unroll
+	for (int j = 0; j < 4; j++)
+#pragma unroll
+		for (int b = 0; b < 4; b++)
+			c ^= s16[(15 - 4 * j - b) * 256 + ((d[j] >> (8 * b)) & 0xffu)];
+	return c;
+}
+
+// ---- 5-bit tables (ecg_kabi.h p5 / a5): every lookup hits a 32-entry table,
+// so the lanes of a ds_read group never collide on a bank ----
+template <int W>
+struct f5 {
+	static constexpr int NF = ECG_CSUM_NF5;			// fields of a 16-byte piece
+	static constexpr int NA = ECG_CSUM_NA5(W / 8);		// fields of the register
+	static constexpr int N = (NF + NA) * 32;		// LDS entries: p5 then a5
+};
+
+// field i of dword x: bits 5i..5i+4 (i = 6: bits 30-31)
+__device__ __forceinline__ uint32_t fld5(uint32_t x, int i)
+{
+	return i == 6 ? x >> 30 : (x >> (5 * i)) & 31u;
+}
+
+// raw CRC (zero register) of one 16-byte piece: 28 lookups
+template <int W, typename T>
+__device__ __forceinline__ T piece_crc5(const uint32_t d[4], const T *p5)
+{
+	T c = 0;
+#pragma unroll
+	for (int j = 0; j < 4; j++)
+#pragma unroll
+		for (int i = 0; i < 7; i++)
+			c ^= p5[(7 * j + i) * 32 + fld5(d[j], i)];
+	return c;
+}
+
+// register -> register shifted by the a5 table's fixed number of zero bytes
+template <int W, typename T>
+__device__ __forceinline__ T lin_map5(T c, const T *a5)
+{
+	T r = 0;
+	if constexpr (W == 16) {
+		const uint32_t x = (uint32_t)c;
+#pragma unroll
+		for (int i = 0; i < 4; i++)
+			r ^= a5[i * 32 + ((x >> (5 * i)) & 31u)];
+	} else {
+#pragma unroll
+		for (int h = 0; h < W / 32; h++) {
+			const uint32_t x = (uint32_t)((uint64_t)c >> (32 * h));
+#pragma unroll
+			for (int i = 0; i < 7; i++)
+				r ^= a5[(7 * h + i) * 32 + fld5(x, i)];
+		}
+	}
+	return r;
+}
+
+// stage p5 and one a5 section (entries at gt + a5_off) into LDS s5[f5<W>::N]
+template <int W, typename T>
+__device__ __forceinline__ void stage5(T *s5, const T *gt, int a5_off, int nthreads)
+{
+	constexpr int NB = W / 8;
+	for (int i = threadIdx.x; i < f5<W>::N; i += nthreads)
+		s5[i] = i < f5<W>::NF * 32 ? gt[ECG_CSUM_OFF_P5(NB) + i] : gt[a5_off + i - f5<W>::NF * 32];
 }
 
 template <int W, bool REFL, typename T>

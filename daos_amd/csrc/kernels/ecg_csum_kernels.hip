@@ -69,18 +69,44 @@ __device__ __forceinline__ void chunk_geom(const ecg_csum_params_t &p, uint64_t 
 	base = p.src + (int64_t)e * p.ext_stride + off;
 }
 
-template <int W, bool REFL, bool ALIGNED>
+// One Horner step of a lane's accumulator: acc * x^(8 * stride) ^ crc(piece),
+// with the 5-bit tables (s5 = p5 then a5) or the byte tables (B8: sl, sh).
+template <int W, bool REFL, bool B8, typename T>
+__device__ __forceinline__ T horner(T acc, const uint32_t d[4], const T *s5, const T *sl, const T *sh)
+{
+	if constexpr (B8)
+		return lin_map<W>(acc, sh) ^ piece_crc<W, REFL>(d, sl);
+	else
+		return lin_map5<W>(acc, s5 + f5<W>::NF * 32) ^ piece_crc5<W>(d, s5);
+}
+
+// LDS images of one kernel: the 5-bit tables (p5, a5), or (B8) the byte tables
+template <int W, bool B8>
+struct crc_lds {
+	using T = typename reg<W>::T;
+	static constexpr int NB = W / 8;
+	static constexpr int N5 = B8 ? 1 : f5<W>::N;
+	static constexpr int NSL = B8 ? NB * 256 : 1;
+};
+
+template <int W, bool REFL, bool ALIGNED, bool B8>
 __global__ __launch_bounds__(CS_BLOCK) void ecg_crc_kernel(ecg_csum_params_t p)
 {
 	using T = typename reg<W>::T;
+	using L = crc_lds<W, B8>;
 	constexpr int NB = W / 8;
-	__shared__ T sl[NB * 256];
-	__shared__ T sh[NB * 256];
+	__shared__ T s5[L::N5];
+	__shared__ T sl[L::NSL];
+	__shared__ T sh[L::NSL];
 	const T *gt = (const T *)p.tbl;
 
-	for (int i = threadIdx.x; i < NB * 256; i += CS_BLOCK) {
-		sl[i] = gt[i];
-		sh[i] = gt[NB * 256 + i];
+	if constexpr (B8) {
+		for (int i = threadIdx.x; i < NB * 256; i += CS_BLOCK) {
+			sl[i] = gt[i];
+			sh[i] = gt[NB * 256 + i];
+		}
+	} else {
+		stage5<W>(s5, gt, ECG_CSUM_OFF_A5_1K(NB), CS_BLOCK);
 	}
 	const int lane = threadIdx.x & 63;
 	const T klane = gt[2 * NB * 256 + lane];
@@ -118,7 +144,7 @@ __global__ __launch_bounds__(CS_BLOCK) void ecg_crc_kernel(ecg_csum_params_t p)
 #pragma unroll
 			for (int u = 0; u < CS_UNROLL; u++) {
 				if (i + u < m)
-					acc = lin_map<W>(acc, sh) ^ piece_crc<W, REFL>(d[u], sl);
+					acc = horner<W, REFL, B8>(acc, d[u], s5, sl, sh);
 			}
 		}
 		acc = mulmod<W, REFL>(klane, acc, poly);
@@ -126,8 +152,8 @@ __global__ __launch_bounds__(CS_BLOCK) void ecg_crc_kernel(ecg_csum_params_t p)
 		if (lane == 0) {
 			T crc = nq == 0 ? init : acc;
 
-			for (uint64_t b = (uint64_t)nq * 16; b < len; b++)
-				crc = byte_step<W, REFL>(crc, base[b], sl);
+			for (uint64_t b = (uint64_t)nq * 16; b < len; b++)	// tail bytes: sl[0] in memory
+				crc = byte_step<W, REFL>(crc, base[b], gt);
 			crc ^= xorout;
 			if constexpr (W == 16)
 				((uint16_t *)p.out)[g] = (uint16_t)crc;
@@ -154,20 +180,26 @@ __device__ __forceinline__ T shfl_xor_t(T v, int s)
 // reads 4 x 256 B contiguous, Horner-steps by G*16 bytes (sh256 table), and
 // the group reduces with shuffles after multiplying by x^(8*16*(G-1-l)) =
 // k64[64 - G + l].  Otherwise as ecg_crc_kernel.
-template <int W, bool REFL>
+template <int W, bool REFL, bool B8>
 __global__ __launch_bounds__(CS_BLOCK) void ecg_crc_group_kernel(ecg_csum_params_t p)
 {
 	using T = typename reg<W>::T;
+	using L = crc_lds<W, B8>;
 	constexpr int NB = W / 8;
 	constexpr int G = ECG_CSUM_GLANES;
 	constexpr int GPW = 64 / G;		// chunks per wave
-	__shared__ T sl[NB * 256];
-	__shared__ T sh[NB * 256];
+	__shared__ T s5[L::N5];
+	__shared__ T sl[L::NSL];
+	__shared__ T sh[L::NSL];
 	const T *gt = (const T *)p.tbl;
 
-	for (int i = threadIdx.x; i < NB * 256; i += CS_BLOCK) {
-		sl[i] = gt[i];
-		sh[i] = gt[ECG_CSUM_OFF_SH256(NB) + i];
+	if constexpr (B8) {
+		for (int i = threadIdx.x; i < NB * 256; i += CS_BLOCK) {
+			sl[i] = gt[i];
+			sh[i] = gt[ECG_CSUM_OFF_SH256(NB) + i];
+		}
+	} else {
+		stage5<W>(s5, gt, ECG_CSUM_OFF_A5_256(NB), CS_BLOCK);
 	}
 	const int lane = threadIdx.x & 63, gl = lane % G;
 	const T klane = gt[ECG_CSUM_OFF_K64(NB) + 64 - G + gl];
@@ -211,7 +243,7 @@ __global__ __launch_bounds__(CS_BLOCK) void ecg_crc_group_kernel(ecg_csum_params
 #pragma unroll
 			for (int u = 0; u < CS_UNROLL; u++) {
 				if (i + u < m)
-					acc = lin_map<W>(acc, sh) ^ piece_crc<W, REFL>(d[u], sl);
+					acc = horner<W, REFL, B8>(acc, d[u], s5, sl, sh);
 			}
 		}
 		acc = mulmod<W, REFL>(klane, acc, poly);
@@ -222,7 +254,7 @@ __global__ __launch_bounds__(CS_BLOCK) void ecg_crc_group_kernel(ecg_csum_params
 			T crc = nq == 0 ? init : acc;
 
 			for (uint64_t b = (uint64_t)nq * 16; b < len; b++)
-				crc = byte_step<W, REFL>(crc, base[b], sl);
+				crc = byte_step<W, REFL>(crc, base[b], gt);
 			crc ^= xorout;
 			if constexpr (W == 16)
 				((uint16_t *)p.out)[g] = (uint16_t)crc;
@@ -242,19 +274,25 @@ __global__ __launch_bounds__(CS_BLOCK) void ecg_crc_group_kernel(ecg_csum_params
 // table entries of its set bits, one bit per lane, multiplied down the wave
 // in 6 butterfly steps -- and the waves' values are XORed through LDS (CRC
 // is linear: crc(A || B) = crc(A) * x^(8|B|) ^ crc(B) for zero registers).
-template <int W, bool REFL, int NW>
+template <int W, bool REFL, int NW, bool B8>
 __global__ __launch_bounds__(64 * NW) void ecg_crc_split_kernel(ecg_csum_params_t p)
 {
 	using T = typename reg<W>::T;
+	using L = crc_lds<W, B8>;
 	constexpr int NB = W / 8;
-	__shared__ T sl[NB * 256];
-	__shared__ T sh[NB * 256];
+	__shared__ T s5[L::N5];
+	__shared__ T sl[L::NSL];
+	__shared__ T sh[L::NSL];
 	__shared__ T part[NW];
 	const T *gt = (const T *)p.tbl;
 
-	for (int i = threadIdx.x; i < NB * 256; i += 64 * NW) {
-		sl[i] = gt[i];
-		sh[i] = gt[NB * 256 + i];
+	if constexpr (B8) {
+		for (int i = threadIdx.x; i < NB * 256; i += 64 * NW) {
+			sl[i] = gt[i];
+			sh[i] = gt[NB * 256 + i];
+		}
+	} else {
+		stage5<W>(s5, gt, ECG_CSUM_OFF_A5_1K(NB), 64 * NW);
 	}
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 	const T klane = gt[2 * NB * 256 + lane];
@@ -296,7 +334,7 @@ __global__ __launch_bounds__(64 * NW) void ecg_crc_split_kernel(ecg_csum_params_
 #pragma unroll
 			for (int u = 0; u < CS_UNROLL; u++) {
 				if (i + u < i1)
-					acc = lin_map<W>(acc, sh) ^ piece_crc<W, REFL>(d[u], sl);
+					acc = horner<W, REFL, B8>(acc, d[u], s5, sl, sh);
 			}
 		}
 		acc = mulmod<W, REFL>(klane, acc, poly);
@@ -327,7 +365,7 @@ __global__ __launch_bounds__(64 * NW) void ecg_crc_split_kernel(ecg_csum_params_
 			if (nq == 0)
 				crc = init;
 			for (uint64_t b = (uint64_t)nq * 16; b < len; b++)
-				crc = byte_step<W, REFL>(crc, base[b], sl);
+				crc = byte_step<W, REFL>(crc, base[b], gt);
 			crc ^= xorout;
 			if constexpr (W == 16)
 				((uint16_t *)p.out)[g] = (uint16_t)crc;
@@ -470,37 +508,56 @@ typedef void (*csum_fn_t)(ecg_csum_params_t);
 struct csum_entry {
 	uint32_t type;
 	bool aligned;
+	bool b8;		/* byte tables (the A/B variant), else 5-bit tables */
 	csum_fn_t fn;
 	const char *name;
 };
 
 const csum_entry g_csum[] = {
-	{1, true, ecg_crc_kernel<16, false, true>, "ecg_crc_kernel<crc16>"},
-	{1, false, ecg_crc_kernel<16, false, false>, "ecg_crc_kernel<crc16,bytes>"},
-	{2, true, ecg_crc_kernel<32, true, true>, "ecg_crc_kernel<crc32>"},
-	{2, false, ecg_crc_kernel<32, true, false>, "ecg_crc_kernel<crc32,bytes>"},
-	{3, true, ecg_crc_kernel<64, true, true>, "ecg_crc_kernel<crc64>"},
-	{3, false, ecg_crc_kernel<64, true, false>, "ecg_crc_kernel<crc64,bytes>"},
-	{7, true, ecg_adler_kernel<true>, "ecg_adler_kernel"},
-	{7, false, ecg_adler_kernel<false>, "ecg_adler_kernel<bytes>"},
+	{1, true, false, ecg_crc_kernel<16, false, true, false>, "ecg_crc_kernel<crc16>"},
+	{1, false, false, ecg_crc_kernel<16, false, false, false>, "ecg_crc_kernel<crc16,bytes>"},
+	{2, true, false, ecg_crc_kernel<32, true, true, false>, "ecg_crc_kernel<crc32>"},
+	{2, false, false, ecg_crc_kernel<32, true, false, false>, "ecg_crc_kernel<crc32,bytes>"},
+	{3, true, false, ecg_crc_kernel<64, true, true, false>, "ecg_crc_kernel<crc64,alt>"},
+	{3, false, false, ecg_crc_kernel<64, true, false, false>, "ecg_crc_kernel<crc64,bytes,alt>"},
+	{1, true, true, ecg_crc_kernel<16, false, true, true>, "ecg_crc_kernel<crc16,alt>"},
+	{1, false, true, ecg_crc_kernel<16, false, false, true>, "ecg_crc_kernel<crc16,bytes,alt>"},
+	{2, true, true, ecg_crc_kernel<32, true, true, true>, "ecg_crc_kernel<crc32,alt>"},
+	{2, false, true, ecg_crc_kernel<32, true, false, true>, "ecg_crc_kernel<crc32,bytes,alt>"},
+	{3, true, true, ecg_crc_kernel<64, true, true, true>, "ecg_crc_kernel<crc64>"},
+	{3, false, true, ecg_crc_kernel<64, true, false, true>, "ecg_crc_kernel<crc64,bytes>"},
+	{7, true, false, ecg_adler_kernel<true>, "ecg_adler_kernel"},
+	{7, false, false, ecg_adler_kernel<false>, "ecg_adler_kernel<bytes>"},
 };
 constexpr uint32_t N_CSUM = sizeof(g_csum) / sizeof(g_csum[0]);
 
 constexpr int SPLIT_NW = ECG_CSUM_SPLIT_NW;	// waves per chunk in the split kernel
 const csum_entry g_split[] = {
-	{1, true, ecg_crc_split_kernel<16, false, SPLIT_NW>, "ecg_crc_split_kernel<crc16>"},
-	{2, true, ecg_crc_split_kernel<32, true, SPLIT_NW>, "ecg_crc_split_kernel<crc32>"},
-	{3, true, ecg_crc_split_kernel<64, true, SPLIT_NW>, "ecg_crc_split_kernel<crc64>"},
-	{7, true, ecg_adler_split_kernel<SPLIT_NW>, "ecg_adler_split_kernel"},
+	{1, true, false, ecg_crc_split_kernel<16, false, SPLIT_NW, false>, "ecg_crc_split_kernel<crc16>"},
+	{2, true, false, ecg_crc_split_kernel<32, true, SPLIT_NW, false>, "ecg_crc_split_kernel<crc32>"},
+	{3, true, false, ecg_crc_split_kernel<64, true, SPLIT_NW, false>, "ecg_crc_split_kernel<crc64,alt>"},
+	{1, true, true, ecg_crc_split_kernel<16, false, SPLIT_NW, true>, "ecg_crc_split_kernel<crc16,alt>"},
+	{2, true, true, ecg_crc_split_kernel<32, true, SPLIT_NW, true>, "ecg_crc_split_kernel<crc32,alt>"},
+	{3, true, true, ecg_crc_split_kernel<64, true, SPLIT_NW, true>, "ecg_crc_split_kernel<crc64>"},
+	{7, true, false, ecg_adler_split_kernel<SPLIT_NW>, "ecg_adler_split_kernel"},
 };
 constexpr uint32_t N_SPLIT = sizeof(g_split) / sizeof(g_split[0]);
 
 const csum_entry g_group[] = {
-	{1, true, ecg_crc_group_kernel<16, false>, "ecg_crc_group_kernel<crc16>"},
-	{2, true, ecg_crc_group_kernel<32, true>, "ecg_crc_group_kernel<crc32>"},
-	{3, true, ecg_crc_group_kernel<64, true>, "ecg_crc_group_kernel<crc64>"},
+	{1, true, false, ecg_crc_group_kernel<16, false, false>, "ecg_crc_group_kernel<crc16>"},
+	{2, true, false, ecg_crc_group_kernel<32, true, false>, "ecg_crc_group_kernel<crc32>"},
+	{3, true, false, ecg_crc_group_kernel<64, true, false>, "ecg_crc_group_kernel<crc64,alt>"},
+	{1, true, true, ecg_crc_group_kernel<16, false, true>, "ecg_crc_group_kernel<crc16,alt>"},
+	{2, true, true, ecg_crc_group_kernel<32, true, true>, "ecg_crc_group_kernel<crc32,alt>"},
+	{3, true, true, ecg_crc_group_kernel<64, true, true>, "ecg_crc_group_kernel<crc64>"},
 };
 constexpr uint32_t N_GROUP = sizeof(g_group) / sizeof(g_group[0]);
+
+/* the entry's table kind matches the request (adler32 has one kind) */
+__host__ inline bool kind_ok(const csum_entry &e, const ecg_csum_params_t *p)
+{
+	return e.type == 7 || e.b8 == (p->byte_tables != 0);
+}
 
 } // namespace
 
@@ -534,7 +591,7 @@ extern "C" int ecg_k_launch_csum(const ecg_csum_params_t *p, void *stream, uint3
 				   (p->variant == 0 && total < 4096 && steps >= 2 * SPLIT_NW);
 
 		for (uint32_t i = 0; split && i < N_SPLIT; i++) {
-			if (g_split[i].type != p->type)
+			if (g_split[i].type != p->type || !kind_ok(g_split[i], p))
 				continue;
 			uint64_t nb = total;
 			const uint64_t cap = max_blocks ? max_blocks : 256 * 8;
@@ -557,7 +614,7 @@ extern "C" int ecg_k_launch_csum(const ecg_csum_params_t *p, void *stream, uint3
 		if (nb > max_blocks)
 			nb = max_blocks;
 		for (uint32_t i = 0; i < N_GROUP; i++) {
-			if (g_group[i].type != p->type)
+			if (g_group[i].type != p->type || !kind_ok(g_group[i], p))
 				continue;
 			hipLaunchKernelGGL(g_group[i].fn, dim3((uint32_t)nb), dim3(CS_BLOCK), 0,
 					   (hipStream_t)stream, *p);
@@ -569,7 +626,7 @@ extern "C" int ecg_k_launch_csum(const ecg_csum_params_t *p, void *stream, uint3
 	if (blocks > max_blocks)
 		blocks = max_blocks;
 	for (uint32_t i = 0; i < N_CSUM; i++) {
-		if (g_csum[i].type == p->type && g_csum[i].aligned == aligned) {
+		if (g_csum[i].type == p->type && g_csum[i].aligned == aligned && kind_ok(g_csum[i], p)) {
 			hipLaunchKernelGGL(g_csum[i].fn, dim3((uint32_t)blocks), dim3(CS_BLOCK), 0,
 					   (hipStream_t)stream, *p);
 			if (kernel_id)

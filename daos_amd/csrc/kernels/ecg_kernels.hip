@@ -215,6 +215,36 @@ __device__ __forceinline__ void mm_tail(const ecg_mm_params_t &P, const u32x4 *t
 	}
 }
 
+// 1D item orders (P.order): which (stripe, 4 KiB column) block `it` of a
+// 1D grid works on.  The hardware dispatcher hands consecutive block ids to
+// the 8 XCDs round-robin, so `it & 7` is (nearly) the block's XCD.
+//   1  stripe-fastest: consecutive blocks touch the same column of
+//      consecutive stripes
+//   2  XCD-blocked, column-fastest: XCD x walks the x-th eighth of the
+//      column-fastest item list (each XCD streams its own stripe range)
+//   3  XCD-blocked, stripe-fastest
+__device__ __forceinline__ void item_map(uint32_t order, uint32_t it, uint32_t total, uint32_t nchunk,
+					 uint32_t S, uint32_t &s, uint32_t &ch)
+{
+	uint32_t g = it;
+
+	if (order >= 2) {
+		const uint32_t per = (total + 7) / 8;	// items per XCD slice
+		const uint32_t x = it & 7, j = it >> 3;
+
+		g = x * per + j;
+		if (g >= total)			// uneven tail: fall back to the plain id
+			g = it;
+	}
+	if (order == 1 || order == 3) {
+		s = g % S;
+		ch = g / S;
+	} else {
+		s = g / nchunk;
+		ch = g - s * nchunk;
+	}
+}
+
 // K, R: compile-time data cells / output rows (0 = runtime, bounded by the
 // ECG_KMAX_* maxima).  ACC: XOR into dst.  DIFF: source = src ^ src2.
 //
@@ -251,6 +281,28 @@ ecg_mm_kernel(const ecg_mm_params_t P)
 	}
 	__syncthreads();
 
+	if (P.order) {
+		// 1D grid over the S x nchunk (stripe, column) items in the order
+		// item_map picks (tuning of the block -> address mapping).
+		const uint32_t total = P.nstripes * nchunk;
+
+		for (uint32_t it = blockIdx.x; it < total; it += gridDim.x) {
+			uint32_t s, ch, z = 0;
+
+			item_map(P.order, it, total, nchunk, P.nstripes, s, ch);
+			const uint64_t cbase = (uint64_t)ch * CHUNK_BYTES;
+
+			asm volatile("" : "+v"(z));
+			const u32x4 *tb = s_tbl + z;
+			if (cbase + CHUNK_BYTES <= C)
+				mm_item<KM, RM, ACC, DIFF>(P, tb, k, rows, s, cbase, lo);
+			else if (cbase + lo + 16 <= C)
+				mm_item<KM, RM, ACC, DIFF>(P, tb, k, rows, s, cbase, lo);
+			else if (cbase + lo < C)
+				mm_tail<RM, ACC, DIFF>(P, tb, k, rows, s, cbase + lo, (int)(C - cbase - lo));
+		}
+		return;
+	}
 	// Normally one item per block (grid = columns x stripes); the loops only
 	// stride when a grid dimension would exceed 65535.
 	for (uint32_t s = blockIdx.y; s < P.nstripes; s += gridDim.y) {
@@ -354,11 +406,12 @@ __device__ __forceinline__ void mmcs_item(const ecg_mmcs_params_t &Q, uint32_t i
 // The outputs are never re-read from HBM: the checksum costs LDS lookups on
 // p/(k+p) of the traffic instead of a second pass over the regenerated
 // cells (ref:src/object/srv_obj_migrate.c:1156 checksums them after encode).
-template <int K, int R, int W, bool REFL>
+template <int K, int R, int W, bool REFL, int TB = 0>
 __global__ void __launch_bounds__(BLOCK, 4)	// >= 4 waves per SIMD: <= 128 VGPRs
 ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 {
 	using T = typename ecg_crc::reg<W>::T;
+	using F5 = ecg_crc::f5<W>;
 	constexpr int NB = W / 8;
 	constexpr int KM = K ? K : ECG_KMAX_K;
 	constexpr int RM = R ? R : ECG_KMAX_R;
@@ -366,8 +419,12 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	constexpr int T2V = (RM + 3) / 4;
 	constexpr int PER_J = RM + T2V;
 	__shared__ u32x4 s_tbl[KM * PER_J];
-	__shared__ T s_sl[NB * 256];
-	__shared__ T s_sh[NB * 256];
+	// CRC tables (TB): 0 5-bit (conflict-free, ecg_kabi.h p5 + a5 shift by
+	// 4 KiB); 1 byte tables sl (slice-by-NB, register folded) + sh4k; 2 byte
+	// tables s16 (16 independent lookups per piece) + sh4k
+	constexpr int NSL = TB == 0 ? F5::N : TB == 1 ? NB * 256 : 16 * 256;
+	__shared__ T s_sl[NSL];
+	__shared__ T s_sh[TB ? NB * 256 : 1];
 	const int k = K ? K : (int)P.k;
 	const int rows = R ? R : (int)P.rows;
 	const uint64_t C = P.cell_bytes;
@@ -382,9 +439,13 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 			reinterpret_cast<uint32_t *>(&s_tbl[j * PER_J + RM])[r] = t.t2;
 		}
 	}
-	for (int i = threadIdx.x; i < NB * 256; i += BLOCK) {
-		s_sl[i] = gt[i];
-		s_sh[i] = gt[ECG_CSUM_OFF_SH4K(NB) + i];
+	if constexpr (TB != 0) {
+		for (int i = threadIdx.x; i < NSL; i += BLOCK)
+			s_sl[i] = gt[(TB == 1 ? 0 : ECG_CSUM_OFF_S16(NB)) + i];
+		for (int i = threadIdx.x; i < NB * 256; i += BLOCK)
+			s_sh[i] = gt[ECG_CSUM_OFF_SH4K(NB) + i];
+	} else {
+		ecg_crc::stage5<W>(s_sl, gt, ECG_CSUM_OFF_A5_4K(NB), BLOCK);
 	}
 	const T *kh = (const T *)Q.kh;
 	const T poly = (T)Q.poly;
@@ -433,7 +494,10 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 				for (int r = 0; r < RM; r++) {
 					if (r < rows) {
 #ifndef ECG_EXP_NO_CRC
-						crc[r] = ecg_crc::lin_map<W>(crc[r], s_sh);
+						if constexpr (TB != 0)
+							crc[r] = ecg_crc::lin_map<W>(crc[r], s_sh);
+						else
+							crc[r] = ecg_crc::lin_map5<W>(crc[r], s_sl + F5::NF * 32);
 #endif
 						if (have) {
 							uint32_t d[4] = {outv[r][0], outv[r][1], outv[r][2], outv[r][3]};
@@ -443,7 +507,12 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 									d[1] ^= (uint32_t)(Q.init >> 32);
 							}
 #ifndef ECG_EXP_NO_CRC
-							crc[r] ^= ecg_crc::piece_crc<W, REFL>(d, s_sl);
+							if constexpr (TB == 1)
+								crc[r] ^= ecg_crc::piece_crc<W, REFL>(d, s_sl);
+							else if constexpr (TB == 2)
+								crc[r] ^= ecg_crc::piece_crc16<W>(d, s_sl);
+							else
+								crc[r] ^= ecg_crc::piece_crc5<W>(d, s_sl);
 #else
 							crc[r] ^= (T)(d[0] ^ d[1] ^ d[2] ^ d[3]);
 #endif
@@ -702,17 +771,28 @@ struct csentry {
 	int k, r, type;
 	mmcs_fn_t fn;
 	const char *name;
+	int b8;		/* CRC table kind TB of the instantiation */
 };
 
 #define CSE(K_, R_, T_, W_, RF_, N_) \
-	{K_, R_, T_, ecg_mm_csum_kernel<K_, R_, W_, RF_>, "ecg_mm_csum_kernel<" #K_ "," #R_ "," N_ ">"}
+	{K_, R_, T_, ecg_mm_csum_kernel<K_, R_, W_, RF_, W_ == 64 ? 1 : 0>, "ecg_mm_csum_kernel<" #K_ "," #R_ "," N_ ">", \
+	 W_ == 64 ? 1 : 0}
 #define CSE3(K_, R_) CSE(K_, R_, 1, 16, false, "crc16"), CSE(K_, R_, 2, 32, true, "crc32"), \
 		     CSE(K_, R_, 3, 64, true, "crc64")
+
+/* the other table kind than the default (crc16/crc32 5-bit, crc64 byte tables) */
+#define CSB(K_, R_, T_, W_, RF_, N_, TB_) \
+	{K_, R_, T_, ecg_mm_csum_kernel<K_, R_, W_, RF_, TB_>, \
+	 "ecg_mm_csum_kernel<" #K_ "," #R_ "," N_ ",tb" #TB_ ">", TB_}
 
 static const csentry g_cskernels[] = {
 	CSE3(2, 1), CSE3(2, 2), CSE3(2, 3), CSE3(4, 1), CSE3(4, 2), CSE3(4, 3),
 	CSE3(8, 1), CSE3(8, 2), CSE3(8, 3), CSE3(16, 1), CSE3(16, 2), CSE3(16, 3),
 	CSE3(0, 0),
+	/* the other table kind, A/B measurements only (ecg_set_csum_variant bits 4/5) */
+	CSB(8, 2, 2, 32, true, "crc32", 1), CSB(8, 2, 2, 32, true, "crc32", 2), CSB(8, 2, 3, 64, true, "crc64", 0),
+	CSB(8, 2, 3, 64, true, "crc64", 2), CSB(4, 2, 2, 32, true, "crc32", 2), CSB(4, 2, 3, 64, true, "crc64", 2),
+	CSB(8, 1, 2, 32, true, "crc32", 2),
 };
 #define N_CSKERNELS ((uint32_t)(sizeof(g_cskernels) / sizeof(g_cskernels[0])))
 #define KID_FUSED 500u		/* fused kernel ids: KID_FUSED + index */
@@ -836,9 +916,28 @@ extern "C" int ecg_k_launch_matmul(const ecg_mm_params_t *p, const ecg_launch_cf
 	// 6.2 TB/s) -- the dispatcher refills CUs faster than a resident block
 	// re-issues its next item's loads.  Both loops still stride for
 	// grids beyond 65535.
+	const uint64_t total = nchunk * p->nstripes;
+	const uint32_t order = cfg ? cfg->order : 0;
+	if (order >= 1 && order <= 3 && total < (1ull << 31) && (order == 1 || total % 8 == 0)) {
+		ecg_mm_params_t q = *p;
+		uint32_t gx = cfg->grid_x ? cfg->grid_x : (uint32_t)total;
+
+		q.order = order;
+		hipLaunchKernelGGL(g_kernels[id].fn, dim3(gx), dim3(BLOCK), 0, st, q);
+		if (kernel_id)
+			*kernel_id = id;
+		return (int)hipGetLastError();
+	}
 	uint32_t gx = cfg && cfg->grid_x ? cfg->grid_x : (uint32_t)(nchunk < 65535 ? nchunk : 65535);
 	uint32_t gy = cfg && cfg->grid_y ? cfg->grid_y : (p->nstripes < 65535 ? p->nstripes : 65535);
-	hipLaunchKernelGGL(g_kernels[id].fn, dim3(gx, gy), dim3(BLOCK), 0, st, *p);
+	if (p->order) {
+		ecg_mm_params_t q = *p;
+
+		q.order = 0;
+		hipLaunchKernelGGL(g_kernels[id].fn, dim3(gx, gy), dim3(BLOCK), 0, st, q);
+	} else {
+		hipLaunchKernelGGL(g_kernels[id].fn, dim3(gx, gy), dim3(BLOCK), 0, st, *p);
+	}
 	if (kernel_id)
 		*kernel_id = id;
 	return (int)hipGetLastError();
@@ -883,13 +982,14 @@ extern "C" int ecg_k_launch_matmul_csum(const ecg_mm_params_t *p, const ecg_mmcs
 		return 1;
 	for (uint32_t i = 0; i < N_CSKERNELS; i++)
 		if (g_cskernels[i].type == (int)q->type && g_cskernels[i].k == (int)p->k &&
-		    g_cskernels[i].r == (int)p->rows) {
+		    g_cskernels[i].r == (int)p->rows && g_cskernels[i].b8 == (int)q->byte_tables) {
 			id = i;
 			break;
 		}
 	if (id == N_CSKERNELS)
 		for (uint32_t i = 0; i < N_CSKERNELS; i++)
-			if (g_cskernels[i].type == (int)q->type && g_cskernels[i].k == 0) {
+			if (g_cskernels[i].type == (int)q->type && g_cskernels[i].k == 0 &&
+			    g_cskernels[i].b8 == (int)q->byte_tables) {
 				id = i;
 				break;
 			}

@@ -79,6 +79,7 @@ _SIGS = [
     ("ecg_device_sync", C.c_int, [vp]),
     ("ecg_dev_copy_kernel", C.c_int, [vp, vp, vp, C.c_size_t, C.c_int, vp]),
     ("ecg_set_launch", C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_uint32]),
+    ("ecg_set_launch_order", C.c_int, [vp, C.c_uint32]),
     # multi-device sharder (ecg_multi.h)
     ("ecg_multi_create", C.c_int, [C.POINTER(C.c_int), C.c_int, C.POINTER(vp)]),
     ("ecg_multi_destroy", None, [vp]),
@@ -411,6 +412,9 @@ class Context:
 
     def set_launch(self, grid_x: int = 0, grid_y: int = 0, variant: int = 0):
         _chk(lib().ecg_set_launch(self.h, grid_x, grid_y, variant), "set_launch")
+
+    def set_order(self, order: int = 0):
+        _chk(lib().ecg_set_launch_order(self.h, order), "set_launch_order")
 
     def copy_kernel(self, dst: int, src: int, nbytes: int, mode: int = 0, stream=None):
         """mode 0 copy, 1 read-only, 2 write-only (HBM rate probes)."""

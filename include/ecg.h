@@ -224,6 +224,11 @@ int ecg_dev_copy_kernel(ecg_ctx_t *ctx, void *dst, const void *src, size_t bytes
 /* ---- launch tuning (benchmarks; 0 = default) ----------------------------
  * variant: 0 auto, 1 runtime-shaped kernel, 2 byte kernel. */
 int ecg_set_launch(ecg_ctx_t *ctx, uint32_t grid_x, uint32_t grid_y, uint32_t variant);
+/* Block -> (stripe, 4 KiB column) mapping of the product kernel: 0 = 2D
+ * grid (columns x stripes, default); 1 = 1D stripe-fastest; 2 = 1D with each
+ * XCD streaming its own eighth of the column-fastest items; 3 = as 2,
+ * stripe-fastest.  Tuning only; results never depend on it. */
+int ecg_set_launch_order(ecg_ctx_t *ctx, uint32_t order);
 
 /* Pointer-table product: ISA-L's per-stripe pointer arrays
  * (ec_encode_data(len, k, rows, tbls, data[], coding[])) batched over

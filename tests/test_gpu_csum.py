@@ -344,3 +344,53 @@ def test_encode_csum_misaligned_csums(oracle, ecglib, ctx):
         assert np.array_equal(got, _want_cell_csums(oracle, 1, cs, 1, want_par).reshape(p, S, nch))
     finally:
         d.free(); par.free(); out.free()
+
+
+@pytest.mark.parametrize("kind", [16, 32])          # byte tables / 5-bit tables forced
+@pytest.mark.parametrize("shape", [1, 2, 3])
+@pytest.mark.parametrize("htype", (1, 2, 3))
+@pytest.mark.parametrize("geom", [(32768, 1, 0, 200000), (4096, 1, 0, 4096 * 7 + 16 * 5),
+                                  ((1 << 20) + 4096, 1, 5, 2 << 20)])
+def test_crc_table_kinds(oracle, ecglib, ctx, kind, shape, htype, geom):
+    """Both CRC table kinds (conflict-free 5-bit tables, byte tables; the
+    default picks per hash) give the oracle's checksums on every kernel shape."""
+    cs, rb, idx, nr = geom
+    L = ecglib.lib()
+    host = np.random.default_rng(kind + shape + htype).integers(0, 256, rb * nr, dtype=np.uint8)
+    assert L.ecg_set_csum_variant(ctx.h, kind | shape) == 0
+    try:
+        got = _dev_csum(ecglib, ctx, htype, cs, rb, idx, nr, host)
+    finally:
+        L.ecg_set_csum_variant(ctx.h, 0)
+    assert np.array_equal(got, oracle.csum_extents(htype, cs, rb, idx, nr, host))
+
+
+@pytest.mark.parametrize("kind", [16, 32, 64])      # fused TB 1 / 0 / 2 forced
+@pytest.mark.parametrize("case", [(8, 2, 1 << 20, 3, 32768, 2), (8, 2, 1 << 20, 3, 32768, 3),
+                                  (4, 2, 256 << 10, 5, 32768, 2), (4, 2, 256 << 10, 5, 32768, 3),
+                                  (8, 1, 3 * 65536 + 48, 4, 65536, 2)])
+def test_encode_csum_fused_table_kinds(oracle, ecglib, ctx, kind, case):
+    """Every fused-kernel table kind (5-bit, slice-by-NB, s16) writes the
+    oracle's parity and checksums; a kind a shape does not instantiate runs
+    the two-pass path (product, then the checksum kernel) with the same
+    results."""
+    k, p, C, S, cs, htype = case
+    L = ecglib.lib()
+    nch = L.ecg_csum_chunk_count(cs, 1, 0, C)
+    cl = L.ecg_csum_len(htype)
+    data = np.random.default_rng(sum(case) + kind).integers(0, 256, S * k * C, dtype=np.uint8)
+    d = ctx.to_device(data)
+    par = ctx.alloc(p * S * C)
+    out = ctx.alloc(p * S * nch * cl)
+    assert L.ecg_set_csum_variant(ctx.h, kind) == 0
+    try:
+        ctx.encode_csum(k, p, C, S, d.ptr, k * C, par.ptr, S * C, C, htype, cs, 1, out.ptr)
+        ctx.sync()
+        want_par = oracle.encode_batch(k, p, C, S, data, nthreads=8, simd=True).reshape(p, S, C)
+        assert np.array_equal(par.download().reshape(p, S, C), want_par)
+        got = out.download().view(DT[cl]).reshape(p, S, nch)
+        want = _want_cell_csums(oracle, htype, cs, 1, want_par).reshape(p, S, nch)
+        assert np.array_equal(got, want), np.argwhere(got != want)[:5]
+    finally:
+        L.ecg_set_csum_variant(ctx.h, 0)
+        d.free(); par.free(); out.free()

@@ -178,6 +178,31 @@ PY
 		step bench_lib4 300 python bench.py --gpus 4 --sharder lib --allow-shared-device --steps 10 \
 			--warmup 2 --no-detail || exit $?
 		;;
+	tune14)
+		step tune14 600 python tools/tune14.py || exit $?
+		;;
+	tunetests)
+		step pytest_tuning 300 python -u -m pytest tests/test_gpu_tuning.py -q -x -p no:cacheprovider \
+			--timeout 120 --timeout-method thread
+		rc=$?; [ $rc -le 1 ] || exit $rc
+		;;
+	crcpmc)
+		rm -rf gpurun_out/pmc_lds
+		step rocprof_lds 120 rocprofv3 --kernel-trace --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE \
+			--output-format csv -d gpurun_out/pmc_lds -o run -- python3 tools/crc_pmc.py fused || exit $?
+		;;
+	crcpmc2)
+		rm -rf gpurun_out/pmc_sq1 gpurun_out/pmc_sq2
+		step rocprof_sq1 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE \
+			SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS \
+			--output-format csv -d gpurun_out/pmc_sq1 -o run -- python3 tools/crc_pmc.py fused || exit $?
+		step rocprof_sq2 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+			SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VMEM_WR \
+			--output-format csv -d gpurun_out/pmc_sq2 -o run -- python3 tools/crc_pmc.py fused || exit $?
+		;;
+	crcab)
+		step crc_ab 600 python tools/crc_ab.py || exit $?
+		;;
 	dist4)
 		step dist4 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
 			--master-port 29537 bench.py --gpus 4 --steps 20 --warmup 3 || exit $?
