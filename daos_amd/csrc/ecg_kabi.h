@@ -174,7 +174,11 @@ typedef struct ecg_mmcs_params {
 	uint32_t ncols;			/* columns per item */
 	uint32_t nh, nh_last;		/* items per chunk / in the last chunk */
 	uint32_t nitems;
-	uint32_t byte_tables;		/* 0 = 5-bit tables, 1 = byte tables (A/B) */
+	uint32_t byte_tables;		/* table kind TB: 0 5-bit, 1 slice-by-NB, 2 s16 */
+	uint32_t wave;			/* 1: one wave per (stripe, chunk) (ecg_mm_csum_wave_kernel):
+					 * kh = [2][64] lane multipliers (full chunk, last chunk),
+					 * checksums stored, not XORed (no zeroing needed) */
+	uint32_t pad3;
 	uint32_t row_slot[ECG_KMAX_R];
 } ecg_mmcs_params_t;
 

@@ -502,7 +502,7 @@ int ecg_matmul_csum(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, 
 	ecg_gf_init();
 	st = ecg_pick_stream(ctx, stream);
 	if (k <= ECG_KMAX_K && rows <= ECG_KMAX_R) {
-		fused = ecg_csum_fused_params(ctx, type, chunksize, rec_size, C, rows, csums, &q);
+		fused = ecg_csum_fused_params(ctx, type, chunksize, rec_size, C, k, rows, csums, &q);
 		if (fused < 0)
 			return fused;
 	}
@@ -529,8 +529,8 @@ int ecg_matmul_csum(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, 
 			for (j = 0; j < k; j++)
 				ecg_build_ptbl(coef[(size_t)r * k + j], &prm->tbl[r][j]);
 		}
-		/* the fused kernel XORs per-wave partials into the checksums */
-		if (aligned16_ok(src, soff, k, sstride, dst, doff, rows, dstride)) {
+		/* the workgroup kernel XORs per-wave partials into the checksums */
+		if (!q.wave && aligned16_ok(src, soff, k, sstride, dst, doff, rows, dstride)) {
 			hipError_t he = hipMemsetAsync(csums, 0, (size_t)rows * S * q.nch * (size_t)cl, st);
 
 			if (he != hipSuccess) {

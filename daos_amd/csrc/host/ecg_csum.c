@@ -484,6 +484,71 @@ static int fused_kh(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, uint3
 	return rc;
 }
 
+/* Lane multipliers of the wave-per-chunk fused kernel (ecg_kabi.h
+ * ecg_mmcs_params wave): kw[0][l] = x^(8*16*(63-l)), kw[1][l] = the same
+ * times x^(-8Z), Z = zero bytes padding the last chunk (`last` bytes) to
+ * whole 1 KiB rows.  Cached with the kh tables (ncols = 0 marks them). */
+static int fused_kw(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, const void **out)
+{
+	const struct crc_def *d = &g_defs[type];
+	const uint64_t m_last = (last + ECG_CSUM_STRIDE - 1) / ECG_CSUM_STRIDE;
+	const uint64_t z = m_last * ECG_CSUM_STRIDE - last;
+	const size_t es = d->width == 64 ? 8 : 4;
+	const uint64_t un = crc_unshift(d, z), step = crc_xpow8(d, 16);
+	unsigned char img[2 * 64 * 8];
+	struct ecg_kh_ent *e;
+	uint64_t c = crc_one(d);
+	void *dev = NULL;
+	hipError_t he;
+
+	pthread_mutex_lock(&ctx->lock);
+	for (int i = 0; i < ECG_NKH_CACHE; i++) {
+		e = &ctx->kh_cache[i];
+		if (e->valid && e->type == type && e->rcs == rcs && e->last == last && e->ncols == 0) {
+			*out = e->dev;
+			pthread_mutex_unlock(&ctx->lock);
+			return 0;
+		}
+	}
+	for (int l = 63; l >= 0; l--) {
+		const uint64_t v[2] = {c, crc_mulmod(d, c, un)};
+
+		for (int row = 0; row < 2; row++) {
+			if (es == 8) {
+				memcpy(img + (row * 64 + l) * 8, &v[row], 8);
+			} else {
+				const uint32_t w = (uint32_t)v[row];
+
+				memcpy(img + (row * 64 + l) * 4, &w, 4);
+			}
+		}
+		c = crc_mulmod(d, c, step);
+	}
+	he = hipMalloc(&dev, 2 * 64 * es);
+	if (he == hipSuccess)
+		he = hipMemcpy(dev, img, 2 * 64 * es, hipMemcpyHostToDevice);
+	if (he != hipSuccess) {
+		if (dev)
+			(void)hipFree(dev);
+		pthread_mutex_unlock(&ctx->lock);
+		return ecg_hip_fail(he, "fused csum lane multipliers");
+	}
+	e = &ctx->kh_cache[ctx->kh_next++ % ECG_NKH_CACHE];
+	if (e->dev) {
+		(void)hipDeviceSynchronize();
+		(void)hipFree(e->dev);
+	}
+	e->valid = 1;
+	e->type = type;
+	e->rcs = rcs;
+	e->last = last;
+	e->ncols = 0;
+	e->dev = dev;
+	*out = dev;
+	pthread_mutex_unlock(&ctx->lock);
+	return 0;
+}
+
 int ecg_csum_extents(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_size,
 		     uint64_t rx_idx, uint64_t rx_nr, const void *buf, int64_t ext_stride,
 		     uint32_t n_ext, void *csums, void *stream)
@@ -585,7 +650,8 @@ int ecg_set_fused_cols(ecg_ctx_t *ctx, uint32_t ncols)
 
 int ecg_set_csum_variant(ecg_ctx_t *ctx, uint32_t variant)
 {
-	if (ctx == NULL || (variant & 15u) > 3 || variant > 127 || (variant & 48u) == 48u)
+	if (ctx == NULL || (variant & 15u) > 3 || variant > 511 || (variant & 48u) == 48u ||
+	    (variant & 384u) == 384u)
 		return ecg_fail(-ECG_DER_INVAL, "set_csum_variant: bad arguments");
 	ctx->csum_variant = variant;
 	return 0;
@@ -596,7 +662,7 @@ int ecg_set_csum_variant(ecg_ctx_t *ctx, uint32_t variant)
  * can take the request, 0 when the caller must run the product and
  * ecg_csum_extents separately, < 0 on error. */
 int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_size,
-			  uint64_t C, int rows, void *csums, ecg_mmcs_params_t *q)
+			  uint64_t C, int k, int rows, void *csums, ecg_mmcs_params_t *q)
 {
 	const uint64_t rcs = ecg_csum_record_chunksize(chunksize, rec_size);
 	const struct crc_def *d;
@@ -637,8 +703,17 @@ int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t
 		return 0;
 	q->nitems = (q->nch - 1) * q->nh + q->nh_last;
 	/* fused kernels: table kind TB (ecg_kernels.hip); bit 6 of csum_variant
-	 * selects the s16 tables (A/B) */
+	 * selects the s16 tables (A/B), bit 7 the wave-per-chunk kernel */
 	q->byte_tables = (ctx->csum_variant & 64u) ? 2 : use_byte_tables(ctx, type);
+	/* the wave-per-chunk kernel for crc64 with k <= 4 (one 64-step multiply
+	 * per lane per chunk instead of per thread per item: EC_4P2 crc64 +42 %
+	 * -> +29 % over the plain encode; with k = 8 its longer serial walk
+	 * loses, tools/crc_ab.py, profiles/r02/crc_ab_fused_wave.log); csum_variant
+	 * bit 7 forces it, bit 8 forbids it (A/B) */
+	q->wave = (ctx->csum_variant & 128u) != 0 ||
+		  (!(ctx->csum_variant & 256u) && type == ECG_HASH_CRC64 && k <= 4);
+	if (q->wave)
+		return fused_kw(ctx, type, rcs, last, &q->kh) ? -ECG_DER_NOMEM : 1;
 	rc = fused_kh(ctx, type, rcs, last, q->ncols, q->nh, q->nh_last, &q->kh);
 	if (rc)
 		return rc;

@@ -126,7 +126,7 @@ int ecg_segs_launch(const struct ecg_segs *v, const void *segs_dev, hipStream_t 
 /* checksums (ecg_csum.c) */
 void ecg_csum_ctx_fini(ecg_ctx_t *ctx);
 int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_size,
-			  uint64_t C, int rows, void *csums, ecg_mmcs_params_t *q);
+			  uint64_t C, int k, int rows, void *csums, ecg_mmcs_params_t *q);
 
 /* product + chunk checksums of every output cell, cells as extents from
  * record index 0; csums[row_slot[r]][s][chunk] (ecg_core.c) */

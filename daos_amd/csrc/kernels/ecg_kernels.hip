@@ -552,6 +552,148 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	}
 }
 
+// Fused product + checksum, one WAVE per (stripe, chunk): the wave walks the
+// chunk's 1 KiB rows in order (lane l: bytes 16l..16l+15 of each row, every
+// load and store a coalesced 1 KiB), computes and stores the product exactly
+// as ecg_mm_kernel does, and Horner-accumulates each output row's pieces
+// with the 1 KiB shift.  At the chunk end each lane multiplies by
+// Q.kh[last][lane] = x^(8*16*(63-lane)) (x^(-8Z) for a last chunk padded by Z
+// zero bytes), the wave XOR-reduces and lane 0 stores the checksum: no
+// atomics, no memset, and one W-step multiply per lane per CHUNK (32 KiB:
+// 32 rows) instead of one per thread per work item of the workgroup kernel
+// -- the multiply dominates crc64's cost there (tools/fused_sweep.py).
+// Tables (TB as ecg_mm_csum_kernel) with the 1 KiB shift.
+template <int K, int R, int W, bool REFL, int TB>
+__global__ void __launch_bounds__(BLOCK, 4)
+ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
+{
+	using T = typename ecg_crc::reg<W>::T;
+	using F5 = ecg_crc::f5<W>;
+	constexpr int NB = W / 8;
+	constexpr int KM = K ? K : ECG_KMAX_K;
+	constexpr int RM = R ? R : ECG_KMAX_R;
+	constexpr bool PF = K != 0 && K <= 8 && W != 64;	// next row's loads in flight
+	constexpr int T2V = (RM + 3) / 4;
+	constexpr int PER_J = RM + T2V;
+	constexpr int NSL = TB == 0 ? F5::N : TB == 1 ? NB * 256 : 16 * 256;
+	__shared__ u32x4 s_tbl[KM * PER_J];
+	__shared__ T s_sl[NSL];
+	__shared__ T s_sh[TB ? NB * 256 : 1];
+	const int k = K ? K : (int)P.k;
+	const int rows = R ? R : (int)P.rows;
+	const uint64_t C = P.cell_bytes;
+	const int lane = threadIdx.x & 63;
+	const uint32_t lo = (uint32_t)lane * 16u;
+	const T *gt = (const T *)Q.tbl;
+
+	for (int i = threadIdx.x; i < KM * RM; i += BLOCK) {
+		const int j = i / RM, r = i % RM;
+		if (j < k && r < rows) {
+			const ecg_ptbl_t &t = P.tbl[r][j];
+			s_tbl[j * PER_J + r] = (u32x4){t.t0lo, t.t0hi, t.t1lo, t.t1hi};
+			reinterpret_cast<uint32_t *>(&s_tbl[j * PER_J + RM])[r] = t.t2;
+		}
+	}
+	if constexpr (TB != 0) {
+		for (int i = threadIdx.x; i < NSL; i += BLOCK)
+			s_sl[i] = gt[(TB == 1 ? 0 : ECG_CSUM_OFF_S16(NB)) + i];
+		for (int i = threadIdx.x; i < NB * 256; i += BLOCK)
+			s_sh[i] = gt[ECG_CSUM_OFF_SH(NB) + i];
+	} else {
+		ecg_crc::stage5<W>(s_sl, gt, ECG_CSUM_OFF_A5_1K(NB), BLOCK);
+	}
+	const T *kw = (const T *)Q.kh;
+	const T poly = (T)Q.poly;
+	__syncthreads();
+
+	const uint64_t total = (uint64_t)P.nstripes * Q.nch;
+	// the wave index is wave-uniform: readfirstlane keeps the item's offsets
+	// in SGPRs (mm_load / mm_compute require it)
+	const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	for (uint64_t g = (uint64_t)blockIdx.x * (BLOCK / 64) + wv; g < total;
+	     g += (uint64_t)gridDim.x * (BLOCK / 64)) {
+		const uint32_t s = (uint32_t)(g / Q.nch), c = (uint32_t)(g - (uint64_t)s * Q.nch);
+		const bool lastc = c + 1 == Q.nch;
+		const uint64_t c0 = (uint64_t)c * Q.chunk_bytes;
+		const uint64_t len = lastc ? C - c0 : Q.chunk_bytes;
+		const uint32_t m = (uint32_t)((len + ECG_CSUM_STRIDE - 1) / ECG_CSUM_STRIDE);
+		T crc[RM];
+		u32x4 xa[KM];
+
+#pragma unroll
+		for (int r = 0; r < RM; r++)
+			crc[r] = 0;
+		if constexpr (PF) {
+			if (c0 + lo + 16 <= C)
+				mm_load<KM, false>(P, k, s, c0, lo, xa);
+		}
+		for (uint32_t i = 0; i < m; i++) {
+			const uint64_t cbase = c0 + (uint64_t)i * ECG_CSUM_STRIDE;
+			const bool have = cbase + lo + 16 <= C;		// C % 16 == 0
+			u32x4 outv[RM];
+			u32x4 xb[PF ? KM : 1];
+			uint32_t z = 0;
+
+			if constexpr (PF) {
+				if (i + 1 < m && cbase + ECG_CSUM_STRIDE + lo + 16 <= C)
+					mm_load<KM, false>(P, k, s, cbase + ECG_CSUM_STRIDE, lo, xb);
+			} else if (have) {
+				mm_load<KM, false>(P, k, s, cbase, lo, xa);
+			}
+			asm volatile("" : "+v"(z));
+			const u32x4 *tb = s_tbl + z;
+			if (cbase + ECG_CSUM_STRIDE <= C)
+				mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, xa, outv);
+			else if (have)
+				mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, xa, outv);
+#pragma unroll
+			for (int r = 0; r < RM; r++) {
+				if (r < rows) {
+					if constexpr (TB != 0)
+						crc[r] = ecg_crc::lin_map<W>(crc[r], s_sh);
+					else
+						crc[r] = ecg_crc::lin_map5<W>(crc[r], s_sl + F5::NF * 32);
+					if (have) {
+						uint32_t d[4] = {outv[r][0], outv[r][1], outv[r][2], outv[r][3]};
+						if (i == 0 && lane == 0) {	// initial register
+							d[0] ^= (uint32_t)Q.init;
+							if constexpr (W == 64)
+								d[1] ^= (uint32_t)(Q.init >> 32);
+						}
+						if constexpr (TB == 1)
+							crc[r] ^= ecg_crc::piece_crc<W, REFL>(d, s_sl);
+						else if constexpr (TB == 2)
+							crc[r] ^= ecg_crc::piece_crc16<W>(d, s_sl);
+						else
+							crc[r] ^= ecg_crc::piece_crc5<W>(d, s_sl);
+					}
+				}
+			}
+			if constexpr (PF) {
+#pragma unroll
+				for (int j = 0; j < KM; j++)
+					xa[j] = xb[j];
+			}
+		}
+		const T kcur = kw[(lastc ? 64 : 0) + lane];
+#pragma unroll
+		for (int r = 0; r < RM; r++) {
+			if (r < rows) {
+				T v = ecg_crc::mulmod<W, REFL>(kcur, crc[r], poly);
+				v = ecg_crc::wave_xor(v);
+				if (lane == 0) {
+					const uint64_t slot = ((uint64_t)Q.row_slot[r] * P.nstripes + s) * Q.nch + c;
+					v ^= (T)Q.xorout;
+					if constexpr (W == 16)
+						((uint16_t *)Q.out)[slot] = (uint16_t)v;
+					else
+						((T *)Q.out)[slot] = v;
+				}
+			}
+		}
+	}
+}
+
 template <int KM, int RM>
 __device__ __forceinline__ void mm_ptr_item(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
 					    uint32_t s, uint64_t cbase, uint32_t lo, const uint64_t *a)
@@ -795,6 +937,21 @@ static const csentry g_cskernels[] = {
 	CSB(8, 1, 2, 32, true, "crc32", 2),
 };
 #define N_CSKERNELS ((uint32_t)(sizeof(g_cskernels) / sizeof(g_cskernels[0])))
+
+#define CSW(K_, R_, T_, W_, RF_, N_) \
+	{K_, R_, T_, ecg_mm_csum_wave_kernel<K_, R_, W_, RF_, W_ == 64 ? 1 : 0>, \
+	 "ecg_mm_csum_wave_kernel<" #K_ "," #R_ "," N_ ">", W_ == 64 ? 1 : 0}
+#define CSW3(K_, R_) CSW(K_, R_, 1, 16, false, "crc16"), CSW(K_, R_, 2, 32, true, "crc32"), \
+		     CSW(K_, R_, 3, 64, true, "crc64")
+
+static const csentry g_cswkernels[] = {
+	CSW3(2, 1), CSW3(4, 2), CSW3(8, 1), CSW3(8, 2), CSW3(16, 2), CSW3(0, 0),
+	/* the default path for crc64 with k <= 4 (ecg_csum.c) */
+	CSW(2, 2, 3, 64, true, "crc64"), CSW(2, 3, 3, 64, true, "crc64"), CSW(4, 1, 3, 64, true, "crc64"),
+	CSW(4, 3, 3, 64, true, "crc64"),
+};
+#define N_CSWKERNELS ((uint32_t)(sizeof(g_cswkernels) / sizeof(g_cswkernels[0])))
+#define KID_FUSED_WAVE 800u
 #define KID_FUSED 500u		/* fused kernel ids: KID_FUSED + index */
 
 typedef void (*mmptr_fn_t)(const ecg_mm_params_t, const uint64_t *);
@@ -854,6 +1011,8 @@ extern "C" const char *ecg_k_kernel_name(uint32_t id)
 		return ecg_k_csum_kernel_name(id);
 	if (id >= KID_FUSED && id < KID_FUSED + N_CSKERNELS)
 		return g_cskernels[id - KID_FUSED].name;
+	if (id >= KID_FUSED_WAVE && id < KID_FUSED_WAVE + N_CSWKERNELS)
+		return g_cswkernels[id - KID_FUSED_WAVE].name;
 	if (id >= KID_PTR && id < KID_PTR + N_PKERNELS)
 		return g_pkernels[id - KID_PTR].name;
 	if (id == KID_PTR_BYTE)
@@ -980,6 +1139,30 @@ extern "C" int ecg_k_launch_matmul_csum(const ecg_mm_params_t *p, const ecg_mmcs
 	if (!aligned16(p) || p->accumulate || p->diff || (p->cell_bytes & 15u) ||
 	    (q->chunk_bytes % CHUNK_BYTES) || q->chunk_bytes == 0)
 		return 1;
+	if (q->wave) {
+		const csentry *tab = g_cswkernels;
+		uint32_t n = N_CSWKERNELS, w = n;
+
+		for (uint32_t i = 0; i < n && w == n; i++)
+			if (tab[i].type == (int)q->type && tab[i].k == (int)p->k && tab[i].r == (int)p->rows &&
+			    tab[i].b8 == (int)q->byte_tables)
+				w = i;
+		for (uint32_t i = 0; i < n && w == n; i++)
+			if (tab[i].type == (int)q->type && tab[i].k == 0 && tab[i].b8 == (int)q->byte_tables)
+				w = i;
+		if (w == n || q->kh == nullptr)
+			return (int)hipErrorInvalidValue;
+		const uint64_t items = (uint64_t)p->nstripes * q->nch;
+		uint64_t gx = (items + BLOCK / 64 - 1) / (BLOCK / 64);
+		if (cfg && cfg->grid_x)
+			gx = cfg->grid_x;
+		if (gx > 0x7fffffffu)
+			gx = 0x7fffffffu;
+		hipLaunchKernelGGL(tab[w].fn, dim3((uint32_t)gx), dim3(BLOCK), 0, (hipStream_t)stream, *p, *q);
+		if (kernel_id)
+			*kernel_id = KID_FUSED_WAVE + w;
+		return (int)hipGetLastError();
+	}
 	for (uint32_t i = 0; i < N_CSKERNELS; i++)
 		if (g_cskernels[i].type == (int)q->type && g_cskernels[i].k == (int)p->k &&
 		    g_cskernels[i].r == (int)p->rows && g_cskernels[i].b8 == (int)q->byte_tables) {

@@ -91,11 +91,16 @@ int ecg_recover_csum(ecg_ctx_t *ctx, int k, int p, uint64_t cell_bytes, uint32_t
  * stride beyond); 0 restores the default. */
 int ecg_set_csum_launch(ecg_ctx_t *ctx, uint32_t max_blocks);
 
-/* Launch tuning: CRC kernel shape for 16-byte aligned extents -- 0 by shape
- * (default: a workgroup per chunk when chunks are long and few, a 16-lane
- * group per chunk when chunks are <= 8 KiB), 1 one wave per chunk, 2 one
- * workgroup per chunk, 3 one 16-lane group per chunk.  Same results either
- * way. */
+/* Launch tuning (A/B measurements; same results either way).  Bits 0-3, CRC
+ * kernel shape for 16-byte aligned extents: 0 by shape (default: a workgroup
+ * per chunk when chunks are long and few, a 16-lane group per chunk when
+ * chunks are <= 8 KiB), 1 one wave per chunk, 2 one workgroup per chunk, 3 one
+ * 16-lane group per chunk.  CRC lookup tables (default per hash: 5-bit for
+ * crc16/crc32, byte tables for crc64): bit 4 forces the byte tables, bit 5 the
+ * 5-bit tables, bit 6 the 16-slice byte tables in the fused kernels.  Fused
+ * kernel shape (default: a wave per chunk for crc64 with k <= 4, else
+ * workgroups over work items): bit 7 forces the wave per chunk, bit 8 the
+ * workgroups. */
 int ecg_set_csum_variant(ecg_ctx_t *ctx, uint32_t variant);
 
 /* Launch tuning: 4 KiB columns per work item of the fused product +

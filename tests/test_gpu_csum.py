@@ -187,10 +187,12 @@ FUSED = [
 ]
 
 
+@pytest.mark.parametrize("wave", [0, 128])
 @pytest.mark.parametrize("case", FUSED)
-def test_encode_csum_fused(oracle, ecglib, ctx, case):
+def test_encode_csum_fused(oracle, ecglib, ctx, case, wave):
     k, p, C, S, cs, rb, htype = case
     L = ecglib.lib()
+    assert L.ecg_set_csum_variant(ctx.h, wave) == 0
     nch = L.ecg_csum_chunk_count(cs, rb, 0, C // rb)
     cl = L.ecg_csum_len(htype)
     rng = np.random.default_rng(sum(case))
@@ -201,7 +203,7 @@ def test_encode_csum_fused(oracle, ecglib, ctx, case):
     try:
         ctx.encode_csum(k, p, C, S, d.ptr, k * C, par.ptr, S * C, C, htype, cs, rb, out.ptr)
         ctx.sync()
-        assert "ecg_mm_csum_kernel" in L.ecg_last_kernel().decode(), L.ecg_last_kernel()
+        assert "ecg_mm_csum" in L.ecg_last_kernel().decode(), L.ecg_last_kernel()
         got_par = par.download().reshape(p, S, C)
         want_par = oracle.encode_batch(k, p, C, S, data, nthreads=8, simd=True).reshape(p, S, C)
         assert np.array_equal(got_par, want_par)
@@ -209,6 +211,7 @@ def test_encode_csum_fused(oracle, ecglib, ctx, case):
         want = _want_cell_csums(oracle, htype, cs, rb, want_par).reshape(p, S, nch)
         assert np.array_equal(got, want), np.argwhere(got != want)[:5]
     finally:
+        L.ecg_set_csum_variant(ctx.h, 0)
         d.free(); par.free(); out.free()
 
 
@@ -240,7 +243,7 @@ def test_encode_csum_fused_items(oracle, ecglib, ctx, case, cols):
     try:
         ctx.encode_csum(k, p, C, S, d.ptr, k * C, par.ptr, S * C, C, htype, cs, 1, out.ptr)
         ctx.sync()
-        assert "ecg_mm_csum_kernel" in L.ecg_last_kernel().decode(), L.ecg_last_kernel()
+        assert "ecg_mm_csum" in L.ecg_last_kernel().decode(), L.ecg_last_kernel()
         want_par = oracle.encode_batch(k, p, C, S, data, nthreads=8, simd=True).reshape(p, S, C)
         assert np.array_equal(par.download().reshape(p, S, C), want_par)
         got = out.download().view(DT[cl]).reshape(p, S, nch)
@@ -253,9 +256,11 @@ def test_encode_csum_fused_items(oracle, ecglib, ctx, case, cols):
 
 @pytest.mark.parametrize("errs", [[3, 9], [9, 3], [8, 9], [0], [0, 1], [5]])
 @pytest.mark.parametrize("htype", (2, 3))
-def test_recover_csum_fused(oracle, ecglib, ctx, errs, htype):
+@pytest.mark.parametrize("wave", [0, 128])
+def test_recover_csum_fused(oracle, ecglib, ctx, errs, htype, wave):
     k, p, C, S, cs = 8, 2, 256 << 10, 6, 32768
     L = ecglib.lib()
+    assert L.ecg_set_csum_variant(ctx.h, wave) == 0
     nch = C // cs
     cl = L.ecg_csum_len(htype)
     rng = np.random.default_rng(len(errs) * 10 + htype)
@@ -279,6 +284,7 @@ def test_recover_csum_fused(oracle, ecglib, ctx, errs, htype):
             want = _want_cell_csums(oracle, htype, cs, 1, stripes[:, e])
             assert np.array_equal(got[i], want), (e, i)
     finally:
+        L.ecg_set_csum_variant(ctx.h, 0)
         d.free(); out.free()
 
 
@@ -365,7 +371,7 @@ def test_crc_table_kinds(oracle, ecglib, ctx, kind, shape, htype, geom):
     assert np.array_equal(got, oracle.csum_extents(htype, cs, rb, idx, nr, host))
 
 
-@pytest.mark.parametrize("kind", [16, 32, 64])      # fused TB 1 / 0 / 2 forced
+@pytest.mark.parametrize("kind", [16, 32, 64, 128, 144, 160])   # fused TB 1 / 0 / 2; wave kernel
 @pytest.mark.parametrize("case", [(8, 2, 1 << 20, 3, 32768, 2), (8, 2, 1 << 20, 3, 32768, 3),
                                   (4, 2, 256 << 10, 5, 32768, 2), (4, 2, 256 << 10, 5, 32768, 3),
                                   (8, 1, 3 * 65536 + 48, 4, 65536, 2)])

@@ -62,7 +62,7 @@ def main():
         for rnd in range(2):
             row["encode_ms"].append(round(timed(lambda: ctx.encode(k, p, C, S, buf.ptr, k * C, par.ptr, pitch, C)), 4))
             for hname, htype in (("crc32", 2), ("crc64", 3)):
-                for tag, var in (("dflt", 0), ("tb0", 32), ("tb1", 16), ("tb2", 64)):
+                for tag, var in (("dflt", 0), ("wave", 128), ("wave_tb0", 160), ("wave_tb1", 144)):
                     L.ecg_set_csum_variant(ctx.h, var)
                     try:
                         ms = timed(lambda: ctx.encode_csum(k, p, C, S, buf.ptr, k * C, par.ptr, pitch, C, htype, 32768,
