@@ -36,7 +36,10 @@ using namespace ecg_crc;
 
 constexpr int CS_BLOCK = 256;
 constexpr int CS_WAVES = CS_BLOCK / 64;
-constexpr int CS_UNROLL = 4;		// pieces in flight per lane
+#ifndef ECG_CS_UNROLL
+#define ECG_CS_UNROLL 4
+#endif
+constexpr int CS_UNROLL = ECG_CS_UNROLL;	// pieces in flight per lane
 constexpr uint32_t ADLER_MOD = 65521;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 

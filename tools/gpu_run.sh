@@ -200,6 +200,10 @@ PY
 			SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VMEM_WR \
 			--output-format csv -d gpurun_out/pmc_sq2 -o run -- python3 tools/crc_pmc.py fused || exit $?
 		;;
+	pmcjson)
+		python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write "ecg_mm_kernel<4, 2" 6442450944 \
+			gpurun_out/pmc_traffic.json || exit $?
+		;;
 	crcab)
 		step crc_ab 600 python tools/crc_ab.py || exit $?
 		;;
