@@ -106,7 +106,17 @@ typedef struct ecg_launch_cfg {
 /* s16[16][256]: register after byte v and then j zero bytes, j < 16 (the
  * raw CRC of a 16-byte piece is 16 independent lookups, no serial fold) */
 #define ECG_CSUM_OFF_S16(NB) (ECG_CSUM_OFF_A5_4K(NB) + ECG_CSUM_NA5(NB) * 32)
-#define ECG_CSUM_TBL_ENTRIES(NB) (ECG_CSUM_OFF_S16(NB) + 16 * 256)
+/* positional p5 tables: p5x*[u-1] = p5 followed by u strides (1 KiB / 256 B)
+ * of zero bytes, u = 1 .. ECG_CSUM_P5U-1 (the standalone CRC kernels shift the
+ * register once per ECG_CSUM_P5U pieces: a5 of 4 KiB / 1 KiB) */
+#define ECG_CSUM_P5U 4
+#define ECG_CSUM_OFF_P5X_1K(NB) (ECG_CSUM_OFF_S16(NB) + 16 * 256)
+#define ECG_CSUM_OFF_P5X_256(NB) (ECG_CSUM_OFF_P5X_1K(NB) + (ECG_CSUM_P5U - 1) * ECG_CSUM_NF5 * 32)
+/* the fused workgroup kernel's 4 KiB column stride: positions and the a5 of
+ * ECG_CSUM_P5U columns */
+#define ECG_CSUM_OFF_P5X_4K(NB) (ECG_CSUM_OFF_P5X_256(NB) + (ECG_CSUM_P5U - 1) * ECG_CSUM_NF5 * 32)
+#define ECG_CSUM_OFF_A5_16K(NB) (ECG_CSUM_OFF_P5X_4K(NB) + (ECG_CSUM_P5U - 1) * ECG_CSUM_NF5 * 32)
+#define ECG_CSUM_TBL_ENTRIES(NB) (ECG_CSUM_OFF_A5_16K(NB) + ECG_CSUM_NA5(NB) * 32)
 #define ECG_CSUM_OFF_P2(NB) (3 * (NB) * 256 + 64 + 256)
 #define ECG_CSUM_OFF_SH256(NB) (3 * (NB) * 256 + 64 + 256 + ECG_CSUM_NP2)
 #define ECG_CSUM_GLANES 16	/* lanes per chunk in the lane-group CRC kernel */
@@ -143,6 +153,13 @@ typedef struct ecg_csum_params {
 } ecg_csum_params_t;
 
 #define ECG_CSUM_SPLIT_NW 8
+/* 1 KiB steps of a wave over len bytes (lanes take 16-byte pieces; a zero
+ * prefix pads to a whole number of ECG_CSUM_P5U-piece Horner steps), and the
+ * steps of each of the split kernel's ECG_CSUM_SPLIT_NW slices */
+#define ECG_CSUM_STEPS(len) \
+	((((len) / 16 + 63) / 64 + ECG_CSUM_P5U - 1) / ECG_CSUM_P5U * ECG_CSUM_P5U)
+#define ECG_CSUM_SPLIT_MS(m) \
+	((((m) + ECG_CSUM_SPLIT_NW - 1) / ECG_CSUM_SPLIT_NW + ECG_CSUM_P5U - 1) / ECG_CSUM_P5U * ECG_CSUM_P5U)
 
 /*
  * Fused product + checksum: a launch of the GF product (ecg_mm_params_t)

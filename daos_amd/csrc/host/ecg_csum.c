@@ -24,18 +24,20 @@ static const struct crc_def g_defs[4] = {
 	[ECG_HASH_CRC64] = {64, 1, 0xC96C5795D7870F42ull, ~0ull, ~0ull},
 };
 
-/* CRC table kind (tools/crc_ab.py, profiles/r02/crc_ab.json): the 5-bit
- * conflict-free tables for crc16 / crc32 (crc32 over 32 KiB chunks 3.9 ->
- * 5.1 TB/s), the byte tables for crc64, where 41 eight-byte lookups per 16 B
- * lose to 24 conflicted ones.  csum_variant bit 4 forces the byte tables,
- * bit 5 the 5-bit tables (A/B runs). */
-static uint32_t use_byte_tables(const ecg_ctx_t *ctx, int type)
+/* CRC table kind (tools/crc_ab.py, profiles/r02/crc_ab*.log): the 5-bit
+ * conflict-free tables.  Standalone kernels (positional tables, one register
+ * shift per 4 pieces: 29.75 lookups per 16 B): every hash, crc32 over 32 KiB
+ * chunks 3.9 -> 5.3-5.5 TB/s, crc64 3.3 -> 3.8.  Fused kernels (one shift per
+ * piece, 35 / 42 lookups): crc16 / crc32; crc64 keeps the byte tables there
+ * (24 conflicted eight-byte lookups, no slower).  csum_variant bit 4 forces
+ * the byte tables, bit 5 the 5-bit tables (A/B runs). */
+static uint32_t use_byte_tables(const ecg_ctx_t *ctx, int type, int fused)
 {
 	if (ctx->csum_variant & 16u)
 		return 1;
 	if (ctx->csum_variant & 32u)
 		return 0;
-	return type == ECG_HASH_CRC64;
+	return fused && type == ECG_HASH_CRC64;
 }
 
 int ecg_csum_len(int type)
@@ -151,7 +153,7 @@ static uint64_t crc_xpow8(const struct crc_def *d, uint64_t n)
  * of m 1 KiB steps (ecg_kabi.h split_sh), cached per context by (type, m). */
 static void split_shifts(ecg_ctx_t *ctx, int type, uint64_t m, uint64_t *sh)
 {
-	const uint64_t ms = (m + ECG_CSUM_SPLIT_NW - 1) / ECG_CSUM_SPLIT_NW;
+	const uint64_t ms = ECG_CSUM_SPLIT_MS(m);
 	struct ecg_split_ent *e;
 
 	pthread_mutex_lock(&ctx->lock);
@@ -216,8 +218,9 @@ static uint64_t crc_raw(const struct crc_def *d, const unsigned char *buf, int l
 /* 5-bit field tables (ecg_kabi.h p5 / a5): field (dword j, field i) covers
  * bits 32j + 5i .. +4 of the piece or register; entry v = XOR of the basis
  * images of v's set bits.  a5 for a shift of n zero bytes. */
-static void build_p5(const struct crc_def *d, uint64_t *p5)
+static void build_p5(const struct crc_def *d, uint64_t zeros, uint64_t *p5)
 {
+	const uint64_t sh = zeros ? crc_xpow8(d, zeros) : 0;
 	uint64_t basis[128];
 	unsigned char piece[16];
 
@@ -225,6 +228,8 @@ static void build_p5(const struct crc_def *d, uint64_t *p5)
 		memset(piece, 0, sizeof(piece));
 		piece[k / 8] = (unsigned char)(1u << (k % 8));
 		basis[k] = crc_raw(d, piece, 16);
+		if (zeros)	/* the piece followed by `zeros` zero bytes */
+			basis[k] = crc_mulmod(d, basis[k], sh);
 	}
 	for (int f = 0; f < ECG_CSUM_NF5; f++) {
 		const int j = f / 7, i = f % 7;
@@ -307,7 +312,16 @@ static void *build_crc_tables(const struct crc_def *d, size_t *bytes)
 		t[ECG_CSUM_OFF_P2(nb) + j] = c;
 		c = crc_mulmod(d, c, c);
 	}
-	build_p5(d, t + ECG_CSUM_OFF_P5(nb));
+	build_p5(d, 0, t + ECG_CSUM_OFF_P5(nb));
+	for (int u = 1; u < ECG_CSUM_P5U; u++) {
+		build_p5(d, (uint64_t)u * ECG_CSUM_STRIDE,
+			 t + ECG_CSUM_OFF_P5X_1K(nb) + (size_t)(u - 1) * ECG_CSUM_NF5 * 32);
+		build_p5(d, (uint64_t)u * ECG_CSUM_GSTRIDE,
+			 t + ECG_CSUM_OFF_P5X_256(nb) + (size_t)(u - 1) * ECG_CSUM_NF5 * 32);
+		build_p5(d, (uint64_t)u * ECG_MMCS_STRIDE,
+			 t + ECG_CSUM_OFF_P5X_4K(nb) + (size_t)(u - 1) * ECG_CSUM_NF5 * 32);
+	}
+	build_a5(d, (uint64_t)ECG_CSUM_P5U * ECG_MMCS_STRIDE, t + ECG_CSUM_OFF_A5_16K(nb));
 	build_a5(d, ECG_CSUM_STRIDE, t + ECG_CSUM_OFF_A5_1K(nb));
 	build_a5(d, ECG_CSUM_GSTRIDE, t + ECG_CSUM_OFF_A5_256(nb));
 	build_a5(d, ECG_MMCS_STRIDE, t + ECG_CSUM_OFF_A5_4K(nb));
@@ -617,9 +631,9 @@ int ecg_csum_extents(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_
 		const int group = shape == 3 || (shape == 0 && !split && steps <= 8);
 
 		prm.variant = split ? 2 : group ? 3 : 1;
-		prm.byte_tables = use_byte_tables(ctx, type);
+		prm.byte_tables = use_byte_tables(ctx, type, 0);
 		for (int c = 0; split && c < 3; c++) {
-			prm.split_m[c] = (lens[c] / 16 + 63) / 64;
+			prm.split_m[c] = ECG_CSUM_STEPS(lens[c]);
 			split_shifts(ctx, type, prm.split_m[c], prm.split_sh[c]);
 		}
 	} else {
@@ -704,7 +718,7 @@ int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t
 	q->nitems = (q->nch - 1) * q->nh + q->nh_last;
 	/* fused kernels: table kind TB (ecg_kernels.hip); bit 6 of csum_variant
 	 * selects the s16 tables (A/B), bit 7 the wave-per-chunk kernel */
-	q->byte_tables = (ctx->csum_variant & 64u) ? 2 : use_byte_tables(ctx, type);
+	q->byte_tables = (ctx->csum_variant & 64u) ? 2 : use_byte_tables(ctx, type, 1);
 	/* the wave-per-chunk kernel for crc64 with k <= 4 (one 64-step multiply
 	 * per lane per chunk instead of per thread per item: EC_4P2 crc64 +42 %
 	 * -> +29 % over the plain encode; with k = 8 its longer serial walk

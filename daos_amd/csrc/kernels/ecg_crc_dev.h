@@ -91,6 +91,18 @@ __device__ __forceinline__ uint32_t fld5(uint32_t x, int i)
 	return i == 6 ? x >> 30 : (x >> (5 * i)) & 31u;
 }
 
+// 3-input XOR (one v_bitop3_b32 per 32 bits)
+__device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c)
+{
+	return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+__device__ __forceinline__ uint64_t x3(uint64_t a, uint64_t b, uint64_t c)
+{
+	return ((uint64_t)x3((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)) << 32) |
+	       x3((uint32_t)a, (uint32_t)b, (uint32_t)c);
+}
+
 // raw CRC (zero register) of one 16-byte piece: 28 lookups
 template <int W, typename T>
 __device__ __forceinline__ T piece_crc5(const uint32_t d[4], const T *p5)
@@ -104,23 +116,123 @@ __device__ __forceinline__ T piece_crc5(const uint32_t d[4], const T *p5)
 	return c;
 }
 
+// raw CRC of one 16-byte piece from the 5-bit tables at q5 + off bytes (off:
+// a wave-uniform multiple of the 32-entry table size, e.g. the position
+// table of a runtime position).  off is laundered so the compiler cannot
+// prove (field & mask) | off disjoint and turn the OR into an add: each
+// lookup address is then a shift and one v_and_or_b32, the cost of a fixed
+// table's lookup.
+template <int W, typename T>
+__device__ __forceinline__ T piece_crc5p(const uint32_t d[4], const T *q5, uint32_t off)
+{
+	constexpr uint32_t ES = sizeof(T) == 8 ? 3 : 2;	// log2 entry bytes
+	constexpr uint32_t M = 31u << ES, TS = 32u << ES;
+	const char *b = (const char *)q5;
+	T c = 0;
+
+	asm volatile("" : "+v"(off));
+#pragma unroll
+	for (int j = 0; j < 4; j++) {
+		const uint32_t x = d[j];
+		const char *t = b + 7 * TS * j;
+		const T e0 = *(const T *)(t + (((x << ES) & M) | off));
+		const T e1 = *(const T *)(t + TS + (((x >> (5 - ES)) & M) | off));
+		const T e2 = *(const T *)(t + 2 * TS + (((x >> (10 - ES)) & M) | off));
+		const T e3 = *(const T *)(t + 3 * TS + (((x >> (15 - ES)) & M) | off));
+		const T e4 = *(const T *)(t + 4 * TS + (((x >> (20 - ES)) & M) | off));
+		const T e5 = *(const T *)(t + 5 * TS + (((x >> (25 - ES)) & M) | off));
+		const T e6 = *(const T *)(t + 6 * TS + (((x >> (30 - ES)) & (3u << ES)) | off));
+		c = x3(c, e0, e1);
+		c = x3(c, e2, e3);
+		c = x3(c, e4, e5);
+		c ^= e6;
+	}
+	return c;
+}
+
+// ---- positional 5-bit tables: a Horner step over U = ECG_CSUM_P5U pieces
+// of a lane, q5[u] being p5 followed by u strides of zero bytes, so the
+// register is shifted once per U pieces (by U strides) instead of per piece:
+// acc' = shift_U(acc) ^ XOR_u q5[U-1-u](piece u).  LDS image: q5[U][NF][32]
+// then the a5 table of the U-stride shift.
+template <int W>
+struct f5u {
+	static constexpr int U = ECG_CSUM_P5U;
+	static constexpr int NF = ECG_CSUM_NF5;
+	static constexpr int NA = ECG_CSUM_NA5(W / 8);
+	static constexpr int N = (U * NF + NA) * 32;
+};
+
+// U pieces d[0..U-1] (in stream order) folded into acc
+template <int W, typename T>
+__device__ __forceinline__ T horner5u(T acc, const uint32_t (*d)[4], const T *q5)
+{
+	constexpr int U = f5u<W>::U, NF = ECG_CSUM_NF5;
+	const T *a5 = q5 + U * NF * 32;
+	T c;
+
+	if constexpr (W == 16) {
+		const uint32_t x = (uint32_t)acc;
+		c = x3(a5[(x & 31u)], a5[32 + ((x >> 5) & 31u)], a5[64 + ((x >> 10) & 31u)]);
+		c ^= a5[96 + ((x >> 15) & 31u)];
+	} else {
+		c = 0;
+#pragma unroll
+		for (int h = 0; h < W / 32; h++) {
+			const uint32_t x = (uint32_t)((uint64_t)acc >> (32 * h));
+			const T *a = a5 + 7 * 32 * h;
+			c = x3(c, a[fld5(x, 0)], a[32 + fld5(x, 1)]);
+			c = x3(c, a[64 + fld5(x, 2)], a[96 + fld5(x, 3)]);
+			c = x3(c, a[128 + fld5(x, 4)], a[160 + fld5(x, 5)]);
+			c ^= a[192 + fld5(x, 6)];
+		}
+	}
+#pragma unroll
+	for (int u = 0; u < U; u++) {
+		const T *p5 = q5 + (U - 1 - u) * NF * 32;
+#pragma unroll
+		for (int j = 0; j < 4; j++) {
+			const uint32_t x = d[u][j];
+			const T *t = p5 + 7 * 32 * j;
+			c = x3(c, t[fld5(x, 0)], t[32 + fld5(x, 1)]);
+			c = x3(c, t[64 + fld5(x, 2)], t[96 + fld5(x, 3)]);
+			c = x3(c, t[128 + fld5(x, 4)], t[160 + fld5(x, 5)]);
+			c ^= t[192 + fld5(x, 6)];
+		}
+	}
+	return c;
+}
+
+// stage q5 (p5 = position 0, positions 1..U-1 at gt + p5x_off) and the
+// U-stride a5 (gt + a5_off) into LDS s5[f5u<W>::N]
+template <int W, typename T>
+__device__ __forceinline__ void stage5u(T *s5, const T *gt, int p5x_off, int a5_off, int nthreads)
+{
+	constexpr int NB = W / 8, P = ECG_CSUM_NF5 * 32, U = f5u<W>::U;
+	for (int i = threadIdx.x; i < f5u<W>::N; i += nthreads)
+		s5[i] = i < P ? gt[ECG_CSUM_OFF_P5(NB) + i]
+		      : i < U * P ? gt[p5x_off + i - P] : gt[a5_off + i - U * P];
+}
+
 // register -> register shifted by the a5 table's fixed number of zero bytes
 template <int W, typename T>
 __device__ __forceinline__ T lin_map5(T c, const T *a5)
 {
-	T r = 0;
+	T r;
 	if constexpr (W == 16) {
 		const uint32_t x = (uint32_t)c;
-#pragma unroll
-		for (int i = 0; i < 4; i++)
-			r ^= a5[i * 32 + ((x >> (5 * i)) & 31u)];
+		r = x3(a5[(x & 31u)], a5[32 + ((x >> 5) & 31u)], a5[64 + ((x >> 10) & 31u)]);
+		r ^= a5[96 + ((x >> 15) & 31u)];
 	} else {
+		r = 0;
 #pragma unroll
 		for (int h = 0; h < W / 32; h++) {
 			const uint32_t x = (uint32_t)((uint64_t)c >> (32 * h));
-#pragma unroll
-			for (int i = 0; i < 7; i++)
-				r ^= a5[(7 * h + i) * 32 + fld5(x, i)];
+			const T *a = a5 + 7 * 32 * h;
+			r = x3(r, a[fld5(x, 0)], a[32 + fld5(x, 1)]);
+			r = x3(r, a[64 + fld5(x, 2)], a[96 + fld5(x, 3)]);
+			r = x3(r, a[128 + fld5(x, 4)], a[160 + fld5(x, 5)]);
+			r ^= a[192 + fld5(x, 6)];
 		}
 	}
 	return r;

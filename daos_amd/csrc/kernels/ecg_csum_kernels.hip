@@ -72,25 +72,44 @@ __device__ __forceinline__ void chunk_geom(const ecg_csum_params_t &p, uint64_t 
 	base = p.src + (int64_t)e * p.ext_stride + off;
 }
 
-// One Horner step of a lane's accumulator: acc * x^(8 * stride) ^ crc(piece),
-// with the 5-bit tables (s5 = p5 then a5) or the byte tables (B8: sl, sh).
-template <int W, bool REFL, bool B8, typename T>
-__device__ __forceinline__ T horner(T acc, const uint32_t d[4], const T *s5, const T *sl, const T *sh)
+// Horner steps of a lane's accumulator over the UN pieces d[0..UN-1] (those
+// with i + u < m): byte tables (B8: sl, sh), one step per piece, acc * x^(8 *
+// stride) ^ crc(piece); 5-bit tables (s5 = positional q5 then a5), one step
+// per UN = ECG_CSUM_P5U pieces (m is then a multiple of UN).
+template <int W, bool REFL, bool B8, int UN, typename T>
+__device__ __forceinline__ T horner(T acc, const uint32_t (*d)[4], int64_t i, int64_t m, const T *s5,
+				    const T *sl, const T *sh)
 {
-	if constexpr (B8)
-		return lin_map<W>(acc, sh) ^ piece_crc<W, REFL>(d, sl);
-	else
-		return lin_map5<W>(acc, s5 + f5<W>::NF * 32) ^ piece_crc5<W>(d, s5);
+	if constexpr (B8) {
+#pragma unroll
+		for (int u = 0; u < UN; u++)
+			if (i + u < m)
+				acc = lin_map<W>(acc, sh) ^ piece_crc<W, REFL>(d[u], sl);
+		return acc;
+	} else {
+		static_assert(UN == ECG_CSUM_P5U, "5-bit path steps ECG_CSUM_P5U pieces at a time");
+		return horner5u<W>(acc, d, s5);
+	}
 }
 
-// LDS images of one kernel: the 5-bit tables (p5, a5), or (B8) the byte tables
+// LDS images of one kernel: the positional 5-bit tables (q5, a5), or (B8) the
+// byte tables; UN pieces in flight per lane
 template <int W, bool B8>
 struct crc_lds {
 	using T = typename reg<W>::T;
 	static constexpr int NB = W / 8;
-	static constexpr int N5 = B8 ? 1 : f5<W>::N;
+	static constexpr int N5 = B8 ? 1 : f5u<W>::N;
 	static constexpr int NSL = B8 ? NB * 256 : 1;
+	static constexpr int UN = B8 ? CS_UNROLL : ECG_CSUM_P5U;
 };
+
+// lane steps of a chunk of nq pieces, `per` pieces per step
+template <bool B8>
+__device__ __forceinline__ int64_t lane_steps(int64_t nq, int64_t per)
+{
+	const int64_t m = (nq + per - 1) / per;
+	return B8 ? m : (m + ECG_CSUM_P5U - 1) / ECG_CSUM_P5U * ECG_CSUM_P5U;
+}
 
 template <int W, bool REFL, bool ALIGNED, bool B8>
 __global__ __launch_bounds__(CS_BLOCK) void ecg_crc_kernel(ecg_csum_params_t p)
@@ -109,7 +128,7 @@ __global__ __launch_bounds__(CS_BLOCK) void ecg_crc_kernel(ecg_csum_params_t p)
 			sh[i] = gt[NB * 256 + i];
 		}
 	} else {
-		stage5<W>(s5, gt, ECG_CSUM_OFF_A5_1K(NB), CS_BLOCK);
+		stage5u<W>(s5, gt, ECG_CSUM_OFF_P5X_1K(NB), ECG_CSUM_OFF_A5_4K(NB), CS_BLOCK);
 	}
 	const int lane = threadIdx.x & 63;
 	const T klane = gt[2 * NB * 256 + lane];
@@ -124,14 +143,14 @@ __global__ __launch_bounds__(CS_BLOCK) void ecg_crc_kernel(ecg_csum_params_t p)
 
 		chunk_geom(p, g, off, len, base);
 		const int64_t nq = (int64_t)(len / 16);
-		const int64_t m = (nq + 63) / 64;
+		const int64_t m = lane_steps<B8>(nq, 64);
 		const int64_t z = m * 64 - nq;
 		T acc = 0;
 
-		for (int64_t i = 0; i < m; i += CS_UNROLL) {
-			uint32_t d[CS_UNROLL][4];
+		for (int64_t i = 0; i < m; i += L::UN) {
+			uint32_t d[L::UN][4];
 #pragma unroll
-			for (int u = 0; u < CS_UNROLL; u++) {
+			for (int u = 0; u < L::UN; u++) {
 				const int64_t q = (i + u) * 64 + lane - z;
 				if (i + u < m && q >= 0) {
 					load16<ALIGNED>(base + 16 * q, d[u]);
@@ -144,11 +163,7 @@ __global__ __launch_bounds__(CS_BLOCK) void ecg_crc_kernel(ecg_csum_params_t p)
 					d[u][0] = d[u][1] = d[u][2] = d[u][3] = 0;
 				}
 			}
-#pragma unroll
-			for (int u = 0; u < CS_UNROLL; u++) {
-				if (i + u < m)
-					acc = horner<W, REFL, B8>(acc, d[u], s5, sl, sh);
-			}
+			acc = horner<W, REFL, B8, L::UN>(acc, d, i, m, s5, sl, sh);
 		}
 		acc = mulmod<W, REFL>(klane, acc, poly);
 		acc = wave_xor(acc);
@@ -202,7 +217,7 @@ __global__ __launch_bounds__(CS_BLOCK) void ecg_crc_group_kernel(ecg_csum_params
 			sh[i] = gt[ECG_CSUM_OFF_SH256(NB) + i];
 		}
 	} else {
-		stage5<W>(s5, gt, ECG_CSUM_OFF_A5_256(NB), CS_BLOCK);
+		stage5u<W>(s5, gt, ECG_CSUM_OFF_P5X_256(NB), ECG_CSUM_OFF_A5_1K(NB), CS_BLOCK);
 	}
 	const int lane = threadIdx.x & 63, gl = lane % G;
 	const T klane = gt[ECG_CSUM_OFF_K64(NB) + 64 - G + gl];
@@ -223,14 +238,14 @@ __global__ __launch_bounds__(CS_BLOCK) void ecg_crc_group_kernel(ecg_csum_params
 		if (live)
 			chunk_geom(p, g, off, len, base);
 		const int64_t nq = (int64_t)(len / 16);
-		const int64_t m = (nq + G - 1) / G;
+		const int64_t m = lane_steps<B8>(nq, G);
 		const int64_t z = m * G - nq;
 		T acc = 0;
 
-		for (int64_t i = 0; i < m; i += CS_UNROLL) {
-			uint32_t d[CS_UNROLL][4];
+		for (int64_t i = 0; i < m; i += L::UN) {
+			uint32_t d[L::UN][4];
 #pragma unroll
-			for (int u = 0; u < CS_UNROLL; u++) {
+			for (int u = 0; u < L::UN; u++) {
 				const int64_t q = (i + u) * G + gl - z;
 				if (i + u < m && q >= 0) {
 					load16<true>(base + 16 * q, d[u]);
@@ -243,11 +258,7 @@ __global__ __launch_bounds__(CS_BLOCK) void ecg_crc_group_kernel(ecg_csum_params
 					d[u][0] = d[u][1] = d[u][2] = d[u][3] = 0;
 				}
 			}
-#pragma unroll
-			for (int u = 0; u < CS_UNROLL; u++) {
-				if (i + u < m)
-					acc = horner<W, REFL, B8>(acc, d[u], s5, sl, sh);
-			}
+			acc = horner<W, REFL, B8, L::UN>(acc, d, i, m, s5, sl, sh);
 		}
 		acc = mulmod<W, REFL>(klane, acc, poly);
 #pragma unroll
@@ -295,7 +306,7 @@ __global__ __launch_bounds__(64 * NW) void ecg_crc_split_kernel(ecg_csum_params_
 			sh[i] = gt[NB * 256 + i];
 		}
 	} else {
-		stage5<W>(s5, gt, ECG_CSUM_OFF_A5_1K(NB), 64 * NW);
+		stage5u<W>(s5, gt, ECG_CSUM_OFF_P5X_1K(NB), ECG_CSUM_OFF_A5_4K(NB), 64 * NW);
 	}
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 	const T klane = gt[2 * NB * 256 + lane];
@@ -310,18 +321,19 @@ __global__ __launch_bounds__(64 * NW) void ecg_crc_split_kernel(ecg_csum_params_
 		const uint8_t *base;
 
 		chunk_geom(p, g, off, len, base);
+		static_assert(NW == ECG_CSUM_SPLIT_NW, "host split shifts assume ECG_CSUM_SPLIT_NW slices");
 		const int64_t nq = (int64_t)(len / 16);
-		const int64_t m = (nq + 63) / 64;
+		const int64_t m = (int64_t)ECG_CSUM_STEPS((uint64_t)len);	// as the host's split_m
 		const int64_t z = m * 64 - nq;
-		const int64_t ms = (m + NW - 1) / NW;
+		const int64_t ms = (int64_t)ECG_CSUM_SPLIT_MS((uint64_t)m);
 		const int64_t i0 = wv * ms < m ? wv * ms : m;
 		const int64_t i1 = i0 + ms < m ? i0 + ms : m;
 		T acc = 0;
 
-		for (int64_t i = i0; i < i1; i += CS_UNROLL) {
-			uint32_t d[CS_UNROLL][4];
+		for (int64_t i = i0; i < i1; i += L::UN) {
+			uint32_t d[L::UN][4];
 #pragma unroll
-			for (int u = 0; u < CS_UNROLL; u++) {
+			for (int u = 0; u < L::UN; u++) {
 				const int64_t q = (i + u) * 64 + lane - z;
 				if (i + u < i1 && q >= 0) {
 					load16<true>(base + 16 * q, d[u]);
@@ -334,11 +346,7 @@ __global__ __launch_bounds__(64 * NW) void ecg_crc_split_kernel(ecg_csum_params_
 					d[u][0] = d[u][1] = d[u][2] = d[u][3] = 0;
 				}
 			}
-#pragma unroll
-			for (int u = 0; u < CS_UNROLL; u++) {
-				if (i + u < i1)
-					acc = horner<W, REFL, B8>(acc, d[u], s5, sl, sh);
-			}
+			acc = horner<W, REFL, B8, L::UN>(acc, d, i, i1, s5, sl, sh);
 		}
 		acc = mulmod<W, REFL>(klane, acc, poly);
 		acc = wave_xor(acc);
@@ -521,14 +529,14 @@ const csum_entry g_csum[] = {
 	{1, false, false, ecg_crc_kernel<16, false, false, false>, "ecg_crc_kernel<crc16,bytes>"},
 	{2, true, false, ecg_crc_kernel<32, true, true, false>, "ecg_crc_kernel<crc32>"},
 	{2, false, false, ecg_crc_kernel<32, true, false, false>, "ecg_crc_kernel<crc32,bytes>"},
-	{3, true, false, ecg_crc_kernel<64, true, true, false>, "ecg_crc_kernel<crc64,alt>"},
-	{3, false, false, ecg_crc_kernel<64, true, false, false>, "ecg_crc_kernel<crc64,bytes,alt>"},
+	{3, true, false, ecg_crc_kernel<64, true, true, false>, "ecg_crc_kernel<crc64>"},
+	{3, false, false, ecg_crc_kernel<64, true, false, false>, "ecg_crc_kernel<crc64,bytes>"},
 	{1, true, true, ecg_crc_kernel<16, false, true, true>, "ecg_crc_kernel<crc16,alt>"},
 	{1, false, true, ecg_crc_kernel<16, false, false, true>, "ecg_crc_kernel<crc16,bytes,alt>"},
 	{2, true, true, ecg_crc_kernel<32, true, true, true>, "ecg_crc_kernel<crc32,alt>"},
 	{2, false, true, ecg_crc_kernel<32, true, false, true>, "ecg_crc_kernel<crc32,bytes,alt>"},
-	{3, true, true, ecg_crc_kernel<64, true, true, true>, "ecg_crc_kernel<crc64>"},
-	{3, false, true, ecg_crc_kernel<64, true, false, true>, "ecg_crc_kernel<crc64,bytes>"},
+	{3, true, true, ecg_crc_kernel<64, true, true, true>, "ecg_crc_kernel<crc64,alt>"},
+	{3, false, true, ecg_crc_kernel<64, true, false, true>, "ecg_crc_kernel<crc64,bytes,alt>"},
 	{7, true, false, ecg_adler_kernel<true>, "ecg_adler_kernel"},
 	{7, false, false, ecg_adler_kernel<false>, "ecg_adler_kernel<bytes>"},
 };
@@ -538,10 +546,10 @@ constexpr int SPLIT_NW = ECG_CSUM_SPLIT_NW;	// waves per chunk in the split kern
 const csum_entry g_split[] = {
 	{1, true, false, ecg_crc_split_kernel<16, false, SPLIT_NW, false>, "ecg_crc_split_kernel<crc16>"},
 	{2, true, false, ecg_crc_split_kernel<32, true, SPLIT_NW, false>, "ecg_crc_split_kernel<crc32>"},
-	{3, true, false, ecg_crc_split_kernel<64, true, SPLIT_NW, false>, "ecg_crc_split_kernel<crc64,alt>"},
+	{3, true, false, ecg_crc_split_kernel<64, true, SPLIT_NW, false>, "ecg_crc_split_kernel<crc64>"},
 	{1, true, true, ecg_crc_split_kernel<16, false, SPLIT_NW, true>, "ecg_crc_split_kernel<crc16,alt>"},
 	{2, true, true, ecg_crc_split_kernel<32, true, SPLIT_NW, true>, "ecg_crc_split_kernel<crc32,alt>"},
-	{3, true, true, ecg_crc_split_kernel<64, true, SPLIT_NW, true>, "ecg_crc_split_kernel<crc64>"},
+	{3, true, true, ecg_crc_split_kernel<64, true, SPLIT_NW, true>, "ecg_crc_split_kernel<crc64,alt>"},
 	{7, true, false, ecg_adler_split_kernel<SPLIT_NW>, "ecg_adler_split_kernel"},
 };
 constexpr uint32_t N_SPLIT = sizeof(g_split) / sizeof(g_split[0]);
@@ -549,10 +557,10 @@ constexpr uint32_t N_SPLIT = sizeof(g_split) / sizeof(g_split[0]);
 const csum_entry g_group[] = {
 	{1, true, false, ecg_crc_group_kernel<16, false, false>, "ecg_crc_group_kernel<crc16>"},
 	{2, true, false, ecg_crc_group_kernel<32, true, false>, "ecg_crc_group_kernel<crc32>"},
-	{3, true, false, ecg_crc_group_kernel<64, true, false>, "ecg_crc_group_kernel<crc64,alt>"},
+	{3, true, false, ecg_crc_group_kernel<64, true, false>, "ecg_crc_group_kernel<crc64>"},
 	{1, true, true, ecg_crc_group_kernel<16, false, true>, "ecg_crc_group_kernel<crc16,alt>"},
 	{2, true, true, ecg_crc_group_kernel<32, true, true>, "ecg_crc_group_kernel<crc32,alt>"},
-	{3, true, true, ecg_crc_group_kernel<64, true, true>, "ecg_crc_group_kernel<crc64>"},
+	{3, true, true, ecg_crc_group_kernel<64, true, true>, "ecg_crc_group_kernel<crc64,alt>"},
 };
 constexpr uint32_t N_GROUP = sizeof(g_group) / sizeof(g_group[0]);
 

@@ -130,6 +130,17 @@ __device__ __forceinline__ void mm_compute(const ecg_mm_params_t &P, const u32x4
 	}
 #pragma unroll
 	for (int j = 0; j < KM; j++) {
+#ifdef ECG_EXP_XOR_ONLY
+		// experimental build (tools/ec_libs.py): XOR instead of the GF
+		// multiply -- same memory traffic, grid and address registers
+		if (j < k) {
+#pragma unroll
+			for (int r = 0; r < RM; r++)
+				if (r < rows)
+					acc[r] ^= x[j];
+		}
+		continue;
+#endif
 		if (j < k) {
 			u32x4 sel0, sel1, sel2;
 #pragma unroll
@@ -411,7 +422,7 @@ __global__ void __launch_bounds__(BLOCK, 4)	// >= 4 waves per SIMD: <= 128 VGPRs
 ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 {
 	using T = typename ecg_crc::reg<W>::T;
-	using F5 = ecg_crc::f5<W>;
+	using F5 = ecg_crc::f5u<W>;
 	constexpr int NB = W / 8;
 	constexpr int KM = K ? K : ECG_KMAX_K;
 	constexpr int RM = R ? R : ECG_KMAX_R;
@@ -419,9 +430,10 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	constexpr int T2V = (RM + 3) / 4;
 	constexpr int PER_J = RM + T2V;
 	__shared__ u32x4 s_tbl[KM * PER_J];
-	// CRC tables (TB): 0 5-bit (conflict-free, ecg_kabi.h p5 + a5 shift by
-	// 4 KiB); 1 byte tables sl (slice-by-NB, register folded) + sh4k; 2 byte
-	// tables s16 (16 independent lookups per piece) + sh4k
+	// CRC tables (TB): 0 5-bit (conflict-free, ecg_kabi.h: positional p5 of
+	// 0..U-1 columns + a5 shift by U columns, U = ECG_CSUM_P5U); 1 byte
+	// tables sl (slice-by-NB, register folded) + sh4k; 2 byte tables s16 (16
+	// independent lookups per piece) + sh4k
 	constexpr int NSL = TB == 0 ? F5::N : TB == 1 ? NB * 256 : 16 * 256;
 	__shared__ T s_sl[NSL];
 	__shared__ T s_sh[TB ? NB * 256 : 1];
@@ -445,7 +457,7 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 		for (int i = threadIdx.x; i < NB * 256; i += BLOCK)
 			s_sh[i] = gt[ECG_CSUM_OFF_SH4K(NB) + i];
 	} else {
-		ecg_crc::stage5<W>(s_sl, gt, ECG_CSUM_OFF_A5_4K(NB), BLOCK);
+		ecg_crc::stage5u<W>(s_sl, gt, ECG_CSUM_OFF_P5X_4K(NB), ECG_CSUM_OFF_A5_16K(NB), BLOCK);
 	}
 	const T *kh = (const T *)Q.kh;
 	const T poly = (T)Q.poly;
@@ -490,14 +502,18 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 					mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, xa, outv);
 				else if (have)
 					mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, xa, outv);
+				// TB 0: column i sits (col1 - 1 - i) columns before the item end;
+				// groups of U columns end at the item end, the register is
+				// shifted by U columns at each group start
+				const uint32_t pos = (col1 - 1 - i) % F5::U;
 #pragma unroll
 				for (int r = 0; r < RM; r++) {
 					if (r < rows) {
 #ifndef ECG_EXP_NO_CRC
 						if constexpr (TB != 0)
 							crc[r] = ecg_crc::lin_map<W>(crc[r], s_sh);
-						else
-							crc[r] = ecg_crc::lin_map5<W>(crc[r], s_sl + F5::NF * 32);
+						else if (pos == F5::U - 1)
+							crc[r] = ecg_crc::lin_map5<W>(crc[r], s_sl + F5::U * F5::NF * 32);
 #endif
 						if (have) {
 							uint32_t d[4] = {outv[r][0], outv[r][1], outv[r][2], outv[r][3]};
@@ -512,7 +528,8 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 							else if constexpr (TB == 2)
 								crc[r] ^= ecg_crc::piece_crc16<W>(d, s_sl);
 							else
-								crc[r] ^= ecg_crc::piece_crc5<W>(d, s_sl);
+								crc[r] ^= ecg_crc::piece_crc5p<W>(
+									d, s_sl, pos * (uint32_t)(F5::NF * 32 * sizeof(T)));
 #else
 							crc[r] ^= (T)(d[0] ^ d[1] ^ d[2] ^ d[3]);
 #endif
@@ -568,7 +585,7 @@ __global__ void __launch_bounds__(BLOCK, 4)
 ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 {
 	using T = typename ecg_crc::reg<W>::T;
-	using F5 = ecg_crc::f5<W>;
+	using F5 = ecg_crc::f5u<W>;
 	constexpr int NB = W / 8;
 	constexpr int KM = K ? K : ECG_KMAX_K;
 	constexpr int RM = R ? R : ECG_KMAX_R;
@@ -600,7 +617,7 @@ ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 		for (int i = threadIdx.x; i < NB * 256; i += BLOCK)
 			s_sh[i] = gt[ECG_CSUM_OFF_SH(NB) + i];
 	} else {
-		ecg_crc::stage5<W>(s_sl, gt, ECG_CSUM_OFF_A5_1K(NB), BLOCK);
+		ecg_crc::stage5u<W>(s_sl, gt, ECG_CSUM_OFF_P5X_1K(NB), ECG_CSUM_OFF_A5_4K(NB), BLOCK);
 	}
 	const T *kw = (const T *)Q.kh;
 	const T poly = (T)Q.poly;
@@ -646,13 +663,14 @@ ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 				mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, xa, outv);
 			else if (have)
 				mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, xa, outv);
+			const uint32_t pos = (m - 1 - i) % F5::U;	// rows to the chunk end, mod U (TB 0)
 #pragma unroll
 			for (int r = 0; r < RM; r++) {
 				if (r < rows) {
 					if constexpr (TB != 0)
 						crc[r] = ecg_crc::lin_map<W>(crc[r], s_sh);
-					else
-						crc[r] = ecg_crc::lin_map5<W>(crc[r], s_sl + F5::NF * 32);
+					else if (pos == F5::U - 1)
+						crc[r] = ecg_crc::lin_map5<W>(crc[r], s_sl + F5::U * F5::NF * 32);
 					if (have) {
 						uint32_t d[4] = {outv[r][0], outv[r][1], outv[r][2], outv[r][3]};
 						if (i == 0 && lane == 0) {	// initial register
@@ -665,7 +683,8 @@ ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 						else if constexpr (TB == 2)
 							crc[r] ^= ecg_crc::piece_crc16<W>(d, s_sl);
 						else
-							crc[r] ^= ecg_crc::piece_crc5<W>(d, s_sl);
+							crc[r] ^= ecg_crc::piece_crc5p<W>(
+								d, s_sl, pos * (uint32_t)(F5::NF * 32 * sizeof(T)));
 					}
 				}
 			}

@@ -356,7 +356,11 @@ def test_encode_csum_misaligned_csums(oracle, ecglib, ctx):
 @pytest.mark.parametrize("shape", [1, 2, 3])
 @pytest.mark.parametrize("htype", (1, 2, 3))
 @pytest.mark.parametrize("geom", [(32768, 1, 0, 200000), (4096, 1, 0, 4096 * 7 + 16 * 5),
-                                  ((1 << 20) + 4096, 1, 5, 2 << 20)])
+                                  ((1 << 20) + 4096, 1, 5, 2 << 20),
+                                  # step counts that are not multiples of the 5-bit path's
+                                  # 4-piece Horner step (zero prefix) in every shape
+                                  ((1 << 20) + 5120 + 48, 1, 3, 3 << 20), (1040, 1, 0, 1040 * 9 + 7),
+                                  (5 * 4096 + 1024, 1, 0, 7 * (5 * 4096 + 1024) - 16)])
 def test_crc_table_kinds(oracle, ecglib, ctx, kind, shape, htype, geom):
     """Both CRC table kinds (conflict-free 5-bit tables, byte tables; the
     default picks per hash) give the oracle's checksums on every kernel shape."""

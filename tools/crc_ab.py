@@ -4,7 +4,7 @@ byte tables (ecg_set_csum_variant bit 4), in one process, interleaved:
   * fused encode + checksums (EC_8P2 x 512 and EC_4P2 x 1024, 1 MiB cells,
     32 KiB chunks) and the parity-shard rebuild row <8,1> against the plain
     encode.
-Median of 7 launches.  -> gpurun_out/crc_ab.json.  Bench infrastructure."""
+Median of 7 launches after 3 warm-up launches.  -> gpurun_out/crc_ab.json.  Bench infrastructure."""
 import json
 import os
 import sys
@@ -23,7 +23,8 @@ def main():
     a, b = ctx.event(), ctx.event()
 
     def timed(fn, reps=7):
-        fn()
+        for _ in range(3):
+            fn()
         ctx.sync()
         ts = []
         for _ in range(reps):
@@ -62,7 +63,8 @@ def main():
         for rnd in range(2):
             row["encode_ms"].append(round(timed(lambda: ctx.encode(k, p, C, S, buf.ptr, k * C, par.ptr, pitch, C)), 4))
             for hname, htype in (("crc32", 2), ("crc64", 3)):
-                for tag, var in (("dflt", 0), ("wave", 128), ("wave_tb0", 160), ("wave_tb1", 144)):
+                for tag, var in (("dflt", 0), ("wg_tb0", 32 | 256), ("wg_tb1", 16 | 256), ("wave_tb0", 160),
+                                 ("wave_tb1", 144)):
                     L.ecg_set_csum_variant(ctx.h, var)
                     try:
                         ms = timed(lambda: ctx.encode_csum(k, p, C, S, buf.ptr, k * C, par.ptr, pitch, C, htype, 32768,

@@ -207,6 +207,16 @@ PY
 	crcab)
 		step crc_ab 600 python tools/crc_ab.py || exit $?
 		;;
+	eclibs)
+		step ec_libs 900 python tools/ec_libs.py daos_amd/lib/libecg.so build/exp/xoronly/libecg.so || exit $?
+		;;
+	fusedpmc)
+		rm -rf gpurun_out/pmc_ffetch gpurun_out/pmc_fwrite
+		step rocprof_ffetch 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv \
+			-d gpurun_out/pmc_ffetch -o run -- python3 tools/crc_pmc.py fused || exit $?
+		step rocprof_fwrite 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv \
+			-d gpurun_out/pmc_fwrite -o run -- python3 tools/crc_pmc.py fused || exit $?
+		;;
 	dist4)
 		step dist4 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
 			--master-port 29537 bench.py --gpus 4 --steps 20 --warmup 3 || exit $?
