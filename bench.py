@@ -485,9 +485,10 @@ def pinned_copy_rates(ctx, n=1 << 30):
     return out
 
 
-def time_kernel(ctx, fn, iters):
+def time_kernel(ctx, fn, iters, warm=3):
     a, b = ctx.event(), ctx.event()
-    fn()
+    for _ in range(warm):
+        fn()
     ctx.sync()
     ms = []
     for _ in range(iters):
@@ -501,7 +502,7 @@ def time_kernel(ctx, fn, iters):
     return ms[len(ms) // 2]
 
 
-def measured_ceilings(ctx, iters=7):
+def measured_ceilings(ctx, iters=11):
     """This box's streaming rates (GB/s), each mode at its best measured
     geometry (profiles/r01/tune2*.json): reads with 512 persistent blocks,
     writes / copies with one 4 x 16 B slice per thread."""
@@ -524,7 +525,7 @@ def mix_ceiling(ceil, read_frac):
     return 1.0 / (read_frac / ceil["read"] + (1 - read_frac) / ceil["write"])
 
 
-def detail_rows(ctx, ceil, iters=7):
+def detail_rows(ctx, ceil, iters=11):
     """Extra device-resident rows (per GPU): the north-star EC_8P2 encode,
     EC_8P2 2-erasure decode, EC_16P2 128 KiB encode, EC_2P1 128 KiB encode.
     Encodes use the client write layout (data [S][k][C], parity [p][S][C] at

@@ -89,6 +89,16 @@ __device__ __forceinline__ void mm_load(const ecg_mm_params_t &P, int k, uint32_
 	}
 }
 
+// mm_load with no branch: lanes whose 16 bytes would pass the cell end read
+// the column's first 16 bytes instead (C % 16 == 0; callers never use those
+// lanes' values)
+template <int KM>
+__device__ __forceinline__ void mm_load_any(const ecg_mm_params_t &P, int k, uint32_t s, uint64_t cbase,
+					    uint32_t lo, u32x4 *x)
+{
+	mm_load<KM, false>(P, k, s, cbase, cbase + lo + 16 <= P.cell_bytes ? lo : 0u, x);
+}
+
 template <int KM, int RM, bool ACC, bool KEEP, bool STORE = true>
 __device__ __forceinline__ void mm_compute(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
 					   uint32_t s, uint64_t cbase, uint32_t lo, const u32x4 *x,
@@ -404,6 +414,72 @@ __device__ __forceinline__ void mmcs_item(const ecg_mmcs_params_t &Q, uint32_t i
 	khrow = (lastc ? Q.nh : 0) + h;
 }
 
+// One column of a fused product + checksum item (the workgroup kernel's 4 KiB
+// columns, the wave kernel's 1 KiB rows; STRIDE bytes): with PF, first the
+// next column's loads into nxt (when `more`), then the product of cur -- the
+// sources already in registers -- and its stores, then each output row's
+// 16-byte piece folded into the row's CRC.  TB 0: pos = columns to the item
+// end mod U selects the positional table; the register is shifted by U
+// columns at each group start (pos == U - 1).  `first`: this piece starts
+// the chunk, the initial register is folded into it.
+template <int KM, int RM, int W, bool REFL, int TB, bool PF, uint32_t STRIDE, typename T>
+__device__ __forceinline__ void mmcs_col(const ecg_mm_params_t &P, const u32x4 *s_tbl, const T *s_sl,
+					 const T *s_sh, int k, int rows, uint32_t s, uint64_t cbase, uint32_t lo,
+					 bool more, bool first, uint64_t init, uint32_t pos, u32x4 *cur, u32x4 *nxt,
+					 T *crc)
+{
+	using F5 = ecg_crc::f5u<W>;
+	const uint64_t C = P.cell_bytes;
+	const bool have = cbase + lo + 16 <= C;		// C % 16 == 0
+	u32x4 outv[RM];
+	uint32_t z = 0;
+
+	if constexpr (PF) {
+		// no branch around the prefetch: a load that may or may not be
+		// issued makes the compiler's waitcnt merge wait for everything
+		// (vmcnt(0)) before the product.  Past the item's last column the
+		// wave re-reads stripe 0's first column (cache-resident, unused).
+		mm_load_any<KM>(P, k, more ? s : 0, more ? cbase + STRIDE : 0, lo, nxt);
+	} else if (have) {
+		mm_load<KM, false>(P, k, s, cbase, lo, cur);
+	}
+	asm volatile("" : "+v"(z));
+	const u32x4 *tb = s_tbl + z;
+	if (cbase + STRIDE <= C)
+		mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, cur, outv);
+	else if (have)
+		mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, cur, outv);
+#pragma unroll
+	for (int r = 0; r < RM; r++) {
+		if (r < rows) {
+#ifndef ECG_EXP_NO_CRC
+			if constexpr (TB != 0)
+				crc[r] = ecg_crc::lin_map<W>(crc[r], s_sh);
+			else if (pos == F5::U - 1)
+				crc[r] = ecg_crc::lin_map5<W>(crc[r], s_sl + F5::U * F5::NF * 32);
+#endif
+			if (have) {
+				uint32_t d[4] = {outv[r][0], outv[r][1], outv[r][2], outv[r][3]};
+				if (first) {	// initial register
+					d[0] ^= (uint32_t)init;
+					if constexpr (W == 64)
+						d[1] ^= (uint32_t)(init >> 32);
+				}
+#ifndef ECG_EXP_NO_CRC
+				if constexpr (TB == 1)
+					crc[r] ^= ecg_crc::piece_crc<W, REFL>(d, s_sl);
+				else if constexpr (TB == 2)
+					crc[r] ^= ecg_crc::piece_crc16<W>(d, s_sl);
+				else
+					crc[r] ^= ecg_crc::piece_crc5p<W>(d, s_sl, pos * (uint32_t)(F5::NF * 32 * sizeof(T)));
+#else
+				crc[r] ^= (T)(d[0] ^ d[1] ^ d[2] ^ d[3]);
+#endif
+			}
+		}
+	}
+}
+
 // Fused product + checksum of every output cell (ecg_kabi.h, ecg_mmcs_params).
 // Block = a stream of (stripe, sub-chunk) items of a few 4 KiB columns each;
 // it walks the columns, computing and storing the outputs exactly as
@@ -479,68 +555,20 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 #pragma unroll
 			for (int r = 0; r < RM; r++)
 				crc[r] = 0;
-			if constexpr (PF) {
-				if (c0 + (uint64_t)i * CHUNK_BYTES + lo + 16 <= C)
-					mm_load<KM, false>(P, k, s, c0 + (uint64_t)i * CHUNK_BYTES, lo, xa);
-			}
-			for (; i < col1; i++) {
-				const uint64_t cbase = c0 + (uint64_t)i * CHUNK_BYTES;
-				const bool have = cbase + lo + 16 <= C;	// C % 16 == 0
-				u32x4 outv[RM];
-				u32x4 xb[PF ? KM : 1];
-				uint32_t z = 0;
-
-				if constexpr (PF) {
-					if (i + 1 < col1 && cbase + CHUNK_BYTES + lo + 16 <= C)
-						mm_load<KM, false>(P, k, s, cbase + CHUNK_BYTES, lo, xb);
-				} else if (have) {
-					mm_load<KM, false>(P, k, s, cbase, lo, xa);
-				}
-				asm volatile("" : "+v"(z));
-				const u32x4 *tb = s_tbl + z;
-				if (cbase + CHUNK_BYTES <= C)
-					mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, xa, outv);
-				else if (have)
-					mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, xa, outv);
-				// TB 0: column i sits (col1 - 1 - i) columns before the item end;
-				// groups of U columns end at the item end, the register is
-				// shifted by U columns at each group start
-				const uint32_t pos = (col1 - 1 - i) % F5::U;
-#pragma unroll
-				for (int r = 0; r < RM; r++) {
-					if (r < rows) {
-#ifndef ECG_EXP_NO_CRC
-						if constexpr (TB != 0)
-							crc[r] = ecg_crc::lin_map<W>(crc[r], s_sh);
-						else if (pos == F5::U - 1)
-							crc[r] = ecg_crc::lin_map5<W>(crc[r], s_sl + F5::U * F5::NF * 32);
-#endif
-						if (have) {
-							uint32_t d[4] = {outv[r][0], outv[r][1], outv[r][2], outv[r][3]};
-							if (i == 0 && threadIdx.x == 0) {	// initial register
-								d[0] ^= (uint32_t)Q.init;
-								if constexpr (W == 64)
-									d[1] ^= (uint32_t)(Q.init >> 32);
-							}
-#ifndef ECG_EXP_NO_CRC
-							if constexpr (TB == 1)
-								crc[r] ^= ecg_crc::piece_crc<W, REFL>(d, s_sl);
-							else if constexpr (TB == 2)
-								crc[r] ^= ecg_crc::piece_crc16<W>(d, s_sl);
-							else
-								crc[r] ^= ecg_crc::piece_crc5p<W>(
-									d, s_sl, pos * (uint32_t)(F5::NF * 32 * sizeof(T)));
-#else
-							crc[r] ^= (T)(d[0] ^ d[1] ^ d[2] ^ d[3]);
-#endif
-						}
-					}
-				}
-				if constexpr (PF) {
-#pragma unroll
-					for (int j = 0; j < KM; j++)
-						xa[j] = xb[j];
-				}
+			u32x4 xb[PF ? KM : 1];
+			if constexpr (PF)
+				mm_load_any<KM>(P, k, s, c0 + (uint64_t)i * CHUNK_BYTES, lo, xa);
+			// two columns per trip, the prefetch buffers swapping roles: a
+			// register copy xa = xb would wait for the prefetched loads
+			// (s_waitcnt vmcnt(0)) and serialise the walk
+			for (; i < col1; i += 2) {
+				mmcs_col<KM, RM, W, REFL, TB, PF, CHUNK_BYTES>(
+					P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)i * CHUNK_BYTES, lo, i + 1 < col1,
+					i == 0 && threadIdx.x == 0, Q.init, (col1 - 1 - i) % F5::U, xa, PF ? xb : xa, crc);
+				if (i + 1 < col1)
+					mmcs_col<KM, RM, W, REFL, TB, PF, CHUNK_BYTES>(
+						P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)(i + 1) * CHUNK_BYTES, lo,
+						i + 2 < col1, false, Q.init, (col1 - 2 - i) % F5::U, PF ? xb : xa, xa, crc);
 			}
 			// each wave XORs its partial into the (zeroed) output: no
 			// workgroup barrier, other waves keep streaming
@@ -640,59 +668,17 @@ ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 #pragma unroll
 		for (int r = 0; r < RM; r++)
 			crc[r] = 0;
-		if constexpr (PF) {
-			if (c0 + lo + 16 <= C)
-				mm_load<KM, false>(P, k, s, c0, lo, xa);
-		}
-		for (uint32_t i = 0; i < m; i++) {
-			const uint64_t cbase = c0 + (uint64_t)i * ECG_CSUM_STRIDE;
-			const bool have = cbase + lo + 16 <= C;		// C % 16 == 0
-			u32x4 outv[RM];
-			u32x4 xb[PF ? KM : 1];
-			uint32_t z = 0;
-
-			if constexpr (PF) {
-				if (i + 1 < m && cbase + ECG_CSUM_STRIDE + lo + 16 <= C)
-					mm_load<KM, false>(P, k, s, cbase + ECG_CSUM_STRIDE, lo, xb);
-			} else if (have) {
-				mm_load<KM, false>(P, k, s, cbase, lo, xa);
-			}
-			asm volatile("" : "+v"(z));
-			const u32x4 *tb = s_tbl + z;
-			if (cbase + ECG_CSUM_STRIDE <= C)
-				mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, xa, outv);
-			else if (have)
-				mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, xa, outv);
-			const uint32_t pos = (m - 1 - i) % F5::U;	// rows to the chunk end, mod U (TB 0)
-#pragma unroll
-			for (int r = 0; r < RM; r++) {
-				if (r < rows) {
-					if constexpr (TB != 0)
-						crc[r] = ecg_crc::lin_map<W>(crc[r], s_sh);
-					else if (pos == F5::U - 1)
-						crc[r] = ecg_crc::lin_map5<W>(crc[r], s_sl + F5::U * F5::NF * 32);
-					if (have) {
-						uint32_t d[4] = {outv[r][0], outv[r][1], outv[r][2], outv[r][3]};
-						if (i == 0 && lane == 0) {	// initial register
-							d[0] ^= (uint32_t)Q.init;
-							if constexpr (W == 64)
-								d[1] ^= (uint32_t)(Q.init >> 32);
-						}
-						if constexpr (TB == 1)
-							crc[r] ^= ecg_crc::piece_crc<W, REFL>(d, s_sl);
-						else if constexpr (TB == 2)
-							crc[r] ^= ecg_crc::piece_crc16<W>(d, s_sl);
-						else
-							crc[r] ^= ecg_crc::piece_crc5p<W>(
-								d, s_sl, pos * (uint32_t)(F5::NF * 32 * sizeof(T)));
-					}
-				}
-			}
-			if constexpr (PF) {
-#pragma unroll
-				for (int j = 0; j < KM; j++)
-					xa[j] = xb[j];
-			}
+		u32x4 xb[PF ? KM : 1];
+		if constexpr (PF)
+			mm_load_any<KM>(P, k, s, c0, lo, xa);
+		for (uint32_t i = 0; i < m; i += 2) {	// two rows per trip (buffers swap, no copy)
+			mmcs_col<KM, RM, W, REFL, TB, PF, ECG_CSUM_STRIDE>(
+				P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)i * ECG_CSUM_STRIDE, lo, i + 1 < m,
+				i == 0 && lane == 0, Q.init, (m - 1 - i) % F5::U, xa, PF ? xb : xa, crc);
+			if (i + 1 < m)
+				mmcs_col<KM, RM, W, REFL, TB, PF, ECG_CSUM_STRIDE>(
+					P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)(i + 1) * ECG_CSUM_STRIDE, lo,
+					i + 2 < m, false, Q.init, (m - 2 - i) % F5::U, PF ? xb : xa, xa, crc);
 		}
 		const T kcur = kw[(lastc ? 64 : 0) + lane];
 #pragma unroll

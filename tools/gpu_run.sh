@@ -81,6 +81,13 @@ for what in "$@"; do
 		done
 		cat gpurun_out/qbench_*.log | grep '^{' > gpurun_out/qbench.jsonl
 		;;
+	qupdate)
+		make -C tests/c > /dev/null || exit 2
+		for c in 32768 131072 1048576; do
+			step qupd_${c} 300 ./build/ctest/queue_bench $c 16 update || exit $?
+		done
+		cat gpurun_out/qupd_*.log | grep '^{' > gpurun_out/queue_update.jsonl
+		;;
 	ctest)
 		make -C tests/c > /dev/null || exit 2
 		step ctest 300 ./build/ctest/test_ecg_c || exit $?
@@ -209,6 +216,10 @@ PY
 		;;
 	eclibs)
 		step ec_libs 900 python tools/ec_libs.py daos_amd/lib/libecg.so build/exp/xoronly/libecg.so || exit $?
+		;;
+	fusedlibs)
+		step fused_libs 900 python tools/fused_libs.py daos_amd/lib/libecg.so build/exp/nocrc/libecg.so \
+			build/exp/nocrcmul/libecg.so || exit $?
 		;;
 	fusedpmc)
 		rm -rf gpurun_out/pmc_ffetch gpurun_out/pmc_fwrite

@@ -6,7 +6,14 @@
  *   queue: ecg_queue_encode()      (batching facade, async completion)
  *   cpu  : ref_simd_encode_data()  (ISA-L-equivalent CPU restatement, the
  *                                   baseline DAOS runs today)
- * and prints one JSON line of GiB/s (user data).  Bench infrastructure.
+ * and prints one JSON line of GiB/s (user data).  With a third argument
+ * "update" the calls are aggregation delta updates of one data cell per call
+ * (agg_update_parity, ref:src/object/srv_ec_aggregate.c:1086-1102):
+ *   isal : xor_gen(old, new -> diff) + ec_encode_data_update(vec_i)  (drop-in)
+ *   queue: ecg_queue_update()
+ *   cpu  : diff loop + ref_simd_encode_data(k = 1, the vec_i column) XORed
+ *          into the parity (ISA-L-equivalent CPU restatement)
+ * and GiB/s counts the updated cell bytes.  Bench infrastructure.
  */
 #include <pthread.h>
 #include <stdio.h>
@@ -24,6 +31,9 @@ static unsigned char *g_cells;		/* T * N stripes of (K + P) cells */
 static unsigned char g_tbls[64 * 8 * 32];
 static ecg_queue_t *g_q;
 static int g_mode;			/* 0 isal, 1 queue, 2 cpu */
+static int g_update;			/* calls are one-cell delta updates */
+static unsigned char *g_new;		/* T * N new cells (update) */
+static unsigned char g_col[64][8 * 32];	/* vec_i -> the P tables of column vec_i */
 
 struct cnt {
 	pthread_mutex_t lock;
@@ -51,11 +61,62 @@ static void done_cb(void *arg, int rc)
 	pthread_mutex_unlock(&g_cnt.lock);
 }
 
+static void update_one(long t, int i)
+{
+	unsigned char *s = g_cells + ((size_t)t * N + i) * (K + P) * CB;
+	unsigned char *nw = g_new + ((size_t)t * N + i) * CB;
+	const int vec_i = (int)((t * N + i) % K);
+	unsigned char *old = s + vec_i * CB, *par[8];
+
+	for (int r = 0; r < P; r++)
+		par[r] = s + (K + r) * CB;
+	if (g_mode == 1) {
+		ecg_queue_update(g_q, K, P, CB, vec_i, old, nw, par, done_cb, NULL);
+		return;
+	}
+	unsigned char *diff = malloc(CB), *tmp[8];
+
+	if (g_mode == 0) {
+		void *arr[3] = {old, nw, diff};
+
+		xor_gen(3, (int)CB, arr);
+		ec_encode_data_update((int)CB, K, P, vec_i, g_tbls, diff, par);
+	} else {
+		for (uint64_t b = 0; b < CB; b += 8) {
+			uint64_t x, y;
+
+			memcpy(&x, old + b, 8);
+			memcpy(&y, nw + b, 8);
+			x ^= y;
+			memcpy(diff + b, &x, 8);
+		}
+		for (int r = 0; r < P; r++)
+			tmp[r] = malloc(CB);
+		ref_simd_encode_data((int)CB, 1, P, g_col[vec_i], &diff, tmp);
+		for (int r = 0; r < P; r++) {
+			for (uint64_t b = 0; b < CB; b += 8) {
+				uint64_t x, y;
+
+				memcpy(&x, par[r] + b, 8);
+				memcpy(&y, tmp[r] + b, 8);
+				x ^= y;
+				memcpy(par[r] + b, &x, 8);
+			}
+			free(tmp[r]);
+		}
+	}
+	free(diff);
+}
+
 static void *worker(void *arg)
 {
 	long t = (long)arg;
 
 	for (int i = 0; i < N; i++) {
+		if (g_update) {
+			update_one(t, i);
+			continue;
+		}
 		unsigned char *s = g_cells + ((size_t)t * N + i) * (K + P) * CB;
 		unsigned char *data[64], *par[8];
 
@@ -92,7 +153,7 @@ static double run(int mode)
 		pthread_mutex_unlock(&g_cnt.lock);
 	}
 	t1 = now();
-	return (double)T * N * K * CB / (t1 - t0) / (1 << 30);
+	return (double)T * N * (g_update ? 1 : K) * CB / (t1 - t0) / (1 << 30);
 }
 
 int main(int argc, char **argv)
@@ -107,11 +168,18 @@ int main(int argc, char **argv)
 		CB = strtoull(argv[1], NULL, 0);
 	if (argc > 2)
 		T = atoi(argv[2]);
+	g_update = argc > 3 && strcmp(argv[3], "update") == 0;
 	g_cells = malloc((size_t)T * N * (K + P) * CB);
+	g_new = malloc((size_t)T * N * CB);
 	for (size_t i = 0; i < (size_t)T * N * (K + P) * CB; i++)
 		g_cells[i] = (unsigned char)(i * 2654435761u >> 13);
+	for (size_t i = 0; i < (size_t)T * N * CB; i++)
+		g_new[i] = (unsigned char)(i * 40503u >> 7);
 	gf_gen_cauchy1_matrix(en, K + P, K);
 	ec_init_tables(K, P, &en[K * K], g_tbls);
+	for (int j = 0; j < K; j++)	/* ISA-L layout: row r, source j at (r * K + j) * 32 */
+		for (int r = 0; r < P; r++)
+			memcpy(&g_col[j][r * 32], &g_tbls[(r * K + j) * 32], 32);
 	if (ecg_ctx_create(0, &ctx) || ecg_queue_create(ctx, &qa, &g_q)) {
 		fprintf(stderr, "no device: %s\n", ecg_strerror());
 		return 1;
@@ -122,13 +190,15 @@ int main(int argc, char **argv)
 	queue = run(1);
 	ecg_queue_stats(g_q, &reqs, &batches);
 	cpu = run(2);
-	printf("{\"k\": %d, \"p\": %d, \"cell_bytes\": %llu, \"threads\": %d, \"stripes_per_thread\": %d, "
+	printf("{\"op\": \"%s\", \"k\": %d, \"p\": %d, \"cell_bytes\": %llu, \"threads\": %d, \"stripes_per_thread\": %d, "
 	       "\"isal_one_stripe_GiBps\": %.2f, \"queue_GiBps\": %.2f, \"queue_requests\": %llu, "
 	       "\"queue_batches\": %llu, \"cpu_gfni_same_threads_GiBps\": %.2f}\n",
-	       K, P, (unsigned long long)CB, T, N, isal, queue, (unsigned long long)reqs,
+	       g_update ? "update" : "encode", K, P, (unsigned long long)CB, T, N, isal, queue,
+	       (unsigned long long)reqs,
 	       (unsigned long long)batches, cpu);
 	ecg_queue_destroy(g_q);
 	ecg_ctx_destroy(ctx);
 	free(g_cells);
+	free(g_new);
 	return 0;
 }
