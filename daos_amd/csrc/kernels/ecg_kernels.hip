@@ -31,6 +31,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #define CHUNK_BYTES 4096u	// 256 lanes x 16 B
 #define BLOCK 256
+#ifndef ECG_FUSED_WPE
+#define ECG_FUSED_WPE 4		// fused kernels: waves per SIMD the register budget targets
+#endif
 
 __device__ __forceinline__ u32x4 ld_nt(const uint8_t *p)
 {
@@ -422,15 +425,32 @@ __device__ __forceinline__ void mmcs_item(const ecg_mmcs_params_t &Q, uint32_t i
 // end mod U selects the positional table; the register is shifted by U
 // columns at each group start (pos == U - 1).  `first`: this piece starts
 // the chunk, the initial register is folded into it.
-template <int KM, int RM, int W, bool REFL, int TB, bool PF, uint32_t STRIDE, typename T>
-__device__ __forceinline__ void mmcs_col(const ecg_mm_params_t &P, const u32x4 *s_tbl, const T *s_sl,
+// The kernel arguments re-read (scalar loads, K$ hits) where they are used:
+// an empty asm on their constant-space address stops the compiler from
+// keeping every cell offset of the launch live in SGPRs across a column loop
+// (the fused kernels spilled SGPRs into VGPR lanes).
+typedef __attribute__((address_space(4))) const ecg_mm_params_t kparams_t;
+
+__device__ __forceinline__ const ecg_mm_params_t &kernarg_fresh()
+{
+	// the kernel's first argument sits at the start of the kernarg segment
+	kparams_t *p = (kparams_t *)__builtin_amdgcn_kernarg_segment_ptr();
+
+	asm volatile("" : "+s"(p));
+	return *(const ecg_mm_params_t *)p;
+}
+
+template <int KM, int RM, int W, bool REFL, int TB, bool PF, uint32_t STRIDE, bool FULL, typename T>
+__device__ __forceinline__ void mmcs_col(const ecg_mm_params_t &P0, const u32x4 *s_tbl, const T *s_sl,
 					 const T *s_sh, int k, int rows, uint32_t s, uint64_t cbase, uint32_t lo,
 					 bool more, bool first, uint64_t init, uint32_t pos, u32x4 *cur, u32x4 *nxt,
 					 T *crc)
 {
 	using F5 = ecg_crc::f5u<W>;
+	const ecg_mm_params_t &P = kernarg_fresh();	// == P0 (first kernel argument)
+	(void)P0;
 	const uint64_t C = P.cell_bytes;
-	const bool have = cbase + lo + 16 <= C;		// C % 16 == 0
+	const bool have = FULL || cbase + lo + 16 <= C;	// C % 16 == 0
 	u32x4 outv[RM];
 	uint32_t z = 0;
 
@@ -445,7 +465,11 @@ __device__ __forceinline__ void mmcs_col(const ecg_mm_params_t &P, const u32x4 *
 	}
 	asm volatile("" : "+v"(z));
 	const u32x4 *tb = s_tbl + z;
-	if (cbase + STRIDE <= C)
+	// FULL (the column lies inside the cell): no branch, so the pipelined
+	// loop of the callers has one path -- a partial-column path that may skip
+	// the loads or use other registers for its stores makes the compiler wait
+	// for everything (vmcnt(0)) at the loop head
+	if (FULL || cbase + STRIDE <= C)
 		mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, cur, outv);
 	else if (have)
 		mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, cur, outv);
@@ -494,7 +518,7 @@ __device__ __forceinline__ void mmcs_col(const ecg_mm_params_t &P, const u32x4 *
 // p/(k+p) of the traffic instead of a second pass over the regenerated
 // cells (ref:src/object/srv_obj_migrate.c:1156 checksums them after encode).
 template <int K, int R, int W, bool REFL, int TB = 0>
-__global__ void __launch_bounds__(BLOCK, 4)	// >= 4 waves per SIMD: <= 128 VGPRs
+__global__ void __launch_bounds__(BLOCK, ECG_FUSED_WPE)	// >= 4 waves per SIMD: <= 128 VGPRs
 ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 {
 	using T = typename ecg_crc::reg<W>::T;
@@ -555,21 +579,34 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 #pragma unroll
 			for (int r = 0; r < RM; r++)
 				crc[r] = 0;
-			u32x4 xb[PF ? KM : 1];
-			if constexpr (PF)
+			// Pipelined pairs of full columns, the prefetch buffers swapping
+			// roles (a register copy xa = xb would wait for the prefetched
+			// loads and serialise the walk); then the rest -- an odd full
+			// column, the partial column of a cell that is not a multiple of
+			// 4 KiB -- one at a time without prefetch, outside the pipelined
+			// loop so that loop has a single path (a path that skips loads or
+			// stores makes the compiler wait for everything at the loop head).
+			const uint64_t nfull = (C - c0) / CHUNK_BYTES;
+			const uint32_t ifull = nfull < col1 ? (uint32_t)nfull : col1;
+			const uint32_t iend = ifull > i ? i + ((ifull - i) & ~1u) : i;
+			if (PF && i < iend) {
+				u32x4 xb[PF ? KM : 1];
+				u32x4 *xc = PF ? xb : xa;
+
 				mm_load_any<KM>(P, k, s, c0 + (uint64_t)i * CHUNK_BYTES, lo, xa);
-			// two columns per trip, the prefetch buffers swapping roles: a
-			// register copy xa = xb would wait for the prefetched loads
-			// (s_waitcnt vmcnt(0)) and serialise the walk
-			for (; i < col1; i += 2) {
-				mmcs_col<KM, RM, W, REFL, TB, PF, CHUNK_BYTES>(
-					P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)i * CHUNK_BYTES, lo, i + 1 < col1,
-					i == 0 && threadIdx.x == 0, Q.init, (col1 - 1 - i) % F5::U, xa, PF ? xb : xa, crc);
-				if (i + 1 < col1)
-					mmcs_col<KM, RM, W, REFL, TB, PF, CHUNK_BYTES>(
+				for (; i < iend; i += 2) {
+					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true>(
+						P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)i * CHUNK_BYTES, lo, true,
+						i == 0 && threadIdx.x == 0, Q.init, (col1 - 1 - i) % F5::U, xa, xc, crc);
+					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true>(
 						P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)(i + 1) * CHUNK_BYTES, lo,
-						i + 2 < col1, false, Q.init, (col1 - 2 - i) % F5::U, PF ? xb : xa, xa, crc);
+						i + 2 < iend, false, Q.init, (col1 - 2 - i) % F5::U, xc, xa, crc);
+				}
 			}
+			for (; i < col1; i++)
+				mmcs_col<KM, RM, W, REFL, TB, false, CHUNK_BYTES, false>(
+					P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)i * CHUNK_BYTES, lo, false,
+					i == 0 && threadIdx.x == 0, Q.init, (col1 - 1 - i) % F5::U, xa, xa, crc);
 			// each wave XORs its partial into the (zeroed) output: no
 			// workgroup barrier, other waves keep streaming
 			const T kcur = kh[khrow * 256 + threadIdx.x];
@@ -609,7 +646,7 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 // -- the multiply dominates crc64's cost there (tools/fused_sweep.py).
 // Tables (TB as ecg_mm_csum_kernel) with the 1 KiB shift.
 template <int K, int R, int W, bool REFL, int TB>
-__global__ void __launch_bounds__(BLOCK, 4)
+__global__ void __launch_bounds__(BLOCK, ECG_FUSED_WPE)
 ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 {
 	using T = typename ecg_crc::reg<W>::T;
@@ -668,18 +705,29 @@ ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 #pragma unroll
 		for (int r = 0; r < RM; r++)
 			crc[r] = 0;
-		u32x4 xb[PF ? KM : 1];
-		if constexpr (PF)
+		// pipelined pairs of full rows, then the rest one at a time (as
+		// ecg_mm_csum_kernel)
+		const uint32_t mfull = (uint32_t)(len / ECG_CSUM_STRIDE);
+		const uint32_t iend = mfull & ~1u;
+		uint32_t i = 0;
+		if (PF && iend) {
+			u32x4 xb[PF ? KM : 1];
+			u32x4 *xc = PF ? xb : xa;
+
 			mm_load_any<KM>(P, k, s, c0, lo, xa);
-		for (uint32_t i = 0; i < m; i += 2) {	// two rows per trip (buffers swap, no copy)
-			mmcs_col<KM, RM, W, REFL, TB, PF, ECG_CSUM_STRIDE>(
-				P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)i * ECG_CSUM_STRIDE, lo, i + 1 < m,
-				i == 0 && lane == 0, Q.init, (m - 1 - i) % F5::U, xa, PF ? xb : xa, crc);
-			if (i + 1 < m)
-				mmcs_col<KM, RM, W, REFL, TB, PF, ECG_CSUM_STRIDE>(
+			for (; i < iend; i += 2) {
+				mmcs_col<KM, RM, W, REFL, TB, true, ECG_CSUM_STRIDE, true>(
+					P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)i * ECG_CSUM_STRIDE, lo, true,
+					i == 0 && lane == 0, Q.init, (m - 1 - i) % F5::U, xa, xc, crc);
+				mmcs_col<KM, RM, W, REFL, TB, true, ECG_CSUM_STRIDE, true>(
 					P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)(i + 1) * ECG_CSUM_STRIDE, lo,
-					i + 2 < m, false, Q.init, (m - 2 - i) % F5::U, PF ? xb : xa, xa, crc);
+					i + 2 < iend, false, Q.init, (m - 2 - i) % F5::U, xc, xa, crc);
+			}
 		}
+		for (; i < m; i++)
+			mmcs_col<KM, RM, W, REFL, TB, false, ECG_CSUM_STRIDE, false>(
+				P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)i * ECG_CSUM_STRIDE, lo, false,
+				i == 0 && lane == 0, Q.init, (m - 1 - i) % F5::U, xa, xa, crc);
 		const T kcur = kw[(lastc ? 64 : 0) + lane];
 #pragma unroll
 		for (int r = 0; r < RM; r++) {

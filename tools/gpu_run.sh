@@ -218,8 +218,7 @@ PY
 		step ec_libs 900 python tools/ec_libs.py daos_amd/lib/libecg.so build/exp/xoronly/libecg.so || exit $?
 		;;
 	fusedlibs)
-		step fused_libs 900 python tools/fused_libs.py daos_amd/lib/libecg.so build/exp/nocrc/libecg.so \
-			build/exp/nocrcmul/libecg.so || exit $?
+		step fused_libs 900 python tools/fused_libs.py daos_amd/lib/libecg.so ${FUSED_LIBS:-} || exit $?
 		;;
 	fusedpmc)
 		rm -rf gpurun_out/pmc_ffetch gpurun_out/pmc_fwrite
