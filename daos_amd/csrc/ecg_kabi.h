@@ -112,11 +112,14 @@ typedef struct ecg_launch_cfg {
 #define ECG_CSUM_P5U 4
 #define ECG_CSUM_OFF_P5X_1K(NB) (ECG_CSUM_OFF_S16(NB) + 16 * 256)
 #define ECG_CSUM_OFF_P5X_256(NB) (ECG_CSUM_OFF_P5X_1K(NB) + (ECG_CSUM_P5U - 1) * ECG_CSUM_NF5 * 32)
-/* the fused workgroup kernel's 4 KiB column stride: positions and the a5 of
- * ECG_CSUM_P5U columns */
+/* the fused workgroup kernel's 4 KiB columns: positional tables of 1 ..
+ * ECG_MMCS_P5U-1 columns and the a5 of ECG_MMCS_P5U columns (an item of at
+ * most ECG_MMCS_P5U columns needs no register shift at all, so its columns can
+ * be walked in any order) */
+#define ECG_MMCS_P5U 8
 #define ECG_CSUM_OFF_P5X_4K(NB) (ECG_CSUM_OFF_P5X_256(NB) + (ECG_CSUM_P5U - 1) * ECG_CSUM_NF5 * 32)
-#define ECG_CSUM_OFF_A5_16K(NB) (ECG_CSUM_OFF_P5X_4K(NB) + (ECG_CSUM_P5U - 1) * ECG_CSUM_NF5 * 32)
-#define ECG_CSUM_TBL_ENTRIES(NB) (ECG_CSUM_OFF_A5_16K(NB) + ECG_CSUM_NA5(NB) * 32)
+#define ECG_CSUM_OFF_A5_32K(NB) (ECG_CSUM_OFF_P5X_4K(NB) + (ECG_MMCS_P5U - 1) * ECG_CSUM_NF5 * 32)
+#define ECG_CSUM_TBL_ENTRIES(NB) (ECG_CSUM_OFF_A5_32K(NB) + ECG_CSUM_NA5(NB) * 32)
 #define ECG_CSUM_OFF_P2(NB) (3 * (NB) * 256 + 64 + 256)
 #define ECG_CSUM_OFF_SH256(NB) (3 * (NB) * 256 + 64 + 256 + ECG_CSUM_NP2)
 #define ECG_CSUM_GLANES 16	/* lanes per chunk in the lane-group CRC kernel */

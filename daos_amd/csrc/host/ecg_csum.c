@@ -318,10 +318,11 @@ static void *build_crc_tables(const struct crc_def *d, size_t *bytes)
 			 t + ECG_CSUM_OFF_P5X_1K(nb) + (size_t)(u - 1) * ECG_CSUM_NF5 * 32);
 		build_p5(d, (uint64_t)u * ECG_CSUM_GSTRIDE,
 			 t + ECG_CSUM_OFF_P5X_256(nb) + (size_t)(u - 1) * ECG_CSUM_NF5 * 32);
+	}
+	for (int u = 1; u < ECG_MMCS_P5U; u++)
 		build_p5(d, (uint64_t)u * ECG_MMCS_STRIDE,
 			 t + ECG_CSUM_OFF_P5X_4K(nb) + (size_t)(u - 1) * ECG_CSUM_NF5 * 32);
-	}
-	build_a5(d, (uint64_t)ECG_CSUM_P5U * ECG_MMCS_STRIDE, t + ECG_CSUM_OFF_A5_16K(nb));
+	build_a5(d, (uint64_t)ECG_MMCS_P5U * ECG_MMCS_STRIDE, t + ECG_CSUM_OFF_A5_32K(nb));
 	build_a5(d, ECG_CSUM_STRIDE, t + ECG_CSUM_OFF_A5_1K(nb));
 	build_a5(d, ECG_CSUM_GSTRIDE, t + ECG_CSUM_OFF_A5_256(nb));
 	build_a5(d, ECG_MMCS_STRIDE, t + ECG_CSUM_OFF_A5_4K(nb));
@@ -403,9 +404,13 @@ static void fused_cols_init(void)
 		g_fused_cols_env = 0;
 }
 
-static uint32_t fused_cols(const ecg_ctx_t *ctx, uint64_t m, int type, int rows)
+static uint32_t fused_cols(const ecg_ctx_t *ctx, uint64_t m, int type, int k, int rows)
 {
-	const uint64_t dflt = type == ECG_HASH_CRC64 || rows > 1 ? 8 : 4;
+	/* tools/fused_libs.py, profiles/r02/fused_libs/: crc64 8 (its W-step per-item
+	 * multiply wants long items); one output row (a parity shard's rebuild) 4;
+	 * crc16 / crc32 with >= 2 rows: 4 for k >= 8 (EC_8P2 +10 % vs +16 % at 8),
+	 * 8 for k <= 4 (EC_4P2 +11.5 % vs +21 % at 4) */
+	const uint64_t dflt = type == ECG_HASH_CRC64 ? 8 : rows == 1 ? 4 : k >= 8 ? 4 : 8;
 	const int env = ctx->fused_cols ? (int)ctx->fused_cols
 					: (pthread_once(&g_fused_cols_once, fused_cols_init), g_fused_cols_env);
 
@@ -706,7 +711,7 @@ int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t
 	m = rcs / ECG_MMCS_STRIDE;
 	q->m = (uint32_t)m;
 	q->m_last = (uint32_t)((last + ECG_MMCS_STRIDE - 1) / ECG_MMCS_STRIDE);
-	q->ncols = fused_cols(ctx, m, type, rows);
+	q->ncols = fused_cols(ctx, m, type, k, rows);
 	/* bound the multiplier table (nh + nh_last rows of 256 entries) for
 	 * very long chunks: at most 2048 items per chunk */
 	if ((m + q->ncols - 1) / q->ncols > 2048)

@@ -155,9 +155,9 @@ __device__ __forceinline__ T piece_crc5p(const uint32_t d[4], const T *q5, uint3
 // register is shifted once per U pieces (by U strides) instead of per piece:
 // acc' = shift_U(acc) ^ XOR_u q5[U-1-u](piece u).  LDS image: q5[U][NF][32]
 // then the a5 table of the U-stride shift.
-template <int W>
+template <int W, int U_ = ECG_CSUM_P5U>
 struct f5u {
-	static constexpr int U = ECG_CSUM_P5U;
+	static constexpr int U = U_;
 	static constexpr int NF = ECG_CSUM_NF5;
 	static constexpr int NA = ECG_CSUM_NA5(W / 8);
 	static constexpr int N = (U * NF + NA) * 32;
@@ -204,12 +204,12 @@ __device__ __forceinline__ T horner5u(T acc, const uint32_t (*d)[4], const T *q5
 }
 
 // stage q5 (p5 = position 0, positions 1..U-1 at gt + p5x_off) and the
-// U-stride a5 (gt + a5_off) into LDS s5[f5u<W>::N]
-template <int W, typename T>
+// U-stride a5 (gt + a5_off) into LDS s5[f5u<W, U>::N]
+template <int W, int U = ECG_CSUM_P5U, typename T>
 __device__ __forceinline__ void stage5u(T *s5, const T *gt, int p5x_off, int a5_off, int nthreads)
 {
-	constexpr int NB = W / 8, P = ECG_CSUM_NF5 * 32, U = f5u<W>::U;
-	for (int i = threadIdx.x; i < f5u<W>::N; i += nthreads)
+	constexpr int NB = W / 8, P = ECG_CSUM_NF5 * 32;
+	for (int i = threadIdx.x; i < f5u<W, U>::N; i += nthreads)
 		s5[i] = i < P ? gt[ECG_CSUM_OFF_P5(NB) + i]
 		      : i < U * P ? gt[p5x_off + i - P] : gt[a5_off + i - U * P];
 }

@@ -31,8 +31,18 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #define CHUNK_BYTES 4096u	// 256 lanes x 16 B
 #define BLOCK 256
+#ifndef ECG_FUSED_PF64
+#define ECG_FUSED_PF64 1	// prefetch in the crc64 fused kernels too
+#endif
+#ifndef ECG_FUSED_PF_MAXK
+#define ECG_FUSED_PF_MAXK 8	// fused kernels: next column's loads in flight for k <= this
+#endif
+// fused kernels: the waves per SIMD their register budget targets.  crc16 /
+// crc32 get the 3-wave budget (<= 168 VGPRs): at a 4-wave budget the register
+// allocator spilled EC_8P2's pipelined loop to scratch, at 3 it settles at
+// 104 VGPRs -- 4 waves anyway, no spills.  crc64 fits 4 waves without spills.
 #ifndef ECG_FUSED_WPE
-#define ECG_FUSED_WPE 4		// fused kernels: waves per SIMD the register budget targets
+#define ECG_FUSED_WPE(W) ((W) == 64 ? 4 : 3)
 #endif
 
 __device__ __forceinline__ u32x4 ld_nt(const uint8_t *p)
@@ -424,7 +434,9 @@ __device__ __forceinline__ void mmcs_item(const ecg_mmcs_params_t &Q, uint32_t i
 // 16-byte piece folded into the row's CRC.  TB 0: pos = columns to the item
 // end mod U selects the positional table; the register is shifted by U
 // columns at each group start (pos == U - 1).  `first`: this piece starts
-// the chunk, the initial register is folded into it.
+// the chunk, the initial register is folded into it.  `next`: the column the
+// prefetch reads (the walk need not be in address order); gshift = false for
+// a walk whose positions all fit the U tables (no register shift at all).
 // The kernel arguments re-read (scalar loads, K$ hits) where they are used:
 // an empty asm on their constant-space address stops the compiler from
 // keeping every cell offset of the launch live in SGPRs across a column loop
@@ -440,13 +452,13 @@ __device__ __forceinline__ const ecg_mm_params_t &kernarg_fresh()
 	return *(const ecg_mm_params_t *)p;
 }
 
-template <int KM, int RM, int W, bool REFL, int TB, bool PF, uint32_t STRIDE, bool FULL, typename T>
+template <int KM, int RM, int W, bool REFL, int TB, bool PF, uint32_t STRIDE, bool FULL, int U, typename T>
 __device__ __forceinline__ void mmcs_col(const ecg_mm_params_t &P0, const u32x4 *s_tbl, const T *s_sl,
-					 const T *s_sh, int k, int rows, uint32_t s, uint64_t cbase, uint32_t lo,
-					 bool more, bool first, uint64_t init, uint32_t pos, u32x4 *cur, u32x4 *nxt,
-					 T *crc)
+					 const T *s_sh, int k, int rows, uint32_t s, uint64_t cbase, uint64_t next,
+					 uint32_t lo, bool more, bool first, uint64_t init, uint32_t pos, bool gshift,
+					 u32x4 *cur, u32x4 *nxt, T *crc)
 {
-	using F5 = ecg_crc::f5u<W>;
+	using F5 = ecg_crc::f5u<W, U>;
 	const ecg_mm_params_t &P = kernarg_fresh();	// == P0 (first kernel argument)
 	(void)P0;
 	const uint64_t C = P.cell_bytes;
@@ -459,9 +471,11 @@ __device__ __forceinline__ void mmcs_col(const ecg_mm_params_t &P0, const u32x4 
 		// issued makes the compiler's waitcnt merge wait for everything
 		// (vmcnt(0)) before the product.  Past the item's last column the
 		// wave re-reads stripe 0's first column (cache-resident, unused).
-		mm_load_any<KM>(P, k, more ? s : 0, more ? cbase + STRIDE : 0, lo, nxt);
-	} else if (have) {
-		mm_load<KM, false>(P, k, s, cbase, lo, cur);
+		mm_load_any<KM>(P, k, more ? s : 0, more ? next : 0, lo, nxt);
+	} else {
+		// unconditional (clamped) loads: a load skipped by some lanes would
+		// keep cur live across columns and items (zero-filled and spilled)
+		mm_load_any<KM>(P, k, s, cbase, lo, cur);
 	}
 	asm volatile("" : "+v"(z));
 	const u32x4 *tb = s_tbl + z;
@@ -479,7 +493,7 @@ __device__ __forceinline__ void mmcs_col(const ecg_mm_params_t &P0, const u32x4 
 #ifndef ECG_EXP_NO_CRC
 			if constexpr (TB != 0)
 				crc[r] = ecg_crc::lin_map<W>(crc[r], s_sh);
-			else if (pos == F5::U - 1)
+			else if (gshift && pos == F5::U - 1)
 				crc[r] = ecg_crc::lin_map5<W>(crc[r], s_sl + F5::U * F5::NF * 32);
 #endif
 			if (have) {
@@ -518,15 +532,16 @@ __device__ __forceinline__ void mmcs_col(const ecg_mm_params_t &P0, const u32x4 
 // p/(k+p) of the traffic instead of a second pass over the regenerated
 // cells (ref:src/object/srv_obj_migrate.c:1156 checksums them after encode).
 template <int K, int R, int W, bool REFL, int TB = 0>
-__global__ void __launch_bounds__(BLOCK, ECG_FUSED_WPE)	// >= 4 waves per SIMD: <= 128 VGPRs
+__global__ void __launch_bounds__(BLOCK, ECG_FUSED_WPE(W))
 ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 {
 	using T = typename ecg_crc::reg<W>::T;
-	using F5 = ecg_crc::f5u<W>;
+	constexpr int UF = ECG_MMCS_P5U;
+	using F5 = ecg_crc::f5u<W, UF>;
 	constexpr int NB = W / 8;
 	constexpr int KM = K ? K : ECG_KMAX_K;
 	constexpr int RM = R ? R : ECG_KMAX_R;
-	constexpr bool PF = K != 0 && K <= 8 && W != 64;	// prefetch: 4*KM more VGPRs (crc64 spills)
+	constexpr bool PF = K != 0 && K <= ECG_FUSED_PF_MAXK && (ECG_FUSED_PF64 || W != 64);	// prefetch: 4*KM more VGPRs
 	constexpr int T2V = (RM + 3) / 4;
 	constexpr int PER_J = RM + T2V;
 	__shared__ u32x4 s_tbl[KM * PER_J];
@@ -557,7 +572,7 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 		for (int i = threadIdx.x; i < NB * 256; i += BLOCK)
 			s_sh[i] = gt[ECG_CSUM_OFF_SH4K(NB) + i];
 	} else {
-		ecg_crc::stage5u<W>(s_sl, gt, ECG_CSUM_OFF_P5X_4K(NB), ECG_CSUM_OFF_A5_16K(NB), BLOCK);
+		ecg_crc::stage5u<W, UF>(s_sl, gt, ECG_CSUM_OFF_P5X_4K(NB), ECG_CSUM_OFF_A5_32K(NB), BLOCK);
 	}
 	const T *kh = (const T *)Q.kh;
 	const T poly = (T)Q.poly;
@@ -580,12 +595,15 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 			for (int r = 0; r < RM; r++)
 				crc[r] = 0;
 			// Pipelined pairs of full columns, the prefetch buffers swapping
-			// roles (a register copy xa = xb would wait for the prefetched
-			// loads and serialise the walk); then the rest -- an odd full
-			// column, the partial column of a cell that is not a multiple of
-			// 4 KiB -- one at a time without prefetch, outside the pipelined
-			// loop so that loop has a single path (a path that skips loads or
-			// stores makes the compiler wait for everything at the loop head).
+			// roles (a register copy xa = xb would wait for the prefetched loads
+			// and serialise the walk); then the rest -- an odd full column, the
+			// partial column of a cell that is not a multiple of 4 KiB -- one at
+			// a time without prefetch, outside the pipelined loop so that loop
+			// has a single path (a path that skips loads or stores makes the
+			// compiler wait for everything at the loop head).  (Walking an
+			// item's columns rotated, so concurrently running items stream
+			// different address residues, measured no better:
+			// profiles/r02/fused_libs/rotation.json.)
 			const uint64_t nfull = (C - c0) / CHUNK_BYTES;
 			const uint32_t ifull = nfull < col1 ? (uint32_t)nfull : col1;
 			const uint32_t iend = ifull > i ? i + ((ifull - i) & ~1u) : i;
@@ -595,18 +613,19 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 
 				mm_load_any<KM>(P, k, s, c0 + (uint64_t)i * CHUNK_BYTES, lo, xa);
 				for (; i < iend; i += 2) {
-					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true>(
-						P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)i * CHUNK_BYTES, lo, true,
-						i == 0 && threadIdx.x == 0, Q.init, (col1 - 1 - i) % F5::U, xa, xc, crc);
-					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true>(
-						P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)(i + 1) * CHUNK_BYTES, lo,
-						i + 2 < iend, false, Q.init, (col1 - 2 - i) % F5::U, xc, xa, crc);
+					const uint64_t cb = c0 + (uint64_t)i * CHUNK_BYTES;
+					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true, UF>(
+						P, s_tbl, s_sl, s_sh, k, rows, s, cb, cb + CHUNK_BYTES, lo, true,
+						i == 0 && threadIdx.x == 0, Q.init, (col1 - 1 - i) % UF, true, xa, xc, crc);
+					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true, UF>(
+						P, s_tbl, s_sl, s_sh, k, rows, s, cb + CHUNK_BYTES, cb + 2 * CHUNK_BYTES, lo,
+						i + 2 < iend, false, Q.init, (col1 - 2 - i) % UF, true, xc, xa, crc);
 				}
 			}
 			for (; i < col1; i++)
-				mmcs_col<KM, RM, W, REFL, TB, false, CHUNK_BYTES, false>(
-					P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)i * CHUNK_BYTES, lo, false,
-					i == 0 && threadIdx.x == 0, Q.init, (col1 - 1 - i) % F5::U, xa, xa, crc);
+				mmcs_col<KM, RM, W, REFL, TB, false, CHUNK_BYTES, false, UF>(
+					P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)i * CHUNK_BYTES, 0, lo, false,
+					i == 0 && threadIdx.x == 0, Q.init, (col1 - 1 - i) % UF, true, xa, xa, crc);
 			// each wave XORs its partial into the (zeroed) output: no
 			// workgroup barrier, other waves keep streaming
 			const T kcur = kh[khrow * 256 + threadIdx.x];
@@ -646,7 +665,7 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 // -- the multiply dominates crc64's cost there (tools/fused_sweep.py).
 // Tables (TB as ecg_mm_csum_kernel) with the 1 KiB shift.
 template <int K, int R, int W, bool REFL, int TB>
-__global__ void __launch_bounds__(BLOCK, ECG_FUSED_WPE)
+__global__ void __launch_bounds__(BLOCK, ECG_FUSED_WPE(W))
 ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 {
 	using T = typename ecg_crc::reg<W>::T;
@@ -654,7 +673,7 @@ ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	constexpr int NB = W / 8;
 	constexpr int KM = K ? K : ECG_KMAX_K;
 	constexpr int RM = R ? R : ECG_KMAX_R;
-	constexpr bool PF = K != 0 && K <= 8 && W != 64;	// next row's loads in flight
+	constexpr bool PF = K != 0 && K <= ECG_FUSED_PF_MAXK && (ECG_FUSED_PF64 || W != 64);	// next row's loads in flight
 	constexpr int T2V = (RM + 3) / 4;
 	constexpr int PER_J = RM + T2V;
 	constexpr int NSL = TB == 0 ? F5::N : TB == 1 ? NB * 256 : 16 * 256;
@@ -716,18 +735,19 @@ ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 
 			mm_load_any<KM>(P, k, s, c0, lo, xa);
 			for (; i < iend; i += 2) {
-				mmcs_col<KM, RM, W, REFL, TB, true, ECG_CSUM_STRIDE, true>(
-					P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)i * ECG_CSUM_STRIDE, lo, true,
-					i == 0 && lane == 0, Q.init, (m - 1 - i) % F5::U, xa, xc, crc);
-				mmcs_col<KM, RM, W, REFL, TB, true, ECG_CSUM_STRIDE, true>(
-					P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)(i + 1) * ECG_CSUM_STRIDE, lo,
-					i + 2 < iend, false, Q.init, (m - 2 - i) % F5::U, xc, xa, crc);
+				const uint64_t cb = c0 + (uint64_t)i * ECG_CSUM_STRIDE;
+				mmcs_col<KM, RM, W, REFL, TB, true, ECG_CSUM_STRIDE, true, F5::U>(
+					P, s_tbl, s_sl, s_sh, k, rows, s, cb, cb + ECG_CSUM_STRIDE, lo, true,
+					i == 0 && lane == 0, Q.init, (m - 1 - i) % F5::U, true, xa, xc, crc);
+				mmcs_col<KM, RM, W, REFL, TB, true, ECG_CSUM_STRIDE, true, F5::U>(
+					P, s_tbl, s_sl, s_sh, k, rows, s, cb + ECG_CSUM_STRIDE, cb + 2 * ECG_CSUM_STRIDE, lo,
+					i + 2 < iend, false, Q.init, (m - 2 - i) % F5::U, true, xc, xa, crc);
 			}
 		}
 		for (; i < m; i++)
-			mmcs_col<KM, RM, W, REFL, TB, false, ECG_CSUM_STRIDE, false>(
-				P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)i * ECG_CSUM_STRIDE, lo, false,
-				i == 0 && lane == 0, Q.init, (m - 1 - i) % F5::U, xa, xa, crc);
+			mmcs_col<KM, RM, W, REFL, TB, false, ECG_CSUM_STRIDE, false, F5::U>(
+				P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)i * ECG_CSUM_STRIDE, 0, lo, false,
+				i == 0 && lane == 0, Q.init, (m - 1 - i) % F5::U, true, xa, xa, crc);
 		const T kcur = kw[(lastc ? 64 : 0) + lane];
 #pragma unroll
 		for (int r = 0; r < RM; r++) {

@@ -2,8 +2,9 @@
 (one subprocess per library, interleaved twice), e.g. -DECG_EXP_NO_CRC (the
 CRC lookups compiled out) and -DECG_EXP_NO_MULMOD (the per-item multiply
 compiled out): EC_8P2 x 512 and EC_4P2 x 1024 (1 MiB cells, random data,
-32 KiB chunks), crc32 / crc64, columns per item 2 / 4 / 8 / 16 and the
-default, against the plain encode.  Median of 15 after 5 warm-up launches.
+32 KiB chunks), crc32 / crc64, columns per item 4 / 8 / 16 and the
+default, against the plain encode, interleaved launch by launch; median of
+15 after 3 warm-up launches each.
 usage: python tools/fused_libs.py lib1.so lib2.so ...  -> gpurun_out/fused_libs.json.
 Bench infrastructure."""
 import json
@@ -30,29 +31,44 @@ for off in range(0, buf.nbytes, blk.size):
 par = ctx.alloc(2 * (1024 * C + 4096))
 out = ctx.alloc(1 << 22)
 
-def timed(fn, reps=15):
-    for _ in range(5):
-        fn()
-    ctx.sync()
-    ts = []
-    for _ in range(reps):
-        ctx.record(a); fn(); ctx.record(b); ts.append(ctx.elapsed_ms(a, b))
-    ts.sort()
-    return ts[reps // 2]
+def cfg(k, p, S, htype, cols, variant=0):
+    pitch = S * C + 4096
+    if htype == 0:
+        return lambda: ctx.encode(k, p, C, S, buf.ptr, k * C, par.ptr, pitch, C)
+    def fn():
+        L.ecg_set_fused_cols(ctx.h, cols)
+        L.ecg_set_csum_variant(ctx.h, variant)
+        ctx.encode_csum(k, p, C, S, buf.ptr, k * C, par.ptr, pitch, C, htype, 32768, 1, out.ptr)
+        L.ecg_set_csum_variant(ctx.h, 0)
+    return fn
 
+# configurations interleaved launch by launch (the box's clocks drift over a
+# long run; back-to-back blocks of one configuration would absorb the drift)
 res = {}
 for k, p, S in ((8, 2, 512), (4, 2, 1024)):
-    pitch = S * C + 4096
-    assert k * S * C <= buf.nbytes and p * pitch <= par.nbytes and p * S * 32 * 8 <= out.nbytes
+    assert k * S * C <= buf.nbytes and 2 * (S * C + 4096) <= par.nbytes and p * S * 32 * 8 <= out.nbytes
     tag = "%%dP%%d_x%%d" %% (k, p, S)
-    res[tag + "_encode_ms"] = round(timed(lambda: ctx.encode(k, p, C, S, buf.ptr, k * C, par.ptr, pitch, C)), 4)
+    cfgs = [(tag + "_encode_ms", cfg(k, p, S, 0, 0))]
     for hname, htype in (("crc32", 2), ("crc64", 3)):
-        for cols in (0, 2, 4, 8, 16):
-            L.ecg_set_fused_cols(ctx.h, cols)
-            ms = timed(lambda: ctx.encode_csum(k, p, C, S, buf.ptr, k * C, par.ptr, pitch, C, htype, 32768, 1, out.ptr))
-            res["%%s_%%s_c%%d_ms" %% (tag, hname, cols)] = round(ms, 4)
-            res["%%s_%%s_c%%d_kernel" %% (tag, hname, cols)] = L.ecg_last_kernel().decode()
-        L.ecg_set_fused_cols(ctx.h, 0)
+        for cols in (0, 4, 8):
+            cfgs.append(("%%s_%%s_c%%d_ms" %% (tag, hname, cols), cfg(k, p, S, htype, cols)))
+        # the wave-per-chunk kernel (csum_variant 128) and the workgroup kernel (256)
+        cfgs.append(("%%s_%%s_wave_ms" %% (tag, hname), cfg(k, p, S, htype, 0, 128)))
+        cfgs.append(("%%s_%%s_wg_ms" %% (tag, hname), cfg(k, p, S, htype, 0, 256)))
+    ts = {n: [] for n, _ in cfgs}
+    for n, fn in cfgs:
+        for _ in range(3):
+            fn()
+        if "crc" in n:
+            res[n.replace("_ms", "_kernel")] = L.ecg_last_kernel().decode()
+    ctx.sync()
+    for rep in range(15):
+        for n, fn in cfgs:
+            ctx.record(a); fn(); ctx.record(b); ts[n].append(ctx.elapsed_ms(a, b))
+    for n, v in ts.items():
+        v.sort()
+        res[n] = round(v[len(v) // 2], 4)
+    L.ecg_set_fused_cols(ctx.h, 0)
 print(json.dumps(res))
 ''' % ROOT
 
