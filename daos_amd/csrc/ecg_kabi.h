@@ -119,7 +119,14 @@ typedef struct ecg_launch_cfg {
 #define ECG_MMCS_P5U 8
 #define ECG_CSUM_OFF_P5X_4K(NB) (ECG_CSUM_OFF_P5X_256(NB) + (ECG_CSUM_P5U - 1) * ECG_CSUM_NF5 * 32)
 #define ECG_CSUM_OFF_A5_32K(NB) (ECG_CSUM_OFF_P5X_4K(NB) + (ECG_MMCS_P5U - 1) * ECG_CSUM_NF5 * 32)
-#define ECG_CSUM_TBL_ENTRIES(NB) (ECG_CSUM_OFF_A5_32K(NB) + ECG_CSUM_NA5(NB) * 32)
+/* reflected CRCs (crc32, crc64): the fused workgroup kernel multiplies a
+ * lane's value by x^(8*16*(63-lane)) nibble by nibble --
+ *   nibl[n][lane] = (n at the register's 4 lowest powers) * x^(8*16*(63-lane))
+ *   r4[m]         = m (register bits 0-3) * x^4, the reduction of a 4-bit shift
+ * (n-major, so lane l's entries sit in bank l: conflict-free) */
+#define ECG_CSUM_OFF_NIBL(NB) (ECG_CSUM_OFF_A5_32K(NB) + ECG_CSUM_NA5(NB) * 32)
+#define ECG_CSUM_OFF_R4(NB) (ECG_CSUM_OFF_NIBL(NB) + 16 * 64)
+#define ECG_CSUM_TBL_ENTRIES(NB) (ECG_CSUM_OFF_R4(NB) + 16)
 #define ECG_CSUM_OFF_P2(NB) (3 * (NB) * 256 + 64 + 256)
 #define ECG_CSUM_OFF_SH256(NB) (3 * (NB) * 256 + 64 + 256 + ECG_CSUM_NP2)
 #define ECG_CSUM_GLANES 16	/* lanes per chunk in the lane-group CRC kernel */
@@ -176,16 +183,19 @@ typedef struct ecg_csum_params {
  * is cut into sub-chunks of ncols columns, item = (c, h) with h < nh (nh_last
  * for the last chunk), numbered c * nh + h; nitems = (nch - 1) * nh + nh_last.
  * A workgroup Horner-accumulates its sub-chunk's columns per thread and then
- * multiplies thread t's value by kh[(row0 + h) * 256 + t] (row0 = 0, or nh for
- * the last chunk) = x^(8 * (16 * (255 - t) + 4096 * (columns after the
- * sub-chunk))) mod P, times x^(-8Z) in the last chunk's rows, Z being the zero
- * bytes that pad the cell to whole columns.  CRC is linear, so the
- * workgroups' values XOR to the chunk's CRC.
+ * moves thread t's value to the end of the chunk: a factor x^(8 * (16 * (255 -
+ * t) + 4096 * (columns after the sub-chunk))) mod P, times x^(-8Z) in the last
+ * chunk's rows, Z being the zero bytes that pad the cell to whole columns.
+ * crc16: kh[(row0 + h) * 256 + t] holds that factor (row0 = 0, or nh for the
+ * last chunk).  Reflected CRCs: the lane part x^(8*16*(63-lane)) comes from the
+ * nibl tables, each wave XOR-reduces, and kh[(row0 + h) * 4 + wave] holds the
+ * rest, x^(8 * (1024 * (3 - wave) + 4096 * (columns after))) (* x^(-8Z)),
+ * applied once per wave.  CRC is linear, so the values XOR to the chunk's CRC.
  */
 typedef struct ecg_mmcs_params {
 	const void *tbl;
 	uint8_t *out;
-	const void *kh;			/* (nh + nh_last) x 256 entries, T as tbl */
+	const void *kh;			/* (nh + nh_last) x 256 (crc16) or x 4 entries, T as tbl */
 	uint64_t chunk_bytes;
 	uint64_t init, xorout, poly;
 	uint32_t nch;

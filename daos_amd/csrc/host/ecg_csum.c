@@ -323,6 +323,20 @@ static void *build_crc_tables(const struct crc_def *d, size_t *bytes)
 		build_p5(d, (uint64_t)u * ECG_MMCS_STRIDE,
 			 t + ECG_CSUM_OFF_P5X_4K(nb) + (size_t)(u - 1) * ECG_CSUM_NF5 * 32);
 	build_a5(d, (uint64_t)ECG_MMCS_P5U * ECG_MMCS_STRIDE, t + ECG_CSUM_OFF_A5_32K(nb));
+	if (d->refl) {
+		/* nibl[n][l] = (n << (W - 4)) * x^(8*16*(63-l)); r4[m] = m * x^4 */
+		for (int l = 0; l < 64; l++)
+			for (int n = 0; n < 16; n++)
+				t[ECG_CSUM_OFF_NIBL(nb) + (size_t)n * 64 + l] =
+					crc_mulmod(d, (uint64_t)n << (d->width - 4), t[ECG_CSUM_OFF_K64(nb) + l]);
+		for (int m = 0; m < 16; m++) {
+			uint64_t c = (uint64_t)m;
+
+			for (int b = 0; b < 4; b++)
+				c = (c >> 1) ^ (d->poly & (0 - (c & 1)));
+			t[ECG_CSUM_OFF_R4(nb) + m] = c;
+		}
+	}
 	build_a5(d, ECG_CSUM_STRIDE, t + ECG_CSUM_OFF_A5_1K(nb));
 	build_a5(d, ECG_CSUM_GSTRIDE, t + ECG_CSUM_OFF_A5_256(nb));
 	build_a5(d, ECG_MMCS_STRIDE, t + ECG_CSUM_OFF_A5_4K(nb));
@@ -419,10 +433,12 @@ static uint32_t fused_cols(const ecg_ctx_t *ctx, uint64_t m, int type, int k, in
 	return (uint32_t)(m < dflt ? m : dflt);
 }
 
-/* Device table of the fused kernel's per-(item row, thread) multipliers
- * (ecg_kabi.h ecg_mmcs_params kh): row h < nh of a full chunk of m columns,
- * rows nh + h of the last chunk (m_last columns, z padding bytes):
- *   kh[row][t] = x^(8*(16*(255-t) + 4096*(columns after item h))) * x^(-8z)
+/* Device table of the fused kernel's per-item multipliers (ecg_kabi.h
+ * ecg_mmcs_params kh): row h < nh of a full chunk of m columns, rows nh + h of
+ * the last chunk (m_last columns, z padding bytes):
+ *   crc16:      kh[row][t] = x^(8*(16*(255-t) + 4096*(columns after item h))) * x^(-8z)
+ *   reflected:  kh[row][w] = x^(8*(1024*(3-w) + 4096*(columns after item h))) * x^(-8z)
+ *               (the lane part comes from the nibl tables)
  * Cached per context by (type, chunk bytes, columns per item, last length). */
 static int fused_kh(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, uint32_t ncols,
 		    uint32_t nh, uint32_t nh_last, const void **out)
@@ -432,6 +448,7 @@ static int fused_kh(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, uint3
 	const uint64_t m_last = (last + ECG_MMCS_STRIDE - 1) / ECG_MMCS_STRIDE;
 	const uint64_t z = m_last * ECG_MMCS_STRIDE - last;
 	const size_t es = d->width == 64 ? 8 : 4, nrow = (size_t)nh + nh_last;
+	const size_t per = d->refl ? 4 : 256;	/* entries per row: waves or threads */
 	struct ecg_kh_ent *e;
 	uint64_t k256[256];
 	unsigned char *img;
@@ -448,7 +465,7 @@ static int fused_kh(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, uint3
 			return 0;
 		}
 	}
-	img = malloc(nrow * 256 * es);
+	img = malloc(nrow * per * es);
 	if (img == NULL) {
 		pthread_mutex_unlock(&ctx->lock);
 		return ecg_fail(-ECG_DER_NOMEM, "fused csum multipliers");
@@ -464,21 +481,23 @@ static int fused_kh(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, uint3
 
 		if (lastc)
 			sh = crc_mulmod(d, sh, crc_unshift(d, z));
-		for (int t = 0; t < 256; t++) {
-			const uint64_t v = crc_mulmod(d, k256[t], sh);
+		for (size_t t = 0; t < per; t++) {
+			/* reflected: wave t's factor (k256[64 w + 63] = x^(8*16*(192-64w))
+			 * = x^(8*1024*(3-w))); crc16: thread t's */
+			const uint64_t v = crc_mulmod(d, k256[per == 4 ? 64 * t + 63 : t], sh);
 
 			if (es == 8) {
-				memcpy(img + (row * 256 + t) * 8, &v, 8);
+				memcpy(img + (row * per + t) * 8, &v, 8);
 			} else {
 				const uint32_t w = (uint32_t)v;
 
-				memcpy(img + (row * 256 + t) * 4, &w, 4);
+				memcpy(img + (row * per + t) * 4, &w, 4);
 			}
 		}
 	}
-	he = hipMalloc(&dev, nrow * 256 * es);
+	he = hipMalloc(&dev, nrow * per * es);
 	if (he == hipSuccess)
-		he = hipMemcpy(dev, img, nrow * 256 * es, hipMemcpyHostToDevice);
+		he = hipMemcpy(dev, img, nrow * per * es, hipMemcpyHostToDevice);
 	free(img);
 	if (he != hipSuccess) {
 		if (dev)

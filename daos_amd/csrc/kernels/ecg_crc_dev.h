@@ -278,6 +278,20 @@ __device__ __forceinline__ T mulmod(T a, T b, T poly)
 	return p;
 }
 
+// a wave-uniform value moved to SGPRs (so arithmetic on it runs on the
+// scalar unit)
+template <typename T>
+__device__ __forceinline__ T uniform(T v)
+{
+	// (the builtin returns int: cast through uint32_t, or the low half would
+	// be sign-extended into the high half)
+	if constexpr (sizeof(T) == 8)
+		return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+		       (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+	else
+		return (T)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_xor(T v)
 {

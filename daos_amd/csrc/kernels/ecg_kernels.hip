@@ -492,7 +492,7 @@ __device__ __forceinline__ void mmcs_col(const ecg_mm_params_t &P0, const u32x4 
 		if (r < rows) {
 #ifndef ECG_EXP_NO_CRC
 			if constexpr (TB != 0)
-				crc[r] = ecg_crc::lin_map<W>(crc[r], s_sh);
+				crc[r] = ecg_crc::lin_map5<W>(crc[r], s_sh);	// a5 of one column
 			else if (gshift && pos == F5::U - 1)
 				crc[r] = ecg_crc::lin_map5<W>(crc[r], s_sl + F5::U * F5::NF * 32);
 #endif
@@ -547,16 +547,25 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	__shared__ u32x4 s_tbl[KM * PER_J];
 	// CRC tables (TB): 0 5-bit (conflict-free, ecg_kabi.h: positional p5 of
 	// 0..U-1 columns + a5 shift by U columns, U = ECG_CSUM_P5U); 1 byte
-	// tables sl (slice-by-NB, register folded) + sh4k; 2 byte tables s16 (16
-	// independent lookups per piece) + sh4k
+	// tables sl (slice-by-NB, register folded) + the a5 4 KiB shift; 2 byte tables s16 (16
+	// independent lookups per piece) + the a5 shift
 	constexpr int NSL = TB == 0 ? F5::N : TB == 1 ? NB * 256 : 16 * 256;
 	__shared__ T s_sl[NSL];
-	__shared__ T s_sh[TB ? NB * 256 : 1];
+	__shared__ T s_sh[TB ? ECG_CSUM_NA5(NB) * 32 : 1];	// TB 1/2: the column shift as 5-bit a5 tables
+	__shared__ T s_nib[REFL ? 16 * 64 : 1];		// reflected: lane multiply tables
+	__shared__ T s_r4[REFL ? 16 : 1];
 	const int k = K ? K : (int)P.k;
 	const int rows = R ? R : (int)P.rows;
 	const uint64_t C = P.cell_bytes;
 	const uint32_t lo = threadIdx.x * 16u;
 	const T *gt = (const T *)Q.tbl;
+
+	if constexpr (REFL) {
+		for (int i = threadIdx.x; i < 16 * 64; i += BLOCK)
+			s_nib[i] = gt[ECG_CSUM_OFF_NIBL(NB) + i];
+		if (threadIdx.x < 16)
+			s_r4[threadIdx.x] = gt[ECG_CSUM_OFF_R4(NB) + threadIdx.x];
+	}
 
 	for (int i = threadIdx.x; i < KM * RM; i += BLOCK) {
 		const int j = i / RM, r = i % RM;
@@ -569,8 +578,8 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	if constexpr (TB != 0) {
 		for (int i = threadIdx.x; i < NSL; i += BLOCK)
 			s_sl[i] = gt[(TB == 1 ? 0 : ECG_CSUM_OFF_S16(NB)) + i];
-		for (int i = threadIdx.x; i < NB * 256; i += BLOCK)
-			s_sh[i] = gt[ECG_CSUM_OFF_SH4K(NB) + i];
+		for (int i = threadIdx.x; i < ECG_CSUM_NA5(NB) * 32; i += BLOCK)
+			s_sh[i] = gt[ECG_CSUM_OFF_A5_4K(NB) + i];
 	} else {
 		ecg_crc::stage5u<W, UF>(s_sl, gt, ECG_CSUM_OFF_P5X_4K(NB), ECG_CSUM_OFF_A5_32K(NB), BLOCK);
 	}
@@ -627,17 +636,31 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 					P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)i * CHUNK_BYTES, 0, lo, false,
 					i == 0 && threadIdx.x == 0, Q.init, (col1 - 1 - i) % UF, true, xa, xa, crc);
 			// each wave XORs its partial into the (zeroed) output: no
-			// workgroup barrier, other waves keep streaming
-			const T kcur = kh[khrow * 256 + threadIdx.x];
+			// workgroup barrier, other waves keep streaming.  Reflected CRCs:
+			// lane l's value times x^(8*16*(63-l)) nibble by nibble (W/4 steps
+			// of two conflict-free LDS lookups), the wave XOR-reduces, and the
+			// wave's uniform factor kh[khrow][wave] is applied once, on the
+			// scalar unit -- instead of a W-step GF(2) multiply per thread on
+			// the VALU (crc64: 64 steps of 64-bit ops).
 #pragma unroll
 			for (int r = 0; r < RM; r++) {
 				if (r < rows) {
-#ifndef ECG_EXP_NO_MULMOD
-					T v = ecg_crc::mulmod<W, REFL>(kcur, crc[r], poly);
-#else
-					T v = kcur ^ crc[r];
-#endif
-					v = ecg_crc::wave_xor(v);
+					T v;
+					if constexpr (REFL) {
+						const uint32_t lane = threadIdx.x & 63u;
+						const T x = crc[r];
+						T u = 0;
+#pragma unroll
+						for (int sft = 0; sft < W; sft += 4)
+							u = (u >> 4) ^ s_r4[(uint32_t)u & 15u] ^
+							    s_nib[((uint32_t)(x >> sft) & 15u) * 64u + lane];
+						u = ecg_crc::wave_xor(u);
+						const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+						v = ecg_crc::mulmod<W, REFL>(kh[khrow * 4u + wv], ecg_crc::uniform(u), poly);
+					} else {
+						v = ecg_crc::mulmod<W, REFL>(kh[khrow * 256 + threadIdx.x], crc[r], poly);
+						v = ecg_crc::wave_xor(v);
+					}
 					if ((threadIdx.x & 63) == 0) {
 						if (threadIdx.x == 0 && khrow == (c + 1 == Q.nch ? Q.nh : 0))
 							v ^= (T)Q.xorout;	// once per chunk
@@ -679,7 +702,7 @@ ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	constexpr int NSL = TB == 0 ? F5::N : TB == 1 ? NB * 256 : 16 * 256;
 	__shared__ u32x4 s_tbl[KM * PER_J];
 	__shared__ T s_sl[NSL];
-	__shared__ T s_sh[TB ? NB * 256 : 1];
+	__shared__ T s_sh[TB ? ECG_CSUM_NA5(NB) * 32 : 1];	// TB 1/2: the column shift as 5-bit a5 tables
 	const int k = K ? K : (int)P.k;
 	const int rows = R ? R : (int)P.rows;
 	const uint64_t C = P.cell_bytes;
@@ -698,8 +721,8 @@ ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	if constexpr (TB != 0) {
 		for (int i = threadIdx.x; i < NSL; i += BLOCK)
 			s_sl[i] = gt[(TB == 1 ? 0 : ECG_CSUM_OFF_S16(NB)) + i];
-		for (int i = threadIdx.x; i < NB * 256; i += BLOCK)
-			s_sh[i] = gt[ECG_CSUM_OFF_SH(NB) + i];
+		for (int i = threadIdx.x; i < ECG_CSUM_NA5(NB) * 32; i += BLOCK)
+			s_sh[i] = gt[ECG_CSUM_OFF_A5_1K(NB) + i];
 	} else {
 		ecg_crc::stage5u<W>(s_sl, gt, ECG_CSUM_OFF_P5X_1K(NB), ECG_CSUM_OFF_A5_4K(NB), BLOCK);
 	}
