@@ -502,6 +502,27 @@ def time_kernel(ctx, fn, iters, warm=3):
     return ms[len(ms) // 2]
 
 
+def time_interleaved(ctx, fns, iters, warm=3):
+    """Median kernel time of each of `fns`, launched in turn (one launch of
+    each per round): the box's clocks drift over a long run, so timing one
+    configuration's block of launches after another's biases a ratio."""
+    a, b = ctx.event(), ctx.event()
+    for fn in fns:
+        for _ in range(warm):
+            fn()
+    ctx.sync()
+    ms = [[] for _ in fns]
+    for _ in range(iters):
+        for i, fn in enumerate(fns):
+            ctx.record(a)
+            fn()
+            ctx.record(b)
+            ms[i].append(ctx.elapsed_ms(a, b))
+    ctx.destroy_event(a)
+    ctx.destroy_event(b)
+    return [sorted(v)[len(v) // 2] for v in ms]
+
+
 def measured_ceilings(ctx, iters=11):
     """This box's streaming rates (GB/s), each mode at its best measured
     geometry (profiles/r01/tune2*.json): reads with 512 persistent blocks,
@@ -576,16 +597,25 @@ def detail_rows(ctx, ceil, iters=11):
     pitch = S * C + PARITY_ROW_PAD
     par = ctx.alloc(p * pitch)
     out = ctx.alloc(p * S * (C // 32768) * 8)
-    enc = time_kernel(ctx, lambda: ctx.encode(k, p, C, S, data.ptr, k * C, par.ptr, pitch, C), iters)
-    for hname, htype in (("crc32", ecg.HASH_CRC32), ("crc64", ecg.HASH_CRC64)):
-        fus = time_kernel(ctx, lambda: ctx.encode_csum(k, p, C, S, data.ptr, k * C, par.ptr, pitch, C,
-                                                       htype, 32768, 1, out.ptr), iters)
+    hashes = (("crc32", ecg.HASH_CRC32), ("crc64", ecg.HASH_CRC64))
+    kernels = {}
+
+    def fused(htype):
+        def fn():
+            ctx.encode_csum(k, p, C, S, data.ptr, k * C, par.ptr, pitch, C, htype, 32768, 1, out.ptr)
+            kernels[htype] = ecg.last_kernel()
+        return fn
+    # the plain encode and both fused launches interleaved (their ratio is the row's point)
+    enc, *fus_ms = time_interleaved(
+        ctx, [lambda: ctx.encode(k, p, C, S, data.ptr, k * C, par.ptr, pitch, C)] +
+        [fused(htype) for _, htype in hashes], iters)
+    for (hname, htype), fus in zip(hashes, fus_ms):
         alg = (k + p) * C * S
         rows[f"EC_8P2_1MiB_encode_{hname}_32KiB_fused"] = {
             "GiBps_user": round(k * C * S / (fus / 1e3) / GIB, 1), "alg_GBps": round(alg / fus / 1e6, 1),
             "roofline_frac": round(alg / fus / 1e6 / HBM_PEAK_GBS, 4), "ms": round(fus, 4),
             "encode_only_ms": round(enc, 4), "checksum_overhead": round(fus / enc - 1, 4),
-            "kernel": ecg.last_kernel()}
+            "kernel": kernels[htype]}
     # rebuild of parity shard p1 over the same 512 fetched stripes (migrate_update_parity,
     # include/ecg_daos.h): one output row + its crc32 chunks, (k + 1) cells of traffic per stripe
     import ctypes
