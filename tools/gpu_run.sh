@@ -220,6 +220,9 @@ PY
 	fusedlibs)
 		step fused_libs 900 python tools/fused_libs.py daos_amd/lib/libecg.so ${FUSED_LIBS:-} || exit $?
 		;;
+	crclibs)
+		step crc_libs 900 python tools/crc_libs.py daos_amd/lib/libecg.so ${CRC_LIBS:-} || exit $?
+		;;
 	fusedpmc)
 		rm -rf gpurun_out/pmc_ffetch gpurun_out/pmc_fwrite
 		step rocprof_ffetch 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv \
