@@ -507,8 +507,8 @@ def time_interleaved(ctx, fns, iters, warm=3):
     each per round): the box's clocks drift over a long run, so timing one
     configuration's block of launches after another's biases a ratio."""
     a, b = ctx.event(), ctx.event()
-    for fn in fns:
-        for _ in range(warm):
+    for _ in range(warm):           # warm-up rounds interleaved like the timed ones
+        for fn in fns:
             fn()
     ctx.sync()
     ms = [[] for _ in fns]
@@ -605,10 +605,14 @@ def detail_rows(ctx, ceil, iters=11):
             ctx.encode_csum(k, p, C, S, data.ptr, k * C, par.ptr, pitch, C, htype, 32768, 1, out.ptr)
             kernels[htype] = ecg.last_kernel()
         return fn
-    # the plain encode and both fused launches interleaved (their ratio is the row's point)
+    # the plain encode and both fused launches interleaved (their ratio is the row's point).
+    # 15 warm-up rounds: when the VALU/LDS-dense fused kernels start after the memory-bound
+    # encode the core clock dips and recovers over ~10 launches (the fused launches ran
+    # 0.94 -> 1.26 -> 0.95 ms while the interleaved encode stayed at 0.82-0.85 ms,
+    # profiles/r02/fused_transient/kernel_trace.csv); the rows report the steady state
     enc, *fus_ms = time_interleaved(
         ctx, [lambda: ctx.encode(k, p, C, S, data.ptr, k * C, par.ptr, pitch, C)] +
-        [fused(htype) for _, htype in hashes], iters)
+        [fused(htype) for _, htype in hashes], iters, warm=15)
     for (hname, htype), fus in zip(hashes, fus_ms):
         alg = (k + p) * C * S
         rows[f"EC_8P2_1MiB_encode_{hname}_32KiB_fused"] = {
@@ -627,7 +631,7 @@ def detail_rows(ctx, ceil, iters=11):
                                                      1, ecg.HASH_CRC32, 32768, par.ptr, out.ptr, pieces, S,
                                                      ctypes.byref(npc), None), "migrate_update_parity")
 
-    ms = time_kernel(ctx, shard, iters)
+    ms = time_kernel(ctx, shard, iters, warm=10)
     alg = (k + 1) * C * S
     rows["EC_8P2_1MiB_rebuild_parity_shard_crc32"] = {
         "GiBps_user": round(k * C * S / (ms / 1e3) / GIB, 1), "alg_GBps": round(alg / ms / 1e6, 1),

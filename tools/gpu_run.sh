@@ -230,6 +230,20 @@ PY
 		step rocprof_fwrite 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv \
 			-d gpurun_out/pmc_fwrite -o run -- python3 tools/crc_pmc.py fused || exit $?
 		;;
+	fusedsq)
+		rm -rf gpurun_out/pmc_fsq1 gpurun_out/pmc_fsq2 gpurun_out/pmc_fgrbm
+		step rocprof_fsq1 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES \
+			SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_ANY \
+			--output-format csv -d gpurun_out/pmc_fsq1 -o run -- python3 tools/fused_pmc.py || exit $?
+		step rocprof_fsq2 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_LDS \
+			SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE \
+			--output-format csv -d gpurun_out/pmc_fsq2 -o run -- python3 tools/fused_pmc.py || exit $?
+		step rocprof_fgrbm 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE GRBM_COUNT \
+			--output-format csv -d gpurun_out/pmc_fgrbm -o run -- python3 tools/fused_pmc.py || exit $?
+		python tools/pmc_summary.py --skip 6 gpurun_out/pmc_fsq1/run_counter_collection.csv \
+			gpurun_out/pmc_fsq2/run_counter_collection.csv gpurun_out/pmc_fgrbm/run_counter_collection.csv \
+			> gpurun_out/fused_sq_summary.jsonl || exit $?
+		;;
 	dist4)
 		step dist4 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
 			--master-port 29537 bench.py --gpus 4 --steps 20 --warmup 3 || exit $?

@@ -1,18 +1,24 @@
 """Mean per-dispatch rocprofv3 counter values by kernel, from one or more
 run_counter_collection.csv files (tools/gpu_run.sh pmc passes), with the
-kernel-trace duration.  Prints one JSON object per kernel.  Analysis helper."""
+kernel-trace duration.  Prints one JSON object per kernel.  `--skip N` drops
+each kernel's first N dispatches (warm-up / clock transient).  Analysis helper."""
 import collections
 import csv
 import json
 import sys
 
 
-def main(paths):
+def main(paths, skip=0):
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for path in paths:
-        for r in csv.DictReader(open(path)):
+        rows = list(csv.DictReader(open(path)))
+        order = collections.defaultdict(list)       # kernel -> its dispatch ids in order
+        for r in rows:
+            if r["Dispatch_Id"] not in order[r["Kernel_Name"]]:
+                order[r["Kernel_Name"]].append(r["Dispatch_Id"])
+        for r in rows:
             name = r["Kernel_Name"]
-            if name.startswith("__amd"):
+            if name.startswith("__amd") or order[name].index(r["Dispatch_Id"]) < skip:
                 continue
             agg[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
             dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
@@ -25,4 +31,8 @@ def main(paths):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:])
+    args = sys.argv[1:]
+    nskip = 0
+    if args and args[0] == "--skip":
+        nskip, args = int(args[1]), args[2:]
+    main(args, nskip)
