@@ -826,10 +826,15 @@ def main():
         rank_devs = [{"shard": i, "device": d, "pci": ecg.pci_bus_id(d)} for i, d in enumerate(devices)]
         S = wl.S
     else:
-        if local >= ndev and not args.allow_shared_device:
-            raise SystemExit(f"bench.py: local rank {local} but {ndev} visible devices "
-                             "(--allow-shared-device to rehearse several ranks on one GPU)")
+        # LOCAL_RANK picks the device among those visible; a launcher that
+        # gives each rank its own HIP_VISIBLE_DEVICES leaves one (index 0).
+        # Sharing is judged on physical devices: the ranks' PCI bus ids,
+        # checked collectively so every rank stops together.
         dev = local % ndev
+        pcis = gather(world, ecg.pci_bus_id(dev))
+        if len(set(pcis)) < world and not args.allow_shared_device:
+            raise SystemExit(f"bench.py: {world} ranks on {len(set(pcis))} distinct devices {sorted(set(pcis))} "
+                             "(--allow-shared-device to rehearse several ranks on one GPU)")
         torch.cuda.set_device(dev)
         ctx = ecg.Context(dev)
         m = None

@@ -1,6 +1,6 @@
 """Standalone CRC kernels (crc16/32/64, 4 / 32 / 1024 KiB chunks over 1 GiB of
 1 MiB cells) timed with several builds of libecg.so, one subprocess per
-library, interleaved twice.  usage: python tools/crc_libs.py lib1.so lib2.so ...
+library, interleaved three times; median of 15 launches after 5 warm-up.  usage: python tools/crc_libs.py lib1.so lib2.so ...
 -> gpurun_out/crc_libs.json.  Bench infrastructure."""
 import json
 import os
@@ -27,12 +27,14 @@ res = {}
 for htype, name in ((1, "crc16"), (2, "crc32"), (3, "crc64")):
     for cs in (4096, 32768, 1 << 20):
         fn = lambda: ctx.csum_extents(htype, cs, 1, 0, C, buf.ptr, C, n, out.ptr)
-        fn(); ctx.sync()
+        for _ in range(5):
+            fn()
+        ctx.sync()
         ts = []
-        for _ in range(7):
+        for _ in range(15):
             ctx.record(a); fn(); ctx.record(b); ts.append(ctx.elapsed_ms(a, b))
         ts.sort()
-        res[f"{name}_cs{cs >> 10}K"] = round(C * n / ts[3] / 1e9, 3)
+        res[f"{name}_cs{cs >> 10}K"] = round(C * n / ts[7] / 1e9, 3)
 print(json.dumps(res))
 ''' % ROOT
 
@@ -40,7 +42,7 @@ print(json.dumps(res))
 def main():
     libs = sys.argv[1:]
     res = {}
-    for rnd in range(2):
+    for rnd in range(3):
         for lib in libs:
             r = subprocess.run([sys.executable, "-c", CHILD, os.path.abspath(lib)], capture_output=True, text=True,
                                timeout=300)
