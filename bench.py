@@ -61,7 +61,7 @@ WORKLOADS = {
     # configs[4]: stripes in pinned host memory, PCIe-inclusive (never the headline)
     "rebuild_stream_8p2": (8, 2, 1 << 20, 64, ("enc_host", "dec_host"), False),
 }
-HOST_CHUNK = 16         # stripes per staging chunk (profiles/r01/pcie.json chunk sweep)
+HOST_CHUNK = 4          # stripes per staging chunk (profiles/r02/host_chunk_sweep/: 16 -> 4 = 0.92 -> 0.945 of H2D)
 MARKER = 0x5A           # erased cells are overwritten with this before any decode runs
 
 
@@ -81,6 +81,8 @@ def parse(argv=None):
                     help="permit more ranks/shards than visible devices (rehearsal on a small box)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--no-detail", action="store_true", help="skip the extra per-config rows")
+    ap.add_argument("--host-chunk", type=int, default=0,
+                    help=f"stripes per staging chunk of the host-resident workloads (default {HOST_CHUNK})")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-only", action="store_true", help="just the timed loop (for rocprofv3)")
     ap.add_argument("--rehearse", action="store_true",
@@ -330,10 +332,11 @@ class HostWorkload:
     ecg_encode_host / ecg_recover_host (H2D || kernel || D2H on 3 streams).
     PCIe-bound by construction."""
 
-    def __init__(self, ctx, k, p, C, S, ops=("enc_host", "dec_host"), err=(0, 1), config_id=9):
+    def __init__(self, ctx, k, p, C, S, ops=("enc_host", "dec_host"), err=(0, 1), config_id=9, chunk=0):
         from tools.datagen import stripe_bytes
 
         self.ctx, self.k, self.p, self.C, self.S, self.err = ctx, k, p, C, S, list(err)
+        self.chunk = chunk or HOST_CHUNK
         self.ops = tuple(ops)
         self.data = ctx.host_alloc(S * k * C)
         self.parity = ctx.host_alloc(S * p * C)
@@ -343,7 +346,7 @@ class HostWorkload:
         for off in range(0, a.size, blk.size):
             n = min(blk.size, a.size - off)
             a[off:off + n] = blk[:n]
-        ctx.encode_host(k, p, C, S, a, self.parity.array, chunk=HOST_CHUNK)
+        ctx.encode_host(k, p, C, S, a, self.parity.array, chunk=self.chunk)
         img = self.stripes.array.reshape(S, k + p, C)
         img[:, :k] = a.reshape(S, k, C)
         img[:, k:] = self.parity.array.reshape(p, S, C).transpose(1, 0, 2)
@@ -354,9 +357,9 @@ class HostWorkload:
     def step(self, timed=False):
         c, k, p, C, S = self.ctx, self.k, self.p, self.C, self.S
         if "enc_host" in self.ops:
-            c.encode_host(k, p, C, S, self.data.array, self.parity.array, chunk=HOST_CHUNK)
+            c.encode_host(k, p, C, S, self.data.array, self.parity.array, chunk=self.chunk)
         if "dec_host" in self.ops:
-            c.recover_host(k, p, C, S, self.stripes.array, self.err, chunk=HOST_CHUNK)
+            c.recover_host(k, p, C, S, self.stripes.array, self.err, chunk=self.chunk)
 
     def kernel_ms(self):
         return {}
@@ -388,7 +391,7 @@ class HostWorkload:
         out = {"decode_regenerated_erased_cells": bool(np.array_equal(img[:, :k], data))}
         img[:, k:] = self.parity.array.reshape(p, S, C).transpose(1, 0, 2)
         img[:, self.err] = MARKER
-        self.ctx.recover_host(k, p, C, S, self.stripes.array, self.err, chunk=HOST_CHUNK)
+        self.ctx.recover_host(k, p, C, S, self.stripes.array, self.err, chunk=self.chunk)
         out["encode_parity_decodes_to_data"] = bool(np.array_equal(img[:, :k], data))
         return out
 
@@ -752,7 +755,7 @@ def host_report(args, ctx, wl, world, rank, value, elapsed, ranks):
         "data": "synthetic: xoshiro256** stripes in pinned host memory",
         "config": {"workload": f"EC_{k}P{p} {C >> 10} KiB cells: per step one encode batch of {S} stripes "
                                f"+ one {{d0,d1}} recovery batch of {S} stripes per GPU, host<->device copies "
-                               f"included ({HOST_CHUNK}-stripe staging chunks)",
+                               f"included ({wl.chunk}-stripe staging chunks)",
                    "name": args.workload, "k": k, "p": p, "cell_bytes": C, "stripes_per_gpu": S,
                    "erasures": wl.err, "parallelism": f"stripe-sharded x{world}, no collective"},
         "roofline": None,
@@ -840,7 +843,8 @@ def main():
         m = None
         if strong:                      # configs[3]: a fixed stripe total split across ranks
             S = S // world + (1 if rank < S % world else 0)
-        wl = (HostWorkload if host else Workload)(ctx, k, p, C, S, ops=ops)
+        wl = (HostWorkload(ctx, k, p, C, S, ops=ops, chunk=args.host_chunk) if host
+              else Workload(ctx, k, p, C, S, ops=ops))
         rank_devs = None
 
     for _ in range(args.warmup):

@@ -718,6 +718,20 @@ static int enc_h2d_parts(void)
 	return g_enc_h2d_parts;
 }
 
+/* Stripes per staging chunk when the caller passes 0: ~32 MiB of input cells
+ * per chunk.  Each call ends by draining its last chunk (kernel + D2H) while
+ * the H2D link idles, so small chunks keep alternating encode / recovery
+ * calls near the link rate: EC_8P2 1 MiB rebuild stream, 64-stripe calls,
+ * 16 / 8 / 4 stripes per chunk = 0.91-0.93 / 0.93-0.94 / 0.945 of the raw
+ * H2D rate (profiles/r02/host_chunk_sweep/); long single calls are flat from
+ * 8 to 32 stripes (profiles/r01/pcie.json). */
+static uint32_t host_chunk_default(int k, uint64_t C)
+{
+	const uint64_t n = (32ull << 20) / ((uint64_t)k * C);
+
+	return n < 1 ? 1 : n > 4096 ? 4096 : (uint32_t)n;
+}
+
 /* parity row r of stripe s at parity + r*prow + s*C (prow = S*C for the
  * [p][S][C] layout; a shard of a larger batch passes the batch's row pitch) */
 int ecg_encode_host_rows(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S, const void *data,
@@ -740,7 +754,7 @@ int ecg_encode_host_rows(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S, c
 	if (S == 0 || C == 0)
 		return 0;
 	if (chunk == 0)
-		chunk = 64;
+		chunk = host_chunk_default(k, C);
 	if (chunk > S)
 		chunk = S;
 	pthread_mutex_lock(&ctx->lock);
@@ -825,7 +839,7 @@ int ecg_recover_host(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 	if (rc)
 		return rc;
 	if (chunk == 0)
-		chunk = 64;
+		chunk = host_chunk_default(k, C);
 	if (chunk > S)
 		chunk = S;
 	pthread_mutex_lock(&ctx->lock);

@@ -144,7 +144,8 @@ int ecg_matmul_host(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned cha
 /* Encode host-resident stripes (data [S][k][C], parity [p][S][C] in host
  * memory; pinned memory from ecg_host_alloc is fastest) by streaming chunks
  * of `chunk_stripes` through device staging on 3 rotating streams
- * (H2D / kernel / D2H overlap).  Synchronous. */
+ * (H2D / kernel / D2H overlap); 0 = about 32 MiB of input cells per chunk.
+ * Synchronous. */
 int ecg_encode_host(ecg_ctx_t *ctx, int k, int p, uint64_t cell_bytes, uint32_t nstripes,
 		    const void *data, void *parity, uint32_t chunk_stripes);
 /* Same for recovery over host [S][k+p][C] stripes: only survivors travel
