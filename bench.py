@@ -84,6 +84,8 @@ def parse(argv=None):
     ap.add_argument("--host-chunk", type=int, default=0,
                     help=f"stripes per staging chunk of the host-resident workloads (default {HOST_CHUNK})")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--wg-per-cu", type=int, default=0,
+                    help="product-kernel blocks per CU (ecg_set_wg_per_cu): 0 per-shape default, 255 uncapped")
     ap.add_argument("--profile-only", action="store_true", help="just the timed loop (for rocprofv3)")
     ap.add_argument("--rehearse", action="store_true",
                     help="CPU-only rehearsal of launcher, barrier and aggregation: no GPU work, the "
@@ -840,6 +842,7 @@ def main():
                              "(--allow-shared-device to rehearse several ranks on one GPU)")
         torch.cuda.set_device(dev)
         ctx = ecg.Context(dev)
+        ctx.set_wg_per_cu(args.wg_per_cu)
         m = None
         if strong:                      # configs[3]: a fixed stripe total split across ranks
             S = S // world + (1 if rank < S % world else 0)

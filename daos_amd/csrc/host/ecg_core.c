@@ -201,6 +201,14 @@ int ecg_set_launch_order(ecg_ctx_t *ctx, uint32_t order)
 	return 0;
 }
 
+int ecg_set_wg_per_cu(ecg_ctx_t *ctx, uint32_t wg_per_cu)
+{
+	if (ctx == NULL || (wg_per_cu > 16 && wg_per_cu != ECG_WG_UNCAPPED))
+		return ecg_fail(-ECG_DER_INVAL, "set_wg_per_cu: bad argument");
+	ctx->cfg.wg_per_cu = wg_per_cu;
+	return 0;
+}
+
 /* ------------------------------------------------------------------------ */
 /* batched GF matrix x cells                                                 */
 /* ------------------------------------------------------------------------ */

@@ -80,6 +80,7 @@ _SIGS = [
     ("ecg_dev_copy_kernel", C.c_int, [vp, vp, vp, C.c_size_t, C.c_int, vp]),
     ("ecg_set_launch", C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_uint32]),
     ("ecg_set_launch_order", C.c_int, [vp, C.c_uint32]),
+    ("ecg_set_wg_per_cu", C.c_int, [vp, C.c_uint32]),
     # multi-device sharder (ecg_multi.h)
     ("ecg_multi_create", C.c_int, [C.POINTER(C.c_int), C.c_int, C.POINTER(vp)]),
     ("ecg_multi_destroy", None, [vp]),
@@ -415,6 +416,10 @@ class Context:
 
     def set_order(self, order: int = 0):
         _chk(lib().ecg_set_launch_order(self.h, order), "set_launch_order")
+
+    def set_wg_per_cu(self, wg_per_cu: int = 0):
+        """Product-kernel blocks per CU: 0 per-shape default, 1..16 cap, 255 none."""
+        _chk(lib().ecg_set_wg_per_cu(self.h, wg_per_cu), "set_wg_per_cu")
 
     def copy_kernel(self, dst: int, src: int, nbytes: int, mode: int = 0, stream=None):
         """mode 0 copy, 1 read-only, 2 write-only (HBM rate probes)."""

@@ -230,6 +230,10 @@ int ecg_set_launch(ecg_ctx_t *ctx, uint32_t grid_x, uint32_t grid_y, uint32_t va
  * XCD streaming its own eighth of the column-fastest items; 3 = as 2,
  * stripe-fastest.  Tuning only; results never depend on it. */
 int ecg_set_launch_order(ecg_ctx_t *ctx, uint32_t order);
+/* Blocks per CU of the product kernel's 2D grid: 0 = the per-shape default
+ * (currently no cap for any shape), 2..16 = that cap, 255 = no cap.  Enforced
+ * with unused dynamic LDS.  Tuning only; results never depend on it. */
+int ecg_set_wg_per_cu(ecg_ctx_t *ctx, uint32_t wg_per_cu);
 
 /* Pointer-table product: ISA-L's per-stripe pointer arrays
  * (ec_encode_data(len, k, rows, tbls, data[], coding[])) batched over
