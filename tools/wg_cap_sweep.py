@@ -3,8 +3,9 @@ classes, device-resident: encode in the client layout (data [S][k][C] ->
 parity [p][S][C] at the padded pitch) and 2-erasure (1 for p = 1) decode in
 the recovery layout [S][k+p][C]; caps interleaved launch by launch (the box's
 clock drifts over a run), median of 9 after 5 warm-up launches, 3 rounds.
-Cells hold seeded random bytes (--const: 0x5A everywhere, as the first sweep).
-usage: python tools/wg_cap_sweep.py [caps...] [--const] -> gpurun_out/wg_cap_sweep.json
+Cells hold seeded random bytes (--const: 0x5A everywhere, as the first sweep);
+--b2b times each cap's launches back to back instead (as bench.py's rows).
+usage: python tools/wg_cap_sweep.py [caps...] [--const] [--b2b] -> gpurun_out/wg_cap_sweep.json
 (algorithmic GB/s).  Bench infrastructure."""
 import json
 import os
@@ -52,13 +53,24 @@ def main():
                         fn()
                 ctx.sync()
                 ts = {cap: [] for cap in caps}
-                for _ in range(9):
+                if "--b2b" in sys.argv[1:]:       # each cap's launches back to back, as bench.py
                     for cap in caps:
                         ctx.set_wg_per_cu(cap)
-                        ctx.record(a)
-                        fn()
-                        ctx.record(b)
-                        ts[cap].append(ctx.elapsed_ms(a, b))
+                        for _ in range(3):
+                            fn()
+                        for _ in range(9):
+                            ctx.record(a)
+                            fn()
+                            ctx.record(b)
+                            ts[cap].append(ctx.elapsed_ms(a, b))
+                else:
+                    for _ in range(9):
+                        for cap in caps:
+                            ctx.set_wg_per_cu(cap)
+                            ctx.record(a)
+                            fn()
+                            ctx.record(b)
+                            ts[cap].append(ctx.elapsed_ms(a, b))
                 row = res.setdefault(tag, {})
                 for cap, v in ts.items():
                     v.sort()
