@@ -1,0 +1,49 @@
+"""Minimal program for rocprofv3 FETCH_SIZE / WRITE_SIZE passes of one EC
+product shape (the EC_8P2 decode and EC_16P2 rows), 5
+launches after 2 warm-up launches, seeded random cells:
+  dec_8p2     EC_8P2 1 MiB x 512, {d0,d1} regenerated in [S][k+p][C]
+  enc_16p2    EC_16P2 128 KiB x 1024, data [S][k][C] -> parity [p][S][C] (padded pitch)
+  dec_16p2    EC_16P2 128 KiB x 1024, {d0,d1} regenerated in [S][k+p][C]
+Run as  rocprofv3 --pmc FETCH_SIZE -- python3 tools/ec_pmc.py dec_8p2  and summarise
+with tools/pmc_traffic.py (algorithmic bytes printed here).  Bench infrastructure."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from daos_amd import ecg  # noqa: E402
+from tools.datagen import stripe_bytes  # noqa: E402
+
+SHAPES = {"dec_8p2": (8, 2, 1 << 20, 512, "dec"), "enc_16p2": (16, 2, 128 << 10, 1024, "enc"),
+          "dec_16p2": (16, 2, 128 << 10, 1024, "dec")}
+
+
+def main():
+    k, p, C, S, op = SHAPES[sys.argv[1]]
+    ctx = ecg.Context(0)
+    st = (k + p) * C
+    buf = ctx.alloc(S * st)
+    blk = stripe_bytes(256 << 20, 5)
+    for off in range(0, buf.nbytes, blk.size):
+        buf.upload(blk[: min(blk.size, buf.nbytes - off)], offset=off)
+    if op == "enc":
+        pitch = S * C + 4096
+        par = ctx.alloc(p * pitch)
+        fn = lambda: ctx.encode(k, p, C, S, buf.ptr, k * C, par.ptr, pitch, C)  # noqa: E731
+        alg = (k + p) * C * S
+    else:
+        par = None
+        fn = lambda: ctx.recover(k, p, C, S, buf.ptr, st, [0, 1])  # noqa: E731
+        alg = (k + 2) * C * S
+    for _ in range(7):
+        fn()
+    ctx.sync()
+    print(f"ec_pmc {sys.argv[1]} kernel {ecg.last_kernel()} alg_bytes_per_launch {alg}", flush=True)
+    buf.free()
+    if par is not None:
+        par.free()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -244,6 +244,21 @@ PY
 			gpurun_out/pmc_fsq2/run_counter_collection.csv gpurun_out/pmc_fgrbm/run_counter_collection.csv \
 			> gpurun_out/fused_sq_summary.jsonl || exit $?
 		;;
+	ecpmc)
+		for w in dec_8p2 enc_16p2 dec_16p2; do
+			rm -rf gpurun_out/pmc_${w}_f gpurun_out/pmc_${w}_w
+			step rocprof_${w}_f 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv \
+				-d gpurun_out/pmc_${w}_f -o run -- python3 tools/ec_pmc.py $w || exit $?
+			step rocprof_${w}_w 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv \
+				-d gpurun_out/pmc_${w}_w -o run -- python3 tools/ec_pmc.py $w || exit $?
+		done
+		python tools/pmc_traffic.py gpurun_out/pmc_dec_8p2_f gpurun_out/pmc_dec_8p2_w "ecg_mm_kernel<8, 2" \
+			5368709120 gpurun_out/pmc_traffic_dec_8p2.json || exit $?
+		python tools/pmc_traffic.py gpurun_out/pmc_enc_16p2_f gpurun_out/pmc_enc_16p2_w "ecg_mm_kernel<16, 2" \
+			2415919104 gpurun_out/pmc_traffic_enc_16p2.json || exit $?
+		python tools/pmc_traffic.py gpurun_out/pmc_dec_16p2_f gpurun_out/pmc_dec_16p2_w "ecg_mm_kernel<16, 2" \
+			2415919104 gpurun_out/pmc_traffic_dec_16p2.json || exit $?
+		;;
 	dist4)
 		step dist4 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
 			--master-port 29537 bench.py --gpus 4 --steps 20 --warmup 3 || exit $?
