@@ -327,6 +327,23 @@ def test_host_pipeline(ctx, oracle):
     assert np.array_equal(broken, stripes)
 
 
+@pytest.mark.parametrize("k,p,C_,S", [(8, 2, 1 << 20, 11), (4, 2, 4096 + 16, 9)])
+def test_host_pipeline_default_chunk(ctx, oracle, k, p, C_, S):
+    """chunk_stripes = 0: the library sizes chunks to ~32 MiB of input cells
+    (EC_8P2 1 MiB: 4 stripes, so 11 stripes take 3 chunks with a ragged last
+    one; tiny cells: one chunk for the whole batch)."""
+    data = rand((S, k, C_), 91 + k)
+    par = np.zeros((p, S, C_), dtype=np.uint8)
+    ctx.encode_host(k, p, C_, S, data, par)
+    want = oracle_parity(oracle, k, p, data)
+    assert np.array_equal(par, want)
+    stripes = np.concatenate([data, want.transpose(1, 0, 2)], axis=1).copy()
+    broken = stripes.copy()
+    broken[:, [0, k]] = 0x5A
+    ctx.recover_host(k, p, C_, S, broken, [0, k])
+    assert np.array_equal(broken, stripes)
+
+
 @pytest.mark.parametrize("errs", [[0, 1], [8, 9], [1, 2], [9, 8], [3], [7, 8]])
 def test_recover_host_erasure_runs(ctx, oracle, errs):
     """Host-resident recovery moves survivors and regenerated cells in runs
