@@ -55,6 +55,9 @@ for k, p, S in ((8, 2, 512), (4, 2, 1024)):
         # the wave-per-chunk kernel (csum_variant 128) and the workgroup kernel (256)
         cfgs.append(("%%s_%%s_wave_ms" %% (tag, hname), cfg(k, p, S, htype, 0, 128)))
         cfgs.append(("%%s_%%s_wg_ms" %% (tag, hname), cfg(k, p, S, htype, 0, 256)))
+        # the workgroup kernel with the 5-bit tables (32) / the byte tables (16)
+        cfgs.append(("%%s_%%s_wg5_ms" %% (tag, hname), cfg(k, p, S, htype, 0, 256 | 32)))
+        cfgs.append(("%%s_%%s_wgb_ms" %% (tag, hname), cfg(k, p, S, htype, 0, 256 | 16)))
     ts = {n: [] for n, _ in cfgs}
     for n, fn in cfgs:
         for _ in range(3):
