@@ -201,6 +201,25 @@ int ecg_set_launch_order(ecg_ctx_t *ctx, uint32_t order)
 	return 0;
 }
 
+int ecg_get_stats(ecg_ctx_t *ctx, ecg_stats_t *out, int reset)
+{
+	uint64_t *f, *o;
+	size_t i, n = sizeof(ecg_stats_t) / sizeof(uint64_t);
+
+	if (ctx == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "get_stats: NULL context");
+	f = (uint64_t *)&ctx->stats;
+	o = (uint64_t *)out;
+	for (i = 0; i < n; i++) {
+		const uint64_t v = reset ? __atomic_exchange_n(&f[i], 0, __ATOMIC_RELAXED)
+					 : __atomic_load_n(&f[i], __ATOMIC_RELAXED);
+
+		if (o)
+			o[i] = v;
+	}
+	return 0;
+}
+
 int ecg_set_wg_per_cu(ecg_ctx_t *ctx, uint32_t wg_per_cu)
 {
 	if (ctx == NULL || (wg_per_cu > 16 && wg_per_cu != ECG_WG_UNCAPPED))
@@ -222,6 +241,7 @@ static int launch(ecg_ctx_t *ctx, const ecg_mm_params_t *prm, hipStream_t st)
 	ecg_trace_pop();
 	if (e != 0)
 		return ecg_hip_fail((hipError_t)e, "kernel launch");
+	ECG_STAT_ADD(ctx, launches, 1);
 	ecg_set_last_kernel(ecg_k_kernel_name(kid));
 	return 0;
 }
@@ -380,6 +400,10 @@ int ecg_encode(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 	rc = ecg_matmul(ctx, k, p, &en[k * k], C, S, data, soff, data_stripe_stride,
 			parity, doff, parity_stripe_stride, 0, stream);
 	ecg_trace_pop();
+	if (rc == 0) {
+		ECG_STAT_ADD(ctx, encode_stripes, S);
+		ECG_STAT_ADD(ctx, encode_bytes, (uint64_t)k * C * S);
+	}
 	return rc;
 }
 
@@ -438,8 +462,13 @@ static int recover_with(ecg_ctx_t *ctx, const struct ecg_rcache_ent *ent, uint64
 		soff[i] = (int64_t)ent->dec_idx[i] * (int64_t)C;
 	for (i = 0; i < ent->nerrs; i++)
 		doff[i] = (int64_t)ent->out_idx[i] * (int64_t)C;
-	return ecg_matmul(ctx, ent->k, ent->nerrs, ent->rows, C, S, stripes, soff,
-			  stripe_stride, stripes, doff, stripe_stride, 0, stream);
+	i = ecg_matmul(ctx, ent->k, ent->nerrs, ent->rows, C, S, stripes, soff,
+		       stripe_stride, stripes, doff, stripe_stride, 0, stream);
+	if (i == 0) {
+		ECG_STAT_ADD(ctx, recover_stripes, S);
+		ECG_STAT_ADD(ctx, recover_bytes, (uint64_t)ent->nerrs * C * S);
+	}
+	return i;
 }
 
 int ecg_recover(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
@@ -549,6 +578,8 @@ int ecg_matmul_csum(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, 
 		e = ecg_k_launch_matmul_csum(prm, &q, &ctx->cfg, (void *)st, &kid);
 		free(prm);
 		if (e == 0) {
+			ECG_STAT_ADD(ctx, launches, 1);
+			ECG_STAT_ADD(ctx, csum_chunks, (uint64_t)rows * S * q.nch);
 			ecg_set_last_kernel(ecg_k_kernel_name(kid));
 			return 0;
 		}
@@ -594,8 +625,13 @@ int ecg_encode_csum(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S, const 
 		doff[i] = (int64_t)i * parity_cell_stride;
 		slot[i] = (uint32_t)i;
 	}
-	return ecg_matmul_csum(ctx, k, p, &en[k * k], C, S, data, soff, data_stripe_stride, parity, doff,
-			   parity_stripe_stride, type, chunksize, rec_size, csums, slot, stream);
+	rc = ecg_matmul_csum(ctx, k, p, &en[k * k], C, S, data, soff, data_stripe_stride, parity, doff,
+			     parity_stripe_stride, type, chunksize, rec_size, csums, slot, stream);
+	if (rc == 0) {
+		ECG_STAT_ADD(ctx, encode_stripes, S);
+		ECG_STAT_ADD(ctx, encode_bytes, (uint64_t)k * C * S);
+	}
+	return rc;
 }
 
 int ecg_recover_csum(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S, void *stripes,
@@ -628,9 +664,14 @@ int ecg_recover_csum(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S, void 
 			if (err_list[j] == ent.out_idx[i])
 				slot[i] = (uint32_t)j;
 	}
-	return ecg_matmul_csum(ctx, ent.k, ent.nerrs, ent.rows, C, S, stripes, soff, stripe_stride,
-			   stripes, doff, stripe_stride, type, chunksize, rec_size, csums, slot,
-			   stream);
+	rc = ecg_matmul_csum(ctx, ent.k, ent.nerrs, ent.rows, C, S, stripes, soff, stripe_stride,
+			     stripes, doff, stripe_stride, type, chunksize, rec_size, csums, slot,
+			     stream);
+	if (rc == 0) {
+		ECG_STAT_ADD(ctx, recover_stripes, S);
+		ECG_STAT_ADD(ctx, recover_bytes, (uint64_t)ent.nerrs * C * S);
+	}
+	return rc;
 }
 
 int ecg_update(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
@@ -664,6 +705,10 @@ int ecg_update(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 		     new_cells, soff, upd_stripe_stride, parity, doff, parity_stripe_stride,
 		     ECG_F_ACCUMULATE, stream);
 	ecg_trace_pop();
+	if (rc == 0) {
+		ECG_STAT_ADD(ctx, update_cells, (uint64_t)nupd * S);
+		ECG_STAT_ADD(ctx, update_bytes, (uint64_t)nupd * C * S);
+	}
 	return rc;
 }
 
@@ -811,6 +856,10 @@ int ecg_encode_host_rows(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S, c
 	for (r = 0; r < ECG_NSLOT; r++)
 		if (ctx->stage.st[r])
 			(void)hipStreamSynchronize(ctx->stage.st[r]);
+	if (rc == 0) {
+		ECG_STAT_ADD(ctx, h2d_bytes, (uint64_t)k * C * S);
+		ECG_STAT_ADD(ctx, d2h_bytes, (uint64_t)p * C * S);
+	}
 	ecg_trace_pop();
 	pthread_mutex_unlock(&ctx->lock);
 	return rc;
@@ -901,6 +950,10 @@ int ecg_recover_host(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S,
 	for (i = 0; i < ECG_NSLOT; i++)
 		if (ctx->stage.st[i])
 			(void)hipStreamSynchronize(ctx->stage.st[i]);
+	if (rc == 0) {
+		ECG_STAT_ADD(ctx, h2d_bytes, (uint64_t)k * C * S);
+		ECG_STAT_ADD(ctx, d2h_bytes, (uint64_t)nerrs * C * S);
+	}
 	ecg_trace_pop();
 	pthread_mutex_unlock(&ctx->lock);
 	return rc;

@@ -666,6 +666,8 @@ int ecg_csum_extents(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_
 	e = ecg_k_launch_csum(&prm, (void *)ecg_pick_stream(ctx, stream), ctx->csum_blocks, &kid);
 	if (e != 0)
 		return ecg_hip_fail((hipError_t)e, "csum kernel launch");
+	ECG_STAT_ADD(ctx, launches, 1);
+	ECG_STAT_ADD(ctx, csum_chunks, (uint64_t)prm.n_ext * prm.nchunks);
 	ecg_set_last_kernel(ecg_k_kernel_name(kid));
 	return 0;
 }

@@ -80,7 +80,11 @@ struct ecg_ctx {
 	} kh_cache[ECG_NKH_CACHE];
 	unsigned kh_next;
 	struct ecg_scratch scratch;
+	ecg_stats_t stats;		/* telemetry (ecg_get_stats), updated with atomics */
 };
+
+/* telemetry: add n to one ecg_stats_t field of ctx (any thread) */
+#define ECG_STAT_ADD(ctx, field, n) __atomic_fetch_add(&(ctx)->stats.field, (uint64_t)(n), __ATOMIC_RELAXED)
 
 /* errors (thread-local detail string) */
 int ecg_fail(int rc, const char *fmt, ...) __attribute__((format(printf, 2, 3)));

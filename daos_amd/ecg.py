@@ -28,6 +28,9 @@ u8p = C.POINTER(C.c_ubyte)
 u32p = C.POINTER(C.c_uint32)
 i64p = C.POINTER(C.c_int64)
 vp = C.c_void_p
+# ecg_stats_t (include/ecg.h), in declaration order
+STATS_FIELDS = ("encode_stripes", "encode_bytes", "recover_stripes", "recover_bytes", "update_cells",
+                "update_bytes", "csum_chunks", "launches", "h2d_bytes", "d2h_bytes")
 
 # (name, restype, argtypes) for every function of include/*.h
 _SIGS = [
@@ -81,6 +84,7 @@ _SIGS = [
     ("ecg_set_launch", C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_uint32]),
     ("ecg_set_launch_order", C.c_int, [vp, C.c_uint32]),
     ("ecg_set_wg_per_cu", C.c_int, [vp, C.c_uint32]),
+    ("ecg_get_stats", C.c_int, [vp, vp, C.c_int]),
     # multi-device sharder (ecg_multi.h)
     ("ecg_multi_create", C.c_int, [C.POINTER(C.c_int), C.c_int, C.POINTER(vp)]),
     ("ecg_multi_destroy", None, [vp]),
@@ -416,6 +420,12 @@ class Context:
 
     def set_order(self, order: int = 0):
         _chk(lib().ecg_set_launch_order(self.h, order), "set_launch_order")
+
+    def stats(self, reset: bool = False) -> dict:
+        """Telemetry counters (include/ecg.h ecg_stats_t) as a dict."""
+        buf = (C.c_uint64 * len(STATS_FIELDS))()
+        _chk(lib().ecg_get_stats(self.h, C.cast(buf, vp), 1 if reset else 0), "get_stats")
+        return dict(zip(STATS_FIELDS, buf))
 
     def set_wg_per_cu(self, wg_per_cu: int = 0):
         """Product-kernel blocks per CU: 0 per-shape default, 1..16 cap, 255 none."""

@@ -222,6 +222,28 @@ int ecg_device_sync(ecg_ctx_t *ctx);
 int ecg_dev_copy_kernel(ecg_ctx_t *ctx, void *dst, const void *src, size_t bytes, int mode,
 			void *stream);
 
+/* ---- telemetry ------------------------------------------------------------
+ * The engine counts EC full-stripe and partial updates with GURT telemetry
+ * (opm_update_ec_full / _partial, ref:src/object/srv_ec.c:21-87); the codec's
+ * own counters, per context since creation or the last reset (relaxed
+ * atomics: safe from any thread, a snapshot is not one consistent instant):
+ *   encode_*   full-stripe products: stripes and user-data bytes (k*C*S)
+ *   recover_*  regenerations: stripes and regenerated bytes (nerrs*C*S)
+ *   update_*   partial-stripe parity updates: updated cells and their bytes
+ *   csum_chunks  checksums computed (standalone and fused)
+ *   launches   codec kernel launches (product, fused, checksum)
+ *   h2d_bytes / d2h_bytes  bytes the host-resident pipelines moved over PCIe */
+typedef struct ecg_stats {
+	uint64_t encode_stripes, encode_bytes;
+	uint64_t recover_stripes, recover_bytes;
+	uint64_t update_cells, update_bytes;
+	uint64_t csum_chunks;
+	uint64_t launches;
+	uint64_t h2d_bytes, d2h_bytes;
+} ecg_stats_t;
+/* Copy the counters to *out (may be NULL) and, if reset != 0, zero them. */
+int ecg_get_stats(ecg_ctx_t *ctx, ecg_stats_t *out, int reset);
+
 /* ---- launch tuning (benchmarks; 0 = default) ----------------------------
  * variant: 0 auto, 1 runtime-shaped kernel, 2 byte kernel. */
 int ecg_set_launch(ecg_ctx_t *ctx, uint32_t grid_x, uint32_t grid_y, uint32_t variant);

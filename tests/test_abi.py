@@ -193,3 +193,14 @@ def test_host_array_checks(ecglib):
         ecglib._host_array(np.zeros(100, dtype=np.uint16), 10, "x")
     with pytest.raises(ValueError):
         ecglib._host_array(np.zeros((10, 10), dtype=np.uint8).T, 10, "x")
+
+
+def test_stats_struct_matches_binding(ecglib):
+    """The Python view of ecg_stats_t lists the header's fields in order."""
+    import re
+
+    src = open(os.path.join(ROOT, "include", "ecg.h")).read()
+    body = re.search(r"typedef struct ecg_stats \{(.*?)\} ecg_stats_t;", src, re.S).group(1)
+    fields = [f.strip() for line in body.split(";") if "uint64_t" in line
+              for f in line.split("uint64_t", 1)[1].split(",")]
+    assert tuple(fields) == ecglib.STATS_FIELDS
