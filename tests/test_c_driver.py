@@ -1,7 +1,10 @@
 """Runs the native C driver (tests/c/test_ecg_c.c): the C-ABI exercised from
-C, plain and with ASan/UBSan on the host code, checked against the oracle.
-Without a GPU only its host-side checks run; under -m gpu the device paths
-(concurrent ISA-L calls from 12 pthreads, batched encode/recover, queue)."""
+C, plain, with ASan/UBSan and with ThreadSanitizer on the host code, checked
+against the oracle.  Without a GPU only its host-side checks run; under -m
+gpu the device paths (concurrent ISA-L calls from 12 pthreads, batched
+encode/recover, queue).  The TSan build runs host-side only: on the GPU boxes
+its runtime (gcc 11) aborts at start-up on the kernel's high-entropy mmap
+layout ("unexpected memory mapping"), with or without PIE."""
 import os
 import subprocess
 
@@ -14,11 +17,12 @@ BIN = os.path.join(ROOT, "build", "ctest")
 @pytest.fixture(scope="module")
 def cbins():
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "c")], check=True)
-    return os.path.join(BIN, "test_ecg_c"), os.path.join(BIN, "test_ecg_c_asan")
+    return os.path.join(BIN, "test_ecg_c"), os.path.join(BIN, "test_ecg_c_asan"), os.path.join(BIN, "test_ecg_c_tsan")
 
 
 def _run(path, gpu):
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:use_sigaltstack=0", UBSAN_OPTIONS="print_stacktrace=1")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:use_sigaltstack=0", UBSAN_OPTIONS="print_stacktrace=1",
+               TSAN_OPTIONS="halt_on_error=1")
     if not gpu:
         env["HIP_VISIBLE_DEVICES"] = ""       # host-only half
     r = subprocess.run([path], env=env, capture_output=True, text=True, timeout=600)
