@@ -47,6 +47,69 @@ static void fill(unsigned char *p, size_t n)
 		p[i] = rnd();
 }
 
+/* Host-side C-ABI from several threads at once, starting together so the
+ * library's one-time initialisations (GF tables, codec table lookups) race:
+ * the ThreadSanitizer build (tests/c/Makefile) checks this part without a
+ * GPU.  Each thread compares against the oracle. */
+struct host_job {
+	int id, bad;
+	pthread_barrier_t *go;
+};
+
+static void *host_thread(void *arg)
+{
+	struct host_job *j = arg;
+	static const int kp[][2] = {{2, 1}, {4, 2}, {8, 2}, {8, 3}, {16, 2}};
+	unsigned char a[(16 + 3) * 16], b[(16 + 3) * 16], inv[16 * 16], tmp[16 * 16];
+	unsigned char tb[16 * 3 * 32], rtb[16 * 3 * 32];
+
+	pthread_barrier_wait(j->go);
+	for (int x = j->id; x < 256; x += 7)
+		for (int y = 0; y < 256; y += 5)
+			j->bad += gf_mul(x, y) != ref_gf_mul(x, y);
+	for (size_t t = 0; t < sizeof(kp) / sizeof(kp[0]); t++) {
+		const int k = kp[t][0], p = kp[t][1];
+
+		gf_gen_cauchy1_matrix(a, k + p, k);
+		ref_gf_gen_cauchy1_matrix(b, k + p, k);
+		j->bad += memcmp(a, b, (size_t)(k + p) * k) != 0;
+		ec_init_tables(k, p, &a[k * k], tb);
+		ref_ec_init_tables(k, p, &b[k * k], rtb);
+		j->bad += memcmp(tb, rtb, (size_t)k * p * 32) != 0;
+		for (int e = 0; e < k + p; e++) {
+			uint32_t err[1] = {(uint32_t)((e + j->id) % (k + p))};
+			unsigned char rows[8 * 16];
+			uint32_t dec[16];
+			int reused = 0;
+
+			j->bad += ecg_recov_matrix(k, p, a, err, 1, rows, dec, &reused) != 0;
+		}
+		memcpy(tmp, a + (size_t)p * k, (size_t)k * k);	/* rows p..p+k-1: invertible */
+		j->bad += gf_invert_matrix(tmp, inv, k) != 0;
+	}
+	j->bad += ecg_obj_ec_codec_get((37u << 24) | 1) == NULL;
+	return NULL;
+}
+
+static void host_threads(void)
+{
+	enum { NT = 8 };
+	pthread_t th[NT];
+	struct host_job jobs[NT];
+	pthread_barrier_t go;
+
+	pthread_barrier_init(&go, NULL, NT);
+	for (int t = 0; t < NT; t++) {
+		jobs[t] = (struct host_job){.id = t, .bad = 0, .go = &go};
+		pthread_create(&th[t], NULL, host_thread, &jobs[t]);
+	}
+	for (int t = 0; t < NT; t++) {
+		pthread_join(th[t], NULL);
+		CHECK(jobs[t].bad == 0, "host thread %d: %d mismatches", t, jobs[t].bad);
+	}
+	pthread_barrier_destroy(&go);
+}
+
 static void host_checks(void)
 {
 	static const int kp[][2] = {{2, 1}, {2, 2}, {4, 1}, {4, 2}, {4, 3}, {8, 1}, {8, 2},
@@ -96,6 +159,7 @@ static void host_checks(void)
 		      "data loss");
 	}
 	CHECK(ecg_obj_ec_codec_init() == 0, "codec_init");
+	host_threads();
 	CHECK(ecg_obj_ec_codec_get((37u << 24) | 1) != NULL, "codec_get 8P2");
 	CHECK(ecg_obj_ec_codec_get((1u << 24) | 1) == NULL, "codec_get RP");
 	ecg_obj_ec_codec_fini();
