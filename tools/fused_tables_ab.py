@@ -1,0 +1,67 @@
+"""Fused product + crc32: the 5-bit tables (default) vs the byte tables
+(ecg_set_csum_variant bit 4) for k >= 8, in one process, the order of the
+configurations rotated every round so neither always follows the plain
+encode (tools/fused_libs.py keeps a fixed order and showed a ~1-2 % position
+bias); median of 21 rounds after 10 warm-up rounds, random cells, 1 MiB
+cells, 32 KiB chunks.  usage: python tools/fused_tables_ab.py [k,p,S ...]
+-> gpurun_out/fused_tables_ab.json.  Bench infrastructure."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from daos_amd import ecg  # noqa: E402
+from tools.datagen import stripe_bytes  # noqa: E402
+
+
+def main():
+    ctx = ecg.Context(0)
+    L = ecg.lib()
+    a, b = ctx.event(), ctx.event()
+    C = 1 << 20
+    buf = ctx.alloc(4 << 30)
+    blk = stripe_bytes(256 << 20, 13)
+    for off in range(0, buf.nbytes, blk.size):
+        buf.upload(blk, offset=off)
+    par = ctx.alloc(3 * (512 * C + 4096))
+    out = ctx.alloc(1 << 22)
+    res = {}
+    shapes = [tuple(int(x) for x in a.split(",")) for a in sys.argv[1:]] or [(8, 2, 512), (8, 3, 512)]
+    for k, p, S in shapes:
+        pitch = S * C + 4096
+
+        def fused(variant, k=k, p=p, S=S, pitch=pitch):
+            def fn():
+                L.ecg_set_csum_variant(ctx.h, variant)
+                ctx.encode_csum(k, p, C, S, buf.ptr, k * C, par.ptr, pitch, C, ecg.HASH_CRC32, 32768, 1, out.ptr)
+                L.ecg_set_csum_variant(ctx.h, 0)
+            return fn
+        cfgs = [("encode", lambda k=k, p=p, S=S, pitch=pitch: ctx.encode(k, p, C, S, buf.ptr, k * C, par.ptr,
+                                                                          pitch, C)),
+                ("crc32_5bit", fused(0)), ("crc32_bytes", fused(16))]
+        ts = {n: [] for n, _ in cfgs}
+        for rnd in range(31):
+            order = cfgs[rnd % len(cfgs):] + cfgs[:rnd % len(cfgs)]
+            for n, fn in order:
+                ctx.record(a)
+                fn()
+                ctx.record(b)
+                if rnd >= 10:
+                    ts[n].append(ctx.elapsed_ms(a, b))
+                else:
+                    ctx.elapsed_ms(a, b)
+        row = {}
+        for n, v in ts.items():
+            v.sort()
+            row[n + "_ms"] = round(v[len(v) // 2], 4)
+        row["overhead_5bit"] = round(row["crc32_5bit_ms"] / row["encode_ms"] - 1, 4)
+        row["overhead_bytes"] = round(row["crc32_bytes_ms"] / row["encode_ms"] - 1, 4)
+        res[f"{k}P{p}_x{S}"] = row
+        print(k, p, row, flush=True)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    json.dump(res, open(os.path.join(ROOT, "gpurun_out", "fused_tables_ab.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
