@@ -32,7 +32,9 @@ PMC pass of this command (`traffic_source` names the file), not measured in
 the run.
 cpu_baseline: the oracle's SIMD ISA-L-equivalent restatement (GFNI/AVX-512
 + OpenMP) on a bounded sample with a >= 1 GiB working set, rank 0 at N=1
-only, all of the box's CPU share and 1 core.
+only: every core of the process's affinity mask (3 repeats, median and
+range) and 1 core, load average before/after, and per-config rows for
+configs 1, 3 and the config-4 per-GPU shard beside the GPU detail rows.
 """
 from __future__ import annotations
 
@@ -79,7 +81,7 @@ def parse(argv=None):
                     help="procs: one process per GPU; lib: one process, the library's ecg_multi sharder")
     ap.add_argument("--allow-shared-device", action="store_true",
                     help="permit more ranks/shards than visible devices (rehearsal on a small box)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
+    ap.add_argument("--cpu-seconds", type=float, default=16.0, help="CPU baseline time budget (headline runs; the per-config rows take about as long again)")
     ap.add_argument("--no-detail", action="store_true", help="skip the extra per-config rows")
     ap.add_argument("--host-chunk", type=int, default=0,
                     help=f"stripes per staging chunk of the host-resident workloads (default {HOST_CHUNK})")
@@ -662,58 +664,112 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(k, p, C, budget_s, ops=("enc", "dec")):
-    """Oracle SIMD restatement (ISA-L-equivalent), OpenMP over stripes, on a
-    bounded sample of the same workload (same ops): a working set of >= 1 GiB
-    of user data (so the 256 MiB L3 of the box's EPYC cannot hold it),
-    repeated for ~60 % of the budget on the box's CPU share, then ~40 % on one
-    core."""
-    import numpy as np
-
-    from oracle import ref
-    from tools.datagen import stripe_bytes
-
+def cpu_share():
+    """What this process may run on: the affinity mask, the machine's count,
+    and the cgroup CPU quota if one is set (cpu.max, in CPUs)."""
     try:
-        cores = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))      # the GPU box's CPU share is 16
-    S = max(32, -(-(1 << 30) // (k * C)))
-    blk = stripe_bytes(min(256 << 20, S * k * C), 2)
-    data = np.resize(blk, S * k * C)
-    stripes = np.empty(S * (k + p) * C, dtype=np.uint8)
-    sv = stripes.reshape(S, k + p, C)
-    sv[:, :k] = data.reshape(S, k, C)
-    pout = np.empty(p * S * C, dtype=np.uint8)     # reused: no page faults in the timed loop
-    ref.encode_batch(k, p, C, S, data, nthreads=cores, simd=True, out=pout)
-    sv[:, k:] = pout.reshape(p, S, C).transpose(1, 0, 2)
-    rc, de, dec, el, gt, reused = ref.recov_codec(k, p, [0, 1])
-    assert rc == 0
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"affinity": aff, "cpu_count": os.cpu_count(), "cgroup_quota_cpus": quota}
 
-    def run(threads, secs):
-        user, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < secs:
-            if "enc" in ops:
-                ref.encode_batch(k, p, C, S, data, nthreads=threads, simd=True, out=pout)
-            if "dec" in ops:
-                ref.recov_batch(k, 2, gt, dec, el, C, (k + p) * C, S, stripes, nthreads=threads, simd=True)
-            user += len(ops) * k * C * S
-        dt = time.perf_counter() - t0
-        return round(user / dt / GIB, 3), round(dt, 1)
 
-    many, t_many = run(cores, 0.6 * budget_s)
-    one, t_one = run(1, 0.4 * budget_s)
-    variant = {0: "scalar", 1: "avx2-vpshufb", 2: "gfni-avx512"}[ref.simd_variant()]
-    ws = S * (k + (k + p) + p) * C
-    return {"value": many, "unit": "GiB/s", "cores": cores, "kind": "port",
-            "one_core": {"value": one, "unit": "GiB/s", "cores": 1, "seconds": t_one},
-            "cpu_model": cpu_model(), "working_set_bytes": ws,
-            "sample": f"EC_{k}P{p} {C >> 10} KiB cells, {S} stripes ({S * k * C / GIB:.2f} GiB of data, "
-                      f"{ws / GIB:.2f} GiB touched), {' + '.join(ops)}, repeated {t_many} s; "
-                      f"ISA-L-equivalent restatement ({variant}, OpenMP)",
-            "note": "r01 reported 129 GiB/s here (32-stripe, 192 MiB sample that partly fits the EPYC's "
-                    "256 MB L3) and 170 GiB/s in DESIGN (tools/cpu_baselines.py, encode-only rows); this "
-                    "line uses a >= 1 GiB working set, so memory bandwidth, not L3, feeds the cores"}
+class CpuCase:
+    """One CPU-baseline workload: the oracle's SIMD ISA-L-equivalent
+    restatement (GFNI/AVX-512 + OpenMP over stripes) on >= 1 GiB of user data
+    (so the 256 MB L3 of the box's EPYC cannot hold it), the same ops as the
+    GPU row it sits beside.  ops: "enc" (data [S][k][C] -> parity [p][S][C])
+    and/or "dec" ({d0,d1}, or {d0} at p = 1, in place in [S][k+p][C])."""
+
+    def __init__(self, k, p, C, ops, config_id=2):
+        import numpy as np
+
+        from oracle import ref
+        from tools.datagen import stripe_bytes
+
+        self.ref, self.k, self.p, self.C, self.ops = ref, k, p, C, tuple(ops)
+        self.S = S = max(32, -(-(1 << 30) // (k * C)))
+        blk = stripe_bytes(min(256 << 20, S * k * C), config_id)
+        self.data = np.resize(blk, S * k * C)
+        self.stripes = np.empty(S * (k + p) * C, dtype=np.uint8)
+        sv = self.stripes.reshape(S, k + p, C)
+        sv[:, :k] = self.data.reshape(S, k, C)
+        self.pout = np.empty(p * S * C, dtype=np.uint8)     # reused: no page faults in the timed loop
+        ref.encode_batch(k, p, C, S, self.data, nthreads=8, simd=True, out=self.pout)
+        sv[:, k:] = self.pout.reshape(p, S, C).transpose(1, 0, 2)
+        self.err = [0, 1] if p >= 2 else [0]
+        rc, _, self.dec, self.el, self.gt, _ = ref.recov_codec(k, p, self.err)
+        assert rc == 0
+        self.ws = S * ((k + p) * C * ("dec" in ops) + (k + p) * C * ("enc" in ops))
+
+    def run(self, threads, secs):
+        k, p, C, S, ref = self.k, self.p, self.C, self.S, self.ref
+        user, n, t0 = 0, 0, time.perf_counter()
+        while time.perf_counter() - t0 < secs or n == 0:
+            if "enc" in self.ops:
+                ref.encode_batch(k, p, C, S, self.data, nthreads=threads, simd=True, out=self.pout)
+            if "dec" in self.ops:
+                ref.recov_batch(k, len(self.err), self.gt, self.dec, self.el, C, (k + p) * C, S, self.stripes,
+                                nthreads=threads, simd=True)
+            user += len(self.ops) * k * C * S
+            n += 1
+        return user / (time.perf_counter() - t0) / GIB
+
+    def row(self, threads, secs, repeats=3):
+        """Median and range of `repeats` runs on `threads`, then one core."""
+        many = sorted(self.run(threads, secs) for _ in range(repeats))
+        one = self.run(1, secs)
+        return {"value": round(many[len(many) // 2], 3), "unit": "GiB/s", "cores": threads,
+                "runs": [round(x, 3) for x in many], "range": [round(many[0], 3), round(many[-1], 3)],
+                "one_core": round(one, 3),
+                "sample": f"EC_{self.k}P{self.p} {self.C >> 10} KiB cells, {self.S} stripes "
+                          f"({self.S * self.k * self.C / GIB:.2f} GiB of data, {self.ws / GIB:.2f} GiB touched), "
+                          f"{' + '.join(self.ops)}{' {d0,d1}' if 'dec' in self.ops else ''}"}
+
+
+# per-config CPU rows beside the GPU detail rows (BASELINE.md §3 shapes, per GPU)
+CPU_CONFIGS = (("EC_2P1_128KiB_encode", 2, 1, 128 << 10, ("enc",), 0),
+               ("EC_8P2_1MiB_decode_d0d1", 8, 2, 1 << 20, ("dec",), 3),
+               ("EC_16P2_128KiB_encode", 16, 2, 128 << 10, ("enc",), 4))
+
+
+def cpu_baseline(k, p, C, budget_s, ops=("enc", "dec"), per_config=True):
+    """The headline workload's CPU rate on every core of this process's
+    affinity mask (3 repeats: median and range; plus one core), the load
+    average before and after, and the same for configs 1, 3 and the config-4
+    per-GPU shard.  Reported beside the GPU rows, never the target."""
+    from oracle import ref
+
+    share = cpu_share()
+    threads = share["affinity"]
+    load0 = [round(x, 2) for x in os.getloadavg()]
+    t_all = time.perf_counter()
+    head = CpuCase(k, p, C, ops, config_id=2)
+    secs = budget_s / 8.0                      # 3 repeats + 1 core = 4 runs of the headline
+    out = head.row(threads, secs)
+    if threads > 16:                           # the 16-thread rate earlier rounds reported
+        out["cores16"] = round(sorted(head.run(16, secs) for _ in range(3))[1], 3)
+    del head
+    out.update({"kind": "port", "cores_available": share, "cpu_model": cpu_model(),
+                "variant": {0: "scalar", 1: "avx2-vpshufb", 2: "gfni-avx512"}[ref.simd_variant()],
+                "what": "ISA-L-equivalent restatement (oracle/ec_simd.c), OpenMP over stripes"})
+    if per_config:
+        rows = {}
+        for name, kk, pp, CC, oo, cid in CPU_CONFIGS:
+            case = CpuCase(kk, pp, CC, oo, config_id=cid)
+            rows[name] = case.row(threads, secs / 2)
+            del case
+        out["configs"] = rows
+    out["load"] = {"before": load0, "after": [round(x, 2) for x in os.getloadavg()]}
+    out["seconds"] = round(time.perf_counter() - t_all, 1)
+    return out
 
 
 def pmc_traffic():
@@ -964,6 +1020,11 @@ def main():
                        "cannot reach 0.70 while parity is written (DESIGN.md §6)"}
     if rank == 0 and world == 1 and not args.no_cpu and m is None:
         out["cpu_baseline"] = cpu_baseline(k, p, C, args.cpu_seconds, ops)
+        if "detail" in out:                   # CPU beside GPU, per config
+            for name, row in out["cpu_baseline"].get("configs", {}).items():
+                if name in out["detail"]:
+                    out["detail"][name]["cpu_GiBps"] = row["value"]
+                    out["detail"][name]["gpu_over_cpu"] = round(out["detail"][name]["GiBps_user"] / row["value"], 1)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if m is not None:

@@ -367,6 +367,7 @@ int ecg_matmul_sel(ecg_ctx_t *ctx, int ncols, int rows, const unsigned char *coe
 	free(prm);
 	if (e)
 		return ecg_hip_fail((hipError_t)e, "matmul_sel launch");
+	ECG_STAT_ADD(ctx, launches, 1);
 	ecg_set_last_kernel(ecg_k_kernel_name(kid));
 	return 0;
 }

@@ -49,6 +49,7 @@
 #define NSLOT_MIN 4	/* staging slots for one device; 2 per device beyond */
 #define NSLOT_MAX 32
 #define NFIN 4		/* completion threads: output scatter + callbacks */
+#define NDSTLOCK 64	/* striped locks serialising update deltas into one parity cell */
 
 enum slot_state { S_FREE, S_FILLING, S_READY, S_INFLIGHT, S_DONE };
 
@@ -103,6 +104,13 @@ struct ecg_queue {
 	pthread_t worker;
 	pthread_t fin[NFIN];
 	int nfin;
+	/* Updates of one stripe submitted back to back (one per updated cell, all
+	 * naming the same parity cells) land in one batch or in batches of
+	 * different devices, and their completions run on different threads:
+	 * the read-modify-write parity ^= delta of two of them must not
+	 * interleave.  A lock striped on the destination address serialises
+	 * exactly those (XOR commutes, so their order does not matter). */
+	pthread_mutex_t dst_lock[NDSTLOCK];
 };
 
 static uint64_t now_ns(void)
@@ -239,6 +247,20 @@ static void launch_slot(struct ecg_queue *q, struct qslot *s)
 		if (e != hipSuccess)
 			rc = ecg_hip_fail(e, "queue D2H");
 	}
+	if (rc == 0) {	/* the queue's work in the device's counters */
+		ECG_STAT_ADD(s->ctx, h2d_bytes, (uint64_t)s->nin * s->C * n);
+		ECG_STAT_ADD(s->ctx, d2h_bytes, (uint64_t)s->rows * s->C * n);
+		if (s->op == OP_ENCODE) {
+			ECG_STAT_ADD(s->ctx, encode_stripes, n);
+			ECG_STAT_ADD(s->ctx, encode_bytes, (uint64_t)s->k * s->C * n);
+		} else if (s->op == OP_RECOVER) {
+			ECG_STAT_ADD(s->ctx, recover_stripes, n);
+			ECG_STAT_ADD(s->ctx, recover_bytes, (uint64_t)s->rows * s->C * n);
+		} else {
+			ECG_STAT_ADD(s->ctx, update_cells, n);
+			ECG_STAT_ADD(s->ctx, update_bytes, (uint64_t)s->C * n);
+		}
+	}
 	s->rc = rc;
 	s->state = S_INFLIGHT;
 	q->batches++;
@@ -264,7 +286,16 @@ static void xor_into(unsigned char *dst, const unsigned char *a, const unsigned 
 		dst[i] = a[i] ^ b[i];
 }
 
-static void finish_req(struct qslot *s, uint32_t i)
+static pthread_mutex_t *dst_lock_of(struct ecg_queue *q, const void *dst)
+{
+	uint64_t a = (uint64_t)(uintptr_t)dst;
+
+	a ^= a >> 17;
+	a *= 0x9E3779B97F4A7C15ull;
+	return &q->dst_lock[a >> 58];	/* top 6 bits: NDSTLOCK = 64 */
+}
+
+static void finish_req(struct ecg_queue *q, struct qslot *s, uint32_t i)
 {
 	const uint64_t out_stride = s->pitch * (uint64_t)s->rows;
 	const unsigned char *out = s->host + s->out_off + i * out_stride;
@@ -272,8 +303,13 @@ static void finish_req(struct qslot *s, uint32_t i)
 
 	ecg_trace_push("ecg:queue_complete");
 	if (s->rc == 0 && s->op == OP_UPDATE)	/* parity ^= coef[r][vec_i] * diff */
-		for (int j = 0; j < s->rows; j++)
+		for (int j = 0; j < s->rows; j++) {
+			pthread_mutex_t *l = dst_lock_of(q, r->dst[j]);
+
+			pthread_mutex_lock(l);
 			xor_into(r->dst[j], r->dst[j], out + j * s->pitch, s->C);
+			pthread_mutex_unlock(l);
+		}
 	else if (s->rc == 0)
 		for (int j = 0; j < s->rows; j++)
 			memcpy(r->dst[j], out + j * s->pitch, s->C);
@@ -305,7 +341,7 @@ static void *fin_main(void *argp)
 		}
 		i = s->fin_next++;
 		pthread_mutex_unlock(&q->lock);
-		finish_req(s, i);
+		finish_req(q, s, i);
 		pthread_mutex_lock(&q->lock);
 		if (++s->fin_done == s->reserved) {
 			q->completed += s->reserved;
@@ -443,6 +479,8 @@ static int queue_create(ecg_ctx_t *const *ctxs, int nctx, const ecg_queue_attr_t
 	pthread_cond_init(&q->cv_slot, NULL);
 	pthread_cond_init(&q->cv_done, NULL);
 	pthread_cond_init(&q->cv_fin, NULL);
+	for (i = 0; i < NDSTLOCK; i++)
+		pthread_mutex_init(&q->dst_lock[i], NULL);
 	for (i = 0; i < q->nslot && e == hipSuccess; i++) {
 		struct qslot *s = &q->slot[i];
 
@@ -531,6 +569,8 @@ void ecg_queue_destroy(ecg_queue_t *q)
 	pthread_cond_destroy(&q->cv_slot);
 	pthread_cond_destroy(&q->cv_done);
 	pthread_cond_destroy(&q->cv_fin);
+	for (int i = 0; i < NDSTLOCK; i++)
+		pthread_mutex_destroy(&q->dst_lock[i]);
 	pthread_mutex_destroy(&q->lock);
 	free(q);
 }

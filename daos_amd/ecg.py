@@ -42,6 +42,7 @@ _SIGS = [
     ("ecg_device_pci_bus_id", C.c_int, [C.c_int, C.c_char_p, C.c_int]),
     ("ecg_strerror", C.c_char_p, []),
     ("ecg_last_kernel", C.c_char_p, []),
+    ("ecg_build_info", C.c_char_p, []),
     ("ecg_gf_mul", C.c_ubyte, [C.c_ubyte, C.c_ubyte]),
     ("ecg_gf_inv", C.c_ubyte, [C.c_ubyte]),
     ("ecg_gen_cauchy1", C.c_int, [C.c_int, C.c_int, u8p]),
@@ -253,6 +254,41 @@ def device_count() -> int:
 
 def last_kernel() -> str:
     return lib().ecg_last_kernel().decode()
+
+
+def build_info() -> dict:
+    """ecg_build_info() of the loaded library: src_sha256, hipcc, arch."""
+    return dict(kv.split("=", 1) for kv in lib().ecg_build_info().decode().split(";"))
+
+
+def source_hash() -> str:
+    """sha256 (16 hex) over the library's sources as they are in this tree --
+    the recipe of daos_amd/csrc/Makefile HASHED (paths relative to csrc,
+    byte-sorted, contents concatenated).  Equal to build_info()["src_sha256"]
+    iff the loaded libecg.so was built from exactly these sources."""
+    import glob
+    import hashlib
+
+    csrc = os.path.join(_HERE, "csrc")
+    pats = ("host/*.c", "host/*.h", "kernels/*.hip", "kernels/*.h", "*.h", "../../include/*.h")
+    rel = {os.path.relpath(f, csrc) if not pat.startswith("..") else "../../include/" + os.path.basename(f)
+           for pat in pats for f in glob.glob(os.path.join(csrc, pat))}
+    rel |= {"Makefile", "exports.map"}
+    h = hashlib.sha256()
+    for r in sorted(rel, key=lambda x: x.encode()):
+        with open(os.path.join(csrc, r), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def code_object_targets() -> list:
+    """Offload targets of the GPU code objects bundled in the loaded
+    libecg.so (from the clang offload bundle entry ids)."""
+    import re
+
+    with open(LIB_PATH, "rb") as f:
+        blob = f.read()
+    return sorted({m.decode() for m in re.findall(rb"amdgcn-amd-amdhsa--(gfx[0-9a-z]+)", blob)})
 
 
 def pci_bus_id(device: int) -> str:
@@ -524,10 +560,19 @@ class Multi:
         _chk(lib().ecg_multi_range(self.h, nstripes, i, C.byref(f), C.byref(c)), "multi_range")
         return f.value, c.value
 
+    def _shards(self, **seqs):
+        """Every per-shard sequence must have one entry per shard: the C side
+        reads n entries of each (a short nstripes would be read past its end,
+        a short pointer list would hand a shard NULL)."""
+        for name, v in seqs.items():
+            if v is None or len(v) != self.n:
+                raise ValueError(f"Multi: {name} has {0 if v is None else len(v)} entries, expected {self.n}")
+
     def encode(self, k: int, p: int, cell_bytes: int, nstripes: Sequence[int], data: Sequence[int],
                data_stripe_stride: int, parity: Sequence[int], parity_cell_stride: int, parity_stripe_stride: int,
                flags: int = 0):
         n = self.n
+        self._shards(nstripes=nstripes, data=data, parity=parity)
         _chk(lib().ecg_multi_encode(self.h, k, p, cell_bytes, _u32(nstripes), (vp * n)(*data), data_stripe_stride,
                                     (vp * n)(*parity), parity_cell_stride, parity_stripe_stride, flags),
              "multi_encode")
@@ -535,6 +580,7 @@ class Multi:
     def recover(self, k: int, p: int, cell_bytes: int, nstripes: Sequence[int], stripes: Sequence[int],
                 stripe_stride: int, err_list: Sequence[int], flags: int = 0):
         n = self.n
+        self._shards(nstripes=nstripes, stripes=stripes)
         _chk(lib().ecg_multi_recover(self.h, k, p, cell_bytes, _u32(nstripes), (vp * n)(*stripes), stripe_stride,
                                      _u32(err_list), len(err_list), flags), "multi_recover")
 

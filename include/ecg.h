@@ -63,6 +63,10 @@ void *ecg_ctx_stream(ecg_ctx_t *ctx);
 const char *ecg_strerror(void);
 /* Name of the kernel the last ecg_* compute call on this thread launched. */
 const char *ecg_last_kernel(void);
+/* Identity of this build: "src_sha256=<16 hex>;hipcc=<version>;arch=gfx950",
+ * the hash over every source, header and build file of the library
+ * (daos_amd/csrc/Makefile HASHED), fixed at build time. */
+const char *ecg_build_info(void);
 
 /* ---- field and matrices (host; setup only) ------------------------------- */
 unsigned char ecg_gf_mul(unsigned char a, unsigned char b);
@@ -232,7 +236,10 @@ int ecg_dev_copy_kernel(ecg_ctx_t *ctx, void *dst, const void *src, size_t bytes
  *   update_*   partial-stripe parity updates: updated cells and their bytes
  *   csum_chunks  checksums computed (standalone and fused)
  *   launches   codec kernel launches (product, fused, checksum)
- *   h2d_bytes / d2h_bytes  bytes the host-resident pipelines moved over PCIe */
+ *   h2d_bytes / d2h_bytes  cell bytes the host-resident pipelines and the
+ *              batching queue moved over PCIe
+ * The batching queue counts its batches on the context of the slot that ran
+ * them (encode / recover / update rows above, and launches). */
 typedef struct ecg_stats {
 	uint64_t encode_stripes, encode_bytes;
 	uint64_t recover_stripes, recover_bytes;

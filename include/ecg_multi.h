@@ -32,7 +32,12 @@ extern "C" {
 #endif
 
 #define ECG_MULTI_MAX 64	/* shards per ecg_multi_t */
-#define ECG_MULTI_ASYNC 0x1u	/* device calls: return once enqueued; ecg_multi_sync waits */
+/* Device-resident calls only: return once every shard's launches are
+ * enqueued; ecg_multi_sync waits for them.  Every buffer the call names must
+ * stay allocated and untouched by the caller until ecg_multi_sync returns
+ * (ecg_multi_destroy also waits).  The _host calls ignore it: they always
+ * return with their outputs in host memory. */
+#define ECG_MULTI_ASYNC 0x1u
 
 typedef struct ecg_multi ecg_multi_t;
 

@@ -75,6 +75,16 @@ def test_gpu_kernels_built_for_gfx950(ecglib):
     assert ".hip_fatbin" in sec
 
 
+def test_build_info_names_this_tree(ecglib):
+    """The library carries the hash of the sources it was built from
+    (ecg_build_info, Makefile HASHED); it equals this tree's, so the .so that
+    travels to the GPU box is the build of the committed sources."""
+    info = ecglib.build_info()
+    assert info["src_sha256"] == ecglib.source_hash()
+    assert info["arch"] == "gfx950" and info["hipcc"].startswith("HIP version")
+    assert ecglib.code_object_targets() == ["gfx950"]
+
+
 def test_no_device_fails_loudly(ecglib):
     if ecglib.device_count() > 0:
         pytest.skip("GPU present")

@@ -166,6 +166,37 @@ def test_queue_update_same_stripe_accumulates(ecglib, ctx, oracle):
     q.close()
 
 
+def test_queue_updates_of_one_stripe_no_flush(ecglib, ctx, oracle):
+    """agg_update_parity's calling pattern (ref:src/object/srv_ec_aggregate.c:
+    1086-1102): one ecg_queue_update per updated cell of a stripe, all naming
+    the same parity cells, submitted back to back with no flush in between --
+    over a queue whose slots sit on two shard contexts, so the deltas of one
+    stripe complete in one batch on different completion threads and in
+    batches of different devices.  Every delta must land: the parity equals
+    the oracle's encode of the fully updated stripes (the
+    read-modify-write parity ^= delta was unsynchronised)."""
+    m = ecglib.Multi([0, 0])
+    q = ecglib.Queue(m, max_batch=4, max_wait_us=200)
+    k, p, C_, NS, ROUNDS = 8, 2, 256 << 10, 3, 3
+    en = oracle.cauchy1(k, p)
+    data = [rand((k, C_), 700 + s) for s in range(NS)]
+    par = [[r.copy() for r in oracle.encode_data(en[k:], d)] for d in data]
+    rid = 0
+    for rnd in range(ROUNDS):
+        for s in range(NS):
+            for j in range(k):
+                new = rand(C_, 1000 + rnd * 100 + s * 10 + j)
+                q.update(rid, k, p, j, data[s][j].copy(), new, par[s])
+                data[s][j] = new
+                rid += 1
+    q.flush()
+    assert all(rc == 0 for rc in q.done.values()) and len(q.done) == rid
+    for s in range(NS):
+        assert np.array_equal(np.stack(par[s]), oracle.encode_data(en[k:], data[s])), s
+    q.close()
+    m.close()
+
+
 def test_isal_dropin_over_device_list(oracle):
     """ECG_DEVICES=0,0,0 gives the synchronous ISA-L drop-in three contexts;
     threads are spread over them and every call stays bit-exact."""

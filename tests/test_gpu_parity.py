@@ -359,114 +359,6 @@ def test_recover_host_erasure_runs(ctx, oracle, errs):
     assert np.array_equal(broken, stripes)
 
 
-# --------------------------------------------------------------- BASELINE sizes
-def _sample_check(oracle, k, p, data_host, par_host, S, stripes):
-    en = oracle.cauchy1(k, p)
-    for s in stripes:
-        want = oracle.encode_data(en[k:], data_host[s])
-        assert np.array_equal(par_host[:, s], want), s
-
-
-def test_config2_ec4p2_1mib_full_size(ctx, oracle):
-    """BASELINE configs[1]: EC_4P2, 1 MiB cells, 1024 stripes (4 GiB data).
-    Every parity byte is checked through the recovery round trip (erase all
-    data cells' partners: recover d0,d1 from d2,d3,p0,p1 and compare), plus
-    16 sampled stripes byte-compared with the oracle."""
-    from tools.datagen import stripe_bytes
-
-    k, p, C_, S = 4, 2, 1 << 20, 1024
-    data = stripe_bytes(S * k * C_, 2).reshape(S, k, C_)
-    stripes = ctx.alloc(S * (k + p) * C_)
-    for s0 in range(0, S, 128):
-        blk = np.zeros((128, k + p, C_), dtype=np.uint8)
-        blk[:, :k] = data[s0:s0 + 128]
-        stripes.upload(blk, offset=s0 * (k + p) * C_)
-    stride = (k + p) * C_
-    ctx.encode(k, p, C_, S, stripes.ptr, stride, stripes.ptr + k * C_, C_, stride)
-    ctx.sync()
-    enc = stripes.download().reshape(S, k + p, C_)
-    rng = np.random.default_rng(0)
-    _sample_check(oracle, k, p, data, enc[:, k:].transpose(1, 0, 2), S, rng.choice(S, 16, replace=False))
-    assert np.array_equal(enc[:, :k], data)                  # data untouched
-    # round trip: erase d0, d1 on device, recover from (d2, d3, p0, p1)
-    zero = np.zeros(C_, dtype=np.uint8)
-    for s in range(0, S, 97):
-        stripes.upload(zero, offset=s * stride)
-    ctx.recover(k, p, C_, S, stripes.ptr, stride, [0, 1])
-    ctx.sync()
-    rec = stripes.download().reshape(S, k + p, C_)
-    assert np.array_equal(rec, enc)
-    stripes.free()
-
-
-def test_config4_ec16p2_full_size_sharded(ctx, oracle):
-    """BASELINE configs[3]: EC_16P2, 128 KiB cells, 8192 stripes (16 GiB of
-    data) sharded over 8 ranks by contiguous stripe ranges.  The 8 shard
-    launches (what 8 GPUs each run, bench.py --workload enc_16p2_strong) must
-    write exactly the parity of one launch over all stripes -- stripes are
-    independent -- and sampled stripes must match the oracle."""
-    from tools.datagen import stripe_bytes
-
-    k, p, C_, S, G = 16, 2, 128 << 10, 8192, 8
-    blk = stripe_bytes(256 << 20, 4)
-    data = ctx.alloc(S * k * C_)
-    for i, off in enumerate(range(0, S * k * C_, blk.size)):
-        data.upload(np.roll(blk, i * 4099), offset=off)      # no two 256 MiB tiles alike
-    full = ctx.alloc(p * S * C_)
-    shard = ctx.alloc(p * S * C_)
-    try:
-        ctx.encode(k, p, C_, S, data.ptr, k * C_, full.ptr, S * C_, C_)
-        per = S // G
-        for g in range(G):
-            ctx.encode(k, p, C_, per, data.ptr + g * per * k * C_, k * C_, shard.ptr + g * per * C_, S * C_, C_)
-        ctx.sync()
-        a, b = full.download(), shard.download()
-        assert np.array_equal(a, b)
-        par = a.reshape(p, S, C_)
-        en = oracle.cauchy1(k, p)
-        for s in np.random.default_rng(4).choice(S, 8, replace=False):
-            cells = data.download(k * C_, offset=int(s) * k * C_).reshape(k, C_)
-            want = oracle.encode_data(en[k:], cells)
-            assert np.array_equal(par[:, s], want), s
-    finally:
-        data.free()
-        full.free()
-        shard.free()
-
-
-def test_config3_ec8p2_1mib_degraded_decode(ctx, oracle):
-    """BASELINE configs[2]: EC_8P2, 1 MiB cells, 512 stripes, cells {d0,d1}
-    missing; recovered bytes must equal the original data."""
-    from tools.datagen import stripe_bytes
-
-    k, p, C_, S = 8, 2, 1 << 20, 512
-    stride = (k + p) * C_
-    data = stripe_bytes(S * k * C_, 3).reshape(S, k, C_)
-    buf = ctx.alloc(S * stride)
-    for s0 in range(0, S, 64):
-        blk = np.zeros((64, k + p, C_), dtype=np.uint8)
-        blk[:, :k] = data[s0:s0 + 64]
-        buf.upload(blk, offset=s0 * stride)
-    ctx.encode(k, p, C_, S, buf.ptr, stride, buf.ptr + k * C_, C_, stride)
-    ctx.sync()
-    par = buf.download().reshape(S, k + p, C_)[:, k:].copy()
-    _sample_check(oracle, k, p, data, par.transpose(1, 0, 2), S, [0, 1, 255, 511])
-    ctx.recover(k, p, C_, S, buf.ptr, stride, [0, 1])        # overwrite d0,d1 in place from survivors
-    ctx.sync()
-    buf.fill(0)                                              # wipe, then recover into a clean copy
-    for s0 in range(0, S, 64):
-        blk = np.zeros((64, k + p, C_), dtype=np.uint8)
-        blk[:, 2:k] = data[s0:s0 + 64, 2:]
-        blk[:, k:] = par[s0:s0 + 64]
-        buf.upload(blk, offset=s0 * stride)
-    ctx.recover(k, p, C_, S, buf.ptr, stride, [0, 1])
-    ctx.sync()
-    got = buf.download().reshape(S, k + p, C_)
-    assert np.array_equal(got[:, :k], data)
-    buf.free()
-
-
-
 # --------------------------------------------------------------- batching facade
 def test_queue_batches_concurrent_one_stripe_calls(ctx, oracle, ecglib):
     """8 threads x 40 one-stripe EC_8P2 encodes (the reference's calling
