@@ -139,6 +139,23 @@ def launch_ranks(args) -> int:
     return rc
 
 
+def rank_numa(args):
+    """A rank of an N-GPU run (N > 1) runs on the CPUs of its GPU's NUMA node:
+    pinned here, from sysfs alone, before torch or libecg start the GPU
+    runtime, so the runtime's threads and this rank's pinned staging inherit
+    it (daos_amd/numa.py).  N = 1 only reports the node."""
+    if args.rehearse:
+        return None
+    from daos_amd import numa
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
+    nvis = len(numa.visible_gpus()) or 1
+    if world > 1 and args.sharder == "procs":
+        return numa.pin_to_device(local % nvis)
+    return numa.placement(local % nvis)
+
+
 def dist_init():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -402,6 +419,24 @@ class HostWorkload:
     def free(self):
         for b in (self.data, self.parity, self.stripes):
             b.free()
+
+
+class HostMultiWorkload(HostWorkload):
+    """`--sharder lib` for configs[4]: ONE batch of S = stripes-per-GPU x N
+    in pinned host memory, split by ecg_multi_encode_host /
+    ecg_multi_recover_host into contiguous stripe ranges, each shard
+    streaming its range through its own device's staging (include/ecg_multi.h)."""
+
+    def __init__(self, m, k, p, C, S_per, ops, chunk=0):
+        self.m = m
+        super().__init__(m.ctxs[0], k, p, C, S_per * m.n, ops=ops, chunk=chunk)
+
+    def step(self, timed=False):
+        k, p, C, S = self.k, self.p, self.C, self.S
+        if "enc_host" in self.ops:
+            self.m.encode_host(k, p, C, S, self.data.array, self.parity.array, chunk=self.chunk)
+        if "dec_host" in self.ops:
+            self.m.recover_host(k, p, C, S, self.stripes.array, self.err, chunk=self.chunk)
 
 
 class MultiWorkload:
@@ -748,14 +783,20 @@ def cpu_baseline(k, p, C, budget_s, ops=("enc", "dec"), per_config=True):
     from oracle import ref
 
     share = cpu_share()
+    # the CPUs this process is granted: its affinity mask, capped by the cgroup
+    # quota when one is set (the GPU box's 256-CPU mask carries a 16-CPU quota:
+    # 256 threads ran at 5 GiB/s there against 97 on 16, gpurun_out r03 bench)
     threads = share["affinity"]
+    if share["cgroup_quota_cpus"]:
+        threads = max(1, min(threads, int(share["cgroup_quota_cpus"])))
     load0 = [round(x, 2) for x in os.getloadavg()]
     t_all = time.perf_counter()
     head = CpuCase(k, p, C, ops, config_id=2)
     secs = budget_s / 8.0                      # 3 repeats + 1 core = 4 runs of the headline
     out = head.row(threads, secs)
-    if threads > 16:                           # the 16-thread rate earlier rounds reported
-        out["cores16"] = round(sorted(head.run(16, secs) for _ in range(3))[1], 3)
+    if threads < share["affinity"]:            # what the whole mask does under the quota (one short run)
+        out["all_affinity_threads"] = {"threads": share["affinity"],
+                                       "value": round(head.run(share["affinity"], secs / 2), 3)}
     del head
     out.update({"kind": "port", "cores_available": share, "cpu_model": cpu_model(),
                 "variant": {0: "scalar", 1: "avx2-vpshufb", 2: "gfni-avx512"}[ref.simd_variant()],
@@ -787,7 +828,7 @@ def pmc_traffic():
 
 
 # ------------------------------------------------------------------ reporting
-def host_report(args, ctx, wl, world, rank, value, elapsed, ranks):
+def host_report(args, ctx, wl, world, rank, value, elapsed, ranks, nshard=1):
     """JSON line of the PCIe-inclusive rebuild stream (configs[4]).  The
     device kernels are not the bound here, the host links are: `roofline`
     is null and `pcie` sets the achieved H2D rate against this box's raw
@@ -811,11 +852,14 @@ def host_report(args, ctx, wl, world, rank, value, elapsed, ranks):
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic: xoshiro256** stripes in pinned host memory",
-        "config": {"workload": f"EC_{k}P{p} {C >> 10} KiB cells: per step one encode batch of {S} stripes "
-                               f"+ one {{d0,d1}} recovery batch of {S} stripes per GPU, host<->device copies "
-                               f"included ({wl.chunk}-stripe staging chunks)",
-                   "name": args.workload, "k": k, "p": p, "cell_bytes": C, "stripes_per_gpu": S,
-                   "erasures": wl.err, "parallelism": f"stripe-sharded x{world}, no collective"},
+        "config": {"workload": f"EC_{k}P{p} {C >> 10} KiB cells: per step one encode batch of {S // nshard} stripes "
+                               f"+ one {{d0,d1}} recovery batch of {S // nshard} stripes per GPU, host<->device "
+                               f"copies included ({wl.chunk}-stripe staging chunks)",
+                   "name": args.workload, "k": k, "p": p, "cell_bytes": C, "stripes_per_gpu": S // nshard,
+                   "erasures": wl.err,
+                   "parallelism": (f"one {S}-stripe host batch split x{nshard} in one process (ecg_multi_*_host), "
+                                   "no collective" if nshard > 1 or args.sharder == "lib"
+                                   else f"stripe-sharded x{world}, no collective")},
         "roofline": None,
         "pcie": {"bound": "pcie", "h2d_GBps_all_ranks": round(h2d, 2), "d2h_GBps_all_ranks": round(d2h, 2)},
         "verified": ver,
@@ -823,7 +867,7 @@ def host_report(args, ctx, wl, world, rank, value, elapsed, ranks):
         "cpu_baseline": None,
     }
     wl.free()
-    if rank == 0 and world == 1 and not args.no_detail:
+    if rank == 0 and world == 1 and nshard == 1 and not args.no_detail:
         raw = pinned_copy_rates(ctx)
         out["pcie"]["measured_pinned_GBps"] = raw
         out["pcie"]["frac_of_h2d"] = round(h2d / raw["h2d"], 4)
@@ -854,6 +898,7 @@ def main():
         raise SystemExit("bench.py: --gpus must be >= 1")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1 and args.sharder == "procs":
         sys.exit(launch_ranks(args))          # parent: no GPU calls before or after
+    numa_info = rank_numa(args)               # before anything starts the GPU runtime
     world, rank, local = dist_init()
     if "WORLD_SIZE" in os.environ and args.sharder == "procs" and world != args.gpus:
         raise SystemExit(f"bench.py: launched as {world} ranks but --gpus {args.gpus}")
@@ -877,13 +922,12 @@ def main():
         devices = list(range(args.gpus)) if args.gpus <= ndev else [i % ndev for i in range(args.gpus)]
         if args.gpus > ndev and not args.allow_shared_device:
             raise SystemExit(f"bench.py: {args.gpus} shards but {ndev} devices (--allow-shared-device to rehearse)")
-        if host:
-            raise SystemExit("bench.py: --sharder lib covers the device-resident workloads")
         m = ecg.Multi(devices)
         ctx = m.ctxs[0]
         dev = devices[0]
         torch.cuda.set_device(dev)
-        wl = MultiWorkload(m, k, p, C, S, ops, strong)
+        wl = (HostMultiWorkload(m, k, p, C, S, ops, chunk=args.host_chunk) if host
+              else MultiWorkload(m, k, p, C, S, ops, strong))
         rank_devs = [{"shard": i, "device": d, "pci": ecg.pci_bus_id(d)} for i, d in enumerate(devices)]
         S = wl.S
     else:
@@ -936,8 +980,14 @@ def main():
         return
 
     if rank_devs is None:
+        numa_rep = {"numa_node": numa_info["numa_node"], "pinned_cpus": numa_info["pinned_cpus"]} \
+            if numa_info and "pinned_cpus" in numa_info else \
+            {"numa_node": ecg.lib().ecg_device_numa_node(dev), "pinned_cpus": 0}
         rank_devs = gather(world, {"rank": rank, "device": dev, "pci": ecg.pci_bus_id(dev),
-                                   "ms_per_step": round(mine / args.steps * 1e3, 3)})
+                                   "ms_per_step": round(mine / args.steps * 1e3, 3), **numa_rep})
+    elif m is not None:
+        for i, r in enumerate(rank_devs):
+            r["numa_node"] = m.numa_node(i)
     n_gpus = len({r["pci"] for r in rank_devs})
     if strong:      # the fixed total, however it was split
         user = WORKLOADS[args.workload][3] * k * C * len(ops) * args.steps
@@ -945,8 +995,11 @@ def main():
         user = wl.user_bytes_per_step() * args.steps * world
     value = user / elapsed / GIB
     if host:
-        ok = host_report(args, ctx, wl, world, rank, value, elapsed, rank_devs)
-        ctx.close()
+        ok = host_report(args, ctx, wl, world, rank, value, elapsed, rank_devs, nshard)
+        if m is not None:
+            m.close()
+        else:
+            ctx.close()
         finish_dist(world)
         if not ok:
             raise SystemExit("bench.py: verification failed (see `verified`)")

@@ -129,7 +129,24 @@ typedef struct ecg_launch_cfg {
  * (n-major, so lane l's entries sit in bank l: conflict-free) */
 #define ECG_CSUM_OFF_NIBL(NB) (ECG_CSUM_OFF_A5_32K(NB) + ECG_CSUM_NA5(NB) * 32)
 #define ECG_CSUM_OFF_R4(NB) (ECG_CSUM_OFF_NIBL(NB) + 16 * 64)
-#define ECG_CSUM_TBL_ENTRIES(NB) (ECG_CSUM_OFF_R4(NB) + 16)
+/* nibble tables (4-bit fields, addressed by one SDWA byte select each;
+ * ecg_crc_dev.h horner4u): a 16-byte piece is 32 nibbles (nibble t = bits
+ * 4t..4t+3 of the piece, little-endian), the register W/4 nibbles.
+ *   q4*[u][32][16]  q4[u][t][v] = raw CRC of the piece whose nibble t is v,
+ *                   followed by u strides of zero bytes (u = 0 .. U-1)
+ *   a4*[16][16]     a4[t][v] = register nibble t = v shifted by the U-stride
+ *                   (rows >= W/4 unused)
+ * 1 KiB stride (wave kernels, U = ECG_CSUM_P5U; a4 of 4 KiB), 256 B stride
+ * (lane-group kernel, U = ECG_CSUM_P5U; a4 of 1 KiB), 4 KiB stride (fused
+ * workgroup kernel, U = ECG_MMCS_P5U; a4 of 32 KiB). */
+#define ECG_CSUM_NQ4 (32 * 16)
+#define ECG_CSUM_OFF_Q4_1K(NB) (ECG_CSUM_OFF_R4(NB) + 16)
+#define ECG_CSUM_OFF_A4_4K(NB) (ECG_CSUM_OFF_Q4_1K(NB) + ECG_CSUM_P5U * ECG_CSUM_NQ4)
+#define ECG_CSUM_OFF_Q4_256(NB) (ECG_CSUM_OFF_A4_4K(NB) + 256)
+#define ECG_CSUM_OFF_A4_1K(NB) (ECG_CSUM_OFF_Q4_256(NB) + ECG_CSUM_P5U * ECG_CSUM_NQ4)
+#define ECG_CSUM_OFF_Q4_4K(NB) (ECG_CSUM_OFF_A4_1K(NB) + 256)
+#define ECG_CSUM_OFF_A4_32K(NB) (ECG_CSUM_OFF_Q4_4K(NB) + ECG_MMCS_P5U * ECG_CSUM_NQ4)
+#define ECG_CSUM_TBL_ENTRIES(NB) (ECG_CSUM_OFF_A4_32K(NB) + 256)
 #define ECG_CSUM_OFF_P2(NB) (3 * (NB) * 256 + 64 + 256)
 #define ECG_CSUM_OFF_SH256(NB) (3 * (NB) * 256 + 64 + 256 + ECG_CSUM_NP2)
 #define ECG_CSUM_GLANES 16	/* lanes per chunk in the lane-group CRC kernel */
@@ -155,7 +172,7 @@ typedef struct ecg_csum_params {
 	uint32_t type;			/* DAOS hash type: 1 crc16, 2 crc32, 3 crc64, 7 adler32 */
 	uint32_t variant;		/* CRC: 0 auto, 1 wave per chunk, 2 workgroup per chunk,
 					 * 3 a 16-lane group per chunk */
-	uint32_t byte_tables;		/* CRC lookups: 0 = 5-bit tables, 1 = byte tables */
+	uint32_t byte_tables;		/* CRC lookups: 0 = 5-bit tables, 1 = byte tables, 2 = nibble tables */
 	uint32_t pad2;
 	/* workgroup-per-chunk CRC: a chunk of m 1 KiB steps is cut into
 	 * ECG_CSUM_SPLIT_NW slices; split_sh[c][w] = x^(8 * bytes after slice w)

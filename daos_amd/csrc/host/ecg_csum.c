@@ -40,6 +40,20 @@ static uint32_t use_byte_tables(const ecg_ctx_t *ctx, int type, int fused)
 	return fused && type == ECG_HASH_CRC64;
 }
 
+/* Standalone CRC kernels (ecg_csum_params_t.byte_tables): 2 = nibble tables
+ * addressed by SDWA byte selects, the default since round 3 -- the kernels
+ * are VALU-issue bound and a nibble lookup costs 1.25 VALU for its address
+ * against 2 for a 5-bit field (profiles/r03/crc_sq, crc_ab); bit 4 forces the
+ * byte tables, bit 5 the 5-bit tables. */
+static uint32_t standalone_tables(const ecg_ctx_t *ctx)
+{
+	if (ctx->csum_variant & 16u)
+		return 1;
+	if (ctx->csum_variant & 32u)
+		return 0;
+	return 2;
+}
+
 int ecg_csum_len(int type)
 {
 	switch (type) {
@@ -245,6 +259,48 @@ static void build_p5(const struct crc_def *d, uint64_t zeros, uint64_t *p5)
 	}
 }
 
+/* nibble tables (ecg_kabi.h q4 / a4): nibble t covers bits 4t..4t+3 of the
+ * piece (q4, the piece followed by `zeros` zero bytes) or of the register
+ * shifted by n zero bytes (a4) */
+static void build_q4(const struct crc_def *d, uint64_t zeros, uint64_t *q4)
+{
+	const uint64_t sh = zeros ? crc_xpow8(d, zeros) : 0;
+	uint64_t basis[128];
+	unsigned char piece[16];
+
+	for (int k = 0; k < 128; k++) {
+		memset(piece, 0, sizeof(piece));
+		piece[k / 8] = (unsigned char)(1u << (k % 8));
+		basis[k] = crc_raw(d, piece, 16);
+		if (zeros)
+			basis[k] = crc_mulmod(d, basis[k], sh);
+	}
+	for (int t = 0; t < 32; t++)
+		for (int v = 0; v < 16; v++) {
+			uint64_t c = 0;
+
+			for (int b = 0; b < 4; b++)
+				if ((v >> b) & 1)
+					c ^= basis[4 * t + b];
+			q4[(size_t)t * 16 + v] = c;
+		}
+}
+
+static void build_a4(const struct crc_def *d, uint64_t n, uint64_t *a4)
+{
+	const uint64_t sh = crc_xpow8(d, n);
+
+	for (int t = 0; t < d->width / 4; t++)
+		for (int v = 0; v < 16; v++) {
+			uint64_t c = 0;
+
+			for (int b = 0; b < 4; b++)
+				if ((v >> b) & 1)
+					c ^= crc_mulmod(d, 1ull << (4 * t + b), sh);
+			a4[(size_t)t * 16 + v] = c;
+		}
+}
+
 static void build_a5(const struct crc_def *d, uint64_t n, uint64_t *a5)
 {
 	const uint64_t sh = crc_xpow8(d, n);
@@ -340,6 +396,15 @@ static void *build_crc_tables(const struct crc_def *d, size_t *bytes)
 	build_a5(d, ECG_CSUM_STRIDE, t + ECG_CSUM_OFF_A5_1K(nb));
 	build_a5(d, ECG_CSUM_GSTRIDE, t + ECG_CSUM_OFF_A5_256(nb));
 	build_a5(d, ECG_MMCS_STRIDE, t + ECG_CSUM_OFF_A5_4K(nb));
+	for (int u = 0; u < ECG_CSUM_P5U; u++) {
+		build_q4(d, (uint64_t)u * ECG_CSUM_STRIDE, t + ECG_CSUM_OFF_Q4_1K(nb) + (size_t)u * ECG_CSUM_NQ4);
+		build_q4(d, (uint64_t)u * ECG_CSUM_GSTRIDE, t + ECG_CSUM_OFF_Q4_256(nb) + (size_t)u * ECG_CSUM_NQ4);
+	}
+	build_a4(d, (uint64_t)ECG_CSUM_P5U * ECG_CSUM_STRIDE, t + ECG_CSUM_OFF_A4_4K(nb));
+	build_a4(d, (uint64_t)ECG_CSUM_P5U * ECG_CSUM_GSTRIDE, t + ECG_CSUM_OFF_A4_1K(nb));
+	for (int u = 0; u < ECG_MMCS_P5U; u++)
+		build_q4(d, (uint64_t)u * ECG_MMCS_STRIDE, t + ECG_CSUM_OFF_Q4_4K(nb) + (size_t)u * ECG_CSUM_NQ4);
+	build_a4(d, (uint64_t)ECG_MMCS_P5U * ECG_MMCS_STRIDE, t + ECG_CSUM_OFF_A4_32K(nb));
 
 	*bytes = n * (size_t)es;
 	if (es == 8)
@@ -655,7 +720,7 @@ int ecg_csum_extents(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_
 		const int group = shape == 3 || (shape == 0 && !split && steps <= 8);
 
 		prm.variant = split ? 2 : group ? 3 : 1;
-		prm.byte_tables = use_byte_tables(ctx, type, 0);
+		prm.byte_tables = standalone_tables(ctx);
 		for (int c = 0; split && c < 3; c++) {
 			prm.split_m[c] = ECG_CSUM_STEPS(lens[c]);
 			split_shifts(ctx, type, prm.split_m[c], prm.split_sh[c]);

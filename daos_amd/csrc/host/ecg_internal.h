@@ -158,6 +158,16 @@ int ecg_trace_active(void);
 
 /* context helpers (ecg_core.c) */
 int ecg_ctx_enter(ecg_ctx_t *ctx);
+
+/* NUMA placement (ecg_numa.c); the cpu_set_t helpers need _GNU_SOURCE in the
+ * including file */
+int ecg_numa_enabled(void);
+#ifdef _GNU_SOURCE
+#include <sched.h>
+int ecg_numa_node_cpus(int node, cpu_set_t *set);
+int ecg_numa_bind_thread(int device, cpu_set_t *saved);
+void ecg_numa_restore_thread(const cpu_set_t *saved);
+#endif
 hipStream_t ecg_pick_stream(ecg_ctx_t *ctx, void *stream);
 
 #endif

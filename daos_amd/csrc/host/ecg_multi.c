@@ -9,11 +9,13 @@
  * ref:src/object/srv_obj_migrate.c:1116-1177) have no cross-stripe data, so
  * the shards never talk to each other.
  */
+#define _GNU_SOURCE
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "../../../include/ecg_multi.h"
+#include "../../../include/ecg_csum.h"
 #include "ecg_internal.h"
 
 struct mjob {
@@ -23,16 +25,28 @@ struct mjob {
 	uint32_t S;			/* host ops: the whole batch */
 	const uint32_t *nstripes;	/* device ops: per shard */
 	const void *const *src;
+	const void *const *src2;	/* updates: new cells (src = old cells) */
 	void *const *dst;
+	void *const *aux;		/* checksum outputs per shard */
 	const void *hsrc;
 	void *hdst;
-	int64_t s1, s2, s3;
-	const uint32_t *err;
+	int64_t s1, s2, s3, s4;
+	const uint32_t *err;		/* erasures; updates: updated cell indices */
 	uint32_t chunk;
 	unsigned flags;
+	/* checksums */
+	int csum_type;
+	uint64_t chunksize, rec_size;
+	/* parity-shard rebuild */
+	uint32_t oc_id, shard;
+	uint64_t e_len, offset, size;
+	int encode;
+	ecg_migrate_piece_t *pieces;
+	const uint32_t *first;		/* per shard: first piece index, [n + 1] */
 };
 
-enum { MOP_ENCODE, MOP_RECOVER, MOP_SYNC, MOP_ENCODE_HOST, MOP_RECOVER_HOST };
+enum { MOP_NOP, MOP_ENCODE, MOP_RECOVER, MOP_SYNC, MOP_ENCODE_HOST, MOP_RECOVER_HOST, MOP_ENCODE_CSUM,
+       MOP_RECOVER_CSUM, MOP_UPDATE, MOP_MIGRATE };
 
 struct mworker {
 	struct ecg_multi *m;
@@ -40,6 +54,7 @@ struct mworker {
 	ecg_ctx_t *ctx;
 	pthread_t th;
 	int started;
+	int numa_node;		/* node the worker runs on, -1 = not pinned */
 	int rc;
 	char err[256];		/* the shard's ecg_strerror() when rc != 0 */
 };
@@ -103,6 +118,8 @@ static int run_one(struct ecg_multi *m, struct mworker *w)
 	int rc = 0;
 
 	switch (j->op) {
+	case MOP_NOP:
+		return 0;
 	case MOP_ENCODE:
 		if (j->nstripes[w->idx] == 0)
 			return 0;
@@ -115,6 +132,43 @@ static int run_one(struct ecg_multi *m, struct mworker *w)
 		rc = ecg_recover(ctx, j->k, j->p, j->C, j->nstripes[w->idx], j->dst[w->idx], j->s1,
 				 j->err, j->nerrs, NULL);
 		break;
+	case MOP_ENCODE_CSUM:
+		if (j->nstripes[w->idx] == 0)
+			return 0;
+		rc = ecg_encode_csum(ctx, j->k, j->p, j->C, j->nstripes[w->idx], j->src[w->idx], j->s1,
+				     j->dst[w->idx], j->s2, j->s3, j->csum_type, j->chunksize, j->rec_size,
+				     j->aux[w->idx], NULL);
+		break;
+	case MOP_RECOVER_CSUM:
+		if (j->nstripes[w->idx] == 0)
+			return 0;
+		rc = ecg_recover_csum(ctx, j->k, j->p, j->C, j->nstripes[w->idx], j->dst[w->idx], j->s1, j->err,
+				      j->nerrs, j->csum_type, j->chunksize, j->rec_size, j->aux[w->idx], NULL);
+		break;
+	case MOP_UPDATE:
+		if (j->nstripes[w->idx] == 0)
+			return 0;
+		rc = ecg_update(ctx, j->k, j->p, j->C, j->nstripes[w->idx], j->nerrs, j->err, j->src[w->idx],
+				j->src2[w->idx], j->s4, j->dst[w->idx], j->s2,
+				j->s3, NULL);
+		break;
+	case MOP_MIGRATE: {
+		uint64_t off = 0, sz = 0;
+		uint32_t got = 0, cap = j->first[w->idx + 1] - j->first[w->idx];
+
+		(void)ecg_multi_migrate_range(m, j->oc_id, j->e_len, j->rec_size, j->offset, j->size, j->encode,
+					      w->idx, &off, &sz);
+		if (sz == 0)
+			return 0;
+		rc = ecg_migrate_update_parity(ctx, j->oc_id, j->e_len, j->rec_size, j->shard, j->src[w->idx], off,
+					       sz, j->encode, j->csum_type, j->chunksize, j->dst[w->idx],
+					       j->aux ? j->aux[w->idx] : NULL, j->pieces + j->first[w->idx], cap,
+					       &got, NULL);
+		if (rc == 0 && got != cap)
+			rc = ecg_fail(-ECG_DER_INVAL, "multi_migrate: shard %d cut %u pieces, planned %u", w->idx,
+				      got, cap);
+		break;
+	}
 	case MOP_SYNC:
 		return ecg_stream_sync(ctx, NULL);
 	case MOP_ENCODE_HOST:
@@ -146,6 +200,9 @@ static void *worker_main(void *arg)
 	struct ecg_multi *m = w->m;
 	uint64_t seen = 0;
 
+	/* on the CPUs of the device's NUMA node: the shard's host-side copies
+	 * and staging then use the memory and PCIe root of its own socket */
+	w->numa_node = ecg_numa_bind_thread(ecg_ctx_device(w->ctx), NULL);
 	pthread_mutex_lock(&m->lock);
 	for (;;) {
 		while (!m->stop && m->gen == seen)
@@ -250,6 +307,10 @@ int ecg_multi_create(const int *devices, int n, ecg_multi_t **out)
 		else
 			m->w[i].started = 1;
 	}
+	if (rc == 0) {		/* every worker has started (and bound itself to its node) */
+		m->job = (struct mjob){.op = MOP_NOP};
+		rc = run_all(m);
+	}
 	if (rc) {
 		ecg_multi_destroy(m);
 		return rc;
@@ -261,6 +322,11 @@ int ecg_multi_create(const int *devices, int n, ecg_multi_t **out)
 int ecg_multi_count(const ecg_multi_t *m)
 {
 	return m ? m->n : 0;
+}
+
+int ecg_multi_numa_node(const ecg_multi_t *m, int i)
+{
+	return m && i >= 0 && i < m->n ? m->w[i].numa_node : -1;
 }
 
 ecg_ctx_t *ecg_multi_ctx(ecg_multi_t *m, int i)
@@ -363,5 +429,147 @@ int ecg_multi_recover_host(ecg_multi_t *m, int k, int p, uint64_t C, uint32_t S,
 			       .err = err_list, .nerrs = nerrs, .chunk = chunk};
 	rc = run_all(m);
 	pthread_mutex_unlock(&m->call);
+	return rc;
+}
+
+/* ---- rebuild / aggregation ops ------------------------------------------- */
+int ecg_multi_encode_csum(ecg_multi_t *m, int k, int p, uint64_t C, const uint32_t *nstripes,
+			  const void *const *data, int64_t dstride, void *const *parity, int64_t pcell,
+			  int64_t pstripe, int type, uint64_t chunksize, uint64_t rec_size, void *const *csums,
+			  unsigned flags)
+{
+	int rc = check_common(m, k, p);
+
+	if (rc)
+		return rc;
+	if (nstripes == NULL || data == NULL || parity == NULL || csums == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "multi_encode_csum: NULL array");
+	pthread_mutex_lock(&m->call);
+	m->job = (struct mjob){.op = MOP_ENCODE_CSUM, .k = k, .p = p, .C = C, .nstripes = nstripes,
+			       .src = data, .dst = parity, .aux = csums, .s1 = dstride, .s2 = pcell,
+			       .s3 = pstripe, .csum_type = type, .chunksize = chunksize, .rec_size = rec_size,
+			       .flags = flags};
+	rc = run_all(m);
+	pthread_mutex_unlock(&m->call);
+	return rc;
+}
+
+int ecg_multi_recover_csum(ecg_multi_t *m, int k, int p, uint64_t C, const uint32_t *nstripes,
+			   void *const *stripes, int64_t stride, const uint32_t *err_list, int nerrs, int type,
+			   uint64_t chunksize, uint64_t rec_size, void *const *csums, unsigned flags)
+{
+	int rc = check_common(m, k, p);
+
+	if (rc)
+		return rc;
+	if (nstripes == NULL || stripes == NULL || err_list == NULL || csums == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "multi_recover_csum: NULL array");
+	if (nerrs > p)
+		return ecg_fail(-ECG_DER_DATA_LOSS, "multi_recover_csum: %d erasures > p=%d", nerrs, p);
+	pthread_mutex_lock(&m->call);
+	m->job = (struct mjob){.op = MOP_RECOVER_CSUM, .k = k, .p = p, .C = C, .nstripes = nstripes,
+			       .dst = stripes, .aux = csums, .s1 = stride, .err = err_list, .nerrs = nerrs,
+			       .csum_type = type, .chunksize = chunksize, .rec_size = rec_size, .flags = flags};
+	rc = run_all(m);
+	pthread_mutex_unlock(&m->call);
+	return rc;
+}
+
+int ecg_multi_update(ecg_multi_t *m, int k, int p, uint64_t C, const uint32_t *nstripes, int nupd,
+		     const uint32_t *cell_idx, const void *const *old_cells, const void *const *new_cells,
+		     int64_t upd_stripe_stride, void *const *parity, int64_t pcell, int64_t pstripe,
+		     unsigned flags)
+{
+	int rc = check_common(m, k, p);
+
+	if (rc)
+		return rc;
+	if (nstripes == NULL || cell_idx == NULL || old_cells == NULL || new_cells == NULL || parity == NULL ||
+	    nupd < 1 || nupd > k)
+		return ecg_fail(-ECG_DER_INVAL, "multi_update: bad argument");
+	pthread_mutex_lock(&m->call);
+	m->job = (struct mjob){.op = MOP_UPDATE, .k = k, .p = p, .C = C, .nstripes = nstripes,
+			       .src = old_cells, .src2 = new_cells, .dst = parity, .err = cell_idx,
+			       .nerrs = nupd, .s4 = upd_stripe_stride, .s2 = pcell,
+			       .s3 = pstripe, .flags = flags};
+	rc = run_all(m);
+	pthread_mutex_unlock(&m->call);
+	return rc;
+}
+
+/* Shard i's records of a fetched range: whole split units (stripes when
+ * encoding, else cells -- the walk's own cut points, so every shard's pieces
+ * are exactly the pieces the single walk cuts there) in contiguous runs;
+ * shard 0 also takes the partial head, the last shard the partial tail. */
+int ecg_multi_migrate_range(const ecg_multi_t *m, uint32_t oc_id, uint64_t e_len, uint64_t iod_size,
+			    uint64_t offset, uint64_t size, int encode, int i, uint64_t *off, uint64_t *sz)
+{
+	uint64_t unit, b0, bl, end = offset + size, units, base, extra, f, c, lo, hi;
+	int k, p, rc;
+
+	if (m == NULL || i < 0 || i >= m->n || off == NULL || sz == NULL || e_len == 0 || iod_size == 0)
+		return ecg_fail(-ECG_DER_INVAL, "multi_migrate_range: bad argument");
+	rc = ecg_obj_ec_class_kp(oc_id, &k, &p);
+	if (rc)
+		return rc;
+	unit = encode ? (uint64_t)k * e_len : e_len;
+	b0 = (offset + unit - 1) / unit * unit;
+	bl = end / unit * unit;
+	if (b0 >= bl) {				/* no whole unit: shard 0 walks it all */
+		*off = offset;
+		*sz = i == 0 ? size : 0;
+		return 0;
+	}
+	units = (bl - b0) / unit;
+	base = units / (uint64_t)m->n;
+	extra = units % (uint64_t)m->n;
+	c = base + ((uint64_t)i < extra ? 1 : 0);
+	f = base * (uint64_t)i + ((uint64_t)i < extra ? (uint64_t)i : extra);
+	lo = i == 0 ? offset : b0 + f * unit;
+	hi = i == m->n - 1 ? end : b0 + (f + c) * unit;
+	*off = lo;
+	*sz = hi - lo;
+	return 0;
+}
+
+int ecg_multi_migrate_update_parity(ecg_multi_t *m, uint32_t oc_id, uint64_t e_len, uint64_t iod_size,
+				    uint32_t shard, const void *const *buffers, uint64_t offset, uint64_t size,
+				    int encode, int csum_type, uint64_t chunksize, void *const *parity_out,
+				    void *const *csums_out, ecg_migrate_piece_t *pieces, uint32_t pieces_cap,
+				    uint32_t *npieces, uint32_t *shard_first, unsigned flags)
+{
+	uint32_t first[ECG_MULTI_MAX + 1];
+	int i, rc;
+
+	if (m == NULL || buffers == NULL || parity_out == NULL || pieces == NULL || npieces == NULL ||
+	    (csum_type && csums_out == NULL))
+		return ecg_fail(-ECG_DER_INVAL, "multi_migrate: NULL argument");
+	first[0] = 0;
+	for (i = 0; i < m->n; i++) {		/* plan: where each shard's pieces go */
+		uint64_t off, sz;
+		uint32_t n = 0;
+
+		rc = ecg_multi_migrate_range(m, oc_id, e_len, iod_size, offset, size, encode, i, &off, &sz);
+		if (rc == 0 && sz)
+			rc = ecg_migrate_plan_size(oc_id, e_len, iod_size, off, sz, encode, csum_type, chunksize, &n,
+						   NULL, NULL);
+		if (rc)
+			return rc;
+		first[i + 1] = first[i] + n;
+	}
+	if (first[m->n] > pieces_cap)
+		return ecg_fail(-ECG_DER_REC2BIG, "multi_migrate: %u pieces > capacity %u", first[m->n], pieces_cap);
+	pthread_mutex_lock(&m->call);
+	m->job = (struct mjob){.op = MOP_MIGRATE, .oc_id = oc_id, .e_len = e_len, .rec_size = iod_size,
+			       .shard = shard, .src = buffers, .offset = offset, .size = size, .encode = encode,
+			       .csum_type = csum_type, .chunksize = chunksize, .dst = parity_out,
+			       .aux = csums_out, .pieces = pieces, .first = first, .flags = flags};
+	rc = run_all(m);
+	pthread_mutex_unlock(&m->call);
+	if (rc == 0) {
+		*npieces = first[m->n];
+		if (shard_first)
+			memcpy(shard_first, first, sizeof(uint32_t) * (size_t)(m->n + 1));
+	}
 	return rc;
 }

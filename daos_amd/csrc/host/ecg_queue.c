@@ -36,6 +36,7 @@
  * (ecg_queue_create_multi): each slot's staging, stream and launches live on
  * its own device.
  */
+#define _GNU_SOURCE
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -492,8 +493,18 @@ static int queue_create(ecg_ctx_t *const *ctxs, int nctx, const ecg_queue_attr_t
 		}
 		s->bytes = q->slot_bytes;
 		e = hipSetDevice(s->ctx->device);
-		if (e == hipSuccess)
-			e = hipHostMalloc((void **)&s->host, s->bytes, hipHostMallocDefault);
+		if (e == hipSuccess) {
+			/* the slot's pinned staging on its device's NUMA node: the
+			 * pages are touched (pinned) by this thread while it runs
+			 * there, and NumaUser keeps the runtime from placing them */
+			cpu_set_t saved;
+			const int node = ecg_numa_bind_thread(s->ctx->device, &saved);
+
+			e = hipHostMalloc((void **)&s->host, s->bytes,
+					  hipHostMallocDefault | (node >= 0 ? hipHostMallocNumaUser : 0));
+			if (node >= 0)
+				ecg_numa_restore_thread(&saved);
+		}
 		if (e == hipSuccess)
 			e = hipMalloc((void **)&s->dev, s->bytes);
 		if (e == hipSuccess)

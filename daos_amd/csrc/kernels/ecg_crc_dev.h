@@ -214,6 +214,149 @@ __device__ __forceinline__ void stage5u(T *s5, const T *gt, int p5x_off, int a5_
 		      : i < U * P ? gt[p5x_off + i - P] : gt[a5_off + i - U * P];
 }
 
+// ---- nibble tables (ecg_kabi.h q4 / a4): a 16-byte piece is 32 nibbles, each
+// indexing a 16-entry table (conflict-free like the 5-bit tables: 16 entries
+// of 4 or 8 bytes sit on distinct banks).  The nibbles are byte-aligned, so a
+// lookup's LDS address is ONE SDWA instruction on a byte of a pre-masked word
+// (v_lshlrev_b32_sdwa: low nibble << log2(entry bytes); v_and_b32_sdwa: the
+// high nibble already shifted into place) and the table's own offset rides in
+// the ds_read's immediate offset -- 10 VALU per 8 lookups of a dword, against
+// 2 per lookup (shift + and) for 5-bit fields.  The CRC kernels are VALU-issue
+// bound (profiles/r03/crc_sq), so this is the count that matters.
+template <int B, int ES>
+__device__ __forceinline__ uint32_t nib_lo_addr(uint32_t lo)
+{
+	uint32_t r;
+	static_assert(B >= 0 && B < 4 && (ES == 2 || ES == 3), "byte select / entry size");
+	if constexpr (B == 0)
+		asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+		    : "=v"(r) : "i"(ES), "v"(lo));
+	else if constexpr (B == 1)
+		asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+		    : "=v"(r) : "i"(ES), "v"(lo));
+	else if constexpr (B == 2)
+		asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+		    : "=v"(r) : "i"(ES), "v"(lo));
+	else
+		asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
+		    : "=v"(r) : "i"(ES), "v"(lo));
+	return r;
+}
+
+template <int B>
+__device__ __forceinline__ uint32_t nib_hi_addr(uint32_t hs, uint32_t mask)
+{
+	uint32_t r;
+	static_assert(B >= 0 && B < 4, "byte select");
+	if constexpr (B == 0)
+		asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+		    : "=v"(r) : "s"(mask), "v"(hs));
+	else if constexpr (B == 1)
+		asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+		    : "=v"(r) : "s"(mask), "v"(hs));
+	else if constexpr (B == 2)
+		asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+		    : "=v"(r) : "s"(mask), "v"(hs));
+	else
+		asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
+		    : "=v"(r) : "s"(mask), "v"(hs));
+	return r;
+}
+
+template <int W, int U_ = ECG_CSUM_P5U>
+struct f4u {
+	static constexpr int U = U_;
+	static constexpr int NF = 32;		// nibbles of a piece
+	static constexpr int NA = W / 4;	// nibbles of the register
+	static constexpr int N = (U * NF + NA) * 16;
+};
+
+// entry of table `tab` (16 entries each) at LDS byte address `a` (an SDWA
+// result) from q: the constant part folds into the ds_read offset
+template <typename T>
+__device__ __forceinline__ T nib_ent(const T *q, int tab, uint32_t a)
+{
+	return *(const T *)((const char *)(q + 16 * tab) + a);
+}
+
+// XOR into c the 8 lookups of dword x (nibbles 8j .. 8j+7 of table group t0)
+template <typename T>
+__device__ __forceinline__ T nib_dword(T c, uint32_t x, const T *q, int t0, uint32_t hmask)
+{
+	constexpr int ES = sizeof(T) == 8 ? 3 : 2;
+	const uint32_t lo = x & 0x0F0F0F0Fu;
+	const uint32_t hs = x >> (4 - ES);
+	c = x3(c, nib_ent(q, t0 + 0, nib_lo_addr<0, ES>(lo)), nib_ent(q, t0 + 1, nib_hi_addr<0>(hs, hmask)));
+	c = x3(c, nib_ent(q, t0 + 2, nib_lo_addr<1, ES>(lo)), nib_ent(q, t0 + 3, nib_hi_addr<1>(hs, hmask)));
+	c = x3(c, nib_ent(q, t0 + 4, nib_lo_addr<2, ES>(lo)), nib_ent(q, t0 + 5, nib_hi_addr<2>(hs, hmask)));
+	c = x3(c, nib_ent(q, t0 + 6, nib_lo_addr<3, ES>(lo)), nib_ent(q, t0 + 7, nib_hi_addr<3>(hs, hmask)));
+	return c;
+}
+
+// high-nibble mask for nib_dword: (x >> (4 - ES)) & mask = high nibble << ES
+template <typename T>
+__device__ __forceinline__ uint32_t nib_hmask()
+{
+	return sizeof(T) == 8 ? 0x78u : 0x3Cu;
+}
+
+// U pieces d[0..U-1] (in stream order) folded into acc with the nibble
+// tables q4 (LDS: q4[U][32][16], then a4[W/4][16] of the U-stride shift)
+template <int W, int U, typename T>
+__device__ __forceinline__ T horner4u(T acc, const uint32_t (*d)[4], const T *q4, uint32_t hmask)
+{
+	const T *a4 = q4 + U * 32 * 16;
+	T c = 0;
+
+#pragma unroll
+	for (int h = 0; h < (W + 31) / 32; h++) {
+		const uint32_t x = W == 16 ? (uint32_t)acc & 0xFFFFu : (uint32_t)((uint64_t)acc >> (32 * h));
+		if constexpr (W == 16) {	// 4 nibbles: bytes 0, 1 of the low half
+			constexpr int ES = sizeof(T) == 8 ? 3 : 2;
+			const uint32_t lo = x & 0x0F0Fu, hs = x >> (4 - ES);
+			c = x3(c, nib_ent(a4, 0, nib_lo_addr<0, ES>(lo)), nib_ent(a4, 1, nib_hi_addr<0>(hs, hmask)));
+			c = x3(c, nib_ent(a4, 2, nib_lo_addr<1, ES>(lo)), nib_ent(a4, 3, nib_hi_addr<1>(hs, hmask)));
+		} else {
+			c = nib_dword(c, x, a4, 8 * h, hmask);
+		}
+	}
+#pragma unroll
+	for (int u = 0; u < U; u++) {
+		const T *p4 = q4 + (U - 1 - u) * 32 * 16;
+#pragma unroll
+		for (int j = 0; j < 4; j++)
+			c = nib_dword(c, d[u][j], p4, 8 * j, hmask);
+	}
+	return c;
+}
+
+// stage q4 (positions 0..U-1 at gt + q4_off) and a4 (gt + a4_off) into LDS
+template <int W, int U, typename T>
+__device__ __forceinline__ void stage4u(T *s4, const T *gt, int q4_off, int a4_off, int nthreads)
+{
+	constexpr int P = U * 32 * 16;
+	for (int i = threadIdx.x; i < f4u<W, U>::N; i += nthreads)
+		s4[i] = i < P ? gt[q4_off + i] : gt[a4_off + i - P];
+}
+
+// lane value * x^(8*16*(63-lane)) for reflected CRCs, nibble by nibble: the
+// per-lane tables nibl[16][64] are read from the table image in HBM/L2 (they
+// depend only on the value, so all W/4 loads issue together), the 4-bit
+// reduction r4 from LDS -- W/4 steps instead of mulmod's W bit steps
+template <int W, typename T>
+__device__ __forceinline__ T lane_mul_nib(T x, const T *gnib, const T *r4, uint32_t lane)
+{
+	T n[W / 4];
+#pragma unroll
+	for (int i = 0; i < W / 4; i++)
+		n[i] = gnib[(((uint32_t)(x >> (4 * i))) & 15u) * 64u + lane];
+	T u = 0;
+#pragma unroll
+	for (int i = 0; i < W / 4; i++)
+		u = (u >> 4) ^ r4[(uint32_t)u & 15u] ^ n[i];
+	return u;
+}
+
 // register -> register shifted by the a5 table's fixed number of zero bytes
 template <int W, typename T>
 __device__ __forceinline__ T lin_map5(T c, const T *a5)

@@ -72,100 +72,173 @@ __device__ __forceinline__ void chunk_geom(const ecg_csum_params_t &p, uint64_t 
 	base = p.src + (int64_t)e * p.ext_stride + off;
 }
 
+// CRC table kinds (ecg_kabi.h): TK_5 conflict-free 5-bit fields, TK_B8 byte
+// tables (the A/B variant), TK_4 nibble fields addressed by SDWA byte selects
+// (the default: fewest VALU per lookup, and the CRC kernels are VALU-issue
+// bound -- profiles/r03/crc_sq)
+constexpr int TK_5 = 0, TK_B8 = 1, TK_4 = 2;
+
 // Horner steps of a lane's accumulator over the UN pieces d[0..UN-1] (those
-// with i + u < m): byte tables (B8: sl, sh), one step per piece, acc * x^(8 *
-// stride) ^ crc(piece); 5-bit tables (s5 = positional q5 then a5), one step
-// per UN = ECG_CSUM_P5U pieces (m is then a multiple of UN).
-template <int W, bool REFL, bool B8, int UN, typename T>
+// with i + u < m): byte tables (sl, sh), one step per piece, acc * x^(8 *
+// stride) ^ crc(piece); 5-bit / nibble tables (s5 = positional q then a),
+// one step per UN = ECG_CSUM_P5U pieces (m is then a multiple of UN).
+template <int W, bool REFL, int TK, int UN, typename T>
 __device__ __forceinline__ T horner(T acc, const uint32_t (*d)[4], int64_t i, int64_t m, const T *s5,
 				    const T *sl, const T *sh)
 {
-	if constexpr (B8) {
+	if constexpr (TK == TK_B8) {
 #pragma unroll
 		for (int u = 0; u < UN; u++)
 			if (i + u < m)
 				acc = lin_map<W>(acc, sh) ^ piece_crc<W, REFL>(d[u], sl);
 		return acc;
+	} else if constexpr (TK == TK_4) {
+		static_assert(UN == ECG_CSUM_P5U, "nibble path steps ECG_CSUM_P5U pieces at a time");
+		return horner4u<W, UN>(acc, d, s5, nib_hmask<T>());
 	} else {
 		static_assert(UN == ECG_CSUM_P5U, "5-bit path steps ECG_CSUM_P5U pieces at a time");
 		return horner5u<W>(acc, d, s5);
 	}
 }
 
-// LDS images of one kernel: the positional 5-bit tables (q5, a5), or (B8) the
-// byte tables; UN pieces in flight per lane
-template <int W, bool B8>
+// LDS images of one kernel: the positional 5-bit or nibble tables (q, a), or
+// the byte tables; UN pieces in flight per lane
+template <int W, int TK>
 struct crc_lds {
 	using T = typename reg<W>::T;
 	static constexpr int NB = W / 8;
-	static constexpr int N5 = B8 ? 1 : f5u<W>::N;
-	static constexpr int NSL = B8 ? NB * 256 : 1;
-	static constexpr int UN = B8 ? CS_UNROLL : ECG_CSUM_P5U;
+	static constexpr int N5 = TK == TK_B8 ? 1 : TK == TK_4 ? f4u<W>::N : f5u<W>::N;
+	static constexpr int NSL = TK == TK_B8 ? NB * 256 : 1;
+	static constexpr int UN = TK == TK_B8 ? CS_UNROLL : ECG_CSUM_P5U;
 };
 
+// positional tables of stride `q_off` (5-bit p5x / nibble q4) and the
+// U-stride shift into LDS
+template <int W, int TK, typename T>
+__device__ __forceinline__ void stage_tables(T *s5, T *sl, T *sh, const T *gt, int p5x_off, int a5_off,
+					     int q4_off, int a4_off, int nthreads)
+{
+	constexpr int NB = W / 8;
+	if constexpr (TK == TK_B8) {
+		for (int i = threadIdx.x; i < NB * 256; i += nthreads) {
+			sl[i] = gt[i];
+			sh[i] = gt[NB * 256 + i];
+		}
+	} else if constexpr (TK == TK_4) {
+		stage4u<W, ECG_CSUM_P5U>(s5, gt, q4_off, a4_off, nthreads);
+	} else {
+		stage5u<W>(s5, gt, p5x_off, a5_off, nthreads);
+	}
+}
+
+// the lane's final shift x^(8*16*(G-1-l)) (G lanes per chunk; klane = its
+// k64 entry): reflected CRCs from the nibl tables (W/4 steps), else mulmod
+template <int W, bool REFL, typename T>
+__device__ __forceinline__ T lane_shift(T acc, T klane, const T *gt, const T *r4, uint32_t nib_lane, T poly)
+{
+	if constexpr (REFL)
+		return lane_mul_nib<W>(acc, gt + ECG_CSUM_OFF_NIBL(W / 8), r4, nib_lane);
+	else
+		return mulmod<W, REFL>(klane, acc, poly);
+}
+
 // lane steps of a chunk of nq pieces, `per` pieces per step
-template <bool B8>
+template <int TK>
 __device__ __forceinline__ int64_t lane_steps(int64_t nq, int64_t per)
 {
 	const int64_t m = (nq + per - 1) / per;
-	return B8 ? m : (m + ECG_CSUM_P5U - 1) / ECG_CSUM_P5U * ECG_CSUM_P5U;
+	return TK == TK_B8 ? m : (m + ECG_CSUM_P5U - 1) / ECG_CSUM_P5U * ECG_CSUM_P5U;
 }
 
-template <int W, bool REFL, bool ALIGNED, bool B8>
+// the U pieces of lane step i (pieces (i+u)*64 + lane - z): `first` masks
+// the zero prefix (q < 0) and folds the initial register into piece 0; later
+// steps are unconditional (q > 0 for i >= ECG_CSUM_P5U since z < 64 U)
+template <int UN, int W, bool ALIGNED, bool FIRST, typename T>
+__device__ __forceinline__ void load_step(const uint8_t *base, int64_t i, int64_t stride_pieces, int64_t lane_q0,
+					  int64_t m, T init, uint32_t (*d)[4])
+{
+#pragma unroll
+	for (int u = 0; u < UN; u++) {
+		const int64_t q = (i + u) * stride_pieces + lane_q0;
+		if constexpr (FIRST) {
+			if (i + u < m && q >= 0) {
+				load16<ALIGNED>(base + 16 * q, d[u]);
+				if (q == 0) {	// fold the initial register into the first bytes
+					d[u][0] ^= (uint32_t)init;
+					if constexpr (W == 64)
+						d[u][1] ^= (uint32_t)((uint64_t)init >> 32);
+				}
+			} else {
+				d[u][0] = d[u][1] = d[u][2] = d[u][3] = 0;
+			}
+		} else {
+			load16<ALIGNED>(base + 16 * q, d[u]);
+		}
+	}
+}
+
+// chunk g's geometry with a 32-bit division when the counts allow (the
+// 64-bit one expands to ~100 VALU per chunk)
+__device__ __forceinline__ void chunk_geom_fast(const ecg_csum_params_t &p, uint64_t g, uint64_t &off,
+						uint64_t &len, const uint8_t *&base)
+{
+	if (((g | p.nchunks) >> 32) == 0) {
+		const uint32_t e = (uint32_t)g / p.nchunks, c = (uint32_t)g - e * p.nchunks;
+
+		off = c == 0 ? 0 : p.first_bytes + (uint64_t)(c - 1) * p.chunk_bytes;
+		len = c == 0 ? p.first_bytes : p.chunk_bytes;
+		if (off + len > p.ext_bytes)
+			len = p.ext_bytes - off;
+		base = p.src + (int64_t)e * p.ext_stride + off;
+	} else {
+		chunk_geom(p, g, off, len, base);
+	}
+}
+
+template <int W, bool REFL, bool ALIGNED, int TK>
 __global__ __launch_bounds__(CS_BLOCK) void ecg_crc_kernel(ecg_csum_params_t p)
 {
 	using T = typename reg<W>::T;
-	using L = crc_lds<W, B8>;
+	using L = crc_lds<W, TK>;
 	constexpr int NB = W / 8;
 	__shared__ T s5[L::N5];
 	__shared__ T sl[L::NSL];
 	__shared__ T sh[L::NSL];
+	__shared__ T r4[REFL ? 16 : 1];
 	const T *gt = (const T *)p.tbl;
 
-	if constexpr (B8) {
-		for (int i = threadIdx.x; i < NB * 256; i += CS_BLOCK) {
-			sl[i] = gt[i];
-			sh[i] = gt[NB * 256 + i];
-		}
-	} else {
-		stage5u<W>(s5, gt, ECG_CSUM_OFF_P5X_1K(NB), ECG_CSUM_OFF_A5_4K(NB), CS_BLOCK);
-	}
+	stage_tables<W, TK>(s5, sl, sh, gt, ECG_CSUM_OFF_P5X_1K(NB), ECG_CSUM_OFF_A5_4K(NB), ECG_CSUM_OFF_Q4_1K(NB),
+			    ECG_CSUM_OFF_A4_4K(NB), CS_BLOCK);
+	if (REFL && threadIdx.x < 16)
+		r4[threadIdx.x] = gt[ECG_CSUM_OFF_R4(NB) + threadIdx.x];
 	const int lane = threadIdx.x & 63;
-	const T klane = gt[2 * NB * 256 + lane];
+	const T klane = REFL ? (T)0 : gt[2 * NB * 256 + lane];
 	const T poly = (T)p.poly, init = (T)p.init, xorout = (T)p.xorout;
 	__syncthreads();
 
 	const uint64_t total = (uint64_t)p.n_ext * p.nchunks;
-	for (uint64_t g = (uint64_t)blockIdx.x * CS_WAVES + (threadIdx.x >> 6); g < total;
-	     g += (uint64_t)gridDim.x * CS_WAVES) {
+	const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	for (uint64_t g = (uint64_t)blockIdx.x * CS_WAVES + wv; g < total; g += (uint64_t)gridDim.x * CS_WAVES) {
 		uint64_t off, len;
 		const uint8_t *base;
 
-		chunk_geom(p, g, off, len, base);
+		chunk_geom_fast(p, g, off, len, base);
 		const int64_t nq = (int64_t)(len / 16);
-		const int64_t m = lane_steps<B8>(nq, 64);
+		const int64_t m = lane_steps<TK>(nq, 64);
 		const int64_t z = m * 64 - nq;
 		T acc = 0;
 
-		for (int64_t i = 0; i < m; i += L::UN) {
+		if (m > 0) {
 			uint32_t d[L::UN][4];
-#pragma unroll
-			for (int u = 0; u < L::UN; u++) {
-				const int64_t q = (i + u) * 64 + lane - z;
-				if (i + u < m && q >= 0) {
-					load16<ALIGNED>(base + 16 * q, d[u]);
-					if (q == 0) {	// fold the initial register into the first bytes
-						d[u][0] ^= (uint32_t)init;
-						if constexpr (W == 64)
-							d[u][1] ^= (uint32_t)((uint64_t)init >> 32);
-					}
-				} else {
-					d[u][0] = d[u][1] = d[u][2] = d[u][3] = 0;
-				}
+
+			load_step<L::UN, W, ALIGNED, true>(base, 0, 64, lane - z, m, init, d);
+			acc = horner<W, REFL, TK, L::UN>(acc, d, 0, m, s5, sl, sh);
+			for (int64_t i = L::UN; i < m; i += L::UN) {
+				load_step<L::UN, W, ALIGNED, TK == TK_B8>(base, i, 64, lane - z, m, init, d);	// byte tables: m need not be a multiple of UN
+				acc = horner<W, REFL, TK, L::UN>(acc, d, i, m, s5, sl, sh);
 			}
-			acc = horner<W, REFL, B8, L::UN>(acc, d, i, m, s5, sl, sh);
 		}
-		acc = mulmod<W, REFL>(klane, acc, poly);
+		acc = lane_shift<W, REFL>(acc, klane, gt, r4, (uint32_t)lane, poly);
 		acc = wave_xor(acc);
 		if (lane == 0) {
 			T crc = nq == 0 ? init : acc;
@@ -198,27 +271,31 @@ __device__ __forceinline__ T shfl_xor_t(T v, int s)
 // reads 4 x 256 B contiguous, Horner-steps by G*16 bytes (sh256 table), and
 // the group reduces with shuffles after multiplying by x^(8*16*(G-1-l)) =
 // k64[64 - G + l].  Otherwise as ecg_crc_kernel.
-template <int W, bool REFL, bool B8>
+template <int W, bool REFL, int TK>
 __global__ __launch_bounds__(CS_BLOCK) void ecg_crc_group_kernel(ecg_csum_params_t p)
 {
 	using T = typename reg<W>::T;
-	using L = crc_lds<W, B8>;
+	using L = crc_lds<W, TK>;
 	constexpr int NB = W / 8;
 	constexpr int G = ECG_CSUM_GLANES;
 	constexpr int GPW = 64 / G;		// chunks per wave
 	__shared__ T s5[L::N5];
 	__shared__ T sl[L::NSL];
 	__shared__ T sh[L::NSL];
+	__shared__ T r4[REFL ? 16 : 1];
 	const T *gt = (const T *)p.tbl;
 
-	if constexpr (B8) {
+	if constexpr (TK == TK_B8) {
 		for (int i = threadIdx.x; i < NB * 256; i += CS_BLOCK) {
 			sl[i] = gt[i];
 			sh[i] = gt[ECG_CSUM_OFF_SH256(NB) + i];
 		}
 	} else {
-		stage5u<W>(s5, gt, ECG_CSUM_OFF_P5X_256(NB), ECG_CSUM_OFF_A5_1K(NB), CS_BLOCK);
+		stage_tables<W, TK>(s5, sl, sh, gt, ECG_CSUM_OFF_P5X_256(NB), ECG_CSUM_OFF_A5_1K(NB),
+				    ECG_CSUM_OFF_Q4_256(NB), ECG_CSUM_OFF_A4_1K(NB), CS_BLOCK);
 	}
+	if (REFL && threadIdx.x < 16)
+		r4[threadIdx.x] = gt[ECG_CSUM_OFF_R4(NB) + threadIdx.x];
 	const int lane = threadIdx.x & 63, gl = lane % G;
 	const T klane = gt[ECG_CSUM_OFF_K64(NB) + 64 - G + gl];
 	const T poly = (T)p.poly, init = (T)p.init, xorout = (T)p.xorout;
@@ -236,31 +313,19 @@ __global__ __launch_bounds__(CS_BLOCK) void ecg_crc_group_kernel(ecg_csum_params
 		const uint8_t *base = p.src;
 
 		if (live)
-			chunk_geom(p, g, off, len, base);
+			chunk_geom_fast(p, g, off, len, base);
 		const int64_t nq = (int64_t)(len / 16);
-		const int64_t m = lane_steps<B8>(nq, G);
+		const int64_t m = lane_steps<TK>(nq, G);
 		const int64_t z = m * G - nq;
 		T acc = 0;
 
 		for (int64_t i = 0; i < m; i += L::UN) {
 			uint32_t d[L::UN][4];
-#pragma unroll
-			for (int u = 0; u < L::UN; u++) {
-				const int64_t q = (i + u) * G + gl - z;
-				if (i + u < m && q >= 0) {
-					load16<true>(base + 16 * q, d[u]);
-					if (q == 0) {
-						d[u][0] ^= (uint32_t)init;
-						if constexpr (W == 64)
-							d[u][1] ^= (uint32_t)((uint64_t)init >> 32);
-					}
-				} else {
-					d[u][0] = d[u][1] = d[u][2] = d[u][3] = 0;
-				}
-			}
-			acc = horner<W, REFL, B8, L::UN>(acc, d, i, m, s5, sl, sh);
+
+			load_step<L::UN, W, true, true>(base, i, G, gl - z, m, init, d);
+			acc = horner<W, REFL, TK, L::UN>(acc, d, i, m, s5, sl, sh);
 		}
-		acc = mulmod<W, REFL>(klane, acc, poly);
+		acc = lane_shift<W, REFL>(acc, klane, gt, r4, (uint32_t)(64 - G + gl), poly);
 #pragma unroll
 		for (int s = G / 2; s >= 1; s >>= 1)
 			acc ^= shfl_xor_t(acc, s);
@@ -288,26 +353,23 @@ __global__ __launch_bounds__(CS_BLOCK) void ecg_crc_group_kernel(ecg_csum_params
 // table entries of its set bits, one bit per lane, multiplied down the wave
 // in 6 butterfly steps -- and the waves' values are XORed through LDS (CRC
 // is linear: crc(A || B) = crc(A) * x^(8|B|) ^ crc(B) for zero registers).
-template <int W, bool REFL, int NW, bool B8>
+template <int W, bool REFL, int NW, int TK>
 __global__ __launch_bounds__(64 * NW) void ecg_crc_split_kernel(ecg_csum_params_t p)
 {
 	using T = typename reg<W>::T;
-	using L = crc_lds<W, B8>;
+	using L = crc_lds<W, TK>;
 	constexpr int NB = W / 8;
 	__shared__ T s5[L::N5];
 	__shared__ T sl[L::NSL];
 	__shared__ T sh[L::NSL];
 	__shared__ T part[NW];
+	__shared__ T r4[REFL ? 16 : 1];
 	const T *gt = (const T *)p.tbl;
 
-	if constexpr (B8) {
-		for (int i = threadIdx.x; i < NB * 256; i += 64 * NW) {
-			sl[i] = gt[i];
-			sh[i] = gt[NB * 256 + i];
-		}
-	} else {
-		stage5u<W>(s5, gt, ECG_CSUM_OFF_P5X_1K(NB), ECG_CSUM_OFF_A5_4K(NB), 64 * NW);
-	}
+	stage_tables<W, TK>(s5, sl, sh, gt, ECG_CSUM_OFF_P5X_1K(NB), ECG_CSUM_OFF_A5_4K(NB), ECG_CSUM_OFF_Q4_1K(NB),
+			    ECG_CSUM_OFF_A4_4K(NB), 64 * NW);
+	if (REFL && threadIdx.x < 16)
+		r4[threadIdx.x] = gt[ECG_CSUM_OFF_R4(NB) + threadIdx.x];
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 	const T klane = gt[2 * NB * 256 + lane];
 	const T one = REFL ? (T)((T)1 << (W - 1)) : (T)1;
@@ -320,7 +382,7 @@ __global__ __launch_bounds__(64 * NW) void ecg_crc_split_kernel(ecg_csum_params_
 		uint64_t off, len;
 		const uint8_t *base;
 
-		chunk_geom(p, g, off, len, base);
+		chunk_geom_fast(p, g, off, len, base);
 		static_assert(NW == ECG_CSUM_SPLIT_NW, "host split shifts assume ECG_CSUM_SPLIT_NW slices");
 		const int64_t nq = (int64_t)(len / 16);
 		const int64_t m = (int64_t)ECG_CSUM_STEPS((uint64_t)len);	// as the host's split_m
@@ -332,23 +394,11 @@ __global__ __launch_bounds__(64 * NW) void ecg_crc_split_kernel(ecg_csum_params_
 
 		for (int64_t i = i0; i < i1; i += L::UN) {
 			uint32_t d[L::UN][4];
-#pragma unroll
-			for (int u = 0; u < L::UN; u++) {
-				const int64_t q = (i + u) * 64 + lane - z;
-				if (i + u < i1 && q >= 0) {
-					load16<true>(base + 16 * q, d[u]);
-					if (q == 0) {	// fold the initial register into the first bytes
-						d[u][0] ^= (uint32_t)init;
-						if constexpr (W == 64)
-							d[u][1] ^= (uint32_t)((uint64_t)init >> 32);
-					}
-				} else {
-					d[u][0] = d[u][1] = d[u][2] = d[u][3] = 0;
-				}
-			}
-			acc = horner<W, REFL, B8, L::UN>(acc, d, i, i1, s5, sl, sh);
+
+			load_step<L::UN, W, true, true>(base, i, 64, lane - z, i1, init, d);
+			acc = horner<W, REFL, TK, L::UN>(acc, d, i, i1, s5, sl, sh);
 		}
-		acc = mulmod<W, REFL>(klane, acc, poly);
+		acc = lane_shift<W, REFL>(acc, klane, gt, r4, (uint32_t)lane, poly);
 		acc = wave_xor(acc);
 		// x^(8 * (m - i1) KiB): the host's constant for this chunk length,
 		// else the product of p2[j] over the set bits j (one bit per lane)
@@ -519,55 +569,70 @@ typedef void (*csum_fn_t)(ecg_csum_params_t);
 struct csum_entry {
 	uint32_t type;
 	bool aligned;
-	bool b8;		/* byte tables (the A/B variant), else 5-bit tables */
+	int tk;			/* CRC table kind (TK_*); adler32: 0 */
 	csum_fn_t fn;
 	const char *name;
 };
 
 const csum_entry g_csum[] = {
-	{1, true, false, ecg_crc_kernel<16, false, true, false>, "ecg_crc_kernel<crc16>"},
-	{1, false, false, ecg_crc_kernel<16, false, false, false>, "ecg_crc_kernel<crc16,bytes>"},
-	{2, true, false, ecg_crc_kernel<32, true, true, false>, "ecg_crc_kernel<crc32>"},
-	{2, false, false, ecg_crc_kernel<32, true, false, false>, "ecg_crc_kernel<crc32,bytes>"},
-	{3, true, false, ecg_crc_kernel<64, true, true, false>, "ecg_crc_kernel<crc64>"},
-	{3, false, false, ecg_crc_kernel<64, true, false, false>, "ecg_crc_kernel<crc64,bytes>"},
-	{1, true, true, ecg_crc_kernel<16, false, true, true>, "ecg_crc_kernel<crc16,alt>"},
-	{1, false, true, ecg_crc_kernel<16, false, false, true>, "ecg_crc_kernel<crc16,bytes,alt>"},
-	{2, true, true, ecg_crc_kernel<32, true, true, true>, "ecg_crc_kernel<crc32,alt>"},
-	{2, false, true, ecg_crc_kernel<32, true, false, true>, "ecg_crc_kernel<crc32,bytes,alt>"},
-	{3, true, true, ecg_crc_kernel<64, true, true, true>, "ecg_crc_kernel<crc64,alt>"},
-	{3, false, true, ecg_crc_kernel<64, true, false, true>, "ecg_crc_kernel<crc64,bytes,alt>"},
-	{7, true, false, ecg_adler_kernel<true>, "ecg_adler_kernel"},
-	{7, false, false, ecg_adler_kernel<false>, "ecg_adler_kernel<bytes>"},
+	{1, true, TK_4, ecg_crc_kernel<16, false, true, TK_4>, "ecg_crc_kernel<crc16>"},
+	{1, false, TK_5, ecg_crc_kernel<16, false, false, TK_5>, "ecg_crc_kernel<crc16,bytes>"},
+	{2, true, TK_4, ecg_crc_kernel<32, true, true, TK_4>, "ecg_crc_kernel<crc32>"},
+	{2, false, TK_5, ecg_crc_kernel<32, true, false, TK_5>, "ecg_crc_kernel<crc32,bytes>"},
+	{3, true, TK_4, ecg_crc_kernel<64, true, true, TK_4>, "ecg_crc_kernel<crc64>"},
+	{3, false, TK_5, ecg_crc_kernel<64, true, false, TK_5>, "ecg_crc_kernel<crc64,bytes>"},
+	{1, true, TK_5, ecg_crc_kernel<16, false, true, TK_5>, "ecg_crc_kernel<crc16,t5>"},
+	{2, true, TK_5, ecg_crc_kernel<32, true, true, TK_5>, "ecg_crc_kernel<crc32,t5>"},
+	{3, true, TK_5, ecg_crc_kernel<64, true, true, TK_5>, "ecg_crc_kernel<crc64,t5>"},
+	{1, true, TK_B8, ecg_crc_kernel<16, false, true, TK_B8>, "ecg_crc_kernel<crc16,alt>"},
+	{1, false, TK_B8, ecg_crc_kernel<16, false, false, TK_B8>, "ecg_crc_kernel<crc16,bytes,alt>"},
+	{2, true, TK_B8, ecg_crc_kernel<32, true, true, TK_B8>, "ecg_crc_kernel<crc32,alt>"},
+	{2, false, TK_B8, ecg_crc_kernel<32, true, false, TK_B8>, "ecg_crc_kernel<crc32,bytes,alt>"},
+	{3, true, TK_B8, ecg_crc_kernel<64, true, true, TK_B8>, "ecg_crc_kernel<crc64,alt>"},
+	{3, false, TK_B8, ecg_crc_kernel<64, true, false, TK_B8>, "ecg_crc_kernel<crc64,bytes,alt>"},
+	{7, true, 0, ecg_adler_kernel<true>, "ecg_adler_kernel"},
+	{7, false, 0, ecg_adler_kernel<false>, "ecg_adler_kernel<bytes>"},
 };
 constexpr uint32_t N_CSUM = sizeof(g_csum) / sizeof(g_csum[0]);
 
 constexpr int SPLIT_NW = ECG_CSUM_SPLIT_NW;	// waves per chunk in the split kernel
 const csum_entry g_split[] = {
-	{1, true, false, ecg_crc_split_kernel<16, false, SPLIT_NW, false>, "ecg_crc_split_kernel<crc16>"},
-	{2, true, false, ecg_crc_split_kernel<32, true, SPLIT_NW, false>, "ecg_crc_split_kernel<crc32>"},
-	{3, true, false, ecg_crc_split_kernel<64, true, SPLIT_NW, false>, "ecg_crc_split_kernel<crc64>"},
-	{1, true, true, ecg_crc_split_kernel<16, false, SPLIT_NW, true>, "ecg_crc_split_kernel<crc16,alt>"},
-	{2, true, true, ecg_crc_split_kernel<32, true, SPLIT_NW, true>, "ecg_crc_split_kernel<crc32,alt>"},
-	{3, true, true, ecg_crc_split_kernel<64, true, SPLIT_NW, true>, "ecg_crc_split_kernel<crc64,alt>"},
-	{7, true, false, ecg_adler_split_kernel<SPLIT_NW>, "ecg_adler_split_kernel"},
+	{1, true, TK_4, ecg_crc_split_kernel<16, false, SPLIT_NW, TK_4>, "ecg_crc_split_kernel<crc16>"},
+	{2, true, TK_4, ecg_crc_split_kernel<32, true, SPLIT_NW, TK_4>, "ecg_crc_split_kernel<crc32>"},
+	{3, true, TK_4, ecg_crc_split_kernel<64, true, SPLIT_NW, TK_4>, "ecg_crc_split_kernel<crc64>"},
+	{1, true, TK_5, ecg_crc_split_kernel<16, false, SPLIT_NW, TK_5>, "ecg_crc_split_kernel<crc16,t5>"},
+	{2, true, TK_5, ecg_crc_split_kernel<32, true, SPLIT_NW, TK_5>, "ecg_crc_split_kernel<crc32,t5>"},
+	{3, true, TK_5, ecg_crc_split_kernel<64, true, SPLIT_NW, TK_5>, "ecg_crc_split_kernel<crc64,t5>"},
+	{1, true, TK_B8, ecg_crc_split_kernel<16, false, SPLIT_NW, TK_B8>, "ecg_crc_split_kernel<crc16,alt>"},
+	{2, true, TK_B8, ecg_crc_split_kernel<32, true, SPLIT_NW, TK_B8>, "ecg_crc_split_kernel<crc32,alt>"},
+	{3, true, TK_B8, ecg_crc_split_kernel<64, true, SPLIT_NW, TK_B8>, "ecg_crc_split_kernel<crc64,alt>"},
+	{7, true, 0, ecg_adler_split_kernel<SPLIT_NW>, "ecg_adler_split_kernel"},
 };
 constexpr uint32_t N_SPLIT = sizeof(g_split) / sizeof(g_split[0]);
 
 const csum_entry g_group[] = {
-	{1, true, false, ecg_crc_group_kernel<16, false, false>, "ecg_crc_group_kernel<crc16>"},
-	{2, true, false, ecg_crc_group_kernel<32, true, false>, "ecg_crc_group_kernel<crc32>"},
-	{3, true, false, ecg_crc_group_kernel<64, true, false>, "ecg_crc_group_kernel<crc64>"},
-	{1, true, true, ecg_crc_group_kernel<16, false, true>, "ecg_crc_group_kernel<crc16,alt>"},
-	{2, true, true, ecg_crc_group_kernel<32, true, true>, "ecg_crc_group_kernel<crc32,alt>"},
-	{3, true, true, ecg_crc_group_kernel<64, true, true>, "ecg_crc_group_kernel<crc64,alt>"},
+	{1, true, TK_4, ecg_crc_group_kernel<16, false, TK_4>, "ecg_crc_group_kernel<crc16>"},
+	{2, true, TK_4, ecg_crc_group_kernel<32, true, TK_4>, "ecg_crc_group_kernel<crc32>"},
+	{3, true, TK_4, ecg_crc_group_kernel<64, true, TK_4>, "ecg_crc_group_kernel<crc64>"},
+	{1, true, TK_5, ecg_crc_group_kernel<16, false, TK_5>, "ecg_crc_group_kernel<crc16,t5>"},
+	{2, true, TK_5, ecg_crc_group_kernel<32, true, TK_5>, "ecg_crc_group_kernel<crc32,t5>"},
+	{3, true, TK_5, ecg_crc_group_kernel<64, true, TK_5>, "ecg_crc_group_kernel<crc64,t5>"},
+	{1, true, TK_B8, ecg_crc_group_kernel<16, false, TK_B8>, "ecg_crc_group_kernel<crc16,alt>"},
+	{2, true, TK_B8, ecg_crc_group_kernel<32, true, TK_B8>, "ecg_crc_group_kernel<crc32,alt>"},
+	{3, true, TK_B8, ecg_crc_group_kernel<64, true, TK_B8>, "ecg_crc_group_kernel<crc64,alt>"},
 };
 constexpr uint32_t N_GROUP = sizeof(g_group) / sizeof(g_group[0]);
 
-/* the entry's table kind matches the request (adler32 has one kind) */
+/* the entry's table kind matches the request (adler32 has one kind; the
+ * byte-granular kernels of unaligned extents have the 5-bit tables unless
+ * the byte tables are asked for) */
 __host__ inline bool kind_ok(const csum_entry &e, const ecg_csum_params_t *p)
 {
-	return e.type == 7 || e.b8 == (p->byte_tables != 0);
+	if (e.type == 7)
+		return true;
+	if (!e.aligned && p->byte_tables == TK_4)
+		return e.tk == TK_5;
+	return e.tk == (int)p->byte_tables;
 }
 
 } // namespace

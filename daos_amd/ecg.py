@@ -40,6 +40,8 @@ _SIGS = [
     ("ecg_ctx_device", C.c_int, [vp]),
     ("ecg_ctx_stream", vp, [vp]),
     ("ecg_device_pci_bus_id", C.c_int, [C.c_int, C.c_char_p, C.c_int]),
+    ("ecg_pci_numa_node", C.c_int, [C.c_char_p]),
+    ("ecg_device_numa_node", C.c_int, [C.c_int]),
     ("ecg_strerror", C.c_char_p, []),
     ("ecg_last_kernel", C.c_char_p, []),
     ("ecg_build_info", C.c_char_p, []),
@@ -90,6 +92,7 @@ _SIGS = [
     ("ecg_multi_create", C.c_int, [C.POINTER(C.c_int), C.c_int, C.POINTER(vp)]),
     ("ecg_multi_destroy", None, [vp]),
     ("ecg_multi_count", C.c_int, [vp]),
+    ("ecg_multi_numa_node", C.c_int, [vp, C.c_int]),
     ("ecg_multi_ctx", vp, [vp, C.c_int]),
     ("ecg_multi_range", C.c_int, [vp, C.c_uint32, C.c_int, u32p, u32p]),
     ("ecg_multi_encode", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, u32p, C.POINTER(vp), C.c_int64,
@@ -97,6 +100,19 @@ _SIGS = [
     ("ecg_multi_recover", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, u32p, C.POINTER(vp), C.c_int64, u32p,
                                     C.c_int, C.c_uint]),
     ("ecg_multi_sync", C.c_int, [vp]),
+    ("ecg_multi_encode_csum", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, u32p, C.POINTER(vp), C.c_int64,
+                                        C.POINTER(vp), C.c_int64, C.c_int64, C.c_int, C.c_uint64, C.c_uint64,
+                                        C.POINTER(vp), C.c_uint]),
+    ("ecg_multi_recover_csum", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, u32p, C.POINTER(vp), C.c_int64, u32p,
+                                         C.c_int, C.c_int, C.c_uint64, C.c_uint64, C.POINTER(vp), C.c_uint]),
+    ("ecg_multi_update", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, u32p, C.c_int, u32p, C.POINTER(vp),
+                                   C.POINTER(vp), C.c_int64, C.POINTER(vp), C.c_int64, C.c_int64, C.c_uint]),
+    ("ecg_multi_migrate_range", C.c_int, [vp, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int,
+                                          C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    ("ecg_multi_migrate_update_parity", C.c_int, [vp, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32,
+                                                  C.POINTER(vp), C.c_uint64, C.c_uint64, C.c_int, C.c_int,
+                                                  C.c_uint64, C.POINTER(vp), C.POINTER(vp), vp, C.c_uint32, u32p,
+                                                  u32p, C.c_uint]),
     ("ecg_multi_encode_host", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, vp, vp, C.c_uint32]),
     ("ecg_multi_recover_host", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, vp, u32p, C.c_int,
                                          C.c_uint32]),
@@ -555,6 +571,10 @@ class Multi:
         self.n = lib().ecg_multi_count(self.h)
         self.ctxs = [Context(_handle=lib().ecg_multi_ctx(self.h, i)) for i in range(self.n)]
 
+    def numa_node(self, i: int) -> int:
+        """NUMA node shard i's worker runs on (-1: not pinned)."""
+        return lib().ecg_multi_numa_node(self.h, i)
+
     def range(self, nstripes: int, i: int):
         f, c = C.c_uint32(), C.c_uint32()
         _chk(lib().ecg_multi_range(self.h, nstripes, i, C.byref(f), C.byref(c)), "multi_range")
@@ -586,6 +606,58 @@ class Multi:
 
     def sync(self):
         _chk(lib().ecg_multi_sync(self.h), "multi_sync")
+
+    def encode_csum(self, k: int, p: int, cell_bytes: int, nstripes: Sequence[int], data: Sequence[int],
+                    data_stripe_stride: int, parity: Sequence[int], parity_cell_stride: int,
+                    parity_stripe_stride: int, htype: int, chunksize: int, rec_size: int, csums: Sequence[int],
+                    flags: int = 0):
+        n = self.n
+        self._shards(nstripes=nstripes, data=data, parity=parity, csums=csums)
+        _chk(lib().ecg_multi_encode_csum(self.h, k, p, cell_bytes, _u32(nstripes), (vp * n)(*data),
+                                         data_stripe_stride, (vp * n)(*parity), parity_cell_stride,
+                                         parity_stripe_stride, htype, chunksize, rec_size, (vp * n)(*csums), flags),
+             "multi_encode_csum")
+
+    def recover_csum(self, k: int, p: int, cell_bytes: int, nstripes: Sequence[int], stripes: Sequence[int],
+                     stripe_stride: int, err_list: Sequence[int], htype: int, chunksize: int, rec_size: int,
+                     csums: Sequence[int], flags: int = 0):
+        n = self.n
+        self._shards(nstripes=nstripes, stripes=stripes, csums=csums)
+        _chk(lib().ecg_multi_recover_csum(self.h, k, p, cell_bytes, _u32(nstripes), (vp * n)(*stripes),
+                                          stripe_stride, _u32(err_list), len(err_list), htype, chunksize, rec_size,
+                                          (vp * n)(*csums), flags), "multi_recover_csum")
+
+    def update(self, k: int, p: int, cell_bytes: int, nstripes: Sequence[int], cell_idx: Sequence[int],
+               old: Sequence[int], new: Sequence[int], upd_stripe_stride: int, parity: Sequence[int],
+               parity_cell_stride: int, parity_stripe_stride: int, flags: int = 0):
+        n = self.n
+        self._shards(nstripes=nstripes, old=old, new=new, parity=parity)
+        _chk(lib().ecg_multi_update(self.h, k, p, cell_bytes, _u32(nstripes), len(cell_idx), _u32(cell_idx),
+                                    (vp * n)(*old), (vp * n)(*new), upd_stripe_stride, (vp * n)(*parity),
+                                    parity_cell_stride, parity_stripe_stride, flags), "multi_update")
+
+    def migrate_range(self, oc_id: int, e_len: int, iod_size: int, offset: int, size: int, encode: bool, i: int):
+        off, sz = C.c_uint64(), C.c_uint64()
+        _chk(lib().ecg_multi_migrate_range(self.h, oc_id, e_len, iod_size, offset, size, int(encode), i,
+                                           C.byref(off), C.byref(sz)), "multi_migrate_range")
+        return off.value, sz.value
+
+    def migrate_update_parity(self, oc_id: int, e_len: int, iod_size: int, shard: int, buffers: Sequence[int],
+                              offset: int, size: int, encode: bool, csum_type: int, chunksize: int,
+                              parity_out: Sequence[int], csums_out: Sequence[int], pieces_cap: int,
+                              flags: int = 0):
+        """Returns (pieces, shard_first): every piece in range order, shard i's
+        at [shard_first[i], shard_first[i+1]) relative to its own buffers."""
+        n = self.n
+        self._shards(buffers=buffers, parity_out=parity_out, csums_out=csums_out)
+        pieces = (MigratePiece * max(1, pieces_cap))()
+        npc = C.c_uint32()
+        first = (C.c_uint32 * (n + 1))()
+        _chk(lib().ecg_multi_migrate_update_parity(self.h, oc_id, e_len, iod_size, shard, (vp * n)(*buffers), offset,
+                                                   size, int(encode), csum_type, chunksize, (vp * n)(*parity_out),
+                                                   (vp * n)(*csums_out), pieces, pieces_cap, C.byref(npc), first,
+                                                   flags), "multi_migrate_update_parity")
+        return list(pieces[:npc.value]), list(first)
 
     def encode_host(self, k: int, p: int, cell_bytes: int, nstripes: int, data: np.ndarray, parity: np.ndarray,
                     chunk: int = 0):

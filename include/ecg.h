@@ -58,6 +58,12 @@ int ecg_ctx_device(const ecg_ctx_t *ctx);
 /* PCI bus id ("0000:c1:00.0") of a visible device: tells ranks or shards
  * that landed on the same physical GPU apart. */
 int ecg_device_pci_bus_id(int device, char *buf, int len);
+/* NUMA node of a PCI device ("0000:23:00.0", any case) from sysfs
+ * (/sys/bus/pci/devices/<bdf>/numa_node), and of a HIP device; -1 when
+ * unknown.  ecg_multi workers run on their device's node and queue staging
+ * is allocated there; $ECG_NUMA=0 turns that off. */
+int ecg_pci_numa_node(const char *pci_bus_id);
+int ecg_device_numa_node(int device);
 /* The context's default stream (used when a call passes stream == NULL). */
 void *ecg_ctx_stream(ecg_ctx_t *ctx);
 const char *ecg_strerror(void);

@@ -224,3 +224,177 @@ sys.exit(1 if bad else 0)
     env = dict(os.environ, ECG_DEVICES="0,0,0")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+# ------------------------------------------------ rebuild / aggregation ops
+DT = {2: np.uint16, 4: np.uint32, 8: np.uint64}
+
+
+def _cell_csums(oracle, htype, cs, cells):
+    C_ = cells.shape[-1]
+    flat = np.ascontiguousarray(cells.reshape(-1, C_))
+    return oracle.csum_extents(htype, cs, 1, 0, C_, flat.reshape(-1), ext_stride=C_, n_ext=flat.shape[0])
+
+
+@pytest.mark.parametrize("htype", [2, 3])
+def test_multi_encode_csum_and_recover_csum(ecglib, ctx, oracle, multi4, htype):
+    """ecg_multi_encode_csum / ecg_multi_recover_csum (the rebuild path's
+    product + chunk checksums, ref:src/object/srv_obj_migrate.c:1122-1160):
+    shard i's stripes and checksums on its own buffers; parity, regenerated
+    cells and every checksum identical to one ecg_encode_csum /
+    ecg_recover_csum over the whole batch and to the oracle."""
+    L = ecglib.lib()
+    k, p, C_, S, cs = 8, 2, 128 << 10, 11, 32768
+    cl, nch = L.ecg_csum_len(htype), C_ // cs
+    data = rand((S, k, C_), 40 + htype)
+    want_par = oracle.encode_batch(k, p, C_, S, data.reshape(-1), nthreads=8, simd=True).reshape(p, S, C_)
+    want_cs = _cell_csums(oracle, htype, cs, want_par).reshape(p, S, nch)
+
+    ranges = [multi4.range(S, i) for i in range(4)]
+    dbufs = [c.to_device(np.ascontiguousarray(data[f:f + n]).reshape(-1) if n else np.zeros(1, np.uint8))
+             for c, (f, n) in zip(multi4.ctxs, ranges)]
+    pbufs = [c.alloc(max(1, p * n * C_)) for c, (f, n) in zip(multi4.ctxs, ranges)]
+    cbufs = [c.alloc(max(8, p * n * nch * cl)) for c, (f, n) in zip(multi4.ctxs, ranges)]
+    try:
+        # each shard writes its parity as [n][p][C] (cell stride C, stripe stride p*C)
+        multi4.encode_csum(k, p, C_, [n for _, n in ranges], [b.ptr for b in dbufs], k * C_,
+                           [b.ptr for b in pbufs], C_, p * C_, htype, cs, 1, [b.ptr for b in cbufs])
+        for (f, n), pb, cb in zip(ranges, pbufs, cbufs):
+            if n == 0:
+                continue
+            got = pb.download(p * n * C_).reshape(n, p, C_)
+            assert np.array_equal(got, want_par[:, f:f + n].transpose(1, 0, 2))
+            gcs = cb.download(p * n * nch * cl).view(DT[cl]).reshape(p, n, nch)
+            assert np.array_equal(gcs, want_cs[:, f:f + n]), (f, n)
+        # one call over everything gives the same bytes
+        one = ctx.to_device(data.reshape(-1))
+        opar = ctx.alloc(p * S * C_)
+        ocs = ctx.alloc(p * S * nch * cl)
+        ctx.encode_csum(k, p, C_, S, one.ptr, k * C_, opar.ptr, C_, p * C_, htype, cs, 1, ocs.ptr)
+        ctx.sync()
+        assert np.array_equal(opar.download().reshape(S, p, C_), want_par.transpose(1, 0, 2))
+        assert np.array_equal(ocs.download().view(DT[cl]).reshape(p, S, nch), want_cs)
+        for b in (one, opar, ocs):
+            b.free()
+    finally:
+        for b in dbufs + pbufs + cbufs:
+            b.free()
+
+    # recover {d0, p1} with checksums, in place in [n][k+p][C] per shard
+    errs = [0, k + 1]
+    img = np.concatenate([data, want_par.transpose(1, 0, 2)], axis=1)
+    sbufs, cbufs = [], []
+    for c, (f, n) in zip(multi4.ctxs, ranges):
+        part = img[f:f + n].copy()
+        part[:, errs] = 0x5A
+        sbufs.append(c.to_device(part.reshape(-1) if n else np.zeros(1, np.uint8)))
+        cbufs.append(c.alloc(max(8, len(errs) * n * nch * cl)))
+    try:
+        multi4.recover_csum(k, p, C_, [n for _, n in ranges], [b.ptr for b in sbufs], (k + p) * C_, errs, htype, cs,
+                            1, [b.ptr for b in cbufs], flags=ecglib.MULTI_ASYNC)
+        multi4.sync()
+        for (f, n), sb, cb in zip(ranges, sbufs, cbufs):
+            if n == 0:
+                continue
+            assert np.array_equal(sb.download((k + p) * n * C_).reshape(n, k + p, C_), img[f:f + n])
+            gcs = cb.download(len(errs) * n * nch * cl).view(DT[cl]).reshape(len(errs), n, nch)
+            for i, e in enumerate(errs):
+                assert np.array_equal(gcs[i], _cell_csums(oracle, htype, cs, img[f:f + n, e]).reshape(n, nch))
+    finally:
+        for b in sbufs + cbufs:
+            b.free()
+
+
+def test_multi_update(ecglib, ctx, oracle, multi4):
+    """ecg_multi_update (agg_update_parity's xor_gen + ec_encode_data_update
+    over a batch, ref:src/object/srv_ec_aggregate.c:1086-1102): cells 1 and 5
+    of every stripe replaced; each shard's parity equals the oracle's encode
+    of the updated stripes and one ecg_update over the whole batch."""
+    k, p, C_, S = 8, 2, 65536, 10
+    en = oracle.cauchy1(k, p)
+    data = rand((S, k, C_), 51)
+    new = rand((S, 2, C_), 52)
+    cells = [1, 5]
+    par = np.stack([oracle.encode_data(en[k:], data[s]) for s in range(S)])          # [S][p][C]
+    upd = data.copy()
+    upd[:, cells] = new
+    want = np.stack([oracle.encode_data(en[k:], upd[s]) for s in range(S)])
+    ranges = [multi4.range(S, i) for i in range(4)]
+    olds = [c.to_device(np.ascontiguousarray(data[f:f + n][:, cells]).reshape(-1)) for c, (f, n) in
+            zip(multi4.ctxs, ranges)]
+    news = [c.to_device(np.ascontiguousarray(new[f:f + n]).reshape(-1)) for c, (f, n) in zip(multi4.ctxs, ranges)]
+    pars = [c.to_device(np.ascontiguousarray(par[f:f + n]).reshape(-1)) for c, (f, n) in zip(multi4.ctxs, ranges)]
+    try:
+        # old/new cells [n][2][C] (cell j of the update at j*C, stripe stride 2C); parity [n][p][C]
+        multi4.update(k, p, C_, [n for _, n in ranges], cells, [b.ptr for b in olds], [b.ptr for b in news], 2 * C_,
+                      [b.ptr for b in pars], C_, p * C_)
+        for (f, n), b in zip(ranges, pars):
+            assert np.array_equal(b.download().reshape(n, p, C_), want[f:f + n]), (f, n)
+    finally:
+        for b in olds + news + pars:
+            b.free()
+
+
+MIGRATE = [  # k, p, e_len, iod_size, offset (records), size (records), encode, csum
+    (4, 2, 1024, 1, 1000, 4096 * 9 + 77, True, 2),       # partial head and tail, 9 whole stripes
+    (8, 2, 512, 8, 4096 * 2, 4096 * 6, True, 3),         # whole stripes only
+    (16, 2, 256, 4, 100, 4096 * 2 + 300, True, 2),       # 2 whole stripes over 4 shards
+    (4, 2, 1024, 1, 512, 9000, False, 2),                # replicate by cells
+    (8, 2, 512, 8, 10, 300, True, 0),                    # no whole stripe: shard 0 alone
+]
+
+
+@pytest.mark.parametrize("case", MIGRATE)
+def test_multi_migrate_update_parity(ecglib, ctx, oracle, multi4, case):
+    """ecg_multi_migrate_update_parity (migrate_update_parity,
+    ref:src/object/srv_obj_migrate.c:1096-1181) sharded over 4 contexts:
+    the shards' sub-ranges tile the fetched range at the walk's own cut
+    points, so the pieces -- recx, bytes, checksums -- are exactly those of
+    one ecg_migrate_update_parity over the whole range and of the oracle."""
+    import ctypes as ct
+
+    from oracle import migrate_py
+
+    k, p, e_len, isz, off, size, enc, csum = case
+    L = ecglib.lib()
+    redun = {(4, 2): 35, (8, 2): 37, (16, 2): 39}[(k, p)]
+    oc = (redun << 24) | 1
+    shard = k + p - 1
+    host = np.random.default_rng(size + k).integers(0, 256, size * isz, dtype=np.uint8)
+    want = migrate_py.update_parity(oracle, k, p, e_len, isz, shard, host, off, size, enc, csum, 32768)
+    subs = [multi4.migrate_range(oc, e_len, isz, off, size, enc, i) for i in range(4)]
+    pos = off
+    for o, z in subs:                                    # contiguous, in order, covering the range
+        assert o == pos or z == 0
+        pos = o + z if z else pos
+    assert pos == off + size
+    cl = {2: 4, 3: 8}.get(csum, 0)
+    bufs, pouts, couts, sizes = [], [], [], []
+    for c, (o, z) in zip(multi4.ctxs, subs):
+        n, npar, cb = ct.c_uint32(), ct.c_uint32(), ct.c_uint64()
+        if z:
+            assert L.ecg_migrate_plan_size(oc, e_len, isz, o, z, int(enc), csum, 32768, ct.byref(n), ct.byref(npar),
+                                           ct.byref(cb)) == 0
+        seg = host[(o - off) * isz:(o - off + z) * isz] if z else np.zeros(1, np.uint8)
+        bufs.append(c.to_device(seg))
+        pouts.append(c.alloc(max(1, npar.value * e_len * isz)))
+        couts.append(c.alloc(max(8, cb.value)))
+    try:
+        pieces, first = multi4.migrate_update_parity(oc, e_len, isz, shard, [b.ptr for b in bufs], off, size, enc,
+                                                     csum, 32768, [b.ptr for b in pouts], [b.ptr for b in couts],
+                                                     len(want) + 4)
+        assert len(pieces) == len(want) and first[0] == 0 and first[-1] == len(want)
+        for i in range(4):
+            pb, cbytes = pouts[i].download(), couts[i].download()
+            seg = host[(subs[i][0] - off) * isz:] if subs[i][1] else None
+            for pc, w in zip(pieces[first[i]:first[i + 1]], want[first[i]:first[i + 1]]):
+                assert (pc.recx.rx_idx, pc.recx.rx_nr) == w["recx"] and bool(pc.parity) == w["parity"]
+                src = pb if pc.parity else seg
+                assert np.array_equal(src[pc.buf_off:pc.buf_off + pc.buf_len], w["bytes"]), (i, w["recx"])
+                if csum:
+                    dt = np.uint32 if cl == 4 else np.uint64
+                    got = cbytes[pc.csum_off:pc.csum_off + pc.nr_csums * cl].view(dt)
+                    assert np.array_equal(got, w["csums"]), (i, w["recx"])
+    finally:
+        for b in bufs + pouts + couts:
+            b.free()

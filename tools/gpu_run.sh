@@ -207,6 +207,21 @@ PY
 			SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VMEM_WR \
 			--output-format csv -d gpurun_out/pmc_sq2 -o run -- python3 tools/crc_pmc.py fused || exit $?
 		;;
+	crcsq)
+		# standalone crc32 / crc64 kernels (32 KiB chunks, 1 GiB): SQ / LDS / GRBM counter passes
+		rm -rf gpurun_out/pmc_csq1 gpurun_out/pmc_csq2 gpurun_out/pmc_cgrbm
+		step rocprof_csq1 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES \
+			SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_ANY \
+			--output-format csv -d gpurun_out/pmc_csq1 -o run -- python3 tools/crc_pmc.py || exit $?
+		step rocprof_csq2 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_LDS \
+			SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE \
+			--output-format csv -d gpurun_out/pmc_csq2 -o run -- python3 tools/crc_pmc.py || exit $?
+		step rocprof_cgrbm 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE GRBM_COUNT \
+			--output-format csv -d gpurun_out/pmc_cgrbm -o run -- python3 tools/crc_pmc.py || exit $?
+		python tools/pmc_summary.py --skip 1 gpurun_out/pmc_csq1/run_counter_collection.csv \
+			gpurun_out/pmc_csq2/run_counter_collection.csv gpurun_out/pmc_cgrbm/run_counter_collection.csv \
+			> gpurun_out/crc_sq_summary.jsonl || exit $?
+		;;
 	pmcjson)
 		python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write "ecg_mm_kernel<4, 2" 6442450944 \
 			gpurun_out/pmc_traffic.json || exit $?
