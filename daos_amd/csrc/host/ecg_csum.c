@@ -755,7 +755,8 @@ int ecg_set_fused_cols(ecg_ctx_t *ctx, uint32_t ncols)
 
 int ecg_set_csum_variant(ecg_ctx_t *ctx, uint32_t variant)
 {
-	if (ctx == NULL || (variant & 15u) > 3 || variant > 511 || (variant & 48u) == 48u ||
+	if (ctx == NULL || (variant & 15u) > 3 || variant > 1023 || (variant & 48u) == 48u ||
+	    (variant & 576u) == 576u ||
 	    (variant & 384u) == 384u)
 		return ecg_fail(-ECG_DER_INVAL, "set_csum_variant: bad arguments");
 	ctx->csum_variant = variant;
@@ -809,7 +810,7 @@ int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t
 	q->nitems = (q->nch - 1) * q->nh + q->nh_last;
 	/* fused kernels: table kind TB (ecg_kernels.hip); bit 6 of csum_variant
 	 * selects the s16 tables (A/B), bit 7 the wave-per-chunk kernel */
-	q->byte_tables = (ctx->csum_variant & 64u) ? 2 : use_byte_tables(ctx, type, 1);
+	q->byte_tables = (ctx->csum_variant & 512u) ? 3 : (ctx->csum_variant & 64u) ? 2 : use_byte_tables(ctx, type, 1);
 	/* the wave-per-chunk kernel for crc64 with k <= 4 (one 64-step multiply
 	 * per lane per chunk instead of per thread per item: EC_4P2 crc64 +42 %
 	 * -> +29 % over the plain encode; with k = 8 its longer serial walk

@@ -357,6 +357,53 @@ __device__ __forceinline__ T lane_mul_nib(T x, const T *gnib, const T *r4, uint3
 	return u;
 }
 
+// raw CRC of one 16-byte piece from the s16 byte tables (16 independent
+// lookups; table 15 - 4j - b for byte b of dword j), each address ONE SDWA
+// instruction (byte << log2(entry bytes)) with the table's offset in the
+// ds_read's immediate: 16 + NB*2 VALU per piece for crc32 instead of ~50 with
+// shift-and-mask addresses.  Byte tables are bank-conflicted (~3x per
+// lookup), so this pays where the LDS has slack -- the fused product +
+// checksum kernels, whose VALU carries the GF product too.
+template <int W, typename T>
+__device__ __forceinline__ T piece_crc16s(const uint32_t d[4], const T *s16)
+{
+	constexpr int ES = sizeof(T) == 8 ? 3 : 2;
+	T c = 0;
+
+#pragma unroll
+	for (int j = 0; j < 4; j++) {
+		const uint32_t x = d[j];
+		c = x3(c, nib_ent(s16, 16 * (15 - 4 * j), nib_lo_addr<0, ES>(x)),
+		       nib_ent(s16, 16 * (14 - 4 * j), nib_lo_addr<1, ES>(x)));
+		c = x3(c, nib_ent(s16, 16 * (13 - 4 * j), nib_lo_addr<2, ES>(x)),
+		       nib_ent(s16, 16 * (12 - 4 * j), nib_lo_addr<3, ES>(x)));
+	}
+	return c;
+}
+
+// register -> register shifted by the a4 table's fixed number of zero bytes
+// (nibble fields, SDWA addresses; a4[16][16], rows >= W/4 unused)
+template <int W, typename T>
+__device__ __forceinline__ T lin_map4(T acc, const T *a4)
+{
+	const uint32_t hmask = nib_hmask<T>();
+	T c = 0;
+
+#pragma unroll
+	for (int h = 0; h < (W + 31) / 32; h++) {
+		const uint32_t x = W == 16 ? (uint32_t)acc & 0xFFFFu : (uint32_t)((uint64_t)acc >> (32 * h));
+		if constexpr (W == 16) {
+			constexpr int ES = sizeof(T) == 8 ? 3 : 2;
+			const uint32_t lo = x & 0x0F0Fu, hs = x >> (4 - ES);
+			c = x3(c, nib_ent(a4, 0, nib_lo_addr<0, ES>(lo)), nib_ent(a4, 1, nib_hi_addr<0>(hs, hmask)));
+			c = x3(c, nib_ent(a4, 2, nib_lo_addr<1, ES>(lo)), nib_ent(a4, 3, nib_hi_addr<1>(hs, hmask)));
+		} else {
+			c = nib_dword(c, x, a4, 8 * h, hmask);
+		}
+	}
+	return c;
+}
+
 // register -> register shifted by the a5 table's fixed number of zero bytes
 template <int W, typename T>
 __device__ __forceinline__ T lin_map5(T c, const T *a5)

@@ -172,30 +172,63 @@ __device__ __forceinline__ void mm_compute(const ecg_mm_params_t &P, const u32x4
 		}
 		continue;
 #endif
+		// sources in pairs: the 6 table terms of two sources fold into the
+		// accumulator with 3 three-input XORs (1.5 per source and row)
+		// instead of 2 per source
+#ifdef ECG_EXP_SERIAL_XOR
 		if (j < k) {
-			u32x4 sel0, sel1, sel2;
+			const bool two = false;		// experimental build: round 2's 2 XORs per source
+#else
+		if (j % 2 == 0 && j < k) {
+			const bool two = j + 1 < KM && j + 1 < k;
+#endif
+			u32x4 sel0[2], sel1[2], sel2[2];
 #pragma unroll
-			for (int w = 0; w < 4; w++) {
-				const uint32_t v = x[j][w];
-				sel0[w] = v & 0x07070707u;
-				sel1[w] = (v >> 3) & 0x07070707u;
-				sel2[w] = (v >> 6) & 0x03030303u;
+			for (int h = 0; h < 2; h++) {
+				if (h == 0 || two) {
+#pragma unroll
+					for (int w = 0; w < 4; w++) {
+						const uint32_t v = x[j + h < KM ? j + h : j][w];
+						sel0[h][w] = v & 0x07070707u;
+						sel1[h][w] = (v >> 3) & 0x07070707u;
+						sel2[h][w] = (v >> 6) & 0x03030303u;
+					}
+				}
 			}
-			u32x4 t2v[T2V];
+			const int j1 = j + 1 < KM ? j + 1 : j;
+			u32x4 t2va[T2V], t2vb[T2V];
 #pragma unroll
-			for (int q = 0; q < T2V; q++)
-				t2v[q] = tb[j * PER_J + RM + q];
+			for (int q = 0; q < T2V; q++) {
+				t2va[q] = tb[j * PER_J + RM + q];
+				if (two)
+					t2vb[q] = tb[j1 * PER_J + RM + q];
+			}
 #pragma unroll
 			for (int r = 0; r < RM; r++) {
 				if (r < rows) {
-					const u32x4 t = tb[j * PER_J + r];
-					const uint32_t t2 = t2v[r / 4][r % 4];
+					const u32x4 ta = tb[j * PER_J + r];
+					const uint32_t t2a = t2va[r / 4][r % 4];
+					if (two) {
+						const u32x4 tbb = tb[j1 * PER_J + r];
+						const uint32_t t2b = t2vb[r / 4][r % 4];
 #pragma unroll
-					for (int w = 0; w < 4; w++) {
-						const uint32_t p0 = __builtin_amdgcn_perm(t[1], t[0], sel0[w]);
-						const uint32_t p1 = __builtin_amdgcn_perm(t[3], t[2], sel1[w]);
-						const uint32_t p2 = __builtin_amdgcn_perm(t2, t2, sel2[w]);
-						acc[r][w] = xor3(acc[r][w], p0, xor3(p1, p2, 0u));
+						for (int w = 0; w < 4; w++) {
+							const uint32_t a0 = __builtin_amdgcn_perm(ta[1], ta[0], sel0[0][w]);
+							const uint32_t a1 = __builtin_amdgcn_perm(ta[3], ta[2], sel1[0][w]);
+							const uint32_t a2 = __builtin_amdgcn_perm(t2a, t2a, sel2[0][w]);
+							const uint32_t b0 = __builtin_amdgcn_perm(tbb[1], tbb[0], sel0[1][w]);
+							const uint32_t b1 = __builtin_amdgcn_perm(tbb[3], tbb[2], sel1[1][w]);
+							const uint32_t b2 = __builtin_amdgcn_perm(t2b, t2b, sel2[1][w]);
+							acc[r][w] = xor3(xor3(acc[r][w], a0, a1), xor3(a2, b0, b1), b2);
+						}
+					} else {
+#pragma unroll
+						for (int w = 0; w < 4; w++) {
+							const uint32_t a0 = __builtin_amdgcn_perm(ta[1], ta[0], sel0[0][w]);
+							const uint32_t a1 = __builtin_amdgcn_perm(ta[3], ta[2], sel1[0][w]);
+							const uint32_t a2 = __builtin_amdgcn_perm(t2a, t2a, sel2[0][w]);
+							acc[r][w] = xor3(acc[r][w], a0, xor3(a1, a2, 0u));
+						}
 					}
 				}
 			}
@@ -499,7 +532,9 @@ __device__ __forceinline__ void mmcs_col(const ecg_mm_params_t &P0, const u32x4 
 	for (int r = 0; r < RM; r++) {
 		if (r < rows) {
 #ifndef ECG_EXP_NO_CRC
-			if constexpr (TB != 0)
+			if constexpr (TB == 3)
+				crc[r] = ecg_crc::lin_map4<W>(crc[r], s_sh);	// a4 of one column
+			else if constexpr (TB != 0)
 				crc[r] = ecg_crc::lin_map5<W>(crc[r], s_sh);	// a5 of one column
 			else if (gshift && pos == F5::U - 1)
 				crc[r] = ecg_crc::lin_map5<W>(crc[r], s_sl + F5::U * F5::NF * 32);
@@ -516,6 +551,8 @@ __device__ __forceinline__ void mmcs_col(const ecg_mm_params_t &P0, const u32x4 
 					crc[r] ^= ecg_crc::piece_crc<W, REFL>(d, s_sl);
 				else if constexpr (TB == 2)
 					crc[r] ^= ecg_crc::piece_crc16<W>(d, s_sl);
+				else if constexpr (TB == 3)
+					crc[r] ^= ecg_crc::piece_crc16s<W>(d, s_sl);
 				else
 					crc[r] ^= ecg_crc::piece_crc5p<W>(d, s_sl, pos * (uint32_t)(F5::NF * 32 * sizeof(T)));
 #else
@@ -559,7 +596,8 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	// independent lookups per piece) + the a5 shift
 	constexpr int NSL = TB == 0 ? F5::N : TB == 1 ? NB * 256 : 16 * 256;
 	__shared__ T s_sl[NSL];
-	__shared__ T s_sh[TB ? ECG_CSUM_NA5(NB) * 32 : 1];	// TB 1/2: the column shift as 5-bit a5 tables
+	// TB 1/2: the column shift as 5-bit a5 tables; TB 3: as nibble a4 tables
+	__shared__ T s_sh[TB == 3 ? 16 * 16 : TB ? ECG_CSUM_NA5(NB) * 32 : 1];
 	__shared__ T s_nib[REFL ? 16 * 64 : 1];		// reflected: lane multiply tables
 	__shared__ T s_r4[REFL ? 16 : 1];
 	const int k = K ? K : (int)P.k;
@@ -586,8 +624,12 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	if constexpr (TB != 0) {
 		for (int i = threadIdx.x; i < NSL; i += BLOCK)
 			s_sl[i] = gt[(TB == 1 ? 0 : ECG_CSUM_OFF_S16(NB)) + i];
-		for (int i = threadIdx.x; i < ECG_CSUM_NA5(NB) * 32; i += BLOCK)
-			s_sh[i] = gt[ECG_CSUM_OFF_A5_4K(NB) + i];
+		if constexpr (TB == 3)
+			for (int i = threadIdx.x; i < 16 * 16; i += BLOCK)
+				s_sh[i] = gt[ECG_CSUM_OFF_A4_4K(NB) + i];
+		else
+			for (int i = threadIdx.x; i < ECG_CSUM_NA5(NB) * 32; i += BLOCK)
+				s_sh[i] = gt[ECG_CSUM_OFF_A5_4K(NB) + i];
 	} else {
 		ecg_crc::stage5u<W, UF>(s_sl, gt, ECG_CSUM_OFF_P5X_4K(NB), ECG_CSUM_OFF_A5_32K(NB), BLOCK);
 	}
@@ -710,7 +752,8 @@ ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	constexpr int NSL = TB == 0 ? F5::N : TB == 1 ? NB * 256 : 16 * 256;
 	__shared__ u32x4 s_tbl[KM * PER_J];
 	__shared__ T s_sl[NSL];
-	__shared__ T s_sh[TB ? ECG_CSUM_NA5(NB) * 32 : 1];	// TB 1/2: the column shift as 5-bit a5 tables
+	// TB 1/2: the row shift as 5-bit a5 tables; TB 3: as nibble a4 tables
+	__shared__ T s_sh[TB == 3 ? 16 * 16 : TB ? ECG_CSUM_NA5(NB) * 32 : 1];
 	const int k = K ? K : (int)P.k;
 	const int rows = R ? R : (int)P.rows;
 	const uint64_t C = P.cell_bytes;
@@ -729,8 +772,12 @@ ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	if constexpr (TB != 0) {
 		for (int i = threadIdx.x; i < NSL; i += BLOCK)
 			s_sl[i] = gt[(TB == 1 ? 0 : ECG_CSUM_OFF_S16(NB)) + i];
-		for (int i = threadIdx.x; i < ECG_CSUM_NA5(NB) * 32; i += BLOCK)
-			s_sh[i] = gt[ECG_CSUM_OFF_A5_1K(NB) + i];
+		if constexpr (TB == 3)
+			for (int i = threadIdx.x; i < 16 * 16; i += BLOCK)
+				s_sh[i] = gt[ECG_CSUM_OFF_A4_1K(NB) + i];
+		else
+			for (int i = threadIdx.x; i < ECG_CSUM_NA5(NB) * 32; i += BLOCK)
+				s_sh[i] = gt[ECG_CSUM_OFF_A5_1K(NB) + i];
 	} else {
 		ecg_crc::stage5u<W>(s_sl, gt, ECG_CSUM_OFF_P5X_1K(NB), ECG_CSUM_OFF_A5_4K(NB), BLOCK);
 	}
@@ -1039,6 +1086,10 @@ static const csentry g_cskernels[] = {
 	CSB(8, 2, 2, 32, true, "crc32", 1), CSB(8, 2, 2, 32, true, "crc32", 2), CSB(8, 2, 3, 64, true, "crc64", 0),
 	CSB(8, 2, 3, 64, true, "crc64", 2), CSB(4, 2, 2, 32, true, "crc32", 2), CSB(4, 2, 3, 64, true, "crc64", 2),
 	CSB(8, 1, 2, 32, true, "crc32", 2),
+	/* TB 3: s16 byte tables with SDWA addresses + nibble a4 column shift */
+	CSB(8, 2, 2, 32, true, "crc32", 3), CSB(8, 2, 3, 64, true, "crc64", 3), CSB(4, 2, 2, 32, true, "crc32", 3),
+	CSB(4, 2, 3, 64, true, "crc64", 3), CSB(8, 1, 2, 32, true, "crc32", 3), CSB(16, 2, 2, 32, true, "crc32", 3),
+	CSB(8, 3, 2, 32, true, "crc32", 3), CSB(4, 1, 2, 32, true, "crc32", 3), CSB(16, 1, 2, 32, true, "crc32", 3),
 };
 #define N_CSKERNELS ((uint32_t)(sizeof(g_cskernels) / sizeof(g_cskernels[0])))
 

@@ -404,3 +404,42 @@ def test_encode_csum_fused_table_kinds(oracle, ecglib, ctx, kind, case):
     finally:
         L.ecg_set_csum_variant(ctx.h, 0)
         d.free(); par.free(); out.free()
+
+
+TB3 = [  # (k, p, htype): the fused kernels' s16 + SDWA + nibble-shift instantiations (csum_variant bit 9)
+    (8, 2, 2), (8, 2, 3), (4, 2, 2), (4, 2, 3), (8, 1, 2), (16, 2, 2), (8, 3, 2), (4, 1, 2), (16, 1, 2),
+]
+
+
+@pytest.mark.parametrize("shape", [256, 0])          # workgroups over work items / the default shape
+@pytest.mark.parametrize("case", TB3)
+def test_encode_csum_tb3_tables(oracle, ecglib, ctx, case, shape):
+    """The TB 3 table kind (s16 byte tables addressed by SDWA byte selects,
+    column shift by nibble a4 tables) gives the oracle's parity and chunk
+    checksums -- ragged last chunk and 16-byte tail of the cell included."""
+    k, p, htype = case
+    C, S, cs = 3 * 32768 + 4096 + 16, 3, 32768
+    L = ecglib.lib()
+    nch = L.ecg_csum_chunk_count(cs, 1, 0, C)
+    cl = L.ecg_csum_len(htype)
+    rng = np.random.default_rng(k * 10 + p + htype)
+    data = rng.integers(0, 256, S * k * C, dtype=np.uint8)
+    d = ctx.to_device(data)
+    par = ctx.alloc(p * S * C)
+    out = ctx.alloc(p * S * nch * cl)
+    try:
+        var = 512 | shape
+        if htype == 3 and k <= 4:
+            var |= 256                                   # crc64 k <= 4 defaults to the wave kernel
+        assert L.ecg_set_csum_variant(ctx.h, var) == 0
+        ctx.encode_csum(k, p, C, S, d.ptr, k * C, par.ptr, S * C, C, htype, cs, 1, out.ptr)
+        ctx.sync()
+        assert L.ecg_last_kernel().decode().endswith(",tb3>"), L.ecg_last_kernel()
+        want_par = oracle.encode_batch(k, p, C, S, data, nthreads=8, simd=True).reshape(p, S, C)
+        assert np.array_equal(par.download().reshape(p, S, C), want_par)
+        got = out.download().view(DT[cl]).reshape(p, S, nch)
+        want = _want_cell_csums(oracle, htype, cs, 1, want_par).reshape(p, S, nch)
+        assert np.array_equal(got, want), np.argwhere(got != want)[:5]
+    finally:
+        L.ecg_set_csum_variant(ctx.h, 0)
+        d.free(); par.free(); out.free()

@@ -1,5 +1,6 @@
-"""Fused product + crc32: the 5-bit tables (default) vs the byte tables
-(ecg_set_csum_variant bit 4) for k >= 8, in one process, the order of the
+"""Fused product + crc32 / crc64 table kinds: the 5-bit tables (crc32's
+default), the byte tables (bit 4; crc64's default), and the s16 byte tables
+with SDWA addresses + nibble column shift (bit 9, TB 3), in one process, the order of the
 configurations rotated every round so neither always follows the plain
 encode (tools/fused_libs.py keeps a fixed order and showed a ~1-2 % position
 bias); median of 21 rounds after 10 warm-up rounds, random cells, 1 MiB
@@ -31,15 +32,25 @@ def main():
     for k, p, S in shapes:
         pitch = S * C + 4096
 
-        def fused(variant, k=k, p=p, S=S, pitch=pitch):
+        def fused(variant, htype=ecg.HASH_CRC32, k=k, p=p, S=S, pitch=pitch):
             def fn():
                 L.ecg_set_csum_variant(ctx.h, variant)
-                ctx.encode_csum(k, p, C, S, buf.ptr, k * C, par.ptr, pitch, C, ecg.HASH_CRC32, 32768, 1, out.ptr)
+                ctx.encode_csum(k, p, C, S, buf.ptr, k * C, par.ptr, pitch, C, htype, 32768, 1, out.ptr)
                 L.ecg_set_csum_variant(ctx.h, 0)
             return fn
         cfgs = [("encode", lambda k=k, p=p, S=S, pitch=pitch: ctx.encode(k, p, C, S, buf.ptr, k * C, par.ptr,
                                                                           pitch, C)),
-                ("crc32_5bit", fused(0)), ("crc32_bytes", fused(16))]
+                ("crc32_5bit", fused(32)), ("crc32_bytes", fused(16)), ("crc32_tb3", fused(512)),
+                ("crc64_dflt", fused(0, ecg.HASH_CRC64)), ("crc64_tb3", fused(512 | 256, ecg.HASH_CRC64))]
+        # a configuration this shape has no instantiation for is dropped
+        ok = []
+        for n, fn in cfgs:
+            try:
+                fn()
+                ok.append((n, fn))
+            except ecg.EcgError:
+                L.ecg_set_csum_variant(ctx.h, 0)
+        cfgs = ok
         ts = {n: [] for n, _ in cfgs}
         for rnd in range(31):
             order = cfgs[rnd % len(cfgs):] + cfgs[:rnd % len(cfgs)]
@@ -55,8 +66,9 @@ def main():
         for n, v in ts.items():
             v.sort()
             row[n + "_ms"] = round(v[len(v) // 2], 4)
-        row["overhead_5bit"] = round(row["crc32_5bit_ms"] / row["encode_ms"] - 1, 4)
-        row["overhead_bytes"] = round(row["crc32_bytes_ms"] / row["encode_ms"] - 1, 4)
+        for n in list(row):
+            if n != "encode_ms":
+                row[n.replace("_ms", "_overhead")] = round(row[n] / row["encode_ms"] - 1, 4)
         res[f"{k}P{p}_x{S}"] = row
         print(k, p, row, flush=True)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
