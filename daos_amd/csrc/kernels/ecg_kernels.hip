@@ -172,63 +172,30 @@ __device__ __forceinline__ void mm_compute(const ecg_mm_params_t &P, const u32x4
 		}
 		continue;
 #endif
-		// sources in pairs: the 6 table terms of two sources fold into the
-		// accumulator with 3 three-input XORs (1.5 per source and row)
-		// instead of 2 per source
-#ifdef ECG_EXP_SERIAL_XOR
 		if (j < k) {
-			const bool two = false;		// experimental build: round 2's 2 XORs per source
-#else
-		if (j % 2 == 0 && j < k) {
-			const bool two = j + 1 < KM && j + 1 < k;
-#endif
-			u32x4 sel0[2], sel1[2], sel2[2];
+			u32x4 sel0, sel1, sel2;
 #pragma unroll
-			for (int h = 0; h < 2; h++) {
-				if (h == 0 || two) {
-#pragma unroll
-					for (int w = 0; w < 4; w++) {
-						const uint32_t v = x[j + h < KM ? j + h : j][w];
-						sel0[h][w] = v & 0x07070707u;
-						sel1[h][w] = (v >> 3) & 0x07070707u;
-						sel2[h][w] = (v >> 6) & 0x03030303u;
-					}
-				}
+			for (int w = 0; w < 4; w++) {
+				const uint32_t v = x[j][w];
+				sel0[w] = v & 0x07070707u;
+				sel1[w] = (v >> 3) & 0x07070707u;
+				sel2[w] = (v >> 6) & 0x03030303u;
 			}
-			const int j1 = j + 1 < KM ? j + 1 : j;
-			u32x4 t2va[T2V], t2vb[T2V];
+			u32x4 t2v[T2V];
 #pragma unroll
-			for (int q = 0; q < T2V; q++) {
-				t2va[q] = tb[j * PER_J + RM + q];
-				if (two)
-					t2vb[q] = tb[j1 * PER_J + RM + q];
-			}
+			for (int q = 0; q < T2V; q++)
+				t2v[q] = tb[j * PER_J + RM + q];
 #pragma unroll
 			for (int r = 0; r < RM; r++) {
 				if (r < rows) {
-					const u32x4 ta = tb[j * PER_J + r];
-					const uint32_t t2a = t2va[r / 4][r % 4];
-					if (two) {
-						const u32x4 tbb = tb[j1 * PER_J + r];
-						const uint32_t t2b = t2vb[r / 4][r % 4];
+					const u32x4 t = tb[j * PER_J + r];
+					const uint32_t t2 = t2v[r / 4][r % 4];
 #pragma unroll
-						for (int w = 0; w < 4; w++) {
-							const uint32_t a0 = __builtin_amdgcn_perm(ta[1], ta[0], sel0[0][w]);
-							const uint32_t a1 = __builtin_amdgcn_perm(ta[3], ta[2], sel1[0][w]);
-							const uint32_t a2 = __builtin_amdgcn_perm(t2a, t2a, sel2[0][w]);
-							const uint32_t b0 = __builtin_amdgcn_perm(tbb[1], tbb[0], sel0[1][w]);
-							const uint32_t b1 = __builtin_amdgcn_perm(tbb[3], tbb[2], sel1[1][w]);
-							const uint32_t b2 = __builtin_amdgcn_perm(t2b, t2b, sel2[1][w]);
-							acc[r][w] = xor3(xor3(acc[r][w], a0, a1), xor3(a2, b0, b1), b2);
-						}
-					} else {
-#pragma unroll
-						for (int w = 0; w < 4; w++) {
-							const uint32_t a0 = __builtin_amdgcn_perm(ta[1], ta[0], sel0[0][w]);
-							const uint32_t a1 = __builtin_amdgcn_perm(ta[3], ta[2], sel1[0][w]);
-							const uint32_t a2 = __builtin_amdgcn_perm(t2a, t2a, sel2[0][w]);
-							acc[r][w] = xor3(acc[r][w], a0, xor3(a1, a2, 0u));
-						}
+					for (int w = 0; w < 4; w++) {
+						const uint32_t p0 = __builtin_amdgcn_perm(t[1], t[0], sel0[w]);
+						const uint32_t p1 = __builtin_amdgcn_perm(t[3], t[2], sel1[w]);
+						const uint32_t p2 = __builtin_amdgcn_perm(t2, t2, sel2[w]);
+						acc[r][w] = xor3(acc[r][w], p0, xor3(p1, p2, 0u));
 					}
 				}
 			}

@@ -21,16 +21,24 @@ def main():
     L = ecg.lib()
     a, b = ctx.event(), ctx.event()
     C = 1 << 20
-    buf = ctx.alloc(4 << 30)
+    shapes = [tuple(int(x) for x in a.split(",")) for a in sys.argv[1:]] or [(8, 2, 512), (8, 3, 512)]
+    # every buffer sized for the largest shape (a shape past a buffer's end
+    # would read or write out of bounds: refuse it instead)
+    data_bytes = max(k * S * C for k, p, S in shapes)
+    par_bytes = max(p * (S * C + 4096) for k, p, S in shapes)
+    out_bytes = max(p * S * (C // 32768) * 8 for k, p, S in shapes)
+    if data_bytes > (8 << 30) or par_bytes > (4 << 30):
+        raise SystemExit(f"fused_tables_ab: shapes too large ({data_bytes} B data, {par_bytes} B parity)")
+    buf = ctx.alloc(data_bytes)
     blk = stripe_bytes(256 << 20, 13)
     for off in range(0, buf.nbytes, blk.size):
-        buf.upload(blk, offset=off)
-    par = ctx.alloc(3 * (512 * C + 4096))
-    out = ctx.alloc(1 << 22)
+        buf.upload(blk[:min(blk.size, buf.nbytes - off)], offset=off)
+    par = ctx.alloc(par_bytes)
+    out = ctx.alloc(out_bytes)
     res = {}
-    shapes = [tuple(int(x) for x in a.split(",")) for a in sys.argv[1:]] or [(8, 2, 512), (8, 3, 512)]
     for k, p, S in shapes:
         pitch = S * C + 4096
+        assert k * S * C <= buf.nbytes and p * pitch <= par.nbytes and p * S * (C // 32768) * 8 <= out.nbytes
 
         def fused(variant, htype=ecg.HASH_CRC32, k=k, p=p, S=S, pitch=pitch):
             def fn():

@@ -223,10 +223,7 @@ PY
 			> gpurun_out/crc_sq_summary.jsonl || exit $?
 		;;
 	fusedab)
-		step fused_tables_ab 600 python tools/fused_tables_ab.py 8,2,512 4,2,1024 16,2,1024 8,1,512 || exit $?
-		;;
-	eclibs2)
-		step ec_libs 900 python tools/ec_libs.py daos_amd/lib/libecg.so build/exp/serialxor/libecg.so || exit $?
+		step fused_tables_ab 600 python tools/fused_tables_ab.py 8,2,512 4,2,1024 16,2,256 8,1,512 || exit $?
 		;;
 	pmcjson)
 		python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write "ecg_mm_kernel<4, 2" 6442450944 \
