@@ -225,6 +225,14 @@ PY
 	fusedab)
 		step fused_tables_ab 600 python tools/fused_tables_ab.py 8,2,512 4,2,1024 16,2,256 8,1,512 || exit $?
 		;;
+	hostlib)
+		step hoststream_lib2 300 python bench.py --workload rebuild_stream_8p2 --gpus 2 --sharder lib \
+			--allow-shared-device --steps 5 --warmup 1 || exit $?
+		step hoststream_n1 300 python bench.py --workload rebuild_stream_8p2 --steps 5 --warmup 1 || exit $?
+		;;
+	placement)
+		step placement_sweep 600 python tools/placement_sweep.py || exit $?
+		;;
 	pmcjson)
 		python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write "ecg_mm_kernel<4, 2" 6442450944 \
 			gpurun_out/pmc_traffic.json || exit $?
