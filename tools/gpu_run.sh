@@ -233,6 +233,9 @@ PY
 	placement)
 		step placement_sweep 600 python tools/placement_sweep.py || exit $?
 		;;
+	placealloc)
+		step placement_alloc 600 python tools/placement_alloc.py || exit $?
+		;;
 	pmcjson)
 		python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write "ecg_mm_kernel<4, 2" 6442450944 \
 			gpurun_out/pmc_traffic.json || exit $?
