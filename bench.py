@@ -52,7 +52,7 @@ sys.path.insert(0, ROOT)
 GIB = float(1 << 30)
 PARITY_ROW_PAD = 4096
 HBM_PEAK_GBS = 8000.0          # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
-ROUND = "r02"
+ROUND = "r03"
 
 # name -> (k, p, cell bytes, stripes, ops, strong scaling?)
 WORKLOADS = {
@@ -818,8 +818,9 @@ def cpu_baseline(k, p, C, budget_s, ops=("enc", "dec"), per_config=True):
 
 def pmc_traffic():
     path = os.path.join(ROOT, "profiles", ROUND, "pmc_traffic.json")
-    if not os.path.exists(path):
-        path = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+    for older in ("r02", "r01"):
+        if not os.path.exists(path):
+            path = os.path.join(ROOT, "profiles", older, "pmc_traffic.json")
     if os.path.exists(path):
         try:
             d = json.load(open(path))
