@@ -4,7 +4,7 @@ cells (the bench row), data [S][k][C] -> parity [p][S][C] at the padded row
 pitch, crc32 / crc64 over 32 KiB chunks, the three launches interleaved for
 `rounds` rounds (default 12; the first few are the clock transient of
 profiles/r02/fused_transient/, tools/pmc_summary.py --skip drops them).  Run as
-  rocprofv3 --pmc SQ_WAVES ... -- python3 tools/fused_pmc.py [rounds]
+  rocprofv3 --pmc SQ_WAVES ... -- python3 tools/fused_pmc.py [rounds] [--lib=path/libecg.so]
 Bench infrastructure (no oracle)."""
 import os
 import sys
@@ -16,7 +16,11 @@ from tools.datagen import stripe_bytes  # noqa: E402
 
 
 def main():
-    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 12
+    args = [a for a in sys.argv[1:] if not a.startswith("--lib=")]
+    for a in sys.argv[1:]:
+        if a.startswith("--lib="):        # an experimental build (tools/build_exp.sh)
+            ecg.LIB_PATH = a.split("=", 1)[1]
+    rounds = int(args[0]) if args else 12
     ctx = ecg.Context(0)
     k, p, C, S = 8, 2, 1 << 20, 512
     data = ctx.alloc(k * S * C)

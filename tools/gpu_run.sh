@@ -260,18 +260,21 @@ PY
 			-d gpurun_out/pmc_fwrite -o run -- python3 tools/crc_pmc.py fused || exit $?
 		;;
 	fusedsq)
-		rm -rf gpurun_out/pmc_fsq1 gpurun_out/pmc_fsq2 gpurun_out/pmc_fgrbm
-		step rocprof_fsq1 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES \
+		# FUSED_LIB=path: counters of an experimental build instead (e.g. -DECG_EXP_NO_CRC)
+		lib=${FUSED_LIB:+--lib=$FUSED_LIB}
+		tag=${FUSED_TAG:-}
+		rm -rf gpurun_out/pmc_fsq1$tag gpurun_out/pmc_fsq2$tag gpurun_out/pmc_fgrbm$tag
+		step rocprof_fsq1$tag 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES \
 			SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_ANY \
-			--output-format csv -d gpurun_out/pmc_fsq1 -o run -- python3 tools/fused_pmc.py || exit $?
-		step rocprof_fsq2 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_LDS \
+			--output-format csv -d gpurun_out/pmc_fsq1$tag -o run -- python3 tools/fused_pmc.py $lib || exit $?
+		step rocprof_fsq2$tag 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_LDS \
 			SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE \
-			--output-format csv -d gpurun_out/pmc_fsq2 -o run -- python3 tools/fused_pmc.py || exit $?
-		step rocprof_fgrbm 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE GRBM_COUNT \
-			--output-format csv -d gpurun_out/pmc_fgrbm -o run -- python3 tools/fused_pmc.py || exit $?
-		python tools/pmc_summary.py --skip 6 gpurun_out/pmc_fsq1/run_counter_collection.csv \
-			gpurun_out/pmc_fsq2/run_counter_collection.csv gpurun_out/pmc_fgrbm/run_counter_collection.csv \
-			> gpurun_out/fused_sq_summary.jsonl || exit $?
+			--output-format csv -d gpurun_out/pmc_fsq2$tag -o run -- python3 tools/fused_pmc.py $lib || exit $?
+		step rocprof_fgrbm$tag 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE GRBM_COUNT \
+			--output-format csv -d gpurun_out/pmc_fgrbm$tag -o run -- python3 tools/fused_pmc.py $lib || exit $?
+		python tools/pmc_summary.py --skip 6 gpurun_out/pmc_fsq1$tag/run_counter_collection.csv \
+			gpurun_out/pmc_fsq2$tag/run_counter_collection.csv gpurun_out/pmc_fgrbm$tag/run_counter_collection.csv \
+			> gpurun_out/fused_sq_summary$tag.jsonl || exit $?
 		;;
 	ecpmc)
 		for w in dec_8p2 enc_16p2 dec_16p2; do
