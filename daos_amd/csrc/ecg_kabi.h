@@ -215,7 +215,8 @@ typedef struct ecg_csum_params {
 typedef struct ecg_mmcs_params {
 	const void *tbl;
 	uint8_t *out;
-	const void *kh;			/* (nh + nh_last) x 256 (crc16) or x 4 entries, T as tbl */
+	const void *kh;			/* (nh + nh_last) x 256 (crc16) or x 4 x [16][64] (reflected:
+					 * per-wave nibble tables, ecg_csum.c fused_kh), T as tbl */
 	uint64_t chunk_bytes;
 	uint64_t init, xorout, poly;
 	uint32_t nch;
@@ -226,7 +227,8 @@ typedef struct ecg_mmcs_params {
 	uint32_t nitems;
 	uint32_t byte_tables;		/* table kind TB: 0 5-bit, 1 slice-by-NB, 2 s16 */
 	uint32_t wave;			/* 1: one wave per (stripe, chunk) (ecg_mm_csum_wave_kernel):
-					 * kh = [2][64] lane multipliers (full chunk, last chunk),
+					 * kh = [2][64] lane multipliers (full chunk, last chunk;
+					 * reflected: [2][16][64] nibble tables of them),
 					 * checksums stored, not XORed (no zeroing needed) */
 	uint32_t pad3;
 	uint32_t row_slot[ECG_KMAX_R];

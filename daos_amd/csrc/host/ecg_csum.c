@@ -502,8 +502,11 @@ static uint32_t fused_cols(const ecg_ctx_t *ctx, uint64_t m, int type, int k, in
  * ecg_mmcs_params kh): row h < nh of a full chunk of m columns, rows nh + h of
  * the last chunk (m_last columns, z padding bytes):
  *   crc16:      kh[row][t] = x^(8*(16*(255-t) + 4096*(columns after item h))) * x^(-8z)
- *   reflected:  kh[row][w] = x^(8*(1024*(3-w) + 4096*(columns after item h))) * x^(-8z)
- *               (the lane part comes from the nibl tables)
+ *   reflected:  the factor f(row, w) = x^(8*(1024*(3-w) + 4096*(columns after
+ *               item h))) * x^(-8z) of wave w, folded into nibble tables with
+ *               the lane part: kh[row][w][n][l] = (n << (W-4)) *
+ *               x^(8*16*(63-l)) * f(row, w) -- the kernel multiplies a lane's
+ *               value by both in W/4 table steps, no scalar multiply
  * Cached per context by (type, chunk bytes, columns per item, last length). */
 static int fused_kh(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, uint32_t ncols,
 		    uint32_t nh, uint32_t nh_last, const void **out)
@@ -513,9 +516,10 @@ static int fused_kh(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, uint3
 	const uint64_t m_last = (last + ECG_MMCS_STRIDE - 1) / ECG_MMCS_STRIDE;
 	const uint64_t z = m_last * ECG_MMCS_STRIDE - last;
 	const size_t es = d->width == 64 ? 8 : 4, nrow = (size_t)nh + nh_last;
-	const size_t per = d->refl ? 4 : 256;	/* entries per row: waves or threads */
+	/* entries per row: 4 waves x [16][64] nibble tables, or 256 threads */
+	const size_t per = d->refl ? 4 * 16 * 64 : 256;
 	struct ecg_kh_ent *e;
-	uint64_t k256[256];
+	uint64_t k256[256], nibl[16 * 64];
 	unsigned char *img;
 	void *dev = NULL;
 	hipError_t he;
@@ -538,6 +542,9 @@ static int fused_kh(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, uint3
 	k256[255] = crc_one(d);
 	for (int t = 254; t >= 0; t--)
 		k256[t] = crc_mulmod(d, k256[t + 1], crc_xpow8(d, 16));
+	for (int n = 0; d->refl && n < 16; n++)
+		for (int l = 0; l < 64; l++)
+			nibl[n * 64 + l] = crc_mulmod(d, (uint64_t)n << (d->width - 4), k256[192 + l]);
 	for (size_t row = 0; row < nrow; row++) {
 		const int lastc = row >= nh;
 		const uint64_t h = lastc ? row - nh : row, mc = lastc ? m_last : m;
@@ -546,17 +553,29 @@ static int fused_kh(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, uint3
 
 		if (lastc)
 			sh = crc_mulmod(d, sh, crc_unshift(d, z));
-		for (size_t t = 0; t < per; t++) {
-			/* reflected: wave t's factor (k256[64 w + 63] = x^(8*16*(192-64w))
-			 * = x^(8*1024*(3-w))); crc16: thread t's */
-			const uint64_t v = crc_mulmod(d, k256[per == 4 ? 64 * t + 63 : t], sh);
+		uint64_t f = 0;
 
+		for (size_t t = 0; t < per; t++) {
+			uint64_t v;
+
+			if (d->refl) {
+				/* wave w's factor (k256[64 w + 63] = x^(8*16*(192-64w)) =
+				 * x^(8*1024*(3-w))) times nibl[n][l] = the nibble n at the
+				 * register's 4 lowest powers times lane l's k256[192 + l] */
+				const size_t w = t / 1024;
+
+				if (t % 1024 == 0)
+					f = crc_mulmod(d, k256[64 * w + 63], sh);
+				v = crc_mulmod(d, nibl[t % 1024], f);
+			} else {	/* crc16: thread t's */
+				v = crc_mulmod(d, k256[t], sh);
+			}
 			if (es == 8) {
 				memcpy(img + (row * per + t) * 8, &v, 8);
 			} else {
-				const uint32_t w = (uint32_t)v;
+				const uint32_t w32 = (uint32_t)v;
 
-				memcpy(img + (row * per + t) * 4, &w, 4);
+				memcpy(img + (row * per + t) * 4, &w32, 4);
 			}
 		}
 	}
@@ -598,7 +617,7 @@ static int fused_kw(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, const
 	const uint64_t z = m_last * ECG_CSUM_STRIDE - last;
 	const size_t es = d->width == 64 ? 8 : 4;
 	const uint64_t un = crc_unshift(d, z), step = crc_xpow8(d, 16);
-	unsigned char img[2 * 64 * 8];
+	unsigned char img[2 * 16 * 64 * 8];
 	struct ecg_kh_ent *e;
 	uint64_t c = crc_one(d);
 	void *dev = NULL;
@@ -613,23 +632,32 @@ static int fused_kw(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, const
 			return 0;
 		}
 	}
+	/* reflected CRCs: per row the [16][64] nibble tables of the lane factor,
+	 * kw[row][n][l] = (n << (W-4)) * k(row, l) (the kernel applies them in W/4
+	 * steps); crc16: the factors themselves, kw[row][l] */
+	const size_t per = d->refl ? 16 * 64 : 64;
+
 	for (int l = 63; l >= 0; l--) {
 		const uint64_t v[2] = {c, crc_mulmod(d, c, un)};
 
-		for (int row = 0; row < 2; row++) {
-			if (es == 8) {
-				memcpy(img + (row * 64 + l) * 8, &v[row], 8);
-			} else {
-				const uint32_t w = (uint32_t)v[row];
+		for (int row = 0; row < 2; row++)
+			for (int n = 0; n < (d->refl ? 16 : 1); n++) {
+				const uint64_t x = d->refl ? crc_mulmod(d, (uint64_t)n << (d->width - 4), v[row]) : v[row];
+				const size_t at = (size_t)row * per + (size_t)n * 64 + (size_t)l;
 
-				memcpy(img + (row * 64 + l) * 4, &w, 4);
+				if (es == 8) {
+					memcpy(img + at * 8, &x, 8);
+				} else {
+					const uint32_t w = (uint32_t)x;
+
+					memcpy(img + at * 4, &w, 4);
+				}
 			}
-		}
 		c = crc_mulmod(d, c, step);
 	}
-	he = hipMalloc(&dev, 2 * 64 * es);
+	he = hipMalloc(&dev, 2 * per * es);
 	if (he == hipSuccess)
-		he = hipMemcpy(dev, img, 2 * 64 * es, hipMemcpyHostToDevice);
+		he = hipMemcpy(dev, img, 2 * per * es, hipMemcpyHostToDevice);
 	if (he != hipSuccess) {
 		if (dev)
 			(void)hipFree(dev);

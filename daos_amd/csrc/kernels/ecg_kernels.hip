@@ -565,8 +565,7 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	__shared__ T s_sl[NSL];
 	// TB 1/2: the column shift as 5-bit a5 tables; TB 3: as nibble a4 tables
 	__shared__ T s_sh[TB == 3 ? 16 * 16 : TB ? ECG_CSUM_NA5(NB) * 32 : 1];
-	__shared__ T s_nib[REFL ? 16 * 64 : 1];		// reflected: lane multiply tables
-	__shared__ T s_r4[REFL ? 16 : 1];
+	__shared__ T s_r4[REFL ? 16 : 1];		// reflected: 4-bit reduction of the lane multiply
 	const int k = K ? K : (int)P.k;
 	const int rows = R ? R : (int)P.rows;
 	const uint64_t C = P.cell_bytes;
@@ -574,8 +573,6 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	const T *gt = (const T *)Q.tbl;
 
 	if constexpr (REFL) {
-		for (int i = threadIdx.x; i < 16 * 64; i += BLOCK)
-			s_nib[i] = gt[ECG_CSUM_OFF_NIBL(NB) + i];
 		if (threadIdx.x < 16)
 			s_r4[threadIdx.x] = gt[ECG_CSUM_OFF_R4(NB) + threadIdx.x];
 	}
@@ -654,26 +651,25 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 					i == 0 && threadIdx.x == 0, Q.init, (col1 - 1 - i) % UF, true, xa, xa, crc);
 			// each wave XORs its partial into the (zeroed) output: no
 			// workgroup barrier, other waves keep streaming.  Reflected CRCs:
-			// lane l's value times x^(8*16*(63-l)) nibble by nibble (W/4 steps
-			// of two conflict-free LDS lookups), the wave XOR-reduces, and the
-			// wave's uniform factor kh[khrow][wave] is applied once, on the
-			// scalar unit -- instead of a W-step GF(2) multiply per thread on
-			// the VALU (crc64: 64 steps of 64-bit ops).
+			// every lane's value is multiplied by its own and its wave's
+			// factors in one nibble-table pass (W/4 steps) and the wave
+			// XOR-reduces; crc16: a W-step multiply per thread.
 #pragma unroll
 			for (int r = 0; r < RM; r++) {
 				if (r < rows) {
 					T v;
 					if constexpr (REFL) {
+						// lane l's value times lane l's AND this wave's item factor,
+						// x^(8*16*(63-l)) * kh[item row][wave], nibble by nibble from
+						// the per-(row, wave) tables Q.kh[row*4 + wave][16][64] (HBM,
+						// L2-resident: the W/4 loads depend only on the value and
+						// issue together); the waves' values then just XOR --
+						// no scalar W-step multiply per item (SQ counters:
+						// profiles/r03/fused_sq)
 						const uint32_t lane = threadIdx.x & 63u;
-						const T x = crc[r];
-						T u = 0;
-#pragma unroll
-						for (int sft = 0; sft < W; sft += 4)
-							u = (u >> 4) ^ s_r4[(uint32_t)u & 15u] ^
-							    s_nib[((uint32_t)(x >> sft) & 15u) * 64u + lane];
-						u = ecg_crc::wave_xor(u);
 						const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-						v = ecg_crc::mulmod<W, REFL>(kh[khrow * 4u + wv], ecg_crc::uniform(u), poly);
+						const T *tab = kh + ((size_t)khrow * 4u + wv) * (16u * 64u);
+						v = ecg_crc::wave_xor(ecg_crc::lane_mul_nib<W>(crc[r], tab, s_r4, lane));
 					} else {
 						v = ecg_crc::mulmod<W, REFL>(kh[khrow * 256 + threadIdx.x], crc[r], poly);
 						v = ecg_crc::wave_xor(v);
@@ -721,6 +717,7 @@ ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	__shared__ T s_sl[NSL];
 	// TB 1/2: the row shift as 5-bit a5 tables; TB 3: as nibble a4 tables
 	__shared__ T s_sh[TB == 3 ? 16 * 16 : TB ? ECG_CSUM_NA5(NB) * 32 : 1];
+	__shared__ T s_r4[REFL ? 16 : 1];		// reflected: 4-bit reduction of the lane multiply
 	const int k = K ? K : (int)P.k;
 	const int rows = R ? R : (int)P.rows;
 	const uint64_t C = P.cell_bytes;
@@ -749,6 +746,8 @@ ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 		ecg_crc::stage5u<W>(s_sl, gt, ECG_CSUM_OFF_P5X_1K(NB), ECG_CSUM_OFF_A5_4K(NB), BLOCK);
 	}
 	const T *kw = (const T *)Q.kh;
+	if (REFL && threadIdx.x < 16)
+		s_r4[threadIdx.x] = gt[ECG_CSUM_OFF_R4(NB) + threadIdx.x];
 	const T poly = (T)Q.poly;
 	__syncthreads();
 
@@ -793,11 +792,14 @@ ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 			mmcs_col<KM, RM, W, REFL, TB, false, ECG_CSUM_STRIDE, false, F5::U>(
 				P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)i * ECG_CSUM_STRIDE, 0, lo, false,
 				i == 0 && lane == 0, Q.init, (m - 1 - i) % F5::U, true, xa, xa, crc);
-		const T kcur = kw[(lastc ? 64 : 0) + lane];
+		// reflected: Q.kh = [2][16][64] nibble tables of the lane factor
+		// (full / last chunk, ecg_csum.c fused_kw), W/4 steps; crc16: [2][64]
+		const T kcur = REFL ? (T)0 : kw[(lastc ? 64 : 0) + lane];
 #pragma unroll
 		for (int r = 0; r < RM; r++) {
 			if (r < rows) {
-				T v = ecg_crc::mulmod<W, REFL>(kcur, crc[r], poly);
+				T v = REFL ? ecg_crc::lane_mul_nib<W>(crc[r], kw + (lastc ? 1024 : 0), s_r4, (uint32_t)lane)
+					   : ecg_crc::mulmod<W, REFL>(kcur, crc[r], poly);
 				v = ecg_crc::wave_xor(v);
 				if (lane == 0) {
 					const uint64_t slot = ((uint64_t)Q.row_slot[r] * P.nstripes + s) * Q.nch + c;
