@@ -146,12 +146,7 @@ typedef struct ecg_launch_cfg {
 #define ECG_CSUM_OFF_A4_1K(NB) (ECG_CSUM_OFF_Q4_256(NB) + ECG_CSUM_P5U * ECG_CSUM_NQ4)
 #define ECG_CSUM_OFF_Q4_4K(NB) (ECG_CSUM_OFF_A4_1K(NB) + 256)
 #define ECG_CSUM_OFF_A4_32K(NB) (ECG_CSUM_OFF_Q4_4K(NB) + ECG_MMCS_P5U * ECG_CSUM_NQ4)
-/* lane factors as independent nibble lookups (reflected CRCs; the fused
- * workgroup kernel's item end): ln16[i][n][l] = (n << 4i) * x^(8*16*(63-l)),
- * i < W/4 -- a lane's value times its factor is the XOR of W/4 lookups that
- * all issue at once, no serial 4-bit Horner chain */
-#define ECG_CSUM_OFF_LN16(NB) (ECG_CSUM_OFF_A4_32K(NB) + 256)
-#define ECG_CSUM_TBL_ENTRIES(NB) (ECG_CSUM_OFF_LN16(NB) + 16 * 16 * 64)
+#define ECG_CSUM_TBL_ENTRIES(NB) (ECG_CSUM_OFF_A4_32K(NB) + 256)
 #define ECG_CSUM_OFF_P2(NB) (3 * (NB) * 256 + 64 + 256)
 #define ECG_CSUM_OFF_SH256(NB) (3 * (NB) * 256 + 64 + 256 + ECG_CSUM_NP2)
 #define ECG_CSUM_GLANES 16	/* lanes per chunk in the lane-group CRC kernel */
@@ -220,9 +215,8 @@ typedef struct ecg_csum_params {
 typedef struct ecg_mmcs_params {
 	const void *tbl;
 	uint8_t *out;
-	const void *kh;			/* (nh + nh_last) x 256 (crc16) or x 4 x [W/4][16] (reflected:
-					 * per-(item row, wave) factors as nibble lookups,
-					 * ecg_csum.c fused_kh), T as tbl */
+	const void *kh;			/* (nh + nh_last) x 256 (crc16) or x 4 x [16][64] (reflected:
+					 * per-wave nibble tables, ecg_csum.c fused_kh), T as tbl */
 	uint64_t chunk_bytes;
 	uint64_t init, xorout, poly;
 	uint32_t nch;

@@ -405,12 +405,6 @@ static void *build_crc_tables(const struct crc_def *d, size_t *bytes)
 	for (int u = 0; u < ECG_MMCS_P5U; u++)
 		build_q4(d, (uint64_t)u * ECG_MMCS_STRIDE, t + ECG_CSUM_OFF_Q4_4K(nb) + (size_t)u * ECG_CSUM_NQ4);
 	build_a4(d, (uint64_t)ECG_MMCS_P5U * ECG_MMCS_STRIDE, t + ECG_CSUM_OFF_A4_32K(nb));
-	if (d->refl)	/* ln16[i][n][l] = (n << 4i) * x^(8*16*(63-l)) */
-		for (int i = 0; i < d->width / 4; i++)
-			for (int n = 0; n < 16; n++)
-				for (int l = 0; l < 64; l++)
-					t[ECG_CSUM_OFF_LN16(nb) + ((size_t)i * 16 + n) * 64 + l] =
-						crc_mulmod(d, (uint64_t)n << (4 * i), t[ECG_CSUM_OFF_K64(nb) + l]);
 
 	*bytes = n * (size_t)es;
 	if (es == 8)
@@ -509,10 +503,10 @@ static uint32_t fused_cols(const ecg_ctx_t *ctx, uint64_t m, int type, int k, in
  * the last chunk (m_last columns, z padding bytes):
  *   crc16:      kh[row][t] = x^(8*(16*(255-t) + 4096*(columns after item h))) * x^(-8z)
  *   reflected:  the factor f(row, w) = x^(8*(1024*(3-w) + 4096*(columns after
- *               item h))) * x^(-8z) of wave w as nibble lookups,
- *               kh[row][w][i][n] = (n << 4i) * f(row, w), i < W/4: lane 0
- *               multiplies the wave's XOR-reduced value by it in W/4
- *               independent lookups (the lane part: ln16 in the CRC tables)
+ *               item h))) * x^(-8z) of wave w, folded into nibble tables with
+ *               the lane part: kh[row][w][n][l] = (n << (W-4)) *
+ *               x^(8*16*(63-l)) * f(row, w) -- the kernel multiplies a lane's
+ *               value by both in W/4 table steps, no scalar multiply
  * Cached per context by (type, chunk bytes, columns per item, last length). */
 static int fused_kh(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, uint32_t ncols,
 		    uint32_t nh, uint32_t nh_last, const void **out)
@@ -522,12 +516,10 @@ static int fused_kh(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, uint3
 	const uint64_t m_last = (last + ECG_MMCS_STRIDE - 1) / ECG_MMCS_STRIDE;
 	const uint64_t z = m_last * ECG_MMCS_STRIDE - last;
 	const size_t es = d->width == 64 ? 8 : 4, nrow = (size_t)nh + nh_last;
-	/* entries per row: 4 waves x [W/4][16] nibble lookups of the wave's
-	 * factor, or 256 threads' factors (crc16) */
-	const size_t nq = (size_t)d->width / 4;
-	const size_t per = d->refl ? 4 * nq * 16 : 256;
+	/* entries per row: 4 waves x [16][64] nibble tables, or 256 threads */
+	const size_t per = d->refl ? 4 * 16 * 64 : 256;
 	struct ecg_kh_ent *e;
-	uint64_t k256[256];
+	uint64_t k256[256], nibl[16 * 64];
 	unsigned char *img;
 	void *dev = NULL;
 	hipError_t he;
@@ -550,6 +542,9 @@ static int fused_kh(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, uint3
 	k256[255] = crc_one(d);
 	for (int t = 254; t >= 0; t--)
 		k256[t] = crc_mulmod(d, k256[t + 1], crc_xpow8(d, 16));
+	for (int n = 0; d->refl && n < 16; n++)
+		for (int l = 0; l < 64; l++)
+			nibl[n * 64 + l] = crc_mulmod(d, (uint64_t)n << (d->width - 4), k256[192 + l]);
 	for (size_t row = 0; row < nrow; row++) {
 		const int lastc = row >= nh;
 		const uint64_t h = lastc ? row - nh : row, mc = lastc ? m_last : m;
@@ -564,14 +559,14 @@ static int fused_kh(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, uint3
 			uint64_t v;
 
 			if (d->refl) {
-				/* wave w's factor f (k256[64 w + 63] = x^(8*16*(192-64w)) =
-				 * x^(8*1024*(3-w)), times the item's shift) applied to the
-				 * nibble n at bits 4i: entry [w][i][n] = (n << 4i) * f */
-				const size_t w = t / (nq * 16), i = (t / 16) % nq, n = t % 16;
+				/* wave w's factor (k256[64 w + 63] = x^(8*16*(192-64w)) =
+				 * x^(8*1024*(3-w))) times nibl[n][l] = the nibble n at the
+				 * register's 4 lowest powers times lane l's k256[192 + l] */
+				const size_t w = t / 1024;
 
-				if (t % (nq * 16) == 0)
+				if (t % 1024 == 0)
 					f = crc_mulmod(d, k256[64 * w + 63], sh);
-				v = crc_mulmod(d, (uint64_t)n << (4 * i), f);
+				v = crc_mulmod(d, nibl[t % 1024], f);
 			} else {	/* crc16: thread t's */
 				v = crc_mulmod(d, k256[t], sh);
 			}

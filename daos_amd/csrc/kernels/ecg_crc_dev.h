@@ -404,24 +404,6 @@ __device__ __forceinline__ T lin_map4(T acc, const T *a4)
 	return c;
 }
 
-// x * K as the XOR of W/4 independent lookups tab[(i*16 + nibble_i(x))*stride
-// + idx] (tab[i][n] = (n << 4i) * K for the column idx): every load depends
-// only on x, so they all issue together -- one memory latency instead of
-// lane_mul_nib's serial 4-bit Horner chain
-template <int W, typename T>
-__device__ __forceinline__ T nib_mul_ind(T x, const T *tab, uint32_t stride, uint32_t idx)
-{
-	T n[W / 4];
-#pragma unroll
-	for (int i = 0; i < W / 4; i++)
-		n[i] = tab[((uint32_t)i * 16u + ((uint32_t)(x >> (4 * i)) & 15u)) * stride + idx];
-	T u = 0;
-#pragma unroll
-	for (int i = 0; i < W / 4; i += 2)
-		u = i + 1 < W / 4 ? x3(u, n[i], n[i + 1]) : u ^ n[i];
-	return u;
-}
-
 // register -> register shifted by the a5 table's fixed number of zero bytes
 template <int W, typename T>
 __device__ __forceinline__ T lin_map5(T c, const T *a5)

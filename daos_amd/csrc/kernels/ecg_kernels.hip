@@ -565,12 +565,17 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	__shared__ T s_sl[NSL];
 	// TB 1/2: the column shift as 5-bit a5 tables; TB 3: as nibble a4 tables
 	__shared__ T s_sh[TB == 3 ? 16 * 16 : TB ? ECG_CSUM_NA5(NB) * 32 : 1];
+	__shared__ T s_r4[REFL ? 16 : 1];		// reflected: 4-bit reduction of the lane multiply
 	const int k = K ? K : (int)P.k;
 	const int rows = R ? R : (int)P.rows;
 	const uint64_t C = P.cell_bytes;
 	const uint32_t lo = threadIdx.x * 16u;
 	const T *gt = (const T *)Q.tbl;
 
+	if constexpr (REFL) {
+		if (threadIdx.x < 16)
+			s_r4[threadIdx.x] = gt[ECG_CSUM_OFF_R4(NB) + threadIdx.x];
+	}
 
 	for (int i = threadIdx.x; i < KM * RM; i += BLOCK) {
 		const int j = i / RM, r = i % RM;
@@ -661,16 +666,10 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 						// issue together); the waves' values then just XOR --
 						// no scalar W-step multiply per item (SQ counters:
 						// profiles/r03/fused_sq)
-						// lane l's value times x^(8*16*(63-l)) (ln16: W/4 independent
-						// lookups, L2-resident), the wave XOR-reduces, lane 0 applies
-						// the wave's item factor (W/4 lookups of kh[row][wave]):
-						// two memory latencies per item row, no serial chain, no
-						// scalar multiply (profiles/r03/fused_sq)
 						const uint32_t lane = threadIdx.x & 63u;
 						const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-						v = ecg_crc::wave_xor(ecg_crc::nib_mul_ind<W>(crc[r], gt + ECG_CSUM_OFF_LN16(NB), 64u, lane));
-						if (lane == 0)
-							v = ecg_crc::nib_mul_ind<W>(v, kh + ((size_t)khrow * 4u + wv) * (W / 4 * 16), 1u, 0u);
+						const T *tab = kh + ((size_t)khrow * 4u + wv) * (16u * 64u);
+						v = ecg_crc::wave_xor(ecg_crc::lane_mul_nib<W>(crc[r], tab, s_r4, lane));
 					} else {
 						v = ecg_crc::mulmod<W, REFL>(kh[khrow * 256 + threadIdx.x], crc[r], poly);
 						v = ecg_crc::wave_xor(v);
