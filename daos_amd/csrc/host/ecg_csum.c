@@ -31,13 +31,18 @@ static const struct crc_def g_defs[4] = {
  * piece, 35 / 42 lookups): crc16 / crc32; crc64 keeps the byte tables there
  * (24 conflicted eight-byte lookups, no slower).  csum_variant bit 4 forces
  * the byte tables, bit 5 the 5-bit tables (A/B runs). */
-static uint32_t use_byte_tables(const ecg_ctx_t *ctx, int type, int fused)
+static uint32_t use_byte_tables(const ecg_ctx_t *ctx, int type, int fused, int k, int rows)
 {
 	if (ctx->csum_variant & 16u)
 		return 1;
 	if (ctx->csum_variant & 32u)
 		return 0;
-	return fused && type == ECG_HASH_CRC64;
+	/* crc32 at EC_8P2 (k = 8, two rows) too: the byte tables beat the 5-bit
+	 * ones in every measurement of that shape -- by 1.5-3.5 % (round 2,
+	 * profiles/r02/fused_tables_ab/), 3.7 % (profiles/r03/fused_tb3/) and
+	 * 3.9 % (profiles/r03/fused_sq/fused_libs_full_vs_nocrc.json, wgb) --
+	 * and lose at every other shape measured (k = 4, 16, one or three rows) */
+	return fused && (type == ECG_HASH_CRC64 || (type == ECG_HASH_CRC32 && k == 8 && rows == 2));
 }
 
 /* Standalone CRC kernels (ecg_csum_params_t.byte_tables): 2 = nibble tables
@@ -838,7 +843,8 @@ int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t
 	q->nitems = (q->nch - 1) * q->nh + q->nh_last;
 	/* fused kernels: table kind TB (ecg_kernels.hip); bit 6 of csum_variant
 	 * selects the s16 tables (A/B), bit 7 the wave-per-chunk kernel */
-	q->byte_tables = (ctx->csum_variant & 512u) ? 3 : (ctx->csum_variant & 64u) ? 2 : use_byte_tables(ctx, type, 1);
+	q->byte_tables = (ctx->csum_variant & 512u) ? 3 : (ctx->csum_variant & 64u) ? 2
+			 : use_byte_tables(ctx, type, 1, k, rows);
 	/* the wave-per-chunk kernel for crc64 with k <= 4 (one 64-step multiply
 	 * per lane per chunk instead of per thread per item: EC_4P2 crc64 +42 %
 	 * -> +29 % over the plain encode; with k = 8 its longer serial walk
