@@ -852,8 +852,12 @@ int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t
 	 * bit 7 forces it, bit 8 forbids it (A/B) */
 	q->wave = (ctx->csum_variant & 128u) != 0 ||
 		  (!(ctx->csum_variant & 256u) && type == ECG_HASH_CRC64 && k <= 4);
-	if (q->wave)
+	if (q->wave) {
+		/* the wave kernel is instantiated with the per-hash default tables
+		 * only (byte tables for crc64, 5-bit for crc16 / crc32) */
+		q->byte_tables = type == ECG_HASH_CRC64;
 		return fused_kw(ctx, type, rcs, last, &q->kh) ? -ECG_DER_NOMEM : 1;
+	}
 	rc = fused_kh(ctx, type, rcs, last, q->ncols, q->nh, q->nh_last, &q->kh);
 	if (rc)
 		return rc;

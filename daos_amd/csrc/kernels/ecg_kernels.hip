@@ -1314,8 +1314,8 @@ extern "C" int ecg_k_launch_matmul_csum(const ecg_mm_params_t *p, const ecg_mmcs
 		for (uint32_t i = 0; i < n && w == n; i++)
 			if (tab[i].type == (int)q->type && tab[i].k == 0 && tab[i].b8 == (int)q->byte_tables)
 				w = i;
-		if (w == n || q->kh == nullptr)
-			return (int)hipErrorInvalidValue;
+		if (w == n || q->kh == nullptr)	// no instantiation (not 1: that means "two-pass")
+			return (int)hipErrorInvalidDeviceFunction;
 		const uint64_t items = (uint64_t)p->nstripes * q->nch;
 		uint64_t gx = (items + BLOCK / 64 - 1) / (BLOCK / 64);
 		if (cfg && cfg->grid_x)
@@ -1340,10 +1340,10 @@ extern "C" int ecg_k_launch_matmul_csum(const ecg_mm_params_t *p, const ecg_mmcs
 				id = i;
 				break;
 			}
-	if (id == N_CSKERNELS)
-		return (int)hipErrorInvalidValue;
+	if (id == N_CSKERNELS)			// no instantiation (not 1: that means "two-pass")
+		return (int)hipErrorInvalidDeviceFunction;
 	if (q->nitems == 0 || q->ncols == 0 || q->kh == nullptr)
-		return (int)hipErrorInvalidValue;
+		return (int)hipErrorInvalidDeviceFunction;
 	// default: ~16 KiB of columns per workgroup (tools/tune8.py,
 	// profiles/r01/tune8_fused_chunks.json: walking more columns per
 	// workgroup loses HBM parallelism, fewer pays a reduction per column);
