@@ -584,6 +584,11 @@ int ecg_matmul_csum(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, 
 			ecg_set_last_kernel(ecg_k_kernel_name(kid));
 			return 0;
 		}
+		/* a tuning variant (ecg_set_csum_variant) may ask for a table kind
+		 * or shape that is not instantiated for these (k, rows): the two
+		 * passes then; the default choice must always exist */
+		if (e == (int)hipErrorInvalidDeviceFunction && ctx->csum_variant != 0)
+			e = 1;
 		if (e != 1)
 			return ecg_hip_fail((hipError_t)e, "fused kernel launch");
 		/* e == 1: operands not 16-byte aligned -> two-pass path */
