@@ -620,7 +620,11 @@ def detail_rows(ctx, ceil, iters=11):
             fn = (lambda buf=buf, k=k, p=p, C=C, S=S, st=st:
                   ctx.recover(k, p, C, S, buf.ptr, st, [0, 1]))
             rd, wr = k, 2
-        ms = time_kernel(ctx, fn, iters)
+        # 10 warm-up launches: the launch tuner (include/ecg.h ecg_set_autotune) times its
+        # two arms over the first 8 launches of a wide shape; the timed launches run its choice
+        ms = time_kernel(ctx, fn, iters, warm=10)
+        tuned = (ctx.tune_state(k, p, C, S, k * C, C) if mode == "enc"
+                 else ctx.tune_state(k, 2, C, S, st, st))
         alg = (rd + wr) * C * S
         gbs = alg / ms / 1e6
         mix = mix_ceiling(ceil, rd / (rd + wr))
@@ -630,6 +634,9 @@ def detail_rows(ctx, ceil, iters=11):
                       "measured_mix_ceiling_GBps": round(mix, 1), "frac_of_measured_mix": round(gbs / mix, 4),
                       "kernel": ecg.last_kernel(), "ms": round(ms, 4),
                       "layout": "client [S][k][C] -> [p][S][C]" if mode == "enc" else "recovery [S][k+p][C]"}
+        if tuned is not None:
+            rows[name]["launch_tuner"] = {"wg_per_cu": None if tuned[0] == 255 else tuned[0],
+                                          "uncapped_ms": round(tuned[1], 4), "capped_ms": round(tuned[2], 4)}
         buf.free()
         if buf2 is not None:
             buf2.free()

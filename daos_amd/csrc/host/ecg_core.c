@@ -111,6 +111,11 @@ int ecg_ctx_create(int device, ecg_ctx_t **out)
 		free(ctx);
 		return ecg_hip_fail(e, "ctx_create");
 	}
+	if (ecg_tune_init(ctx)) {
+		(void)hipStreamDestroy(ctx->stream);
+		free(ctx);
+		return -ECG_DER_NOMEM;
+	}
 	*out = ctx;
 	return 0;
 }
@@ -139,6 +144,7 @@ void ecg_ctx_destroy(ecg_ctx_t *ctx)
 	stage_free(ctx);
 	ecg_scratch_free(ctx);
 	ecg_csum_ctx_fini(ctx);
+	ecg_tune_fini(ctx);
 	(void)hipStreamDestroy(ctx->stream);
 	pthread_mutex_destroy(&ctx->lock);
 	free(ctx);
@@ -237,7 +243,7 @@ static int launch(ecg_ctx_t *ctx, const ecg_mm_params_t *prm, hipStream_t st)
 	int e;
 
 	ecg_trace_push("ecg:launch");
-	e = ecg_k_launch_matmul(prm, &ctx->cfg, (void *)st, &kid);
+	e = ecg_tune_launch(ctx, prm, st, &kid);
 	ecg_trace_pop();
 	if (e != 0)
 		return ecg_hip_fail((hipError_t)e, "kernel launch");

@@ -80,6 +80,7 @@ struct ecg_ctx {
 	} kh_cache[ECG_NKH_CACHE];
 	unsigned kh_next;
 	struct ecg_scratch scratch;
+	struct ecg_tuner *tuner;	/* blocks-per-CU cap per shape (ecg_tune.c) */
 	ecg_stats_t stats;		/* telemetry (ecg_get_stats), updated with atomics */
 };
 
@@ -155,6 +156,14 @@ int ecg_parse_devices(const char *spec, int *dev, int max);
 void ecg_trace_push(const char *name);
 void ecg_trace_pop(void);
 int ecg_trace_active(void);
+
+/* launch tuner (ecg_tune.c): product launches of wide shapes measure the
+ * blocks-per-CU cap against none and keep the faster */
+#define ECG_NTUNE 16
+struct ecg_tuner;
+int ecg_tune_init(ecg_ctx_t *ctx);
+void ecg_tune_fini(ecg_ctx_t *ctx);
+int ecg_tune_launch(ecg_ctx_t *ctx, const ecg_mm_params_t *p, hipStream_t st, uint32_t *kid);
 
 /* context helpers (ecg_core.c) */
 int ecg_ctx_enter(ecg_ctx_t *ctx);

@@ -1,0 +1,311 @@
+/*
+ * ecg_tune.c -- per-context launch tuner for the product kernel's
+ * blocks-per-CU cap.
+ *
+ * Wide stripes (k = 8, 16) keep k + rows cell streams in flight per block;
+ * with every block the registers allow resident, the HBM streams of an
+ * EC_16P2 launch run up to ~9 % below what the same launch reaches at 2
+ * blocks per CU -- on some boxes.  Round 2 and 3 measured the sign of the
+ * effect per box and per timing pattern: back to back the cap
+ * won on one box in every allocation trial and lost 4-6 % on another, and no
+ * pointer residue predicts it.  The library therefore measures instead of
+ * guessing: the first launches of each large wide shape in a context run as
+ * two back-to-back blocks -- ECG_TUNE_W + ECG_TUNE_T launches uncapped, then
+ * as many at the candidate cap -- timed with HIP events on the launch stream;
+ * once the events have completed (queried without blocking on a later launch
+ * of the shape) the faster arm is kept for the shape, the cap only when it
+ * wins by more than ECG_TUNE_MARGIN.  Results never depend on the choice
+ * (tests/test_gpu_tuning.py); only launch geometry does.
+ *
+ * Not tuned: launches with an explicit ecg_set_wg_per_cu, grids of <= 2048
+ * blocks (latency-bound), k <= 4 (every cap loses, profiles/r02/wg_cap),
+ * streams under graph capture, and contexts with tuning off
+ * (ecg_set_autotune(ctx, 0) or ECG_AUTOTUNE=0 in the environment).
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "ecg_internal.h"
+
+#define ECG_TUNE_W 1		/* untimed launches at the start of each arm */
+#define ECG_TUNE_T 3		/* timed launches per arm (median) */
+#define ECG_TUNE_ARM (ECG_TUNE_W + ECG_TUNE_T)
+#define ECG_TUNE_MARGIN 0.015	/* the cap must win by more than 1.5 % */
+
+struct ecg_tune_ent {
+	int valid, decided, events;
+	uint32_t k, rows, acc, diff;
+	uint64_t C;
+	uint32_t S;
+	int64_t sstride, dstride;	/* layout: encode and recovery shapes differ here */
+	uint32_t cand;		/* candidate cap */
+	uint32_t choice;	/* decided: the cap, or ECG_WG_UNCAPPED */
+	uint32_t n;		/* launches of the shape so far */
+	uint64_t stamp;
+	hipEvent_t ev[2][ECG_TUNE_T][2];
+	float ms[2];		/* decided: median per arm */
+};
+
+struct ecg_tuner {
+	pthread_mutex_t lock;
+	int enabled;		/* -1 = not yet read from the environment */
+	uint64_t clock;
+	struct ecg_tune_ent ent[ECG_NTUNE];
+};
+
+static uint32_t candidate_cap(const ecg_mm_params_t *p)
+{
+	const uint64_t blocks = ((p->cell_bytes + 4095) / 4096) * (uint64_t)p->nstripes;
+
+	if (blocks <= 2048 || p->rows == 0)
+		return 0;
+	if (p->k >= 16)
+		return 2;	/* profiles/r02/wg_cap: k = 16 best at 2 blocks per CU */
+	if (p->k >= 8)
+		return 3;	/* k = 8 at 3 */
+	return 0;
+}
+
+int ecg_tune_init(ecg_ctx_t *ctx)
+{
+	struct ecg_tuner *t = calloc(1, sizeof(*t));
+
+	if (t == NULL)
+		return ecg_fail(-ECG_DER_NOMEM, "tune_init: calloc");
+	pthread_mutex_init(&t->lock, NULL);
+	t->enabled = -1;
+	ctx->tuner = t;
+	return 0;
+}
+
+static void ent_free(struct ecg_tune_ent *e)
+{
+	int a, i, j;
+
+	if (e->events)
+		for (a = 0; a < 2; a++)
+			for (i = 0; i < ECG_TUNE_T; i++)
+				for (j = 0; j < 2; j++)
+					(void)hipEventDestroy(e->ev[a][i][j]);
+	memset(e, 0, sizeof(*e));
+}
+
+void ecg_tune_fini(ecg_ctx_t *ctx)
+{
+	struct ecg_tuner *t = ctx->tuner;
+	int i;
+
+	if (t == NULL)
+		return;
+	for (i = 0; i < ECG_NTUNE; i++)
+		ent_free(&t->ent[i]);
+	pthread_mutex_destroy(&t->lock);
+	free(t);
+	ctx->tuner = NULL;
+}
+
+static int enabled(struct ecg_tuner *t)
+{
+	if (t->enabled < 0) {
+		const char *s = getenv("ECG_AUTOTUNE");
+
+		t->enabled = !(s && s[0] == '0');
+	}
+	return t->enabled;
+}
+
+int ecg_set_autotune(ecg_ctx_t *ctx, int on)
+{
+	struct ecg_tuner *t;
+	int i;
+
+	if (ctx == NULL || ctx->tuner == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "set_autotune: NULL context");
+	t = ctx->tuner;
+	pthread_mutex_lock(&t->lock);
+	t->enabled = on ? 1 : 0;
+	if (on < 0 || on > 1) {		/* 2: forget every decision, tuning on */
+		for (i = 0; i < ECG_NTUNE; i++)
+			ent_free(&t->ent[i]);
+		t->enabled = 1;
+	}
+	pthread_mutex_unlock(&t->lock);
+	return 0;
+}
+
+static int same_shape(const struct ecg_tune_ent *e, const ecg_mm_params_t *p)
+{
+	return e->valid && e->k == p->k && e->rows == p->rows && e->acc == p->accumulate && e->diff == p->diff &&
+	       e->C == p->cell_bytes && e->S == p->nstripes &&
+	       e->sstride == p->src_stripe_stride && e->dstride == p->dst_stripe_stride;
+}
+
+static struct ecg_tune_ent *lookup(struct ecg_tuner *t, const ecg_mm_params_t *p, int create)
+{
+	struct ecg_tune_ent *old = &t->ent[0];
+	int i;
+
+	for (i = 0; i < ECG_NTUNE; i++) {
+		if (same_shape(&t->ent[i], p)) {
+			t->ent[i].stamp = ++t->clock;
+			return &t->ent[i];
+		}
+		if (!t->ent[i].valid || (old->valid && t->ent[i].stamp < old->stamp))
+			old = &t->ent[i];
+	}
+	if (!create)
+		return NULL;
+	ent_free(old);
+	old->valid = 1;
+	old->k = p->k;
+	old->rows = p->rows;
+	old->acc = p->accumulate;
+	old->diff = p->diff;
+	old->C = p->cell_bytes;
+	old->S = p->nstripes;
+	old->sstride = p->src_stripe_stride;
+	old->dstride = p->dst_stripe_stride;
+	old->stamp = ++t->clock;
+	return old;
+}
+
+static float median3(float a, float b, float c)
+{
+	if (a > b) { float x = a; a = b; b = x; }
+	if (b > c) { float x = b; b = c; c = x; }
+	return a > b ? a : b;
+}
+
+/* all timed events complete: decide (returns 1), else 0 */
+static int try_decide(struct ecg_tune_ent *e)
+{
+	float ms[2][ECG_TUNE_T];
+	int a, i;
+
+	if (hipEventQuery(e->ev[1][ECG_TUNE_T - 1][1]) != hipSuccess)
+		return 0;
+	for (a = 0; a < 2; a++)
+		for (i = 0; i < ECG_TUNE_T; i++)
+			if (hipEventElapsedTime(&ms[a][i], e->ev[a][i][0], e->ev[a][i][1]) != hipSuccess)
+				ms[a][i] = -1.0f;
+	for (a = 0; a < 2; a++)
+		e->ms[a] = median3(ms[a][0], ms[a][1], ms[a][2]);
+	e->decided = 1;
+	e->choice = ECG_WG_UNCAPPED;
+	if (e->ms[0] > 0.0f && e->ms[1] > 0.0f && e->ms[1] < e->ms[0] * (1.0f - (float)ECG_TUNE_MARGIN))
+		e->choice = e->cand;
+	return 1;
+}
+
+static int make_events(struct ecg_tune_ent *e)
+{
+	int a, i, j;
+
+	for (a = 0; a < 2; a++)
+		for (i = 0; i < ECG_TUNE_T; i++)
+			for (j = 0; j < 2; j++)
+				if (hipEventCreate(&e->ev[a][i][j]) != hipSuccess) {
+					/* destroy what was made; the shape stays untuned */
+					int n = (a * ECG_TUNE_T + i) * 2 + j, m;
+
+					for (m = 0; m < n; m++)
+						(void)hipEventDestroy(e->ev[m / (2 * ECG_TUNE_T)][(m / 2) % ECG_TUNE_T][m % 2]);
+					return -1;
+				}
+	e->events = 1;
+	return 0;
+}
+
+int ecg_tune_launch(ecg_ctx_t *ctx, const ecg_mm_params_t *p, hipStream_t st, uint32_t *kid)
+{
+	struct ecg_tuner *t = ctx->tuner;
+	ecg_launch_cfg_t cfg = ctx->cfg;
+	struct ecg_tune_ent *e;
+	hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+	uint32_t cand;
+	int arm, idx, timed = 0, rc;
+
+	cand = candidate_cap(p);
+	if (t == NULL || cand == 0 || cfg.wg_per_cu != 0 || cfg.variant != 0 || cfg.order != 0 ||
+	    cfg.grid_x != 0 || cfg.grid_y != 0)
+		return ecg_k_launch_matmul(p, &ctx->cfg, (void *)st, kid);
+	if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+		return ecg_k_launch_matmul(p, &ctx->cfg, (void *)st, kid);
+
+	pthread_mutex_lock(&t->lock);
+	if (!enabled(t)) {
+		pthread_mutex_unlock(&t->lock);
+		return ecg_k_launch_matmul(p, &ctx->cfg, (void *)st, kid);
+	}
+	e = lookup(t, p, 1);
+	e->cand = cand;
+	if (e->decided || (e->n >= 2 * ECG_TUNE_ARM && try_decide(e))) {
+		cfg.wg_per_cu = e->choice;
+		pthread_mutex_unlock(&t->lock);
+		return ecg_k_launch_matmul(p, &cfg, (void *)st, kid);
+	}
+	if (e->n >= 2 * ECG_TUNE_ARM) {		/* timings still in flight: run uncapped */
+		cfg.wg_per_cu = ECG_WG_UNCAPPED;
+		pthread_mutex_unlock(&t->lock);
+		return ecg_k_launch_matmul(p, &cfg, (void *)st, kid);
+	}
+	if (!e->events && make_events(e)) {
+		e->decided = 1;
+		e->choice = ECG_WG_UNCAPPED;
+		cfg.wg_per_cu = ECG_WG_UNCAPPED;
+		pthread_mutex_unlock(&t->lock);
+		return ecg_k_launch_matmul(p, &cfg, (void *)st, kid);
+	}
+	/* probing: arm 0 uncapped, arm 1 capped, each W untimed + T timed, back
+	 * to back; the lock is held across the timed launch so concurrent callers
+	 * of the shape cannot interleave inside an event pair */
+	arm = e->n < ECG_TUNE_ARM ? 0 : 1;
+	idx = (int)(e->n % ECG_TUNE_ARM) - ECG_TUNE_W;
+	e->n++;
+	cfg.wg_per_cu = arm ? cand : ECG_WG_UNCAPPED;
+	if (idx >= 0)
+		timed = hipEventRecord(e->ev[arm][idx][0], st) == hipSuccess;
+	rc = ecg_k_launch_matmul(p, &cfg, (void *)st, kid);
+	if (timed && (rc != 0 || hipEventRecord(e->ev[arm][idx][1], st) != hipSuccess)) {
+		e->decided = 1;		/* give up on this shape: uncapped */
+		e->choice = ECG_WG_UNCAPPED;
+	}
+	pthread_mutex_unlock(&t->lock);
+	return rc;
+}
+
+int ecg_tune_state(ecg_ctx_t *ctx, int k, int rows, uint64_t cell_bytes, uint32_t nstripes, int64_t sstride,
+		   int64_t dstride, uint32_t *cap, float *ms_uncapped, float *ms_capped)
+{
+	struct ecg_tuner *t;
+	struct ecg_tune_ent *e;
+	ecg_mm_params_t *p;
+	int rc;
+
+	if (ctx == NULL || ctx->tuner == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "tune_state: NULL context");
+	t = ctx->tuner;
+	p = calloc(1, sizeof(*p));
+	if (p == NULL)
+		return ecg_fail(-ECG_DER_NOMEM, "tune_state: calloc");
+	p->k = (uint32_t)k;
+	p->rows = (uint32_t)rows;
+	p->cell_bytes = cell_bytes;
+	p->nstripes = nstripes;
+	p->src_stripe_stride = sstride;
+	p->dst_stripe_stride = dstride;
+	pthread_mutex_lock(&t->lock);
+	e = lookup(t, p, 0);
+	if (e && !e->decided && e->n >= 2 * ECG_TUNE_ARM)
+		(void)try_decide(e);
+	rc = e && e->decided ? 1 : 0;
+	if (cap)
+		*cap = e && e->decided ? e->choice : 0;
+	if (ms_uncapped)
+		*ms_uncapped = e && e->decided ? e->ms[0] : 0.0f;
+	if (ms_capped)
+		*ms_capped = e && e->decided ? e->ms[1] : 0.0f;
+	pthread_mutex_unlock(&t->lock);
+	free(p);
+	return rc;
+}

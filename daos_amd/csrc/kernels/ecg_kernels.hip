@@ -467,8 +467,12 @@ __device__ __forceinline__ void mmcs_col(const ecg_mm_params_t &P0, const u32x4 
 					 u32x4 *cur, u32x4 *nxt, T *crc)
 {
 	using F5 = ecg_crc::f5u<W, U>;
+#ifdef ECG_EXP_KARG_CACHED
+	const ecg_mm_params_t &P = P0;			// experimental: arguments held by the compiler
+#else
 	const ecg_mm_params_t &P = kernarg_fresh();	// == P0 (first kernel argument)
 	(void)P0;
+#endif
 	const uint64_t C = P.cell_bytes;
 	const bool have = FULL || cbase + lo + 16 <= C;	// C % 16 == 0
 	u32x4 outv[RM];

@@ -87,6 +87,9 @@ _SIGS = [
     ("ecg_set_launch", C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_uint32]),
     ("ecg_set_launch_order", C.c_int, [vp, C.c_uint32]),
     ("ecg_set_wg_per_cu", C.c_int, [vp, C.c_uint32]),
+    ("ecg_set_autotune", C.c_int, [vp, C.c_int]),
+    ("ecg_tune_state", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, C.c_int64, C.c_int64, u32p,
+                                 C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     ("ecg_get_stats", C.c_int, [vp, vp, C.c_int]),
     # multi-device sharder (ecg_multi.h)
     ("ecg_multi_create", C.c_int, [C.POINTER(C.c_int), C.c_int, C.POINTER(vp)]),
@@ -482,6 +485,21 @@ class Context:
     def set_wg_per_cu(self, wg_per_cu: int = 0):
         """Product-kernel blocks per CU: 0 per-shape default, 1..16 cap, 255 none."""
         _chk(lib().ecg_set_wg_per_cu(self.h, wg_per_cu), "set_wg_per_cu")
+
+    def set_autotune(self, on: int = 1):
+        """Launch tuner (include/ecg.h ecg_set_autotune): 0 off, 1 on, 2 on and forget decisions."""
+        _chk(lib().ecg_set_autotune(self.h, on), "set_autotune")
+
+    def tune_state(self, k: int, rows: int, cell_bytes: int, nstripes: int, src_stride: int, dst_stride: int):
+        """None while the shape is probing or unseen, else (cap, ms_uncapped, ms_capped);
+        cap 255 = the tuner kept no cap.  Strides: encode k*C and the parity stripe
+        stride; in-place recovery (k+p)*C for both."""
+        cap, a, b = C.c_uint32(0), C.c_float(0), C.c_float(0)
+        rc = lib().ecg_tune_state(self.h, k, rows, cell_bytes, nstripes, src_stride, dst_stride, C.byref(cap),
+                                  C.byref(a), C.byref(b))
+        if rc < 0:
+            _chk(rc, "tune_state")
+        return (cap.value, a.value, b.value) if rc == 1 else None
 
     def copy_kernel(self, dst: int, src: int, nbytes: int, mode: int = 0, stream=None):
         """mode 0 copy, 1 read-only, 2 write-only (HBM rate probes)."""

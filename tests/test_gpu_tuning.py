@@ -77,3 +77,67 @@ def test_wg_per_cu_rejects_bad_values(ctx):
     with pytest.raises(Exception):
         ctx.set_wg_per_cu(17)
     ctx.set_wg_per_cu(0)
+
+
+def test_autotune_probes_decides_and_keeps_bytes(ctx, oracle):
+    """The launch tuner (ecg_tune.c) runs the first 8 launches of a wide shape
+    as 4 uncapped + 4 capped, then keeps the faster: every launch -- probing,
+    capped or not, and after the decision -- writes the oracle's parity, and
+    the decision is one of the two arms."""
+    k, p, S, C_ = 16, 2, 300, 32768          # 8 columns x 300 stripes = 2400 blocks (> 2048: tuned)
+    data = rand((S, k, C_), 1601)
+    en = oracle.cauchy1(k, p)
+    want = np.stack([oracle.encode_data(en[k:], data[s]) for s in range(S)], axis=1)   # [p][S][C]
+    ctx.set_autotune(2)
+    try:
+        d = ctx.to_device(data)
+        assert ctx.tune_state(k, p, C_, S, k * C_, C_) is None
+        pars = [ctx.alloc(p * S * C_) for _ in range(10)]
+        for par in pars:
+            ctx.encode(k, p, C_, S, d.ptr, k * C_, par.ptr, S * C_, C_)
+        ctx.sync()
+        st = ctx.tune_state(k, p, C_, S, k * C_, C_)
+        assert st is not None and st[0] in (2, 255) and st[1] > 0 and st[2] > 0
+        for par in pars:
+            assert np.array_equal(par.download().reshape(p, S, C_), want)
+        # decided shapes keep their choice; the recovery shape (rows = 2, in
+        # place) is tuned on its own and recovers the same bytes
+        img = np.concatenate([data, want.transpose(1, 0, 2)], axis=1)          # [S][k+p][C]
+        for i in range(9):
+            lost = img.copy()
+            lost[:, [i % k, k]] = 0x3C
+            stb = ctx.to_device(lost)
+            ctx.recover(k, p, C_, S, stb.ptr, (k + p) * C_, [i % k, k])
+            ctx.sync()
+            assert np.array_equal(stb.download().reshape(S, k + p, C_), img)
+            stb.free()
+        st = ctx.tune_state(k, p, C_, S, (k + p) * C_, (k + p) * C_)
+        assert st is not None and st[0] in (2, 255)
+        for b in pars + [d]:
+            b.free()
+    finally:
+        ctx.set_autotune(1)
+
+
+def test_autotune_off_and_explicit_cap_skip_tuning(ctx):
+    k, p, S, C_ = 8, 2, 96, 131072            # 32 columns x 96 stripes = 3072 blocks
+    d = ctx.alloc(S * k * C_)
+    par = ctx.alloc(p * S * C_)
+    try:
+        ctx.set_autotune(2)
+        ctx.set_autotune(0)
+        for _ in range(10):
+            ctx.encode(k, p, C_, S, d.ptr, k * C_, par.ptr, S * C_, C_)
+        ctx.sync()
+        assert ctx.tune_state(k, p, C_, S, k * C_, C_) is None
+        ctx.set_autotune(1)
+        ctx.set_wg_per_cu(255)
+        for _ in range(10):
+            ctx.encode(k, p, C_, S, d.ptr, k * C_, par.ptr, S * C_, C_)
+        ctx.sync()
+        assert ctx.tune_state(k, p, C_, S, k * C_, C_) is None
+    finally:
+        ctx.set_wg_per_cu(0)
+        ctx.set_autotune(1)
+        d.free()
+        par.free()
