@@ -208,15 +208,17 @@ typedef struct ecg_csum_params {
  * chunk's rows, Z being the zero bytes that pad the cell to whole columns.
  * crc16: kh[(row0 + h) * 256 + t] holds that factor (row0 = 0, or nh for the
  * last chunk).  Reflected CRCs: the lane part x^(8*16*(63-lane)) comes from the
- * nibl tables, each wave XOR-reduces, and kh[(row0 + h) * 4 + wave] holds the
- * rest, x^(8 * (1024 * (3 - wave) + 4096 * (columns after))) (* x^(-8Z)),
- * applied once per wave.  CRC is linear, so the values XOR to the chunk's CRC.
+ * nibl tables (staged in LDS), each wave XOR-reduces, and the rest f =
+ * x^(8 * (1024 * (3 - wave) + 4096 * (columns after))) (* x^(-8Z)) is applied
+ * once per wave, bit-parallel: kh[((row0 + h) * 4 + wave) * 64 + b] = e_b * f
+ * (e_b = the register with only bit b set, zero for b >= W).  CRC is linear,
+ * so the values XOR to the chunk's CRC.
  */
 typedef struct ecg_mmcs_params {
 	const void *tbl;
 	uint8_t *out;
-	const void *kh;			/* (nh + nh_last) x 256 (crc16) or x 4 x [16][64] (reflected:
-					 * per-wave nibble tables, ecg_csum.c fused_kh), T as tbl */
+	const void *kh;			/* (nh + nh_last) x 256 (crc16) or x 4 x 64 (reflected:
+					 * per-wave bit-products, ecg_csum.c fused_kh), T as tbl */
 	uint64_t chunk_bytes;
 	uint64_t init, xorout, poly;
 	uint32_t nch;
@@ -228,7 +230,8 @@ typedef struct ecg_mmcs_params {
 	uint32_t byte_tables;		/* table kind TB: 0 5-bit, 1 slice-by-NB, 2 s16 */
 	uint32_t wave;			/* 1: one wave per (stripe, chunk) (ecg_mm_csum_wave_kernel):
 					 * kh = [2][64] lane multipliers (full chunk, last chunk;
-					 * reflected: [2][16][64] nibble tables of them),
+					 * reflected: [64] bit-products of the last chunk's
+					 * x^(-8Z), the lane factors from the nibl tables),
 					 * checksums stored, not XORed (no zeroing needed) */
 	uint32_t pad3;
 	uint32_t row_slot[ECG_KMAX_R];

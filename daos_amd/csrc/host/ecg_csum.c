@@ -508,10 +508,11 @@ static uint32_t fused_cols(const ecg_ctx_t *ctx, uint64_t m, int type, int k, in
  * the last chunk (m_last columns, z padding bytes):
  *   crc16:      kh[row][t] = x^(8*(16*(255-t) + 4096*(columns after item h))) * x^(-8z)
  *   reflected:  the factor f(row, w) = x^(8*(1024*(3-w) + 4096*(columns after
- *               item h))) * x^(-8z) of wave w, folded into nibble tables with
- *               the lane part: kh[row][w][n][l] = (n << (W-4)) *
- *               x^(8*16*(63-l)) * f(row, w) -- the kernel multiplies a lane's
- *               value by both in W/4 table steps, no scalar multiply
+ *               item h))) * x^(-8z) of wave w as its W bit-products,
+ *               kh[row][w][b] = e_b * f(row, w) (e_b: the register with only
+ *               bit b set; entries b >= W zero) -- the kernel applies the lane
+ *               part from the LDS nibl tables and then f bit-parallel, lane b
+ *               contributing kh[row][w][b] when bit b of the wave's sum is set
  * Cached per context by (type, chunk bytes, columns per item, last length). */
 static int fused_kh(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, uint32_t ncols,
 		    uint32_t nh, uint32_t nh_last, const void **out)
@@ -521,10 +522,10 @@ static int fused_kh(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, uint3
 	const uint64_t m_last = (last + ECG_MMCS_STRIDE - 1) / ECG_MMCS_STRIDE;
 	const uint64_t z = m_last * ECG_MMCS_STRIDE - last;
 	const size_t es = d->width == 64 ? 8 : 4, nrow = (size_t)nh + nh_last;
-	/* entries per row: 4 waves x [16][64] nibble tables, or 256 threads */
-	const size_t per = d->refl ? 4 * 16 * 64 : 256;
+	/* entries per row: 4 waves x 64 bit-products, or 256 threads */
+	const size_t per = d->refl ? 4 * 64 : 256;
 	struct ecg_kh_ent *e;
-	uint64_t k256[256], nibl[16 * 64];
+	uint64_t k256[256];
 	unsigned char *img;
 	void *dev = NULL;
 	hipError_t he;
@@ -547,9 +548,6 @@ static int fused_kh(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, uint3
 	k256[255] = crc_one(d);
 	for (int t = 254; t >= 0; t--)
 		k256[t] = crc_mulmod(d, k256[t + 1], crc_xpow8(d, 16));
-	for (int n = 0; d->refl && n < 16; n++)
-		for (int l = 0; l < 64; l++)
-			nibl[n * 64 + l] = crc_mulmod(d, (uint64_t)n << (d->width - 4), k256[192 + l]);
 	for (size_t row = 0; row < nrow; row++) {
 		const int lastc = row >= nh;
 		const uint64_t h = lastc ? row - nh : row, mc = lastc ? m_last : m;
@@ -565,13 +563,12 @@ static int fused_kh(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, uint3
 
 			if (d->refl) {
 				/* wave w's factor (k256[64 w + 63] = x^(8*16*(192-64w)) =
-				 * x^(8*1024*(3-w))) times nibl[n][l] = the nibble n at the
-				 * register's 4 lowest powers times lane l's k256[192 + l] */
-				const size_t w = t / 1024;
+				 * x^(8*1024*(3-w))) times the item's shift, as bit-products */
+				const size_t w = t / 64, b = t % 64;
 
-				if (t % 1024 == 0)
+				if (b == 0)
 					f = crc_mulmod(d, k256[64 * w + 63], sh);
-				v = crc_mulmod(d, nibl[t % 1024], f);
+				v = b < (size_t)d->width ? crc_mulmod(d, (uint64_t)1 << b, f) : 0;
 			} else {	/* crc16: thread t's */
 				v = crc_mulmod(d, k256[t], sh);
 			}
@@ -611,10 +608,13 @@ static int fused_kh(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, uint3
 	return rc;
 }
 
-/* Lane multipliers of the wave-per-chunk fused kernel (ecg_kabi.h
- * ecg_mmcs_params wave): kw[0][l] = x^(8*16*(63-l)), kw[1][l] = the same
- * times x^(-8Z), Z = zero bytes padding the last chunk (`last` bytes) to
- * whole 1 KiB rows.  Cached with the kh tables (ncols = 0 marks them). */
+/* Multipliers of the wave-per-chunk fused kernel (ecg_kabi.h
+ * ecg_mmcs_params wave), Z = zero bytes padding the last chunk (`last` bytes)
+ * to whole 1 KiB rows.  crc16: the lane factors kw[0][l] = x^(8*16*(63-l)),
+ * kw[1][l] = the same times x^(-8Z).  Reflected CRCs take the lane factor from
+ * the nibl tables of the CRC image and need only x^(-8Z) for a last chunk, as
+ * W bit-products kw[b] = e_b * x^(-8Z) (64 entries, b >= W zero).  Cached
+ * with the kh tables (ncols = 0 marks them). */
 static int fused_kw(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, const void **out)
 {
 	const struct crc_def *d = &g_defs[type];
@@ -637,32 +637,29 @@ static int fused_kw(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, const
 			return 0;
 		}
 	}
-	/* reflected CRCs: per row the [16][64] nibble tables of the lane factor,
-	 * kw[row][n][l] = (n << (W-4)) * k(row, l) (the kernel applies them in W/4
-	 * steps); crc16: the factors themselves, kw[row][l] */
-	const size_t per = d->refl ? 16 * 64 : 64;
+	const size_t nent = d->refl ? 64 : 2 * 64;
 
 	for (int l = 63; l >= 0; l--) {
 		const uint64_t v[2] = {c, crc_mulmod(d, c, un)};
 
-		for (int row = 0; row < 2; row++)
-			for (int n = 0; n < (d->refl ? 16 : 1); n++) {
-				const uint64_t x = d->refl ? crc_mulmod(d, (uint64_t)n << (d->width - 4), v[row]) : v[row];
-				const size_t at = (size_t)row * per + (size_t)n * 64 + (size_t)l;
+		for (int row = 0; row < (d->refl ? 1 : 2); row++) {
+			/* reflected: entry l = e_l * x^(-8Z); crc16: lane l's factor */
+			const uint64_t x = d->refl ? (l < d->width ? crc_mulmod(d, (uint64_t)1 << l, un) : 0) : v[row];
+			const size_t at = (size_t)row * 64 + (size_t)l;
 
-				if (es == 8) {
-					memcpy(img + at * 8, &x, 8);
-				} else {
-					const uint32_t w = (uint32_t)x;
+			if (es == 8) {
+				memcpy(img + at * 8, &x, 8);
+			} else {
+				const uint32_t w = (uint32_t)x;
 
-					memcpy(img + at * 4, &w, 4);
-				}
+				memcpy(img + at * 4, &w, 4);
 			}
+		}
 		c = crc_mulmod(d, c, step);
 	}
-	he = hipMalloc(&dev, 2 * per * es);
+	he = hipMalloc(&dev, nent * es);
 	if (he == hipSuccess)
-		he = hipMemcpy(dev, img, 2 * per * es, hipMemcpyHostToDevice);
+		he = hipMemcpy(dev, img, nent * es, hipMemcpyHostToDevice);
 	if (he != hipSuccess) {
 		if (dev)
 			(void)hipFree(dev);

@@ -570,6 +570,7 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	// TB 1/2: the column shift as 5-bit a5 tables; TB 3: as nibble a4 tables
 	__shared__ T s_sh[TB == 3 ? 16 * 16 : TB ? ECG_CSUM_NA5(NB) * 32 : 1];
 	__shared__ T s_r4[REFL ? 16 : 1];		// reflected: 4-bit reduction of the lane multiply
+	__shared__ T s_nibl[REFL ? 16 * 64 : 1];	// reflected: the lane factors' nibble tables
 	const int k = K ? K : (int)P.k;
 	const int rows = R ? R : (int)P.rows;
 	const uint64_t C = P.cell_bytes;
@@ -579,6 +580,8 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	if constexpr (REFL) {
 		if (threadIdx.x < 16)
 			s_r4[threadIdx.x] = gt[ECG_CSUM_OFF_R4(NB) + threadIdx.x];
+		for (int i = threadIdx.x; i < 16 * 64; i += BLOCK)
+			s_nibl[i] = gt[ECG_CSUM_OFF_NIBL(NB) + i];
 	}
 
 	for (int i = threadIdx.x; i < KM * RM; i += BLOCK) {
@@ -618,6 +621,17 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 
 			mmcs_item(Q, it, c, i, col1, khrow);
 			const uint64_t c0 = (uint64_t)c * Q.chunk_bytes;
+			// reflected: this wave's item factor as W bit-products, lane b
+			// holding e_b * f(item row, wave) (ecg_csum.c fused_kh); loaded
+			// now, used after the walk -- its latency hides behind the walk
+			T kbv = 0;
+			if constexpr (REFL) {
+				const uint32_t lane = threadIdx.x & 63u;
+				const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
+				if (lane < (uint32_t)W)
+					kbv = kh[((size_t)khrow * 4u + wv) * 64u + lane];
+			}
 #pragma unroll
 			for (int r = 0; r < RM; r++)
 				crc[r] = 0;
@@ -655,25 +669,28 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 					i == 0 && threadIdx.x == 0, Q.init, (col1 - 1 - i) % UF, true, xa, xa, crc);
 			// each wave XORs its partial into the (zeroed) output: no
 			// workgroup barrier, other waves keep streaming.  Reflected CRCs:
-			// every lane's value is multiplied by its own and its wave's
-			// factors in one nibble-table pass (W/4 steps) and the wave
-			// XOR-reduces; crc16: a W-step multiply per thread.
+			// every lane's value is multiplied by its lane factor
+			// x^(8*16*(63-l)) from the LDS nibble tables (W/4 steps), the wave
+			// XOR-reduces, and the wave's sum is multiplied by the item factor
+			// bit-parallel -- lane b keeps e_b * f if bit b of the sum is set,
+			// one more XOR reduction.  No table read in the tail depends on
+			// HBM: the r03 per-(row, wave) nibble tables in HBM cost crc64 up
+			// to 30 % at 4-column items (serialised L2 round trips under the
+			// streaming load, tools/fused_libs.py -DECG_EXP_NO_TAIL,
+			// profiles/r03/fused_tail/).  crc16: a W-step multiply per thread.
 #pragma unroll
 			for (int r = 0; r < RM; r++) {
 				if (r < rows) {
 					T v;
 					if constexpr (REFL) {
-						// lane l's value times lane l's AND this wave's item factor,
-						// x^(8*16*(63-l)) * kh[item row][wave], nibble by nibble from
-						// the per-(row, wave) tables Q.kh[row*4 + wave][16][64] (HBM,
-						// L2-resident: the W/4 loads depend only on the value and
-						// issue together); the waves' values then just XOR --
-						// no scalar W-step multiply per item (SQ counters:
-						// profiles/r03/fused_sq)
 						const uint32_t lane = threadIdx.x & 63u;
-						const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-						const T *tab = kh + ((size_t)khrow * 4u + wv) * (16u * 64u);
-						v = ecg_crc::wave_xor(ecg_crc::lane_mul_nib<W>(crc[r], tab, s_r4, lane));
+#ifdef ECG_EXP_NO_TAIL
+						(void)kbv;	// experimental: no lane / item factor (wrong checksums)
+						v = ecg_crc::wave_xor(crc[r]);
+#else
+						v = ecg_crc::wave_xor(ecg_crc::lane_mul_nib<W>(crc[r], s_nibl, s_r4, lane));
+						v = ecg_crc::wave_xor(((v >> (lane & (uint32_t)(W - 1))) & 1u) ? kbv : (T)0);
+#endif
 					} else {
 						v = ecg_crc::mulmod<W, REFL>(kh[khrow * 256 + threadIdx.x], crc[r], poly);
 						v = ecg_crc::wave_xor(v);
@@ -749,9 +766,14 @@ ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	} else {
 		ecg_crc::stage5u<W>(s_sl, gt, ECG_CSUM_OFF_P5X_1K(NB), ECG_CSUM_OFF_A5_4K(NB), BLOCK);
 	}
+	__shared__ T s_nibl[REFL ? 16 * 64 : 1];	// reflected: the lane factors' nibble tables
 	const T *kw = (const T *)Q.kh;
-	if (REFL && threadIdx.x < 16)
-		s_r4[threadIdx.x] = gt[ECG_CSUM_OFF_R4(NB) + threadIdx.x];
+	if constexpr (REFL) {
+		if (threadIdx.x < 16)
+			s_r4[threadIdx.x] = gt[ECG_CSUM_OFF_R4(NB) + threadIdx.x];
+		for (int i = threadIdx.x; i < 16 * 64; i += BLOCK)
+			s_nibl[i] = gt[ECG_CSUM_OFF_NIBL(NB) + i];
+	}
 	const T poly = (T)Q.poly;
 	__syncthreads();
 
@@ -768,6 +790,10 @@ ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 		const uint32_t m = (uint32_t)((len + ECG_CSUM_STRIDE - 1) / ECG_CSUM_STRIDE);
 		T crc[RM];
 		u32x4 xa[KM];
+		// reflected, last chunk of a cell: the zero padding's inverse shift
+		// x^(-8Z) as W bit-products (lane b: e_b * x^(-8Z)), loaded now and
+		// used after the walk; crc16: the lane's multiplier
+		const T kcur = REFL ? (lastc && lane < W ? kw[lane] : (T)0) : kw[(lastc ? 64 : 0) + lane];
 
 #pragma unroll
 		for (int r = 0; r < RM; r++)
@@ -796,15 +822,18 @@ ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 			mmcs_col<KM, RM, W, REFL, TB, false, ECG_CSUM_STRIDE, false, F5::U>(
 				P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)i * ECG_CSUM_STRIDE, 0, lo, false,
 				i == 0 && lane == 0, Q.init, (m - 1 - i) % F5::U, true, xa, xa, crc);
-		// reflected: Q.kh = [2][16][64] nibble tables of the lane factor
-		// (full / last chunk, ecg_csum.c fused_kw), W/4 steps; crc16: [2][64]
-		const T kcur = REFL ? (T)0 : kw[(lastc ? 64 : 0) + lane];
+		// reflected: the lane factor x^(8*16*(63-l)) from the LDS nibble
+		// tables (W/4 steps), the wave XOR-reduces, a last chunk's sum is
+		// multiplied by x^(-8Z) bit-parallel (ecg_csum.c fused_kw); crc16: a
+		// W-step multiply per lane by Q.kh[2][64]
 #pragma unroll
 		for (int r = 0; r < RM; r++) {
 			if (r < rows) {
-				T v = REFL ? ecg_crc::lane_mul_nib<W>(crc[r], kw + (lastc ? 1024 : 0), s_r4, (uint32_t)lane)
+				T v = REFL ? ecg_crc::lane_mul_nib<W>(crc[r], s_nibl, s_r4, (uint32_t)lane)
 					   : ecg_crc::mulmod<W, REFL>(kcur, crc[r], poly);
 				v = ecg_crc::wave_xor(v);
+				if (REFL && lastc)
+					v = ecg_crc::wave_xor(((v >> ((uint32_t)lane & (uint32_t)(W - 1))) & 1u) ? kcur : (T)0);
 				if (lane == 0) {
 					const uint64_t slot = ((uint64_t)Q.row_slot[r] * P.nstripes + s) * Q.nch + c;
 					v ^= (T)Q.xorout;
