@@ -471,11 +471,12 @@ void ecg_csum_ctx_fini(ecg_ctx_t *ctx)
 		}
 }
 
-/* Columns per fused-kernel work item: 4 for one output row of crc16/crc32
- * (parity-shard rebuild), else 8 (every reduction multiplies `rows` values;
- * crc64's costs twice crc32's); a whole chunk when shorter.  Measured A/B in
- * one process on random data (tools/tune12.py, profiles/r01/tune12.json);
- * ecg_set_fused_cols / ECG_FUSED_COLS override. */
+/* Columns per fused-kernel work item (a whole chunk when shorter): fewer
+ * columns per item walk a chunk with more workgroups in parallel, more
+ * amortise the per-item reduction.  Measured A/B in one process on random
+ * data (tools/tune12.py, tools/fused_libs.py; profiles/r01/tune12.json,
+ * profiles/r02/fused_libs/, profiles/r03/fused_tail/); ecg_set_fused_cols /
+ * ECG_FUSED_COLS override. */
 static int g_fused_cols_env;
 static pthread_once_t g_fused_cols_once = PTHREAD_ONCE_INIT;
 
@@ -490,11 +491,11 @@ static void fused_cols_init(void)
 
 static uint32_t fused_cols(const ecg_ctx_t *ctx, uint64_t m, int type, int k, int rows)
 {
-	/* tools/fused_libs.py, profiles/r02/fused_libs/: crc64 8 (its W-step per-item
-	 * multiply wants long items); one output row (a parity shard's rebuild) 4;
-	 * crc16 / crc32 with >= 2 rows: 4 for k >= 8 (EC_8P2 +10 % vs +16 % at 8),
-	 * 8 for k <= 4 (EC_4P2 +11.5 % vs +21 % at 4) */
-	const uint64_t dflt = type == ECG_HASH_CRC64 ? 8 : rows == 1 ? 4 : k >= 8 ? 4 : 8;
+	/* tools/fused_libs.py, profiles/r02/fused_libs/, profiles/r03/fused_tail/:
+	 * one output row (a parity shard's rebuild) 4; >= 2 rows: 4 for k >= 8
+	 * (EC_8P2 crc32 +8 % vs +18 % at 8; crc64, now that its item tail reads no
+	 * HBM, +12.5 % vs +20 %), 8 for k <= 4 (EC_4P2 crc32 +8 % vs +15 % at 4) */
+	const uint64_t dflt = rows == 1 ? 4 : k >= 8 ? 4 : 8;
 	const int env = ctx->fused_cols ? (int)ctx->fused_cols
 					: (pthread_once(&g_fused_cols_once, fused_cols_init), g_fused_cols_env);
 
@@ -842,13 +843,12 @@ int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t
 	 * selects the s16 tables (A/B), bit 7 the wave-per-chunk kernel */
 	q->byte_tables = (ctx->csum_variant & 512u) ? 3 : (ctx->csum_variant & 64u) ? 2
 			 : use_byte_tables(ctx, type, 1, k, rows);
-	/* the wave-per-chunk kernel for crc64 with k <= 4 (one 64-step multiply
-	 * per lane per chunk instead of per thread per item: EC_4P2 crc64 +42 %
-	 * -> +29 % over the plain encode; with k = 8 its longer serial walk
-	 * loses, tools/crc_ab.py, profiles/r02/crc_ab_fused_wave.log); csum_variant
-	 * bit 7 forces it, bit 8 forbids it (A/B) */
-	q->wave = (ctx->csum_variant & 128u) != 0 ||
-		  (!(ctx->csum_variant & 256u) && type == ECG_HASH_CRC64 && k <= 4);
+	/* the workgroup kernel for every shape: since its item tail no longer
+	 * reads HBM (round 3) it beats the wave-per-chunk kernel for crc64 at
+	 * EC_4P2 too (+13 % vs +19 % over the plain encode, profiles/r03/fused_tail/);
+	 * csum_variant bit 7 forces the wave kernel (A/B), bit 8 is kept as the
+	 * old "forbid" bit */
+	q->wave = (ctx->csum_variant & 128u) != 0;
 	if (q->wave) {
 		/* the wave kernel is instantiated with the per-hash default tables
 		 * only (byte tables for crc64, 5-bit for crc16 / crc32) */

@@ -482,6 +482,30 @@ __device__ __forceinline__ T uniform(T v)
 		return (T)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
 }
 
+// XOR of one 32-bit word over the 64 lanes, as a wave-uniform value: DPP
+// steps inside rows (pairs, quads, half-row and row mirrors), row broadcasts
+// across rows, lane 63 read into an SGPR -- VALU only, no LDS crossbar
+// (ds_bpermute) round trips.  Every lane must be active.
+__device__ __forceinline__ uint32_t wave_xor_dpp32(uint32_t x)
+{
+	x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);	// quad_perm [1,0,3,2]
+	x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);	// quad_perm [2,3,0,1]
+	x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false);	// row_half_mirror
+	x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false);	// row_mirror
+	x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);	// row_bcast:15 -> rows 1, 3
+	x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);	// row_bcast:31 -> rows 2, 3
+	return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_xor_uniform(T v)
+{
+	if constexpr (sizeof(T) == 8)
+		return ((uint64_t)wave_xor_dpp32((uint32_t)(v >> 32)) << 32) | wave_xor_dpp32((uint32_t)v);
+	else
+		return (T)wave_xor_dpp32((uint32_t)v);
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_xor(T v)
 {

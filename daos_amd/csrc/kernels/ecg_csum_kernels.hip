@@ -239,7 +239,7 @@ __global__ __launch_bounds__(CS_BLOCK) void ecg_crc_kernel(ecg_csum_params_t p)
 			}
 		}
 		acc = lane_shift<W, REFL>(acc, klane, gt, r4, (uint32_t)lane, poly);
-		acc = wave_xor(acc);
+		acc = wave_xor_uniform(acc);	// DPP, no ds_bpermute
 		if (lane == 0) {
 			T crc = nq == 0 ? init : acc;
 
@@ -399,7 +399,7 @@ __global__ __launch_bounds__(64 * NW) void ecg_crc_split_kernel(ecg_csum_params_
 			acc = horner<W, REFL, TK, L::UN>(acc, d, i, i1, s5, sl, sh);
 		}
 		acc = lane_shift<W, REFL>(acc, klane, gt, r4, (uint32_t)lane, poly);
-		acc = wave_xor(acc);
+		acc = wave_xor_uniform(acc);	// DPP, no ds_bpermute
 		// x^(8 * (m - i1) KiB): the host's constant for this chunk length,
 		// else the product of p2[j] over the set bits j (one bit per lane)
 		T f;

@@ -678,31 +678,47 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 			// to 30 % at 4-column items (serialised L2 round trips under the
 			// streaming load, tools/fused_libs.py -DECG_EXP_NO_TAIL,
 			// profiles/r03/fused_tail/).  crc16: a W-step multiply per thread.
+			// The rows are finished side by side (one basic block: their
+			// lookup chains and reductions interleave), reduced with DPP into
+			// wave-uniform values, then lane 0 XORs them into the output.
+			T v[RM];
+			const uint32_t lane = threadIdx.x & 63u;
 #pragma unroll
 			for (int r = 0; r < RM; r++) {
-				if (r < rows) {
-					T v;
-					if constexpr (REFL) {
-						const uint32_t lane = threadIdx.x & 63u;
+				if constexpr (REFL) {
 #ifdef ECG_EXP_NO_TAIL
-						(void)kbv;	// experimental: no lane / item factor (wrong checksums)
-						v = ecg_crc::wave_xor(crc[r]);
+					v[r] = crc[r];	// experimental: no lane / item factor (wrong checksums)
 #else
-						v = ecg_crc::wave_xor(ecg_crc::lane_mul_nib<W>(crc[r], s_nibl, s_r4, lane));
-						v = ecg_crc::wave_xor(((v >> (lane & (uint32_t)(W - 1))) & 1u) ? kbv : (T)0);
+					v[r] = ecg_crc::lane_mul_nib<W>(crc[r], s_nibl, s_r4, lane);
 #endif
-					} else {
-						v = ecg_crc::mulmod<W, REFL>(kh[khrow * 256 + threadIdx.x], crc[r], poly);
-						v = ecg_crc::wave_xor(v);
-					}
-					if ((threadIdx.x & 63) == 0) {
+				} else {
+					v[r] = ecg_crc::mulmod<W, REFL>(kh[khrow * 256 + threadIdx.x], crc[r], poly);
+				}
+			}
+#pragma unroll
+			for (int r = 0; r < RM; r++)
+				v[r] = ecg_crc::wave_xor_uniform(v[r]);
+#if !defined(ECG_EXP_NO_TAIL)
+			if constexpr (REFL) {
+#pragma unroll
+				for (int r = 0; r < RM; r++)
+					v[r] = ecg_crc::wave_xor_uniform(((v[r] >> (lane & (uint32_t)(W - 1))) & 1u) ? kbv : (T)0);
+			}
+#else
+			(void)kbv;
+#endif
+			if (lane == 0) {
+#pragma unroll
+				for (int r = 0; r < RM; r++) {
+					if (r < rows) {
+						T x = v[r];
 						if (threadIdx.x == 0 && khrow == (c + 1 == Q.nch ? Q.nh : 0))
-							v ^= (T)Q.xorout;	// once per chunk
+							x ^= (T)Q.xorout;	// once per chunk
 						const uint64_t slot = ((uint64_t)Q.row_slot[r] * P.nstripes + s) * Q.nch + c;
 						if constexpr (W == 16)
-							atomicXor((uint32_t *)Q.out + slot / 2, (uint32_t)v << (16 * (slot & 1)));
+							atomicXor((uint32_t *)Q.out + slot / 2, (uint32_t)x << (16 * (slot & 1)));
 						else
-							atomicXor((T *)Q.out + slot, v);
+							atomicXor((T *)Q.out + slot, x);
 					}
 				}
 			}
@@ -826,21 +842,30 @@ ecg_mm_csum_wave_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 		// tables (W/4 steps), the wave XOR-reduces, a last chunk's sum is
 		// multiplied by x^(-8Z) bit-parallel (ecg_csum.c fused_kw); crc16: a
 		// W-step multiply per lane by Q.kh[2][64]
+		T v[RM];
+#pragma unroll
+		for (int r = 0; r < RM; r++)
+			v[r] = REFL ? ecg_crc::lane_mul_nib<W>(crc[r], s_nibl, s_r4, (uint32_t)lane)
+				    : ecg_crc::mulmod<W, REFL>(kcur, crc[r], poly);
+#pragma unroll
+		for (int r = 0; r < RM; r++)
+			v[r] = ecg_crc::wave_xor_uniform(v[r]);
+		if (REFL && lastc) {
+#pragma unroll
+			for (int r = 0; r < RM; r++)
+				v[r] = ecg_crc::wave_xor_uniform(((v[r] >> ((uint32_t)lane & (uint32_t)(W - 1))) & 1u) ? kcur
+													  : (T)0);
+		}
 #pragma unroll
 		for (int r = 0; r < RM; r++) {
 			if (r < rows) {
-				T v = REFL ? ecg_crc::lane_mul_nib<W>(crc[r], s_nibl, s_r4, (uint32_t)lane)
-					   : ecg_crc::mulmod<W, REFL>(kcur, crc[r], poly);
-				v = ecg_crc::wave_xor(v);
-				if (REFL && lastc)
-					v = ecg_crc::wave_xor(((v >> ((uint32_t)lane & (uint32_t)(W - 1))) & 1u) ? kcur : (T)0);
 				if (lane == 0) {
 					const uint64_t slot = ((uint64_t)Q.row_slot[r] * P.nstripes + s) * Q.nch + c;
-					v ^= (T)Q.xorout;
+					const T x = v[r] ^ (T)Q.xorout;
 					if constexpr (W == 16)
-						((uint16_t *)Q.out)[slot] = (uint16_t)v;
+						((uint16_t *)Q.out)[slot] = (uint16_t)x;
 					else
-						((T *)Q.out)[slot] = v;
+						((T *)Q.out)[slot] = x;
 				}
 			}
 		}

@@ -79,7 +79,7 @@ print(json.dumps(res))
 def main():
     libs = sys.argv[1:]
     out = {}
-    for rnd in range(2):
+    for rnd in range(int(os.environ.get("FUSED_ROUNDS", "2"))):
         for lib in libs:
             r = subprocess.run([sys.executable, "-c", CHILD, lib], capture_output=True, text=True, timeout=400)
             if r.returncode != 0:
