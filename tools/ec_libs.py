@@ -59,7 +59,7 @@ print(json.dumps(res))
 def main():
     libs = sys.argv[1:]
     out = {}
-    for rnd in range(2):
+    for rnd in range(int(os.environ.get("EC_ROUNDS", "2"))):
         for lib in libs:
             r = subprocess.run([sys.executable, "-c", CHILD, lib], capture_output=True, text=True, timeout=300)
             if r.returncode != 0:

@@ -247,7 +247,7 @@ PY
 		step crc_ab 600 python tools/crc_ab.py || exit $?
 		;;
 	eclibs)
-		step ec_libs 900 python tools/ec_libs.py daos_amd/lib/libecg.so build/exp/xoronly/libecg.so || exit $?
+		step ec_libs 900 python tools/ec_libs.py daos_amd/lib/libecg.so ${EC_LIBS:-build/exp/xoronly/libecg.so} || exit $?
 		;;
 	fusedlibs)
 		step fused_libs 900 python tools/fused_libs.py daos_amd/lib/libecg.so ${FUSED_LIBS:-} || exit $?
