@@ -53,6 +53,11 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #define ECG_FUSED_WPE(W) ((W) == 64 ? 4 : 3)
 #endif
 
+template <bool B>
+struct ecg_bool {
+	static constexpr bool value = B;
+};
+
 __device__ __forceinline__ u32x4 ld_nt(const uint8_t *p)
 {
 	return __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
@@ -576,48 +581,86 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	const uint64_t C = P.cell_bytes;
 	const uint32_t lo = threadIdx.x * 16u;
 	const T *gt = (const T *)Q.tbl;
-
-	if constexpr (REFL) {
-		if (threadIdx.x < 16)
-			s_r4[threadIdx.x] = gt[ECG_CSUM_OFF_R4(NB) + threadIdx.x];
-		for (int i = threadIdx.x; i < 16 * 64; i += BLOCK)
-			s_nibl[i] = gt[ECG_CSUM_OFF_NIBL(NB) + i];
-	}
-
-	for (int i = threadIdx.x; i < KM * RM; i += BLOCK) {
-		const int j = i / RM, r = i % RM;
-		if (j < k && r < rows) {
-			const ecg_ptbl_t &t = P.tbl[r][j];
-			s_tbl[j * PER_J + r] = (u32x4){t.t0lo, t.t0hi, t.t1lo, t.t1hi};
-			reinterpret_cast<uint32_t *>(&s_tbl[j * PER_J + RM])[r] = t.t2;
-		}
-	}
-	if constexpr (TB != 0) {
-		for (int i = threadIdx.x; i < NSL; i += BLOCK)
-			s_sl[i] = gt[(TB == 1 ? 0 : ECG_CSUM_OFF_S16(NB)) + i];
-		if constexpr (TB == 3)
-			for (int i = threadIdx.x; i < 16 * 16; i += BLOCK)
-				s_sh[i] = gt[ECG_CSUM_OFF_A4_4K(NB) + i];
-		else
-			for (int i = threadIdx.x; i < ECG_CSUM_NA5(NB) * 32; i += BLOCK)
-				s_sh[i] = gt[ECG_CSUM_OFF_A5_4K(NB) + i];
-	} else {
-		ecg_crc::stage5u<W, UF>(s_sl, gt, ECG_CSUM_OFF_P5X_4K(NB), ECG_CSUM_OFF_A5_32K(NB), BLOCK);
-	}
 	const T *kh = (const T *)Q.kh;
 	const T poly = (T)Q.poly;
+
+	// Prologue.  The tables are staged in two phases around the first
+	// column's HBM loads: every entry this thread stages is loaded into
+	// registers (L2 hits), then the workgroup's first item's first column is
+	// requested, then the entries are written to LDS -- vmcnt counts in issue
+	// order, so the writes wait only for the table loads and the staging and
+	// barrier run in the shadow of the first HBM round trip (a workgroup
+	// normally owns exactly one item).
+	constexpr int P5 = ECG_CSUM_NF5 * 32;
+	constexpr int NSH = TB == 3 ? 16 * 16 : TB ? ECG_CSUM_NA5(NB) * 32 : 0;
+	constexpr int NNB = REFL ? 16 * 64 + 16 : 0;		// nibl, then r4
+	constexpr int NST = NSL + NSH + NNB;
+	constexpr int QST = (NST + BLOCK - 1) / BLOCK;
+	static_assert(KM * RM <= BLOCK, "one product-table entry per thread");
+	auto st_src = [&](int i) -> int {		// entry i of the staged image -> index in gt
+		if (i < NSL) {
+			if constexpr (TB == 0)
+				return i < P5 ? ECG_CSUM_OFF_P5(NB) + i
+				     : i < UF * P5 ? ECG_CSUM_OFF_P5X_4K(NB) + i - P5 : ECG_CSUM_OFF_A5_32K(NB) + i - UF * P5;
+			else
+				return (TB == 1 ? 0 : ECG_CSUM_OFF_S16(NB)) + i;
+		}
+		i -= NSL;
+		if (i < NSH)
+			return (TB == 3 ? ECG_CSUM_OFF_A4_4K(NB) : ECG_CSUM_OFF_A5_4K(NB)) + i;
+		i -= NSH;
+		return i < 16 * 64 ? ECG_CSUM_OFF_NIBL(NB) + i : ECG_CSUM_OFF_R4(NB) + i - 16 * 64;
+	};
+	auto st_dst = [&](int i) -> T * {
+		if (i < NSL)
+			return &s_sl[i];
+		i -= NSL;
+		if (i < NSH)
+			return &s_sh[i];
+		i -= NSH;
+		return i < 16 * 64 ? &s_nibl[i] : &s_r4[i - 16 * 64];
+	};
+	T sv[QST];
+#pragma unroll
+	for (int q = 0; q < QST; q++)
+		if (q * BLOCK + (int)threadIdx.x < NST)
+			sv[q] = gt[st_src(q * BLOCK + (int)threadIdx.x)];
+	const int tj = (int)threadIdx.x / RM, tr = (int)threadIdx.x % RM;
+	const bool tst = (int)threadIdx.x < KM * RM && tj < k && tr < rows;
+	ecg_ptbl_t tv;
+	if (tst)
+		tv = P.tbl[tr][tj];
+
+	// the first item's first column (unconditional, clamped: a load only
+	// some paths issue makes the compiler wait for everything)
+	u32x4 xa[KM];
+	if constexpr (PF) {
+		uint32_t c, i, col1, khrow;
+
+		mmcs_item(Q, blockIdx.x, c, i, col1, khrow);
+		const uint64_t c0 = (uint64_t)c * Q.chunk_bytes + (uint64_t)i * CHUNK_BYTES;
+		mm_load_any<KM>(P, k, c0 < C ? blockIdx.y : 0u, c0 < C ? c0 : 0u, lo, xa);
+	}
+#pragma unroll
+	for (int q = 0; q < QST; q++)
+		if (q * BLOCK + (int)threadIdx.x < NST)
+			*st_dst(q * BLOCK + (int)threadIdx.x) = sv[q];
+	if (tst) {
+		s_tbl[tj * PER_J + tr] = (u32x4){tv.t0lo, tv.t0hi, tv.t1lo, tv.t1hi};
+		reinterpret_cast<uint32_t *>(&s_tbl[tj * PER_J + RM])[tr] = tv.t2;
+	}
 	__syncthreads();
 
-	// The workgroup's work: items blockIdx.x, blockIdx.x + gridDim.x, ... of
-	// stripe blockIdx.y (+ gridDim.y ...), each item's 4 KiB columns in
-	// order.  With PF the next column's loads are issued before this
-	// column's product, so HBM requests stay in flight across it.  Live state
-	// is kept small on purpose: the crc64 instantiations ran out of SGPRs.
-	for (uint32_t s = blockIdx.y; s < P.nstripes; s += gridDim.y) {
-		for (uint32_t it = blockIdx.x; it < Q.nitems; it += gridDim.x) {
+	// One item: its 4 KiB columns in order.  With PF the next column's loads
+	// are issued before this column's product, so HBM requests stay in
+	// flight across it.  Live state is kept small on purpose: the crc64
+	// instantiations ran out of SGPRs.
+	// PRE: this is the workgroup's first item, its first column already
+	// requested into xa by the prologue
+	auto walk = [&](uint32_t s, uint32_t it, auto pre) {
+			constexpr bool PRE = decltype(pre)::value;
 			uint32_t c, i, col1, khrow;
 			T crc[RM];
-			u32x4 xa[KM];
 
 			mmcs_item(Q, it, c, i, col1, khrow);
 			const uint64_t c0 = (uint64_t)c * Q.chunk_bytes;
@@ -652,7 +695,8 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 				u32x4 xb[PF ? KM : 1];
 				u32x4 *xc = PF ? xb : xa;
 
-				mm_load_any<KM>(P, k, s, c0 + (uint64_t)i * CHUNK_BYTES, lo, xa);
+				if constexpr (!PRE)
+					mm_load_any<KM>(P, k, s, c0 + (uint64_t)i * CHUNK_BYTES, lo, xa);
 				for (; i < iend; i += 2) {
 					const uint64_t cb = c0 + (uint64_t)i * CHUNK_BYTES;
 					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true, UF>(
@@ -722,8 +766,14 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 					}
 				}
 			}
-		}
-	}
+	};
+	// The workgroup's work: items blockIdx.x, blockIdx.x + gridDim.x, ... of
+	// stripe blockIdx.y (+ gridDim.y ...) -- the grid never exceeds the item
+	// and stripe counts, so the first is always there
+	walk(blockIdx.y, blockIdx.x, ecg_bool<true>{});
+	for (uint32_t s = blockIdx.y; s < P.nstripes; s += gridDim.y)
+		for (uint32_t it = s == blockIdx.y ? blockIdx.x + gridDim.x : blockIdx.x; it < Q.nitems; it += gridDim.x)
+			walk(s, it, ecg_bool<false>{});
 }
 
 // Fused product + checksum, one WAVE per (stripe, chunk): the wave walks the
