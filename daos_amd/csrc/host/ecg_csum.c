@@ -786,8 +786,8 @@ int ecg_set_fused_cols(ecg_ctx_t *ctx, uint32_t ncols)
 
 int ecg_set_csum_variant(ecg_ctx_t *ctx, uint32_t variant)
 {
-	if (ctx == NULL || (variant & 15u) > 3 || variant > 1023 || (variant & 48u) == 48u ||
-	    (variant & 576u) == 576u ||
+	if (ctx == NULL || (variant & 15u) > 3 || variant > 2047 || (variant & 48u) == 48u ||
+	    (variant & 576u) == 576u || ((variant & 1024u) && (variant & 704u)) ||
 	    (variant & 384u) == 384u)
 		return ecg_fail(-ECG_DER_INVAL, "set_csum_variant: bad arguments");
 	ctx->csum_variant = variant;
@@ -830,6 +830,16 @@ int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t
 	q->m = (uint32_t)m;
 	q->m_last = (uint32_t)((last + ECG_MMCS_STRIDE - 1) / ECG_MMCS_STRIDE);
 	q->ncols = fused_cols(ctx, m, type, k, rows);
+	/* fused kernels: table kind TB (ecg_kernels.hip); bit 6 of csum_variant
+	 * selects the s16 tables (A/B), bit 9 TB 3, bit 10 TB 4, bit 7 the
+	 * wave-per-chunk kernel */
+	q->byte_tables = (ctx->csum_variant & 1024u) ? 4 : (ctx->csum_variant & 512u) ? 3
+			 : (ctx->csum_variant & 64u) ? 2 : use_byte_tables(ctx, type, 1, k, rows);
+	/* TB 4's unrolled walk takes items of exactly 4 full columns (positional
+	 * nibble tables); other items fall back to the per-column shift */
+	if (q->byte_tables == 4 && !ctx->fused_cols && !(pthread_once(&g_fused_cols_once, fused_cols_init),
+							   g_fused_cols_env))
+		q->ncols = (uint32_t)(m < 4 ? m : 4);
 	/* bound the multiplier table (nh + nh_last rows of 256 entries) for
 	 * very long chunks: at most 2048 items per chunk */
 	if ((m + q->ncols - 1) / q->ncols > 2048)
@@ -839,10 +849,6 @@ int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t
 	if ((uint64_t)(q->nch - 1) * q->nh + q->nh_last > UINT32_MAX)
 		return 0;
 	q->nitems = (q->nch - 1) * q->nh + q->nh_last;
-	/* fused kernels: table kind TB (ecg_kernels.hip); bit 6 of csum_variant
-	 * selects the s16 tables (A/B), bit 7 the wave-per-chunk kernel */
-	q->byte_tables = (ctx->csum_variant & 512u) ? 3 : (ctx->csum_variant & 64u) ? 2
-			 : use_byte_tables(ctx, type, 1, k, rows);
 	/* the workgroup kernel for every shape: since its item tail no longer
 	 * reads HBM (round 3) it beats the wave-per-chunk kernel for crc64 at
 	 * EC_4P2 too (+13 % vs +19 % over the plain encode, profiles/r03/fused_tail/);

@@ -381,6 +381,21 @@ __device__ __forceinline__ T piece_crc16s(const uint32_t d[4], const T *s16)
 	return c;
 }
 
+// raw CRC of one 16-byte piece from one position's nibble tables q4[32][16]
+// (32 conflict-free lookups, one SDWA address each; the fused workgroup
+// kernel's TB 4: the position selects how many columns follow the piece)
+template <typename T>
+__device__ __forceinline__ T piece_crc4(const uint32_t d[4], const T *q4)
+{
+	const uint32_t hmask = nib_hmask<T>();
+	T c = 0;
+
+#pragma unroll
+	for (int j = 0; j < 4; j++)
+		c = nib_dword(c, d[j], q4, 8 * j, hmask);
+	return c;
+}
+
 // register -> register shifted by the a4 table's fixed number of zero bytes
 // (nibble fields, SDWA addresses; a4[16][16], rows >= W/4 unused)
 template <int W, typename T>

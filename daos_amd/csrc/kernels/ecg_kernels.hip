@@ -465,7 +465,8 @@ __device__ __forceinline__ const ecg_mm_params_t &kernarg_fresh()
 	return *(const ecg_mm_params_t *)p;
 }
 
-template <int KM, int RM, int W, bool REFL, int TB, bool PF, uint32_t STRIDE, bool FULL, int U, typename T>
+template <int KM, int RM, int W, bool REFL, int TB, bool PF, uint32_t STRIDE, bool FULL, int U, int FP = -1,
+	  typename T>
 __device__ __forceinline__ void mmcs_col(const ecg_mm_params_t &P0, const u32x4 *s_tbl, const T *s_sl,
 					 const T *s_sh, int k, int rows, uint32_t s, uint64_t cbase, uint64_t next,
 					 uint32_t lo, bool more, bool first, uint64_t init, uint32_t pos, bool gshift,
@@ -508,8 +509,10 @@ __device__ __forceinline__ void mmcs_col(const ecg_mm_params_t &P0, const u32x4 
 	for (int r = 0; r < RM; r++) {
 		if (r < rows) {
 #ifndef ECG_EXP_NO_CRC
-			if constexpr (TB == 3)
+			if constexpr (TB == 3 || (TB == 4 && FP < 0))
 				crc[r] = ecg_crc::lin_map4<W>(crc[r], s_sh);	// a4 of one column
+			else if constexpr (TB == 4)
+				;	// fixed position FP: no register shift
 			else if constexpr (TB != 0)
 				crc[r] = ecg_crc::lin_map5<W>(crc[r], s_sh);	// a5 of one column
 			else if (gshift && pos == F5::U - 1)
@@ -529,6 +532,8 @@ __device__ __forceinline__ void mmcs_col(const ecg_mm_params_t &P0, const u32x4 
 					crc[r] ^= ecg_crc::piece_crc16<W>(d, s_sl);
 				else if constexpr (TB == 3)
 					crc[r] ^= ecg_crc::piece_crc16s<W>(d, s_sl);
+				else if constexpr (TB == 4)	// nibble tables of position FP (0: Horner with the shift)
+					crc[r] ^= ecg_crc::piece_crc4(d, s_sl + (FP < 0 ? 0 : FP) * ECG_CSUM_NQ4);
 				else
 					crc[r] ^= ecg_crc::piece_crc5p<W>(d, s_sl, pos * (uint32_t)(F5::NF * 32 * sizeof(T)));
 #else
@@ -570,10 +575,14 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	// 0..U-1 columns + a5 shift by U columns, U = ECG_CSUM_P5U); 1 byte
 	// tables sl (slice-by-NB, register folded) + the a5 4 KiB shift; 2 byte tables s16 (16
 	// independent lookups per piece) + the a5 shift
-	constexpr int NSL = TB == 0 ? F5::N : TB == 1 ? NB * 256 : 16 * 256;
+	// 4 nibble tables q4 of the first FQ4 positions (4 KiB stride): a piece is
+	// 32 conflict-free lookups, and an item of exactly FQ4 full columns takes
+	// each column's position from the unrolled walk (no register shift)
+	constexpr int FQ4 = 4;
+	constexpr int NSL = TB == 0 ? F5::N : TB == 1 ? NB * 256 : TB == 4 ? FQ4 * ECG_CSUM_NQ4 : 16 * 256;
 	__shared__ T s_sl[NSL];
-	// TB 1/2: the column shift as 5-bit a5 tables; TB 3: as nibble a4 tables
-	__shared__ T s_sh[TB == 3 ? 16 * 16 : TB ? ECG_CSUM_NA5(NB) * 32 : 1];
+	// TB 1/2: the column shift as 5-bit a5 tables; TB 3/4: as nibble a4 tables
+	__shared__ T s_sh[TB >= 3 ? 16 * 16 : TB ? ECG_CSUM_NA5(NB) * 32 : 1];
 	__shared__ T s_r4[REFL ? 16 : 1];		// reflected: 4-bit reduction of the lane multiply
 	__shared__ T s_nibl[REFL ? 16 * 64 : 1];	// reflected: the lane factors' nibble tables
 	const int k = K ? K : (int)P.k;
@@ -592,7 +601,7 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	// barrier run in the shadow of the first HBM round trip (a workgroup
 	// normally owns exactly one item).
 	constexpr int P5 = ECG_CSUM_NF5 * 32;
-	constexpr int NSH = TB == 3 ? 16 * 16 : TB ? ECG_CSUM_NA5(NB) * 32 : 0;
+	constexpr int NSH = TB >= 3 ? 16 * 16 : TB ? ECG_CSUM_NA5(NB) * 32 : 0;
 	constexpr int NNB = REFL ? 16 * 64 + 16 : 0;		// nibl, then r4
 	constexpr int NST = NSL + NSH + NNB;
 	constexpr int QST = (NST + BLOCK - 1) / BLOCK;
@@ -603,11 +612,11 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 				return i < P5 ? ECG_CSUM_OFF_P5(NB) + i
 				     : i < UF * P5 ? ECG_CSUM_OFF_P5X_4K(NB) + i - P5 : ECG_CSUM_OFF_A5_32K(NB) + i - UF * P5;
 			else
-				return (TB == 1 ? 0 : ECG_CSUM_OFF_S16(NB)) + i;
+				return (TB == 1 ? 0 : TB == 4 ? ECG_CSUM_OFF_Q4_4K(NB) : ECG_CSUM_OFF_S16(NB)) + i;
 		}
 		i -= NSL;
 		if (i < NSH)
-			return (TB == 3 ? ECG_CSUM_OFF_A4_4K(NB) : ECG_CSUM_OFF_A5_4K(NB)) + i;
+			return (TB >= 3 ? ECG_CSUM_OFF_A4_4K(NB) : ECG_CSUM_OFF_A5_4K(NB)) + i;
 		i -= NSH;
 		return i < 16 * 64 ? ECG_CSUM_OFF_NIBL(NB) + i : ECG_CSUM_OFF_R4(NB) + i - 16 * 64;
 	};
@@ -690,6 +699,30 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 			// profiles/r02/fused_libs/rotation.json.)
 			const uint64_t nfull = (C - c0) / CHUNK_BYTES;
 			const uint32_t ifull = nfull < col1 ? (uint32_t)nfull : col1;
+			if constexpr (TB == 4 && PF) {
+				// an item of exactly FQ4 full columns: positions FQ4-1 .. 0
+				// as constants, the prefetch buffers alternating
+				if (col1 - i == FQ4 && ifull == col1) {
+					u32x4 xb[KM];
+					const uint64_t cb = c0 + (uint64_t)i * CHUNK_BYTES;
+
+					if constexpr (!PRE)
+						mm_load_any<KM>(P, k, s, cb, lo, xa);
+					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true, UF, 3>(
+						P, s_tbl, s_sl, s_sh, k, rows, s, cb, cb + CHUNK_BYTES, lo, true,
+						i == 0 && threadIdx.x == 0, Q.init, 0, false, xa, xb, crc);
+					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true, UF, 2>(
+						P, s_tbl, s_sl, s_sh, k, rows, s, cb + CHUNK_BYTES, cb + 2 * CHUNK_BYTES, lo, true,
+						false, Q.init, 0, false, xb, xa, crc);
+					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true, UF, 1>(
+						P, s_tbl, s_sl, s_sh, k, rows, s, cb + 2 * CHUNK_BYTES, cb + 3 * CHUNK_BYTES, lo, true,
+						false, Q.init, 0, false, xa, xb, crc);
+					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true, UF, 0>(
+						P, s_tbl, s_sl, s_sh, k, rows, s, cb + 3 * CHUNK_BYTES, 0, lo, false,
+						false, Q.init, 0, false, xb, xa, crc);
+					i = col1;
+				}
+			}
 			const uint32_t iend = ifull > i ? i + ((ifull - i) & ~1u) : i;
 			if (PF && i < iend) {
 				u32x4 xb[PF ? KM : 1];
@@ -1163,6 +1196,11 @@ static const csentry g_cskernels[] = {
 	CSB(8, 2, 2, 32, true, "crc32", 1), CSB(8, 2, 2, 32, true, "crc32", 2), CSB(8, 2, 3, 64, true, "crc64", 0),
 	CSB(8, 2, 3, 64, true, "crc64", 2), CSB(4, 2, 2, 32, true, "crc32", 2), CSB(4, 2, 3, 64, true, "crc64", 2),
 	CSB(8, 1, 2, 32, true, "crc32", 2),
+	/* TB 4: positional nibble tables (4 KiB stride, 4 positions) + nibble a4 column shift */
+	CSB(8, 2, 2, 32, true, "crc32", 4), CSB(8, 2, 3, 64, true, "crc64", 4), CSB(4, 2, 2, 32, true, "crc32", 4),
+	CSB(4, 2, 3, 64, true, "crc64", 4), CSB(8, 1, 2, 32, true, "crc32", 4), CSB(8, 1, 3, 64, true, "crc64", 4),
+	CSB(16, 2, 2, 32, true, "crc32", 4), CSB(16, 2, 3, 64, true, "crc64", 4),
+	CSB(8, 3, 2, 32, true, "crc32", 4), CSB(8, 3, 3, 64, true, "crc64", 4),
 	/* TB 3: s16 byte tables with SDWA addresses + nibble a4 column shift */
 	CSB(8, 2, 2, 32, true, "crc32", 3), CSB(8, 2, 3, 64, true, "crc64", 3), CSB(4, 2, 2, 32, true, "crc32", 3),
 	CSB(4, 2, 3, 64, true, "crc64", 3), CSB(8, 1, 2, 32, true, "crc32", 3), CSB(16, 2, 2, 32, true, "crc32", 3),

@@ -101,7 +101,9 @@ int ecg_set_csum_launch(ecg_ctx_t *ctx, uint32_t max_blocks);
  * kernel shape (default: a wave per chunk for crc64 with k <= 4, else
  * workgroups over work items): bit 7 forces the wave per chunk, bit 8 the
  * workgroups.  Bit 9: the fused kernels' s16 byte tables with SDWA addresses
- * and the nibble column shift (TB 3).  Standalone CRC kernels default to the
+ * and the nibble column shift (TB 3).  Bit 10: the fused workgroup kernel's
+ * positional nibble tables (TB 4; items of 4 columns unless set otherwise;
+ * not combinable with bits 6, 7, 9).  Standalone CRC kernels default to the
  * nibble tables; bit 4 / bit 5 select the byte / 5-bit tables there too. */
 int ecg_set_csum_variant(ecg_ctx_t *ctx, uint32_t variant);
 

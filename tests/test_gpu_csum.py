@@ -443,3 +443,43 @@ def test_encode_csum_tb3_tables(oracle, ecglib, ctx, case, shape):
     finally:
         L.ecg_set_csum_variant(ctx.h, 0)
         d.free(); par.free(); out.free()
+
+
+TB4 = [  # (k, p, htype): the fused workgroup kernel's positional nibble instantiations (csum_variant bit 10)
+    (8, 2, 2), (8, 2, 3), (4, 2, 2), (4, 2, 3), (8, 1, 2), (8, 1, 3), (16, 2, 2), (16, 2, 3), (8, 3, 2), (8, 3, 3),
+]
+
+
+@pytest.mark.parametrize("cols", [0, 3, 8])        # 4-column items (the unrolled walk) / other items (the shift)
+@pytest.mark.parametrize("case", TB4)
+def test_encode_csum_tb4_tables(oracle, ecglib, ctx, case, cols):
+    """The TB 4 table kind (nibble tables of 4 column positions, one SDWA
+    address per lookup; items of exactly 4 full columns unrolled with constant
+    positions, other items Horner-folded with the nibble column shift) gives the
+    oracle's parity and chunk checksums -- ragged last chunk and 16-byte tail
+    of the cell included."""
+    k, p, htype = case
+    C, S, cs = 3 * 32768 + 4096 + 16, 3, 32768
+    L = ecglib.lib()
+    nch = L.ecg_csum_chunk_count(cs, 1, 0, C)
+    cl = L.ecg_csum_len(htype)
+    rng = np.random.default_rng(k * 10 + p + htype + cols)
+    data = rng.integers(0, 256, S * k * C, dtype=np.uint8)
+    d = ctx.to_device(data)
+    par = ctx.alloc(p * S * C)
+    out = ctx.alloc(p * S * nch * cl)
+    try:
+        assert L.ecg_set_csum_variant(ctx.h, 1024) == 0
+        assert L.ecg_set_fused_cols(ctx.h, cols) == 0
+        ctx.encode_csum(k, p, C, S, d.ptr, k * C, par.ptr, S * C, C, htype, cs, 1, out.ptr)
+        ctx.sync()
+        assert L.ecg_last_kernel().decode().endswith(",tb4>"), L.ecg_last_kernel()
+        want_par = oracle.encode_batch(k, p, C, S, data, nthreads=8, simd=True).reshape(p, S, C)
+        assert np.array_equal(par.download().reshape(p, S, C), want_par)
+        got = out.download().view(DT[cl]).reshape(p, S, nch)
+        want = _want_cell_csums(oracle, htype, cs, 1, want_par).reshape(p, S, nch)
+        assert np.array_equal(got, want), np.argwhere(got != want)[:5]
+    finally:
+        L.ecg_set_csum_variant(ctx.h, 0)
+        L.ecg_set_fused_cols(ctx.h, 0)
+        d.free(); par.free(); out.free()

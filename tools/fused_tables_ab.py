@@ -1,6 +1,7 @@
 """Fused product + crc32 / crc64 table kinds: the 5-bit tables (crc32's
 default), the byte tables (bit 4; crc64's default), and the s16 byte tables
-with SDWA addresses + nibble column shift (bit 9, TB 3), in one process, the order of the
+with SDWA addresses + nibble column shift (bit 9, TB 3; with AB_OLD_KINDS=1),
+and the positional nibble tables (bit 10, TB 4), against each hash's default, in one process, the order of the
 configurations rotated every round so neither always follows the plain
 encode (tools/fused_libs.py keeps a fixed order and showed a ~1-2 % position
 bias); median of 21 rounds after 10 warm-up rounds, random cells, 1 MiB
@@ -48,8 +49,11 @@ def main():
             return fn
         cfgs = [("encode", lambda k=k, p=p, S=S, pitch=pitch: ctx.encode(k, p, C, S, buf.ptr, k * C, par.ptr,
                                                                           pitch, C)),
-                ("crc32_5bit", fused(32)), ("crc32_bytes", fused(16)), ("crc32_tb3", fused(512)),
-                ("crc64_dflt", fused(0, ecg.HASH_CRC64)), ("crc64_tb3", fused(512 | 256, ecg.HASH_CRC64))]
+                ("crc32_dflt", fused(0)), ("crc32_tb4", fused(1024)),
+                ("crc64_dflt", fused(0, ecg.HASH_CRC64)), ("crc64_tb4", fused(1024, ecg.HASH_CRC64))]
+        if os.environ.get("AB_OLD_KINDS"):
+            cfgs += [("crc32_5bit", fused(32)), ("crc32_bytes", fused(16)), ("crc32_tb3", fused(512)),
+                     ("crc64_tb3", fused(512 | 256, ecg.HASH_CRC64))]
         # a configuration this shape has no instantiation for is dropped
         ok = []
         for n, fn in cfgs:
