@@ -589,7 +589,13 @@ def mix_ceiling(ceil, read_frac):
     return 1.0 / (read_frac / ceil["read"] + (1 - read_frac) / ceil["write"])
 
 
-def detail_rows(ctx, ceil, iters=11):
+DETAIL_SHAPES = (("EC_8P2_1MiB_encode", 8, 2, 1 << 20, 512, "enc"),
+                 ("EC_8P2_1MiB_decode_d0d1", 8, 2, 1 << 20, 512, "dec"),
+                 ("EC_16P2_128KiB_encode", 16, 2, 128 << 10, 1024, "enc"),
+                 ("EC_2P1_128KiB_encode", 2, 1, 128 << 10, 1024, "enc"))
+
+
+def detail_rows(ctx, ceil, iters=11, shapes=DETAIL_SHAPES, csum=True):
     """Extra device-resident rows (per GPU): the north-star EC_8P2 encode,
     EC_8P2 2-erasure decode, EC_16P2 128 KiB encode, EC_2P1 128 KiB encode.
     Encodes use the client write layout (data [S][k][C], parity [p][S][C] at
@@ -598,10 +604,7 @@ def detail_rows(ctx, ceil, iters=11):
     from daos_amd import ecg
 
     rows = {}
-    for name, k, p, C, S, mode in (("EC_8P2_1MiB_encode", 8, 2, 1 << 20, 512, "enc"),
-                                   ("EC_8P2_1MiB_decode_d0d1", 8, 2, 1 << 20, 512, "dec"),
-                                   ("EC_16P2_128KiB_encode", 16, 2, 128 << 10, 1024, "enc"),
-                                   ("EC_2P1_128KiB_encode", 2, 1, 128 << 10, 1024, "enc")):
+    for name, k, p, C, S, mode in shapes:
         st = (k + p) * C
         # encodes: the data cells alone, [S][k][C] (DAOS's client write buffer); decodes:
         # the whole recovery image [S][k+p][C]
@@ -621,9 +624,12 @@ def detail_rows(ctx, ceil, iters=11):
             fn = (lambda buf=buf, k=k, p=p, C=C, S=S, st=st:
                   ctx.recover(k, p, C, S, buf.ptr, st, [0, 1]))
             rd, wr = k, 2
-        # 10 warm-up launches: the launch tuner (include/ecg.h ecg_set_autotune) times its
-        # two arms over the first 8 launches of a wide shape; the timed launches run its choice
-        ms = time_kernel(ctx, fn, iters, warm=10)
+        # 40 warm-up launches: the launch tuner (include/ecg.h ecg_set_autotune) times its
+        # two arms over the first 8 launches of a wide shape; the timed launches run its choice.
+        # After the switch to the chosen geometry the first ~10-20 launches run up to 12 %
+        # slow (EC_16P2 cap 2: 0.434 ms, then 0.38, tools/state_check3.py,
+        # profiles/r03/tuner_check/), so the timed launches start after those
+        ms = time_kernel(ctx, fn, iters, warm=40)
         tuned = (ctx.tune_state(k, p, C, S, k * C, C) if mode == "enc"
                  else ctx.tune_state(k, 2, C, S, st, st))
         alg = (rd + wr) * C * S
@@ -641,6 +647,8 @@ def detail_rows(ctx, ceil, iters=11):
         buf.free()
         if buf2 is not None:
             buf2.free()
+    if not csum:
+        return rows
     # checksums of regenerated cells (include/ecg_csum.h): EC_8P2 encode with
     # crc32 over 32 KiB chunks of the parity, fused vs the product alone, and
     # the standalone checksum kernel over 1 GiB of 1 MiB cells
@@ -684,7 +692,7 @@ def detail_rows(ctx, ceil, iters=11):
                                                      1, ecg.HASH_CRC32, 32768, par.ptr, out.ptr, pieces, S,
                                                      ctypes.byref(npc), None), "migrate_update_parity")
 
-    ms = time_kernel(ctx, shard, iters, warm=10)
+    ms = time_kernel(ctx, shard, iters, warm=40)
     alg = (k + 1) * C * S
     rows["EC_8P2_1MiB_rebuild_parity_shard_crc32"] = {
         "GiBps_user": round(k * C * S / (ms / 1e3) / GIB, 1), "alg_GBps": round(alg / ms / 1e6, 1),
