@@ -495,7 +495,10 @@ static uint32_t fused_cols(const ecg_ctx_t *ctx, uint64_t m, int type, int k, in
 	 * one output row (a parity shard's rebuild) 4; >= 2 rows: 4 for k >= 8
 	 * (EC_8P2 crc32 +8 % vs +18 % at 8; crc64, now that its item tail reads no
 	 * HBM, +12.5 % vs +20 %), 8 for k <= 4 (EC_4P2 crc32 +8 % vs +15 % at 4) */
-	const uint64_t dflt = rows == 1 ? 4 : k >= 8 ? 4 : 8;
+	/* round 3, after the item tail stopped reading HBM: crc32 at EC_8P2 (byte
+	 * tables) walks 2 columns best -- +6.0 / +7.3 % vs +9.0 / +9.9 % at 4 on two
+	 * boxes; k = 16 and one or three rows keep 4 (profiles/r03/fused_cols/) */
+	const uint64_t dflt = type == ECG_HASH_CRC32 && k == 8 && rows == 2 ? 2 : rows == 1 ? 4 : k >= 8 ? 4 : 8;
 	const int env = ctx->fused_cols ? (int)ctx->fused_cols
 					: (pthread_once(&g_fused_cols_once, fused_cols_init), g_fused_cols_env);
 

@@ -109,8 +109,9 @@ int ecg_set_csum_variant(ecg_ctx_t *ctx, uint32_t variant);
 
 /* Launch tuning: 4 KiB columns per work item of the fused product +
  * checksum kernels (ecg_encode_csum / ecg_recover_csum); 0 restores the
- * default (env ECG_FUSED_COLS, else by hash type, k and output rows: 8 for
- * crc64, 4 for one row or k >= 8, else 8).  Same results either way. */
+ * default (env ECG_FUSED_COLS, else by hash type, k and output rows: 2 for
+ * crc32 with k = 8 and two rows, 4 for one row or k >= 8, else 8; 4 with the
+ * TB 4 tables).  Same results either way. */
 int ecg_set_fused_cols(ecg_ctx_t *ctx, uint32_t ncols);
 
 #ifdef __cplusplus

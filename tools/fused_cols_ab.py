@@ -2,7 +2,8 @@
 4 / 8; 1 = one 4 KiB column per workgroup, the plain kernel's shape) for crc32
 and crc64 against the plain encode, EC_8P2 x 512 and EC_4P2 x 1024 (1 MiB
 cells, 32 KiB chunks, random data); configurations rotated every round, median
-of 21 after 10 warm-up rounds.  -> gpurun_out/fused_cols_ab.json.  Bench infrastructure."""
+of 21 after 10 warm-up rounds.  Env AB_SHAPES="k,p,S ...", AB_COLS="2,4",
+AB_HASH="crc32" narrow it.  -> gpurun_out/fused_cols_ab.json.  Bench infrastructure."""
 import json
 import os
 import sys
@@ -25,9 +26,14 @@ def main():
     par = ctx.alloc(2 * (1024 * C + 4096))
     out = ctx.alloc(2 * 1024 * 32 * 8)
     res = {}
-    for k, p, S in ((8, 2, 512), (4, 2, 1024)):
+    shapes = [tuple(int(x) for x in a.split(",")) for a in os.environ.get("AB_SHAPES", "").split()]
+    colset = [int(x) for x in os.environ.get("AB_COLS", "1,2,4,8,0").split(",")]
+    hashes = [(h, hn) for h, hn in ((ecg.HASH_CRC32, "crc32"), (ecg.HASH_CRC64, "crc64"))
+              if hn in os.environ.get("AB_HASH", "crc32,crc64")]
+    for k, p, S in shapes or ((8, 2, 512), (4, 2, 1024)):
         pitch = S * C + 4096
-        assert k * S * C <= buf.nbytes and p * pitch <= par.nbytes
+        if not (k * S * C <= buf.nbytes and p * pitch <= par.nbytes and p * S * 32 * 8 <= out.nbytes):
+            raise SystemExit(f"fused_cols_ab: shape {k},{p},{S} exceeds the buffers")
 
         def fused(cols, htype, var=0, k=k, p=p, S=S, pitch=pitch):
             def fn():
@@ -38,8 +44,8 @@ def main():
                 L.ecg_set_csum_variant(ctx.h, 0)
             return fn
         cfgs = [("encode", lambda k=k, p=p, S=S, pitch=pitch: ctx.encode(k, p, C, S, buf.ptr, k * C, par.ptr, pitch, C))]
-        for h, hn in ((ecg.HASH_CRC32, "crc32"), (ecg.HASH_CRC64, "crc64")):
-            for cols in (1, 2, 4, 8, 0):
+        for h, hn in hashes:
+            for cols in colset:
                 cfgs.append((f"{hn}_c{cols}", fused(cols, h, 256 if cols else 0)))
         ts = {n: [] for n, _ in cfgs}
         for rnd in range(31):
