@@ -10,8 +10,9 @@
  * won on one box in every allocation trial and lost 4-6 % on another, and no
  * pointer residue predicts it.  The library therefore measures instead of
  * guessing: the first launches of each large wide shape in a context run as
- * two back-to-back blocks -- ECG_TUNE_W + ECG_TUNE_T launches uncapped, then
- * as many at the candidate cap -- timed with HIP events on the launch stream;
+ * two back-to-back blocks -- ECG_TUNE_W0 + ECG_TUNE_T launches uncapped, then
+ * ECG_TUNE_W1 + ECG_TUNE_T at the candidate cap, the last ECG_TUNE_T of each
+ * timed with HIP events on the launch stream;
  * once the events have completed (queried without blocking on a later launch
  * of the shape) the faster arm is kept for the shape, the cap only when it
  * wins by more than ECG_TUNE_MARGIN.  Results never depend on the choice
@@ -27,9 +28,16 @@
 
 #include "ecg_internal.h"
 
-#define ECG_TUNE_W 1		/* untimed launches at the start of each arm */
+#define ECG_TUNE_W0 1		/* untimed launches at the start of the uncapped arm */
+/* ... and of the capped arm: the first ~10-20 launches after a switch to a
+ * capped geometry run up to 12 % slow (EC_16P2 at 2 blocks per CU: 0.434 ms,
+ * then 0.38, tools/state_check3.py, profiles/r03/tuner_check/) -- timing them
+ * rejected caps that win in the steady state.  Switching back to uncapped
+ * shows no such transient, and a kept cap needs no switch at all. */
+#define ECG_TUNE_W1 16
 #define ECG_TUNE_T 3		/* timed launches per arm (median) */
-#define ECG_TUNE_ARM (ECG_TUNE_W + ECG_TUNE_T)
+#define ECG_TUNE_ARM0 (ECG_TUNE_W0 + ECG_TUNE_T)
+#define ECG_TUNE_PROBE (ECG_TUNE_ARM0 + ECG_TUNE_W1 + ECG_TUNE_T)
 #define ECG_TUNE_MARGIN 0.015	/* the cap must win by more than 1.5 % */
 
 struct ecg_tune_ent {
@@ -239,12 +247,12 @@ int ecg_tune_launch(ecg_ctx_t *ctx, const ecg_mm_params_t *p, hipStream_t st, ui
 	}
 	e = lookup(t, p, 1);
 	e->cand = cand;
-	if (e->decided || (e->n >= 2 * ECG_TUNE_ARM && try_decide(e))) {
+	if (e->decided || (e->n >= ECG_TUNE_PROBE && try_decide(e))) {
 		cfg.wg_per_cu = e->choice;
 		pthread_mutex_unlock(&t->lock);
 		return ecg_k_launch_matmul(p, &cfg, (void *)st, kid);
 	}
-	if (e->n >= 2 * ECG_TUNE_ARM) {		/* timings still in flight: run uncapped */
+	if (e->n >= ECG_TUNE_PROBE) {		/* timings still in flight: run uncapped */
 		cfg.wg_per_cu = ECG_WG_UNCAPPED;
 		pthread_mutex_unlock(&t->lock);
 		return ecg_k_launch_matmul(p, &cfg, (void *)st, kid);
@@ -259,8 +267,8 @@ int ecg_tune_launch(ecg_ctx_t *ctx, const ecg_mm_params_t *p, hipStream_t st, ui
 	/* probing: arm 0 uncapped, arm 1 capped, each W untimed + T timed, back
 	 * to back; the lock is held across the timed launch so concurrent callers
 	 * of the shape cannot interleave inside an event pair */
-	arm = e->n < ECG_TUNE_ARM ? 0 : 1;
-	idx = (int)(e->n % ECG_TUNE_ARM) - ECG_TUNE_W;
+	arm = e->n < ECG_TUNE_ARM0 ? 0 : 1;
+	idx = arm ? (int)(e->n - ECG_TUNE_ARM0) - ECG_TUNE_W1 : (int)e->n - ECG_TUNE_W0;
 	e->n++;
 	cfg.wg_per_cu = arm ? cand : ECG_WG_UNCAPPED;
 	if (idx >= 0)
@@ -296,7 +304,7 @@ int ecg_tune_state(ecg_ctx_t *ctx, int k, int rows, uint64_t cell_bytes, uint32_
 	p->dst_stripe_stride = dstride;
 	pthread_mutex_lock(&t->lock);
 	e = lookup(t, p, 0);
-	if (e && !e->decided && e->n >= 2 * ECG_TUNE_ARM)
+	if (e && !e->decided && e->n >= ECG_TUNE_PROBE)
 		(void)try_decide(e);
 	rc = e && e->decided ? 1 : 0;
 	if (cap)

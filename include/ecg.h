@@ -270,9 +270,10 @@ int ecg_set_launch_order(ecg_ctx_t *ctx, uint32_t order);
  * with unused dynamic LDS.  Tuning only; results never depend on it. */
 int ecg_set_wg_per_cu(ecg_ctx_t *ctx, uint32_t wg_per_cu);
 /* Launch tuner (on by default; ECG_AUTOTUNE=0 in the environment turns it off
- * for new contexts): the first 8 product launches of each wide shape (k >= 8,
- * > 2048 blocks) in a context run 4 uncapped then 4 at the candidate cap (k = 16:
- * 2 blocks per CU, k = 8: 3), timed with events on the launch stream; once the
+ * for new contexts): the first 23 product launches of each wide shape (k >= 8,
+ * > 2048 blocks) in a context run 4 uncapped then 19 at the candidate cap (k = 16:
+ * 2 blocks per CU, k = 8: 3), the last 3 of each arm timed with events on the
+ * launch stream (a switch to a cap runs slow for its first ~10-20 launches); once the
  * timings have completed the faster is kept for the shape (the cap only when
  * it wins by > 1.5 %).  Skipped when ecg_set_wg_per_cu or ecg_set_launch /
  * _order set a geometry, and on streams under graph capture.  on: 0 off, 1 on,

@@ -79,9 +79,12 @@ def test_wg_per_cu_rejects_bad_values(ctx):
     ctx.set_wg_per_cu(0)
 
 
+PROBE = 23   # ecg_tune.c ECG_TUNE_PROBE: launches before the decision
+
+
 def test_autotune_probes_decides_and_keeps_bytes(ctx, oracle):
-    """The launch tuner (ecg_tune.c) runs the first 8 launches of a wide shape
-    as 4 uncapped + 4 capped, then keeps the faster: every launch -- probing,
+    """The launch tuner (ecg_tune.c) runs the first 23 launches of a wide shape
+    as 4 uncapped + 19 capped, then keeps the faster: every launch -- probing,
     capped or not, and after the decision -- writes the oracle's parity, and
     the decision is one of the two arms."""
     k, p, S, C_ = 16, 2, 300, 32768          # 8 columns x 300 stripes = 2400 blocks (> 2048: tuned)
@@ -92,7 +95,7 @@ def test_autotune_probes_decides_and_keeps_bytes(ctx, oracle):
     try:
         d = ctx.to_device(data)
         assert ctx.tune_state(k, p, C_, S, k * C_, C_) is None
-        pars = [ctx.alloc(p * S * C_) for _ in range(10)]
+        pars = [ctx.alloc(p * S * C_) for _ in range(PROBE + 2)]
         for par in pars:
             ctx.encode(k, p, C_, S, d.ptr, k * C_, par.ptr, S * C_, C_)
         ctx.sync()
@@ -103,7 +106,7 @@ def test_autotune_probes_decides_and_keeps_bytes(ctx, oracle):
         # decided shapes keep their choice; the recovery shape (rows = 2, in
         # place) is tuned on its own and recovers the same bytes
         img = np.concatenate([data, want.transpose(1, 0, 2)], axis=1)          # [S][k+p][C]
-        for i in range(9):
+        for i in range(PROBE + 1):
             lost = img.copy()
             lost[:, [i % k, k]] = 0x3C
             stb = ctx.to_device(lost)
@@ -126,13 +129,13 @@ def test_autotune_off_and_explicit_cap_skip_tuning(ctx):
     try:
         ctx.set_autotune(2)
         ctx.set_autotune(0)
-        for _ in range(10):
+        for _ in range(PROBE + 2):
             ctx.encode(k, p, C_, S, d.ptr, k * C_, par.ptr, S * C_, C_)
         ctx.sync()
         assert ctx.tune_state(k, p, C_, S, k * C_, C_) is None
         ctx.set_autotune(1)
         ctx.set_wg_per_cu(255)
-        for _ in range(10):
+        for _ in range(PROBE + 2):
             ctx.encode(k, p, C_, S, d.ptr, k * C_, par.ptr, S * C_, C_)
         ctx.sync()
         assert ctx.tune_state(k, p, C_, S, k * C_, C_) is None
