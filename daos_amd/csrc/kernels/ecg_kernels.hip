@@ -52,6 +52,15 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef ECG_FUSED_WPE
 #define ECG_FUSED_WPE(W) ((W) == 64 ? 4 : 3)
 #endif
+// fused workgroup kernel: fold each column's outputs into the CRC one column
+// later, while the next column's product is computed (independent work the
+// scheduler can interleave with the lookup chains).  Bit 0: crc16/crc32,
+// bit 1: crc64.  Measured (tools/fused_libs.py, 3 interleaved rounds,
+// profiles/r03/defer/): EC_8P2 x 512 crc64 0.906 -> 0.886 ms (encode 0.838),
+// crc32 and EC_4P2 unchanged within +-0.5 %.
+#ifndef ECG_FUSED_DEFER
+#define ECG_FUSED_DEFER 3
+#endif
 
 template <bool B>
 struct ecg_bool {
@@ -465,46 +474,23 @@ __device__ __forceinline__ const ecg_mm_params_t &kernarg_fresh()
 	return *(const ecg_mm_params_t *)p;
 }
 
-template <int KM, int RM, int W, bool REFL, int TB, bool PF, uint32_t STRIDE, bool FULL, int U, int FP = -1,
-	  typename T>
-__device__ __forceinline__ void mmcs_col(const ecg_mm_params_t &P0, const u32x4 *s_tbl, const T *s_sl,
-					 const T *s_sh, int k, int rows, uint32_t s, uint64_t cbase, uint64_t next,
-					 uint32_t lo, bool more, bool first, uint64_t init, uint32_t pos, bool gshift,
-					 u32x4 *cur, u32x4 *nxt, T *crc)
+// A column's outputs waiting to be folded (ECG_FUSED_DEFER): the fold of
+// column i runs after column i+1's product.  The zero state (have = false,
+// gshift = false) folds to nothing on a zero register.
+template <int RM>
+struct mmcs_pend {
+	u32x4 v[RM];
+	bool have, first, gshift;
+	uint32_t pos;
+};
+
+// Fold one column's output pieces into the rows' CRC registers: the register
+// shift of the table kind, then the piece's lookups (see mmcs_col).
+template <int RM, int W, bool REFL, int TB, int U, int FP, typename T>
+__device__ __forceinline__ void mmcs_fold(const T *s_sl, const T *s_sh, int rows, const u32x4 *outv, bool have,
+					  bool first, uint64_t init, uint32_t pos, bool gshift, T *crc)
 {
 	using F5 = ecg_crc::f5u<W, U>;
-#ifdef ECG_EXP_KARG_CACHED
-	const ecg_mm_params_t &P = P0;			// experimental: arguments held by the compiler
-#else
-	const ecg_mm_params_t &P = kernarg_fresh();	// == P0 (first kernel argument)
-	(void)P0;
-#endif
-	const uint64_t C = P.cell_bytes;
-	const bool have = FULL || cbase + lo + 16 <= C;	// C % 16 == 0
-	u32x4 outv[RM];
-	uint32_t z = 0;
-
-	if constexpr (PF) {
-		// no branch around the prefetch: a load that may or may not be
-		// issued makes the compiler's waitcnt merge wait for everything
-		// (vmcnt(0)) before the product.  Past the item's last column the
-		// wave re-reads stripe 0's first column (cache-resident, unused).
-		mm_load_any<KM>(P, k, more ? s : 0, more ? next : 0, lo, nxt);
-	} else {
-		// unconditional (clamped) loads: a load skipped by some lanes would
-		// keep cur live across columns and items (zero-filled and spilled)
-		mm_load_any<KM>(P, k, s, cbase, lo, cur);
-	}
-	asm volatile("" : "+v"(z));
-	const u32x4 *tb = s_tbl + z;
-	// FULL (the column lies inside the cell): no branch, so the pipelined
-	// loop of the callers has one path -- a partial-column path that may skip
-	// the loads or use other registers for its stores makes the compiler wait
-	// for everything (vmcnt(0)) at the loop head
-	if (FULL || cbase + STRIDE <= C)
-		mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, cur, outv);
-	else if (have)
-		mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, cur, outv);
 #pragma unroll
 	for (int r = 0; r < RM; r++) {
 		if (r < rows) {
@@ -544,6 +530,68 @@ __device__ __forceinline__ void mmcs_col(const ecg_mm_params_t &P0, const u32x4 
 	}
 }
 
+// DF: 0 fold this column now; 1 fold the pending column (fixed position FPP)
+// and leave this one pending; 2 leave this one pending (nothing pending yet).
+template <int KM, int RM, int W, bool REFL, int TB, bool PF, uint32_t STRIDE, bool FULL, int U, int FP = -1,
+	  int DF = 0, int FPP = -1, typename T>
+__device__ __forceinline__ void mmcs_col(const ecg_mm_params_t &P0, const u32x4 *s_tbl, const T *s_sl,
+					 const T *s_sh, int k, int rows, uint32_t s, uint64_t cbase, uint64_t next,
+					 uint32_t lo, bool more, bool first, uint64_t init, uint32_t pos, bool gshift,
+					 u32x4 *cur, u32x4 *nxt, T *crc, mmcs_pend<RM> *pd = nullptr)
+{
+#ifdef ECG_EXP_KARG_CACHED
+	const ecg_mm_params_t &P = P0;			// experimental: arguments held by the compiler
+#else
+	const ecg_mm_params_t &P = kernarg_fresh();	// == P0 (first kernel argument)
+	(void)P0;
+#endif
+	const uint64_t C = P.cell_bytes;
+	const bool have = FULL || cbase + lo + 16 <= C;	// C % 16 == 0
+	u32x4 outv[RM];
+	uint32_t z = 0;
+
+	if constexpr (PF) {
+		// no branch around the prefetch: a load that may or may not be
+		// issued makes the compiler's waitcnt merge wait for everything
+		// (vmcnt(0)) before the product.  Past the item's last column the
+		// wave re-reads stripe 0's first column (cache-resident, unused).
+		mm_load_any<KM>(P, k, more ? s : 0, more ? next : 0, lo, nxt);
+	} else {
+		// unconditional (clamped) loads: a load skipped by some lanes would
+		// keep cur live across columns and items (zero-filled and spilled)
+		mm_load_any<KM>(P, k, s, cbase, lo, cur);
+	}
+	asm volatile("" : "+v"(z));
+	const u32x4 *tb = s_tbl + z;
+	// FULL (the column lies inside the cell): no branch, so the pipelined
+	// loop of the callers has one path -- a partial-column path that may skip
+	// the loads or use other registers for its stores makes the compiler wait
+	// for everything (vmcnt(0)) at the loop head
+	if constexpr (!FULL && DF != 0) {
+#pragma unroll
+		for (int r = 0; r < RM; r++)
+			outv[r] = (u32x4){0, 0, 0, 0};
+	}
+	if (FULL || cbase + STRIDE <= C)
+		mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, cur, outv);
+	else if (have)
+		mm_compute<KM, RM, false, true>(P, tb, k, rows, s, cbase, lo, cur, outv);
+	if constexpr (DF == 0) {
+		mmcs_fold<RM, W, REFL, TB, U, FP>(s_sl, s_sh, rows, outv, have, first, init, pos, gshift, crc);
+	} else {
+		if constexpr (DF == 1)
+			mmcs_fold<RM, W, REFL, TB, U, FPP>(s_sl, s_sh, rows, pd->v, pd->have, pd->first, init, pd->pos,
+							   pd->gshift, crc);
+#pragma unroll
+		for (int r = 0; r < RM; r++)
+			pd->v[r] = outv[r];
+		pd->have = have;
+		pd->first = first;
+		pd->pos = pos;
+		pd->gshift = gshift;
+	}
+}
+
 // Fused product + checksum of every output cell (ecg_kabi.h, ecg_mmcs_params).
 // Block = a stream of (stripe, sub-chunk) items of a few 4 KiB columns each;
 // it walks the columns, computing and storing the outputs exactly as
@@ -568,6 +616,7 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 	constexpr int KM = K ? K : ECG_KMAX_K;
 	constexpr int RM = R ? R : ECG_KMAX_R;
 	constexpr bool PF = K != 0 && K <= ECG_FUSED_PF_MAXK && (ECG_FUSED_PF64 || W != 64);	// prefetch: 4*KM more VGPRs
+	constexpr bool DEFER = (ECG_FUSED_DEFER & (W == 64 ? 2 : 1)) != 0;	// fold one column late
 	constexpr int T2V = (RM + 3) / 4;
 	constexpr int PER_J = RM + T2V;
 	__shared__ u32x4 s_tbl[KM * PER_J];
@@ -699,6 +748,17 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 			// profiles/r02/fused_libs/rotation.json.)
 			const uint64_t nfull = (C - c0) / CHUNK_BYTES;
 			const uint32_t ifull = nfull < col1 ? (uint32_t)nfull : col1;
+			// DEFER: each column's fold runs one column late (mmcs_pend);
+			// the zero state folds to nothing on the zero register
+			mmcs_pend<RM> pd;
+			constexpr int D1 = DEFER ? 1 : 0;	// steady state
+			constexpr int D2 = DEFER ? 2 : 0;	// a walk's first column
+			bool tb4done = false;
+#pragma unroll
+			for (int r = 0; r < RM; r++)
+				pd.v[r] = (u32x4){0, 0, 0, 0};
+			pd.have = pd.first = pd.gshift = false;
+			pd.pos = 0;
 			if constexpr (TB == 4 && PF) {
 				// an item of exactly FQ4 full columns: positions FQ4-1 .. 0
 				// as constants, the prefetch buffers alternating
@@ -708,18 +768,22 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 
 					if constexpr (!PRE)
 						mm_load_any<KM>(P, k, s, cb, lo, xa);
-					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true, UF, 3>(
+					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true, UF, 3, D2>(
 						P, s_tbl, s_sl, s_sh, k, rows, s, cb, cb + CHUNK_BYTES, lo, true,
-						i == 0 && threadIdx.x == 0, Q.init, 0, false, xa, xb, crc);
-					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true, UF, 2>(
+						i == 0 && threadIdx.x == 0, Q.init, 0, false, xa, xb, crc, &pd);
+					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true, UF, 2, D1, 3>(
 						P, s_tbl, s_sl, s_sh, k, rows, s, cb + CHUNK_BYTES, cb + 2 * CHUNK_BYTES, lo, true,
-						false, Q.init, 0, false, xb, xa, crc);
-					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true, UF, 1>(
+						false, Q.init, 0, false, xb, xa, crc, &pd);
+					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true, UF, 1, D1, 2>(
 						P, s_tbl, s_sl, s_sh, k, rows, s, cb + 2 * CHUNK_BYTES, cb + 3 * CHUNK_BYTES, lo, true,
-						false, Q.init, 0, false, xa, xb, crc);
-					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true, UF, 0>(
+						false, Q.init, 0, false, xa, xb, crc, &pd);
+					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true, UF, 0, D1, 1>(
 						P, s_tbl, s_sl, s_sh, k, rows, s, cb + 3 * CHUNK_BYTES, 0, lo, false,
-						false, Q.init, 0, false, xb, xa, crc);
+						false, Q.init, 0, false, xb, xa, crc, &pd);
+					if constexpr (DEFER)
+						mmcs_fold<RM, W, REFL, TB, UF, 0>(s_sl, s_sh, rows, pd.v, pd.have, pd.first,
+										  Q.init, pd.pos, pd.gshift, crc);
+					tb4done = true;
 					i = col1;
 				}
 			}
@@ -730,20 +794,36 @@ ecg_mm_csum_kernel(const ecg_mm_params_t P, const ecg_mmcs_params_t Q)
 
 				if constexpr (!PRE)
 					mm_load_any<KM>(P, k, s, c0 + (uint64_t)i * CHUNK_BYTES, lo, xa);
+				if constexpr (DEFER) {
+					// the first trip peeled: nothing pending at its first column
+					const uint64_t cb = c0 + (uint64_t)i * CHUNK_BYTES;
+					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true, UF, -1, D2>(
+						P, s_tbl, s_sl, s_sh, k, rows, s, cb, cb + CHUNK_BYTES, lo, true,
+						i == 0 && threadIdx.x == 0, Q.init, (col1 - 1 - i) % UF, true, xa, xc, crc, &pd);
+					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true, UF, -1, D1>(
+						P, s_tbl, s_sl, s_sh, k, rows, s, cb + CHUNK_BYTES, cb + 2 * CHUNK_BYTES, lo,
+						i + 2 < iend, false, Q.init, (col1 - 2 - i) % UF, true, xc, xa, crc, &pd);
+					i += 2;
+				}
 				for (; i < iend; i += 2) {
 					const uint64_t cb = c0 + (uint64_t)i * CHUNK_BYTES;
-					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true, UF>(
+					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true, UF, -1, D1>(
 						P, s_tbl, s_sl, s_sh, k, rows, s, cb, cb + CHUNK_BYTES, lo, true,
-						i == 0 && threadIdx.x == 0, Q.init, (col1 - 1 - i) % UF, true, xa, xc, crc);
-					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true, UF>(
+						i == 0 && threadIdx.x == 0, Q.init, (col1 - 1 - i) % UF, true, xa, xc, crc, &pd);
+					mmcs_col<KM, RM, W, REFL, TB, true, CHUNK_BYTES, true, UF, -1, D1>(
 						P, s_tbl, s_sl, s_sh, k, rows, s, cb + CHUNK_BYTES, cb + 2 * CHUNK_BYTES, lo,
-						i + 2 < iend, false, Q.init, (col1 - 2 - i) % UF, true, xc, xa, crc);
+						i + 2 < iend, false, Q.init, (col1 - 2 - i) % UF, true, xc, xa, crc, &pd);
 				}
 			}
 			for (; i < col1; i++)
-				mmcs_col<KM, RM, W, REFL, TB, false, CHUNK_BYTES, false, UF>(
+				mmcs_col<KM, RM, W, REFL, TB, false, CHUNK_BYTES, false, UF, -1, D1>(
 					P, s_tbl, s_sl, s_sh, k, rows, s, c0 + (uint64_t)i * CHUNK_BYTES, 0, lo, false,
-					i == 0 && threadIdx.x == 0, Q.init, (col1 - 1 - i) % UF, true, xa, xa, crc);
+					i == 0 && threadIdx.x == 0, Q.init, (col1 - 1 - i) % UF, true, xa, xa, crc, &pd);
+			if constexpr (DEFER) {
+				if (!tb4done)
+					mmcs_fold<RM, W, REFL, TB, UF, -1>(s_sl, s_sh, rows, pd.v, pd.have, pd.first, Q.init,
+									   pd.pos, pd.gshift, crc);
+			}
 			// each wave XORs its partial into the (zeroed) output: no
 			// workgroup barrier, other waves keep streaming.  Reflected CRCs:
 			// every lane's value is multiplied by its lane factor

@@ -24,6 +24,10 @@ def oracle():
 def ecglib():
     from daos_amd import ecg
 
+    # ECG_TEST_LIB: run the suite against an experimental build of libecg.so
+    # (tools/build_exp.sh) -- A/B candidates must pass parity before timing
+    if os.environ.get("ECG_TEST_LIB"):
+        ecg.LIB_PATH = os.path.abspath(os.environ["ECG_TEST_LIB"])
     ecg.lib()
     return ecg
 

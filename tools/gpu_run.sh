@@ -294,6 +294,17 @@ PY
 		python tools/pmc_traffic.py gpurun_out/pmc_dec_16p2_f gpurun_out/pmc_dec_16p2_w "ecg_mm_kernel<16, 2" \
 			2415919104 gpurun_out/pmc_traffic_dec_16p2.json || exit $?
 		;;
+	exp)
+		# EXP_LIBS="build/exp/a/libecg.so ...": checksum parity of each experimental build, then the fused A/B
+		for lib in ${EXP_LIBS}; do
+			tag=$(basename "$(dirname "$lib")")
+			ECG_TEST_LIB=$lib step exptests_$tag 300 python -u -m pytest tests/test_gpu_csum.py tests/test_migrate.py \
+				-q -x -p no:cacheprovider --timeout 120 --timeout-method thread
+			rc=$?; [ $rc -eq 0 ] || exit $rc
+		done
+		FUSED_ROUNDS=${FUSED_ROUNDS:-3} step fused_libs 900 python tools/fused_libs.py daos_amd/lib/libecg.so ${EXP_LIBS} \
+			|| exit $?
+		;;
 	dist4)
 		step dist4 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
 			--master-port 29537 bench.py --gpus 4 --steps 20 --warmup 3 || exit $?
