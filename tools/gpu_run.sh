@@ -230,6 +230,9 @@ PY
 			--allow-shared-device --steps 5 --warmup 1 || exit $?
 		step hoststream_n1 300 python bench.py --workload rebuild_stream_8p2 --steps 5 --warmup 1 || exit $?
 		;;
+	fusedblocked)
+		step fused_blocked 600 python tools/fused_blocked.py || exit $?
+		;;
 	fusedcols)
 		step fused_cols_ab 600 python tools/fused_cols_ab.py || exit $?
 		;;
