@@ -52,7 +52,7 @@ sys.path.insert(0, ROOT)
 GIB = float(1 << 30)
 PARITY_ROW_PAD = 4096
 HBM_PEAK_GBS = 8000.0          # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
-ROUND = "r03"
+ROUND = "r04"
 
 # name -> (k, p, cell bytes, stripes, ops, strong scaling?)
 WORKLOADS = {
@@ -242,17 +242,18 @@ class Workload:
         self.prow = S * C + PARITY_ROW_PAD
         self.data = ctx.alloc(max(1, S * k * C))
         self.parity = ctx.alloc(p * self.prow)
-        self.stripes = ctx.alloc(max(1, S * (k + p) * C))
+        # the recovery image only when this workload decodes
+        self.stripes = ctx.alloc(max(1, S * (k + p) * C)) if "dec" in self.ops else None
         self.events = []        # per timed step: (start, stop) per op
         if S == 0:
             return
         fill_device(ctx, self.data, S * k * C, config_id)
-        # recovery buffer: a consistent [S][k+p][C] image (encode in place)
-        self.img_blk = fill_device(ctx, self.stripes, S * (k + p) * C, config_id + 1)
-        st = (k + p) * C
-        ctx.encode(k, p, C, S, self.stripes.ptr, st, self.stripes.ptr + k * C, C, st)
-        ctx.sync()
         if "dec" in self.ops:
+            # recovery buffer: a consistent [S][k+p][C] image (encode in place)
+            self.img_blk = fill_device(ctx, self.stripes, S * (k + p) * C, config_id + 1)
+            st = (k + p) * C
+            ctx.encode(k, p, C, S, self.stripes.ptr, st, self.stripes.ptr + k * C, C, st)
+            ctx.sync()
             from daos_amd import ecg
 
             for s in range(S):
@@ -342,7 +343,8 @@ class Workload:
 
     def free(self):
         for b in (self.data, self.parity, self.stripes):
-            b.free()
+            if b is not None:
+                b.free()
 
 
 class HostWorkload:
@@ -595,6 +597,36 @@ DETAIL_SHAPES = (("EC_8P2_1MiB_encode", 8, 2, 1 << 20, 512, "enc"),
                  ("EC_2P1_128KiB_encode", 2, 1, 128 << 10, 1024, "enc"))
 
 
+def offset_rows(ctx, aligned, iters=11):
+    """EC_8P2 1 MiB client-layout encode with the parity rows at a byte offset
+    of their allocation (DAOS rounds parity rows to 8 bytes only,
+    ref:src/object/cli_ec.c:86; user cells carry no alignment,
+    ref:src/object/cli_ec.c:510-536): +8 runs the dwordx2-lane kernel, +4 the
+    dword-lane kernel, +1 the byte kernel (on 32 stripes: it is ~50x slower).
+    Each row's `of_aligned` = aligned ms / this ms."""
+    from daos_amd import ecg
+
+    k, p, C = 8, 2, 1 << 20
+    rows = {}
+    for off, S, warm in ((8, 512, 40), (4, 512, 40), (1, 32, 2)):
+        data = ctx.alloc(S * k * C)
+        fill_device(ctx, data, S * k * C, 7)
+        pitch = S * C + PARITY_ROW_PAD
+        par = ctx.alloc(p * pitch + 64)
+        ms = time_kernel(ctx, lambda: ctx.encode(k, p, C, S, data.ptr, k * C, par.ptr + off, pitch, C), iters,
+                         warm=warm)
+        alg = (k + p) * C * S
+        row = {"parity_offset_bytes": off, "stripes": S, "ms": round(ms, 4),
+               "GiBps_user": round(k * C * S / (ms / 1e3) / GIB, 1), "alg_GBps": round(alg / ms / 1e6, 1),
+               "roofline_frac": round(alg / ms / 1e6 / HBM_PEAK_GBS, 4), "kernel": ecg.last_kernel()}
+        if aligned and S == 512:
+            row["of_aligned"] = round(aligned["ms"] / ms, 4)
+        rows[f"EC_8P2_1MiB_encode_parity_off{off}"] = row
+        data.free()
+        par.free()
+    return rows
+
+
 def detail_rows(ctx, ceil, iters=11, shapes=DETAIL_SHAPES, csum=True):
     """Extra device-resident rows (per GPU): the north-star EC_8P2 encode,
     EC_8P2 2-erasure decode, EC_16P2 128 KiB encode, EC_2P1 128 KiB encode.
@@ -647,6 +679,7 @@ def detail_rows(ctx, ceil, iters=11, shapes=DETAIL_SHAPES, csum=True):
         buf.free()
         if buf2 is not None:
             buf2.free()
+    rows.update(offset_rows(ctx, rows.get("EC_8P2_1MiB_encode"), iters))
     if not csum:
         return rows
     # checksums of regenerated cells (include/ecg_csum.h): EC_8P2 encode with
@@ -846,7 +879,7 @@ def cpu_baseline(k, p, C, budget_s, ops=("enc", "dec"), per_config=True):
 
 def pmc_traffic():
     path = os.path.join(ROOT, "profiles", ROUND, "pmc_traffic.json")
-    for older in ("r02", "r01"):
+    for older in ("r03", "r02", "r01"):          # the newest committed pass
         if not os.path.exists(path):
             path = os.path.join(ROOT, "profiles", older, "pmc_traffic.json")
     if os.path.exists(path):
@@ -857,6 +890,122 @@ def pmc_traffic():
         except (OSError, ValueError):
             return None
     return None
+
+
+# ------------------------------------------------------------------ multi-GPU config legs
+# BASELINE configs[3] and configs[4] are multi-GPU configurations; the driver's
+# scaling run only invokes `bench.py --gpus N`, so every headline run (N = 1
+# included, so the driver's N = 1, 2, 4, 8 runs give both legs a curve) runs
+# them after the headline, each with its own barrier / max-over-ranks timing:
+#   configs[3]: EC_16P2, 128 KiB cells, 8192 stripes in total, split over the
+#     N ranks by contiguous stripe ranges (strong scaling; the reference's
+#     per-stripe loop ref:src/object/cli_ec.c:627-659 is what the ranges cut);
+#   configs[4]: the EC_8P2 rebuild stream -- per rank one encode batch and one
+#     {d0,d1} recovery batch of 64 stripes, stripes in pinned host memory
+#     allocated after the rank pinned itself to its GPU's NUMA node, so the
+#     pages are node-local (weak scaling; the rebuild walk of
+#     ref:src/object/srv_obj_migrate.c:1116-1177 is per object, so objects
+#     partition across GPUs).
+LEG_STRONG = "config3_EC_16P2_128KiB_x8192_strong"
+LEG_STREAM = "config4_EC_8P2_1MiB_rebuild_stream"
+STRONG_TOTAL = 8192
+
+
+def split_range(total, world, rank):
+    """Contiguous stripe range [first, first + n) of `rank` (ecg_multi_range's cut)."""
+    base, extra = divmod(total, world)
+    n = base + (1 if rank < extra else 0)
+    return rank * base + min(rank, extra), n
+
+
+def timed_leg(world, steps, warm, step, sync):
+    """warm untimed steps, then `steps` timed from a common barrier; returns
+    (this rank's seconds, the max over ranks)."""
+    for _ in range(warm):
+        step(False)
+    sync()
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(True)
+    sync()
+    mine = time.perf_counter() - t0
+    barrier(world)
+    return mine, max_over_ranks(world, mine)
+
+
+def leg_strong(args, ctx, world, rank, steps):
+    """configs[3] on this rank's contiguous share of the 8192 stripes."""
+    k, p, C = 16, 2, 128 << 10
+    first, S = split_range(STRONG_TOTAL, world, rank)
+    if args.rehearse:
+        wl = None
+        step, sync = (lambda timed: time.sleep(1e-4 * S / 1024)), (lambda: None)
+    else:
+        wl = Workload(ctx, k, p, C, S, ops=("enc",), config_id=4)
+        step, sync = wl.step, ctx.sync
+    # 40 warm-up launches: the launch tuner's probe of this shape (ecg_tune.c)
+    mine, tmax = timed_leg(world, steps, 0 if args.rehearse else 40, step, sync)
+    row = {"rank": rank, "first_stripe": first, "stripes": S, "ms_per_step": round(mine / steps * 1e3, 4)}
+    if wl is not None:
+        kms = wl.kernel_ms()["enc"]
+        launch = sum(kms) / len(kms)
+        alg = wl.alg_bytes("enc")
+        row.update({"launch_ms": round(launch, 4), "alg_GBps": round(alg / launch / 1e6, 1),
+                    "roofline_frac": round(alg / launch / 1e6 / HBM_PEAK_GBS, 4), "kernel": _last_kernel()})
+        row["verified"] = all(wl.verify().values())      # after reading the timed launches' kernel
+        wl.free()
+    rows = gather(world, row)
+    return {"config": f"EC_{k}P{p} {C >> 10} KiB cells, {STRONG_TOTAL} stripes in total split over {world} "
+                      "rank(s) by contiguous ranges, client-layout encode, device-resident",
+            "value_GiBps": None if args.rehearse else round(STRONG_TOTAL * k * C * steps / tmax / GIB, 2),
+            "unit": "GiB/s", "scaling": "strong", "steps": steps, "ms_per_step": round(tmax / steps * 1e3, 4),
+            "ranks": rows, "verified": all(r.get("verified", True) for r in rows),
+            **({"rehearsal": True} if args.rehearse else {})}
+
+
+def leg_stream(args, ctx, world, rank, steps, numa_info):
+    """configs[4] per rank from node-local pinned buffers."""
+    k, p, C, S = 8, 2, 1 << 20, 64
+    if args.rehearse:
+        wl = None
+        step, sync = (lambda timed: time.sleep(2e-4)), (lambda: None)
+    else:
+        wl = HostWorkload(ctx, k, p, C, S, chunk=args.host_chunk)
+        step, sync = wl.step, ctx.sync
+    mine, tmax = timed_leg(world, steps, 0 if args.rehearse else 2, step, sync)
+    row = {"rank": rank, "ms_per_step": round(mine / steps * 1e3, 4),
+           "numa_node": (numa_info or {}).get("numa_node"), "pinned_cpus": (numa_info or {}).get("pinned_cpus")}
+    user = 2 * k * C * S
+    if wl is not None:
+        h2d = wl.h2d_bytes_per_step() * steps / mine / 1e9
+        raw = pinned_copy_rates(ctx, n=256 << 20)
+        row.update({"h2d_GBps": round(h2d, 2), "d2h_GBps": round(wl.d2h_bytes_per_step() * steps / mine / 1e9, 2),
+                    "measured_pinned_GBps": raw, "frac_of_h2d": round(h2d / raw["h2d"], 4),
+                    "verified": all(wl.verify().values())})
+        wl.free()
+    rows = gather(world, row)
+    return {"config": f"EC_{k}P{p} {C >> 20} MiB cells: per rank one encode batch + one {{d0,d1}} recovery "
+                      f"batch of {S} stripes per step, stripes in NUMA-local pinned host memory, "
+                      f"host<->device copies included ({args.host_chunk or HOST_CHUNK}-stripe staging chunks)",
+            "value_GiBps": None if args.rehearse else round(world * user * steps / tmax / GIB, 2),
+            "unit": "GiB/s", "scaling": "weak", "bound": "pcie", "steps": steps,
+            "ms_per_step": round(tmax / steps * 1e3, 4), "ranks": rows,
+            "verified": all(r.get("verified", True) for r in rows),
+            **({"rehearsal": True} if args.rehearse else {})}
+
+
+def config_legs(args, ctx, world, rank, numa_info):
+    steps = max(5, args.steps)
+    return {LEG_STRONG: leg_strong(args, ctx, world, rank, steps),
+            LEG_STREAM: leg_stream(args, ctx, world, rank, min(steps, 10), numa_info)}
+
+
+def _last_kernel():
+    from daos_amd import ecg
+
+    return ecg.last_kernel()
+
 
 
 # ------------------------------------------------------------------ reporting
@@ -910,17 +1059,20 @@ def host_report(args, ctx, wl, world, rank, value, elapsed, ranks, nshard=1):
 
 def rehearse(args, world, rank, local):
     """CPU-only rehearsal of the N-rank plumbing (launcher, env, barrier,
-    max-over-ranks, gather): each rank 'steps' by sleeping 1 ms per step."""
+    max-over-ranks, gather): each rank 'steps' by sleeping 1 ms per step,
+    then the configs[3] / configs[4] legs run their split, timing and
+    aggregation with sleeps for the GPU work."""
     barrier(world)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         time.sleep(0.001 * (1 + rank))
     elapsed = max_over_ranks(world, time.perf_counter() - t0)
     ranks = gather(world, {"rank": rank, "local_rank": local, "pid": os.getpid()})
+    legs = config_legs(args, None, world, rank, None) if args.workload == "enc_dec_4p2" else {}
     if rank == 0:
         print(json.dumps({"metric": "rehearsal (no GPU work)", "rehearsal": True, "value": None, "n_ranks": world,
                           "steps": args.steps, "ms_per_step": round(elapsed / max(1, args.steps) * 1e3, 3),
-                          "ranks": ranks}), flush=True)
+                          "ranks": ranks, "detail": legs}), flush=True)
     finish_dist(world)
 
 
@@ -1086,6 +1238,11 @@ def main():
         "cpu_baseline": None,
     }
     wl.free()
+    legs = {}
+    if args.workload == "enc_dec_4p2" and m is None and not args.no_detail:
+        legs = config_legs(args, ctx, world, rank, numa_info)
+        out["detail"] = dict(legs)
+        ok = ok and all(v["verified"] for v in legs.values())
     if rank == 0 and world == 1 and not args.no_detail:
         ceil = measured_ceilings(ctx)
         mix = mix_ceiling(ceil, k / (k + p))      # enc (k in, p out) and dec (k in, 2 out) alike at p = 2
@@ -1093,7 +1250,7 @@ def main():
         out["roofline"]["measured_mix_ceiling_GBps"] = round(mix, 1)
         out["roofline"]["frac_of_measured_mix"] = round(achieved / mix, 4)
         det = detail_rows(ctx, ceil)
-        out["detail"] = det
+        out["detail"] = {**det, **legs}
         e8 = det["EC_8P2_1MiB_encode"]
         out["roofline"]["north_star"] = {
             "target": ">= 70 % of per-GPU HBM-read roofline on EC_8P2 encode at 1 MiB cells, device-resident",

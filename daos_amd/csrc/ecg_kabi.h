@@ -172,8 +172,7 @@ typedef struct ecg_csum_params {
 	uint32_t type;			/* DAOS hash type: 1 crc16, 2 crc32, 3 crc64, 7 adler32 */
 	uint32_t variant;		/* CRC: 0 auto, 1 wave per chunk, 2 workgroup per chunk,
 					 * 3 a 16-lane group per chunk */
-	uint32_t byte_tables;		/* CRC lookups: 0 = 5-bit tables, 1 = byte tables, 2 = nibble tables */
-	uint32_t pad2;
+	uint32_t pad1, pad2;
 	/* workgroup-per-chunk CRC: a chunk of m 1 KiB steps is cut into
 	 * ECG_CSUM_SPLIT_NW slices; split_sh[c][w] = x^(8 * bytes after slice w)
 	 * mod P for the chunk lengths' step counts split_m[c] (first, middle and
@@ -227,12 +226,6 @@ typedef struct ecg_mmcs_params {
 	uint32_t ncols;			/* columns per item */
 	uint32_t nh, nh_last;		/* items per chunk / in the last chunk */
 	uint32_t nitems;
-	uint32_t byte_tables;		/* table kind TB: 0 5-bit, 1 slice-by-NB, 2 s16 */
-	uint32_t wave;			/* 1: one wave per (stripe, chunk) (ecg_mm_csum_wave_kernel):
-					 * kh = [2][64] lane multipliers (full chunk, last chunk;
-					 * reflected: [64] bit-products of the last chunk's
-					 * x^(-8Z), the lane factors from the nibl tables),
-					 * checksums stored, not XORed (no zeroing needed) */
 	uint32_t pad3;
 	uint32_t row_slot[ECG_KMAX_R];
 } ecg_mmcs_params_t;
@@ -272,10 +265,15 @@ int ecg_k_launch_matmul_sel(const ecg_mm_params_t *p, const uint8_t *sel_dev, ui
  * mode 0 copy, 1 read-only, 2 write-only. */
 int ecg_k_launch_copy(const void *src, void *dst, uint64_t bytes, int mode, void *stream,
 		      uint32_t max_blocks, uint32_t *kernel_id);
-/* Fused product + checksum (kernels/ecg_kernels.hip).  Returns 1 (and
+/* Fused product + checksum (kernels/ecg_fused_kernels.hip).  Returns 1 (and
  * launches nothing) when the operands are not 16-byte aligned. */
 int ecg_k_launch_matmul_csum(const ecg_mm_params_t *p, const ecg_mmcs_params_t *q,
 			     const ecg_launch_cfg_t *cfg, void *stream, uint32_t *kernel_id);
+#define ECG_KID_FUSED 500u	/* fused kernel ids start here (below ECG_KID_COPY_SEGS) */
+const char *ecg_k_fused_kernel_name(uint32_t kernel_id);
+/* The common alignment (16, 8, 4 or 1 bytes) of every cell address of a
+ * product launch: the lane access granule the product kernels use. */
+uint32_t ecg_k_align_granule(const ecg_mm_params_t *p);
 /* Pointer-table product (kernels/ecg_kernels.hip): cells_dev[s*(k+rows)+j] =
  * device address of input cell j / output cell j-k of stripe s.  aligned = all
  * addresses 16-byte aligned (else the byte-granular kernel). */

@@ -574,7 +574,7 @@ int ecg_matmul_csum(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, 
 				ecg_build_ptbl(coef[(size_t)r * k + j], &prm->tbl[r][j]);
 		}
 		/* the workgroup kernel XORs per-wave partials into the checksums */
-		if (!q.wave && aligned16_ok(src, soff, k, sstride, dst, doff, rows, dstride)) {
+		if (aligned16_ok(src, soff, k, sstride, dst, doff, rows, dstride)) {
 			hipError_t he = hipMemsetAsync(csums, 0, (size_t)rows * S * q.nch * (size_t)cl, st);
 
 			if (he != hipSuccess) {
@@ -590,11 +590,6 @@ int ecg_matmul_csum(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, 
 			ecg_set_last_kernel(ecg_k_kernel_name(kid));
 			return 0;
 		}
-		/* a tuning variant (ecg_set_csum_variant) may ask for a table kind
-		 * or shape that is not instantiated for these (k, rows): the two
-		 * passes then; the default choice must always exist */
-		if (e == (int)hipErrorInvalidDeviceFunction && ctx->csum_variant != 0)
-			e = 1;
 		if (e != 1)
 			return ecg_hip_fail((hipError_t)e, "fused kernel launch");
 		/* e == 1: operands not 16-byte aligned -> two-pass path */

@@ -24,40 +24,12 @@ static const struct crc_def g_defs[4] = {
 	[ECG_HASH_CRC64] = {64, 1, 0xC96C5795D7870F42ull, ~0ull, ~0ull},
 };
 
-/* CRC table kind (tools/crc_ab.py, profiles/r02/crc_ab*.log): the 5-bit
- * conflict-free tables.  Standalone kernels (positional tables, one register
- * shift per 4 pieces: 29.75 lookups per 16 B): every hash, crc32 over 32 KiB
- * chunks 3.9 -> 5.3-5.5 TB/s, crc64 3.3 -> 3.8.  Fused kernels (one shift per
- * piece, 35 / 42 lookups): crc16 / crc32; crc64 keeps the byte tables there
- * (24 conflicted eight-byte lookups, no slower).  csum_variant bit 4 forces
- * the byte tables, bit 5 the 5-bit tables (A/B runs). */
-static uint32_t use_byte_tables(const ecg_ctx_t *ctx, int type, int fused, int k, int rows)
-{
-	if (ctx->csum_variant & 16u)
-		return 1;
-	if (ctx->csum_variant & 32u)
-		return 0;
-	/* crc32 at EC_8P2 (k = 8, two rows) too: the byte tables beat the 5-bit
-	 * ones in every measurement of that shape -- by 1.5-3.5 % (round 2,
-	 * profiles/r02/fused_tables_ab/), 3.7 % (profiles/r03/fused_tb3/) and
-	 * 3.9 % (profiles/r03/fused_sq/fused_libs_full_vs_nocrc.json, wgb) --
-	 * and lose at every other shape measured (k = 4, 16, one or three rows) */
-	return fused && (type == ECG_HASH_CRC64 || (type == ECG_HASH_CRC32 && k == 8 && rows == 2));
-}
-
-/* Standalone CRC kernels (ecg_csum_params_t.byte_tables): 2 = nibble tables
- * addressed by SDWA byte selects, the default since round 3 -- the kernels
- * are VALU-issue bound and a nibble lookup costs 1.25 VALU for its address
- * against 2 for a 5-bit field (profiles/r03/crc_sq, crc_ab); bit 4 forces the
- * byte tables, bit 5 the 5-bit tables. */
-static uint32_t standalone_tables(const ecg_ctx_t *ctx)
-{
-	if (ctx->csum_variant & 16u)
-		return 1;
-	if (ctx->csum_variant & 32u)
-		return 0;
-	return 2;
-}
+/* CRC table kinds are fixed per kernel (ecg_kernels.hip CS_TB,
+ * ecg_csum_kernels.hip kind_ok): standalone kernels use the nibble tables
+ * (SDWA-addressed, conflict-free; profiles/r03/crc_sq/), their byte-granular
+ * variants the 5-bit tables; the fused kernels the byte tables for crc64 and
+ * for crc32 at EC_8P2, the 5-bit tables elsewhere (profiles/r02/fused_tables_ab/,
+ * profiles/r03/fused_tb3/, fused_tb4/).  The other kinds were A/B builds. */
 
 int ecg_csum_len(int type)
 {
@@ -612,80 +584,6 @@ static int fused_kh(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, uint3
 	return rc;
 }
 
-/* Multipliers of the wave-per-chunk fused kernel (ecg_kabi.h
- * ecg_mmcs_params wave), Z = zero bytes padding the last chunk (`last` bytes)
- * to whole 1 KiB rows.  crc16: the lane factors kw[0][l] = x^(8*16*(63-l)),
- * kw[1][l] = the same times x^(-8Z).  Reflected CRCs take the lane factor from
- * the nibl tables of the CRC image and need only x^(-8Z) for a last chunk, as
- * W bit-products kw[b] = e_b * x^(-8Z) (64 entries, b >= W zero).  Cached
- * with the kh tables (ncols = 0 marks them). */
-static int fused_kw(ecg_ctx_t *ctx, int type, uint64_t rcs, uint64_t last, const void **out)
-{
-	const struct crc_def *d = &g_defs[type];
-	const uint64_t m_last = (last + ECG_CSUM_STRIDE - 1) / ECG_CSUM_STRIDE;
-	const uint64_t z = m_last * ECG_CSUM_STRIDE - last;
-	const size_t es = d->width == 64 ? 8 : 4;
-	const uint64_t un = crc_unshift(d, z), step = crc_xpow8(d, 16);
-	unsigned char img[2 * 16 * 64 * 8];
-	struct ecg_kh_ent *e;
-	uint64_t c = crc_one(d);
-	void *dev = NULL;
-	hipError_t he;
-
-	pthread_mutex_lock(&ctx->lock);
-	for (int i = 0; i < ECG_NKH_CACHE; i++) {
-		e = &ctx->kh_cache[i];
-		if (e->valid && e->type == type && e->rcs == rcs && e->last == last && e->ncols == 0) {
-			*out = e->dev;
-			pthread_mutex_unlock(&ctx->lock);
-			return 0;
-		}
-	}
-	const size_t nent = d->refl ? 64 : 2 * 64;
-
-	for (int l = 63; l >= 0; l--) {
-		const uint64_t v[2] = {c, crc_mulmod(d, c, un)};
-
-		for (int row = 0; row < (d->refl ? 1 : 2); row++) {
-			/* reflected: entry l = e_l * x^(-8Z); crc16: lane l's factor */
-			const uint64_t x = d->refl ? (l < d->width ? crc_mulmod(d, (uint64_t)1 << l, un) : 0) : v[row];
-			const size_t at = (size_t)row * 64 + (size_t)l;
-
-			if (es == 8) {
-				memcpy(img + at * 8, &x, 8);
-			} else {
-				const uint32_t w = (uint32_t)x;
-
-				memcpy(img + at * 4, &w, 4);
-			}
-		}
-		c = crc_mulmod(d, c, step);
-	}
-	he = hipMalloc(&dev, nent * es);
-	if (he == hipSuccess)
-		he = hipMemcpy(dev, img, nent * es, hipMemcpyHostToDevice);
-	if (he != hipSuccess) {
-		if (dev)
-			(void)hipFree(dev);
-		pthread_mutex_unlock(&ctx->lock);
-		return ecg_hip_fail(he, "fused csum lane multipliers");
-	}
-	e = &ctx->kh_cache[ctx->kh_next++ % ECG_NKH_CACHE];
-	if (e->dev) {
-		(void)hipDeviceSynchronize();
-		(void)hipFree(e->dev);
-	}
-	e->valid = 1;
-	e->type = type;
-	e->rcs = rcs;
-	e->last = last;
-	e->ncols = 0;
-	e->dev = dev;
-	*out = dev;
-	pthread_mutex_unlock(&ctx->lock);
-	return 0;
-}
-
 int ecg_csum_extents(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_size,
 		     uint64_t rx_idx, uint64_t rx_nr, const void *buf, int64_t ext_stride,
 		     uint32_t n_ext, void *csums, void *stream)
@@ -741,9 +639,7 @@ int ecg_csum_extents(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_
 		 * (tools/bench_csum.py shape_* rows) */
 		const uint64_t total = (uint64_t)n_ext * prm.nchunks;
 		const uint64_t steps = (rcs / 16 + 63) / 64;
-		const uint32_t shape = ctx->csum_variant & 15u;
-		const int split = shape == 2 ||
-				  (shape == 0 && total < 4096 && steps >= 2 * ECG_CSUM_SPLIT_NW);
+		const int split = total < 4096 && steps >= 2 * ECG_CSUM_SPLIT_NW;
 		const uint64_t lens[3] = {
 			prm.first_bytes, rcs,
 			prm.nchunks >= 2 ? prm.ext_bytes - prm.first_bytes - (uint64_t)(prm.nchunks - 2) * rcs
@@ -751,16 +647,15 @@ int ecg_csum_extents(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t rec_
 
 		/* short chunks (<= 8 KiB): a 16-lane group each, so the per-lane
 		 * final multiply is paid once per >= 8 pieces instead of per 1-2 */
-		const int group = shape == 3 || (shape == 0 && !split && steps <= 8);
+		const int group = !split && steps <= 8;
 
 		prm.variant = split ? 2 : group ? 3 : 1;
-		prm.byte_tables = standalone_tables(ctx);
 		for (int c = 0; split && c < 3; c++) {
 			prm.split_m[c] = ECG_CSUM_STEPS(lens[c]);
 			split_shifts(ctx, type, prm.split_m[c], prm.split_sh[c]);
 		}
 	} else {
-		prm.variant = ctx->csum_variant & 15u;	/* adler32: the kernel picks by shape when 0 */
+		prm.variant = 0;	/* adler32: the kernel picks by shape */
 	}
 	e = ecg_k_launch_csum(&prm, (void *)ecg_pick_stream(ctx, stream), ctx->csum_blocks, &kid);
 	if (e != 0)
@@ -784,16 +679,6 @@ int ecg_set_fused_cols(ecg_ctx_t *ctx, uint32_t ncols)
 	if (ctx == NULL || ncols > 4096)
 		return ecg_fail(-ECG_DER_INVAL, "set_fused_cols: bad arguments");
 	ctx->fused_cols = ncols;
-	return 0;
-}
-
-int ecg_set_csum_variant(ecg_ctx_t *ctx, uint32_t variant)
-{
-	if (ctx == NULL || (variant & 15u) > 3 || variant > 2047 || (variant & 48u) == 48u ||
-	    (variant & 576u) == 576u || ((variant & 1024u) && (variant & 704u)) ||
-	    (variant & 384u) == 384u)
-		return ecg_fail(-ECG_DER_INVAL, "set_csum_variant: bad arguments");
-	ctx->csum_variant = variant;
 	return 0;
 }
 
@@ -833,16 +718,6 @@ int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t
 	q->m = (uint32_t)m;
 	q->m_last = (uint32_t)((last + ECG_MMCS_STRIDE - 1) / ECG_MMCS_STRIDE);
 	q->ncols = fused_cols(ctx, m, type, k, rows);
-	/* fused kernels: table kind TB (ecg_kernels.hip); bit 6 of csum_variant
-	 * selects the s16 tables (A/B), bit 9 TB 3, bit 10 TB 4, bit 7 the
-	 * wave-per-chunk kernel */
-	q->byte_tables = (ctx->csum_variant & 1024u) ? 4 : (ctx->csum_variant & 512u) ? 3
-			 : (ctx->csum_variant & 64u) ? 2 : use_byte_tables(ctx, type, 1, k, rows);
-	/* TB 4's unrolled walk takes items of exactly 4 full columns (positional
-	 * nibble tables); other items fall back to the per-column shift */
-	if (q->byte_tables == 4 && !ctx->fused_cols && !(pthread_once(&g_fused_cols_once, fused_cols_init),
-							   g_fused_cols_env))
-		q->ncols = (uint32_t)(m < 4 ? m : 4);
 	/* bound the multiplier table (nh + nh_last rows of 256 entries) for
 	 * very long chunks: at most 2048 items per chunk */
 	if ((m + q->ncols - 1) / q->ncols > 2048)
@@ -853,17 +728,9 @@ int ecg_csum_fused_params(ecg_ctx_t *ctx, int type, uint64_t chunksize, uint64_t
 		return 0;
 	q->nitems = (q->nch - 1) * q->nh + q->nh_last;
 	/* the workgroup kernel for every shape: since its item tail no longer
-	 * reads HBM (round 3) it beats the wave-per-chunk kernel for crc64 at
-	 * EC_4P2 too (+13 % vs +19 % over the plain encode, profiles/r03/fused_tail/);
-	 * csum_variant bit 7 forces the wave kernel (A/B), bit 8 is kept as the
-	 * old "forbid" bit */
-	q->wave = (ctx->csum_variant & 128u) != 0;
-	if (q->wave) {
-		/* the wave kernel is instantiated with the per-hash default tables
-		 * only (byte tables for crc64, 5-bit for crc16 / crc32) */
-		q->byte_tables = type == ECG_HASH_CRC64;
-		return fused_kw(ctx, type, rcs, last, &q->kh) ? -ECG_DER_NOMEM : 1;
-	}
+	 * reads HBM (round 3) it beats the wave-per-chunk kernel of rounds 1-2
+	 * for crc64 at EC_4P2 too (+13 % vs +19 % over the plain encode,
+	 * profiles/r03/fused_tail/); the wave kernel was retired in round 4 */
 	rc = fused_kh(ctx, type, rcs, last, q->ncols, q->nh, q->nh_last, &q->kh);
 	if (rc)
 		return rc;

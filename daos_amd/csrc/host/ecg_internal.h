@@ -62,7 +62,6 @@ struct ecg_ctx {
 #define ECG_NCSUM_TBL 4
 	void *csum_tbl[ECG_NCSUM_TBL];	/* device CRC tables by hash type (ecg_csum.c) */
 	uint32_t csum_blocks;		/* csum grid cap, 0 = kernel default */
-	uint32_t csum_variant;		/* CRC kernel choice, 0 = by shape */
 	uint32_t fused_cols;		/* fused kernel columns per item, 0 = default */
 #define ECG_NSPLIT_CACHE 8
 	struct ecg_split_ent {		/* workgroup-per-chunk CRC shifts (ecg_csum.c) */

@@ -287,13 +287,42 @@ static void xor_into(unsigned char *dst, const unsigned char *a, const unsigned 
 		dst[i] = a[i] ^ b[i];
 }
 
-static pthread_mutex_t *dst_lock_of(struct ecg_queue *q, const void *dst)
+/* Striped locks over the ADDRESS RANGE of a parity cell: the address space
+ * is cut into 64 KiB regions, each region hashed to one of NDSTLOCK locks.
+ * parity ^= delta runs region by region under that region's lock, so two
+ * updates whose parity bytes overlap -- through the same cell pointer or
+ * through different pointers into one buffer -- serialise on every region
+ * they share (XOR commutes: the order does not matter, only that each
+ * read-modify-write of a byte is whole).  One lock is held at a time: no
+ * lock ordering to get wrong. */
+#define DST_REGION_SHIFT 16
+
+static pthread_mutex_t *region_lock(struct ecg_queue *q, uint64_t region)
 {
-	uint64_t a = (uint64_t)(uintptr_t)dst;
+	uint64_t a = region;
 
 	a ^= a >> 17;
 	a *= 0x9E3779B97F4A7C15ull;
 	return &q->dst_lock[a >> 58];	/* top 6 bits: NDSTLOCK = 64 */
+}
+
+static void xor_into_locked(struct ecg_queue *q, unsigned char *dst, const unsigned char *delta, uint64_t n)
+{
+	uint64_t a = (uint64_t)(uintptr_t)dst;
+	const uint64_t end = a + n;
+
+	while (a < end) {
+		uint64_t next = ((a >> DST_REGION_SHIFT) + 1) << DST_REGION_SHIFT;
+		pthread_mutex_t *l = region_lock(q, a >> DST_REGION_SHIFT);
+		unsigned char *d = (unsigned char *)(uintptr_t)a;
+
+		if (next > end)
+			next = end;
+		pthread_mutex_lock(l);
+		xor_into(d, d, delta + (a - (uint64_t)(uintptr_t)dst), next - a);
+		pthread_mutex_unlock(l);
+		a = next;
+	}
 }
 
 static void finish_req(struct ecg_queue *q, struct qslot *s, uint32_t i)
@@ -304,13 +333,8 @@ static void finish_req(struct ecg_queue *q, struct qslot *s, uint32_t i)
 
 	ecg_trace_push("ecg:queue_complete");
 	if (s->rc == 0 && s->op == OP_UPDATE)	/* parity ^= coef[r][vec_i] * diff */
-		for (int j = 0; j < s->rows; j++) {
-			pthread_mutex_t *l = dst_lock_of(q, r->dst[j]);
-
-			pthread_mutex_lock(l);
-			xor_into(r->dst[j], r->dst[j], out + j * s->pitch, s->C);
-			pthread_mutex_unlock(l);
-		}
+		for (int j = 0; j < s->rows; j++)
+			xor_into_locked(q, r->dst[j], out + j * s->pitch, s->C);
 	else if (s->rc == 0)
 		for (int j = 0; j < s->rows; j++)
 			memcpy(r->dst[j], out + j * s->pitch, s->C);

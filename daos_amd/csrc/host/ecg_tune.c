@@ -2,7 +2,7 @@
  * ecg_tune.c -- per-context launch tuner for the product kernel's
  * blocks-per-CU cap.
  *
- * Wide stripes (k = 8, 16) keep k + rows cell streams in flight per block;
+ * Wide stripes (k = 16) keep k + rows cell streams in flight per block;
  * with every block the registers allow resident, the HBM streams of an
  * EC_16P2 launch run up to ~9 % below what the same launch reaches at 2
  * blocks per CU -- on some boxes.  Round 2 and 3 measured the sign of the
@@ -22,6 +22,19 @@
  * blocks (latency-bound), k <= 4 (every cap loses, profiles/r02/wg_cap),
  * streams under graph capture, and contexts with tuning off
  * (ecg_set_autotune(ctx, 0) or ECG_AUTOTUNE=0 in the environment).
+ *
+ * Shapes are keyed coarsely (round 4): by (k, rows,
+ * acc, diff, cell bytes, lane granule, layout class) where the layout class
+ * is "interleaved" (source and destination share one stripe stride: in-place
+ * recovery, the recovery-layout encode) or "separate" (the client write
+ * layout).  The batch size is not part of the key: callers whose batches
+ * vary (queue flushes, the last batch of a rebuild, per-shard counts) share
+ * one decision, and the arms compare the median time PER BLOCK, so a probe
+ * stays valid when batch sizes change under it.  A probe runs on the stream
+ * of the launch that started it (launches of the shape on other streams run
+ * uncapped meanwhile), every event of both arms must have completed with a
+ * valid time before a decision (an invalid one restarts the probe, at most
+ * twice), and a context starts at most ECG_TUNE_MAX_CYCLES probes.
  */
 #include <stdlib.h>
 #include <string.h>
@@ -31,47 +44,59 @@
 #define ECG_TUNE_W0 1		/* untimed launches at the start of the uncapped arm */
 /* ... and of the capped arm: the first ~10-20 launches after a switch to a
  * capped geometry run up to 12 % slow (EC_16P2 at 2 blocks per CU: 0.434 ms,
- * then 0.38, tools/state_check3.py, profiles/r03/tuner_check/) -- timing them
- * rejected caps that win in the steady state.  Switching back to uncapped
- * shows no such transient, and a kept cap needs no switch at all. */
+ * then 0.38, profiles/r03/tuner_check/) -- timing them rejected caps that win
+ * in the steady state.  Switching back to uncapped shows no such transient,
+ * and a kept cap needs no switch at all. */
 #define ECG_TUNE_W1 16
 #define ECG_TUNE_T 3		/* timed launches per arm (median) */
 #define ECG_TUNE_ARM0 (ECG_TUNE_W0 + ECG_TUNE_T)
 #define ECG_TUNE_PROBE (ECG_TUNE_ARM0 + ECG_TUNE_W1 + ECG_TUNE_T)
 #define ECG_TUNE_MARGIN 0.015	/* the cap must win by more than 1.5 % */
+#define ECG_TUNE_MAX_CYCLES 64	/* probe cycles per context */
+#define ECG_TUNE_RESTARTS 2	/* probes restarted after invalid timings */
 
 struct ecg_tune_ent {
-	int valid, decided, events;
-	uint32_t k, rows, acc, diff;
+	int valid, decided, events, restarts;
+	uint32_t k, rows, acc, diff, g, layout;
 	uint64_t C;
-	uint32_t S;
-	int64_t sstride, dstride;	/* layout: encode and recovery shapes differ here */
+	hipStream_t stream;	/* the probe's stream */
 	uint32_t cand;		/* candidate cap */
 	uint32_t choice;	/* decided: the cap, or ECG_WG_UNCAPPED */
-	uint32_t n;		/* launches of the shape so far */
+	uint32_t n;		/* probing launches so far */
 	uint64_t stamp;
 	hipEvent_t ev[2][ECG_TUNE_T][2];
-	float ms[2];		/* decided: median per arm */
+	uint64_t blocks[2][ECG_TUNE_T];	/* blocks of each timed launch */
+	float ms[2];		/* decided: median per arm, scaled to the last timed launch */
 };
 
 struct ecg_tuner {
 	pthread_mutex_t lock;
 	int enabled;		/* -1 = not yet read from the environment */
 	uint64_t clock;
+	uint64_t cycles;	/* probe cycles started */
+	uint64_t probe_launches;	/* launches that ran as part of a probe */
 	struct ecg_tune_ent ent[ECG_NTUNE];
 };
 
+static uint64_t mm_blocks(const ecg_mm_params_t *p)
+{
+	return ((p->cell_bytes + 4095) / 4096) * (uint64_t)p->nstripes;
+}
+
 static uint32_t candidate_cap(const ecg_mm_params_t *p)
 {
-	const uint64_t blocks = ((p->cell_bytes + 4095) / 4096) * (uint64_t)p->nstripes;
-
-	if (blocks <= 2048 || p->rows == 0)
+	if (mm_blocks(p) <= 2048 || p->rows == 0)
 		return 0;
 	if (p->k >= 16)
 		return 2;	/* profiles/r02/wg_cap: k = 16 best at 2 blocks per CU */
-	if (p->k >= 8)
-		return 3;	/* k = 8 at 3 */
+	/* k = 8: since its product kernel loads in two phases (round 4) every
+	 * cap loses -- 3 blocks per CU +7-10 % (profiles/r04/ec_ab/) */
 	return 0;
+}
+
+static uint32_t layout_class(const ecg_mm_params_t *p)
+{
+	return p->src_stripe_stride == p->dst_stripe_stride;	/* 1: interleaved, 0: separate */
 }
 
 int ecg_tune_init(ecg_ctx_t *ctx)
@@ -135,34 +160,46 @@ int ecg_set_autotune(ecg_ctx_t *ctx, int on)
 	if (on < 0 || on > 1) {		/* 2: forget every decision, tuning on */
 		for (i = 0; i < ECG_NTUNE; i++)
 			ent_free(&t->ent[i]);
+		t->cycles = t->probe_launches = 0;
 		t->enabled = 1;
 	}
 	pthread_mutex_unlock(&t->lock);
 	return 0;
 }
 
-static int same_shape(const struct ecg_tune_ent *e, const ecg_mm_params_t *p)
+static int same_shape(const struct ecg_tune_ent *e, const ecg_mm_params_t *p, uint32_t g)
 {
 	return e->valid && e->k == p->k && e->rows == p->rows && e->acc == p->accumulate && e->diff == p->diff &&
-	       e->C == p->cell_bytes && e->S == p->nstripes &&
-	       e->sstride == p->src_stripe_stride && e->dstride == p->dst_stripe_stride;
+	       e->C == p->cell_bytes && e->layout == layout_class(p) && (g == 0 || e->g == g);
 }
 
-static struct ecg_tune_ent *lookup(struct ecg_tuner *t, const ecg_mm_params_t *p, int create)
+/* g = 0 matches any lane granule (ecg_tune_state) */
+static struct ecg_tune_ent *lookup(struct ecg_tuner *t, const ecg_mm_params_t *p, uint32_t g, int create)
 {
-	struct ecg_tune_ent *old = &t->ent[0];
+	struct ecg_tune_ent *old = NULL;
 	int i;
 
 	for (i = 0; i < ECG_NTUNE; i++) {
-		if (same_shape(&t->ent[i], p)) {
+		if (same_shape(&t->ent[i], p, g)) {
 			t->ent[i].stamp = ++t->clock;
 			return &t->ent[i];
 		}
-		if (!t->ent[i].valid || (old->valid && t->ent[i].stamp < old->stamp))
-			old = &t->ent[i];
 	}
-	if (!create)
+	if (!create || t->cycles >= ECG_TUNE_MAX_CYCLES)
 		return NULL;
+	/* a free slot, else the least recently used decided shape, else the
+	 * least recently used probing one */
+	for (i = 0; i < ECG_NTUNE; i++) {
+		struct ecg_tune_ent *e = &t->ent[i];
+
+		if (!e->valid) {
+			old = e;
+			break;
+		}
+		if (old == NULL || (e->decided && !old->decided) ||
+		    (e->decided == old->decided && e->stamp < old->stamp))
+			old = e;
+	}
 	ent_free(old);
 	old->valid = 1;
 	old->k = p->k;
@@ -170,10 +207,10 @@ static struct ecg_tune_ent *lookup(struct ecg_tuner *t, const ecg_mm_params_t *p
 	old->acc = p->accumulate;
 	old->diff = p->diff;
 	old->C = p->cell_bytes;
-	old->S = p->nstripes;
-	old->sstride = p->src_stripe_stride;
-	old->dstride = p->dst_stripe_stride;
+	old->g = g;
+	old->layout = layout_class(p);
 	old->stamp = ++t->clock;
+	t->cycles++;
 	return old;
 }
 
@@ -184,23 +221,42 @@ static float median3(float a, float b, float c)
 	return a > b ? a : b;
 }
 
-/* all timed events complete: decide (returns 1), else 0 */
+/* every timed event of both arms complete: decide (returns 1); a timing
+ * that cannot be read restarts the probe (returns -1, at most
+ * ECG_TUNE_RESTARTS times, then uncapped); 0 while events are pending. */
 static int try_decide(struct ecg_tune_ent *e)
 {
-	float ms[2][ECG_TUNE_T];
-	int a, i;
+	float per[2][ECG_TUNE_T], ms;
+	uint64_t ref = e->blocks[1][ECG_TUNE_T - 1];
+	int a, i, bad = 0;
 
-	if (hipEventQuery(e->ev[1][ECG_TUNE_T - 1][1]) != hipSuccess)
-		return 0;
 	for (a = 0; a < 2; a++)
 		for (i = 0; i < ECG_TUNE_T; i++)
-			if (hipEventElapsedTime(&ms[a][i], e->ev[a][i][0], e->ev[a][i][1]) != hipSuccess)
-				ms[a][i] = -1.0f;
+			if (hipEventQuery(e->ev[a][i][1]) != hipSuccess)
+				return 0;
 	for (a = 0; a < 2; a++)
-		e->ms[a] = median3(ms[a][0], ms[a][1], ms[a][2]);
+		for (i = 0; i < ECG_TUNE_T; i++) {
+			if (hipEventElapsedTime(&ms, e->ev[a][i][0], e->ev[a][i][1]) != hipSuccess || !(ms > 0.0f) ||
+			    e->blocks[a][i] == 0)
+				bad = 1;
+			else
+				per[a][i] = ms / (float)e->blocks[a][i];
+		}
+	if (bad) {
+		if (e->restarts++ < ECG_TUNE_RESTARTS) {
+			e->n = 0;
+			return -1;
+		}
+		e->decided = 1;
+		e->choice = ECG_WG_UNCAPPED;
+		e->ms[0] = e->ms[1] = 0.0f;
+		return 1;
+	}
+	for (a = 0; a < 2; a++)
+		e->ms[a] = median3(per[a][0], per[a][1], per[a][2]) * (float)ref;
 	e->decided = 1;
 	e->choice = ECG_WG_UNCAPPED;
-	if (e->ms[0] > 0.0f && e->ms[1] > 0.0f && e->ms[1] < e->ms[0] * (1.0f - (float)ECG_TUNE_MARGIN))
+	if (e->ms[1] < e->ms[0] * (1.0f - (float)ECG_TUNE_MARGIN))
 		e->choice = e->cand;
 	return 1;
 }
@@ -230,12 +286,15 @@ int ecg_tune_launch(ecg_ctx_t *ctx, const ecg_mm_params_t *p, hipStream_t st, ui
 	ecg_launch_cfg_t cfg = ctx->cfg;
 	struct ecg_tune_ent *e;
 	hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-	uint32_t cand;
+	uint32_t cand, g;
 	int arm, idx, timed = 0, rc;
 
 	cand = candidate_cap(p);
 	if (t == NULL || cand == 0 || cfg.wg_per_cu != 0 || cfg.variant != 0 || cfg.order != 0 ||
 	    cfg.grid_x != 0 || cfg.grid_y != 0)
+		return ecg_k_launch_matmul(p, &ctx->cfg, (void *)st, kid);
+	g = ecg_k_align_granule(p);
+	if (g == 1)			/* the byte kernel has no blocks-per-CU geometry */
 		return ecg_k_launch_matmul(p, &ctx->cfg, (void *)st, kid);
 	if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
 		return ecg_k_launch_matmul(p, &ctx->cfg, (void *)st, kid);
@@ -245,14 +304,25 @@ int ecg_tune_launch(ecg_ctx_t *ctx, const ecg_mm_params_t *p, hipStream_t st, ui
 		pthread_mutex_unlock(&t->lock);
 		return ecg_k_launch_matmul(p, &ctx->cfg, (void *)st, kid);
 	}
-	e = lookup(t, p, 1);
-	e->cand = cand;
-	if (e->decided || (e->n >= ECG_TUNE_PROBE && try_decide(e))) {
+	e = lookup(t, p, g, 1);
+	if (e == NULL) {		/* probe budget spent: untuned shapes run uncapped */
+		cfg.wg_per_cu = ECG_WG_UNCAPPED;
+		pthread_mutex_unlock(&t->lock);
+		return ecg_k_launch_matmul(p, &cfg, (void *)st, kid);
+	}
+	if (e->n == 0 && !e->decided) {
+		e->stream = st;		/* the probe runs on the stream that starts it */
+		e->cand = cand;
+	}
+	if (!e->decided && e->n >= ECG_TUNE_PROBE)
+		(void)try_decide(e);
+	if (e->decided) {
 		cfg.wg_per_cu = e->choice;
 		pthread_mutex_unlock(&t->lock);
 		return ecg_k_launch_matmul(p, &cfg, (void *)st, kid);
 	}
-	if (e->n >= ECG_TUNE_PROBE) {		/* timings still in flight: run uncapped */
+	if (e->n >= ECG_TUNE_PROBE || st != e->stream) {
+		/* timings still in flight, or another stream: run uncapped */
 		cfg.wg_per_cu = ECG_WG_UNCAPPED;
 		pthread_mutex_unlock(&t->lock);
 		return ecg_k_launch_matmul(p, &cfg, (void *)st, kid);
@@ -270,9 +340,12 @@ int ecg_tune_launch(ecg_ctx_t *ctx, const ecg_mm_params_t *p, hipStream_t st, ui
 	arm = e->n < ECG_TUNE_ARM0 ? 0 : 1;
 	idx = arm ? (int)(e->n - ECG_TUNE_ARM0) - ECG_TUNE_W1 : (int)e->n - ECG_TUNE_W0;
 	e->n++;
-	cfg.wg_per_cu = arm ? cand : ECG_WG_UNCAPPED;
-	if (idx >= 0)
+	t->probe_launches++;
+	cfg.wg_per_cu = arm ? e->cand : ECG_WG_UNCAPPED;
+	if (idx >= 0) {
 		timed = hipEventRecord(e->ev[arm][idx][0], st) == hipSuccess;
+		e->blocks[arm][idx] = mm_blocks(p);
+	}
 	rc = ecg_k_launch_matmul(p, &cfg, (void *)st, kid);
 	if (timed && (rc != 0 || hipEventRecord(e->ev[arm][idx][1], st) != hipSuccess)) {
 		e->decided = 1;		/* give up on this shape: uncapped */
@@ -303,7 +376,7 @@ int ecg_tune_state(ecg_ctx_t *ctx, int k, int rows, uint64_t cell_bytes, uint32_
 	p->src_stripe_stride = sstride;
 	p->dst_stripe_stride = dstride;
 	pthread_mutex_lock(&t->lock);
-	e = lookup(t, p, 0);
+	e = lookup(t, p, 0, 0);
 	if (e && !e->decided && e->n >= ECG_TUNE_PROBE)
 		(void)try_decide(e);
 	rc = e && e->decided ? 1 : 0;
@@ -316,4 +389,26 @@ int ecg_tune_state(ecg_ctx_t *ctx, int k, int rows, uint64_t cell_bytes, uint32_
 	pthread_mutex_unlock(&t->lock);
 	free(p);
 	return rc;
+}
+
+int ecg_tune_counters(ecg_ctx_t *ctx, uint64_t *probe_cycles, uint64_t *probe_launches, uint32_t *shapes)
+{
+	struct ecg_tuner *t;
+	uint32_t n = 0;
+	int i;
+
+	if (ctx == NULL || ctx->tuner == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "tune_counters: NULL context");
+	t = ctx->tuner;
+	pthread_mutex_lock(&t->lock);
+	for (i = 0; i < ECG_NTUNE; i++)
+		n += t->ent[i].valid != 0;
+	if (probe_cycles)
+		*probe_cycles = t->cycles;
+	if (probe_launches)
+		*probe_launches = t->probe_launches;
+	if (shapes)
+		*shapes = n;
+	pthread_mutex_unlock(&t->lock);
+	return 0;
 }

@@ -581,15 +581,6 @@ const csum_entry g_csum[] = {
 	{2, false, TK_5, ecg_crc_kernel<32, true, false, TK_5>, "ecg_crc_kernel<crc32,bytes>"},
 	{3, true, TK_4, ecg_crc_kernel<64, true, true, TK_4>, "ecg_crc_kernel<crc64>"},
 	{3, false, TK_5, ecg_crc_kernel<64, true, false, TK_5>, "ecg_crc_kernel<crc64,bytes>"},
-	{1, true, TK_5, ecg_crc_kernel<16, false, true, TK_5>, "ecg_crc_kernel<crc16,t5>"},
-	{2, true, TK_5, ecg_crc_kernel<32, true, true, TK_5>, "ecg_crc_kernel<crc32,t5>"},
-	{3, true, TK_5, ecg_crc_kernel<64, true, true, TK_5>, "ecg_crc_kernel<crc64,t5>"},
-	{1, true, TK_B8, ecg_crc_kernel<16, false, true, TK_B8>, "ecg_crc_kernel<crc16,alt>"},
-	{1, false, TK_B8, ecg_crc_kernel<16, false, false, TK_B8>, "ecg_crc_kernel<crc16,bytes,alt>"},
-	{2, true, TK_B8, ecg_crc_kernel<32, true, true, TK_B8>, "ecg_crc_kernel<crc32,alt>"},
-	{2, false, TK_B8, ecg_crc_kernel<32, true, false, TK_B8>, "ecg_crc_kernel<crc32,bytes,alt>"},
-	{3, true, TK_B8, ecg_crc_kernel<64, true, true, TK_B8>, "ecg_crc_kernel<crc64,alt>"},
-	{3, false, TK_B8, ecg_crc_kernel<64, true, false, TK_B8>, "ecg_crc_kernel<crc64,bytes,alt>"},
 	{7, true, 0, ecg_adler_kernel<true>, "ecg_adler_kernel"},
 	{7, false, 0, ecg_adler_kernel<false>, "ecg_adler_kernel<bytes>"},
 };
@@ -600,12 +591,6 @@ const csum_entry g_split[] = {
 	{1, true, TK_4, ecg_crc_split_kernel<16, false, SPLIT_NW, TK_4>, "ecg_crc_split_kernel<crc16>"},
 	{2, true, TK_4, ecg_crc_split_kernel<32, true, SPLIT_NW, TK_4>, "ecg_crc_split_kernel<crc32>"},
 	{3, true, TK_4, ecg_crc_split_kernel<64, true, SPLIT_NW, TK_4>, "ecg_crc_split_kernel<crc64>"},
-	{1, true, TK_5, ecg_crc_split_kernel<16, false, SPLIT_NW, TK_5>, "ecg_crc_split_kernel<crc16,t5>"},
-	{2, true, TK_5, ecg_crc_split_kernel<32, true, SPLIT_NW, TK_5>, "ecg_crc_split_kernel<crc32,t5>"},
-	{3, true, TK_5, ecg_crc_split_kernel<64, true, SPLIT_NW, TK_5>, "ecg_crc_split_kernel<crc64,t5>"},
-	{1, true, TK_B8, ecg_crc_split_kernel<16, false, SPLIT_NW, TK_B8>, "ecg_crc_split_kernel<crc16,alt>"},
-	{2, true, TK_B8, ecg_crc_split_kernel<32, true, SPLIT_NW, TK_B8>, "ecg_crc_split_kernel<crc32,alt>"},
-	{3, true, TK_B8, ecg_crc_split_kernel<64, true, SPLIT_NW, TK_B8>, "ecg_crc_split_kernel<crc64,alt>"},
 	{7, true, 0, ecg_adler_split_kernel<SPLIT_NW>, "ecg_adler_split_kernel"},
 };
 constexpr uint32_t N_SPLIT = sizeof(g_split) / sizeof(g_split[0]);
@@ -614,25 +599,16 @@ const csum_entry g_group[] = {
 	{1, true, TK_4, ecg_crc_group_kernel<16, false, TK_4>, "ecg_crc_group_kernel<crc16>"},
 	{2, true, TK_4, ecg_crc_group_kernel<32, true, TK_4>, "ecg_crc_group_kernel<crc32>"},
 	{3, true, TK_4, ecg_crc_group_kernel<64, true, TK_4>, "ecg_crc_group_kernel<crc64>"},
-	{1, true, TK_5, ecg_crc_group_kernel<16, false, TK_5>, "ecg_crc_group_kernel<crc16,t5>"},
-	{2, true, TK_5, ecg_crc_group_kernel<32, true, TK_5>, "ecg_crc_group_kernel<crc32,t5>"},
-	{3, true, TK_5, ecg_crc_group_kernel<64, true, TK_5>, "ecg_crc_group_kernel<crc64,t5>"},
-	{1, true, TK_B8, ecg_crc_group_kernel<16, false, TK_B8>, "ecg_crc_group_kernel<crc16,alt>"},
-	{2, true, TK_B8, ecg_crc_group_kernel<32, true, TK_B8>, "ecg_crc_group_kernel<crc32,alt>"},
-	{3, true, TK_B8, ecg_crc_group_kernel<64, true, TK_B8>, "ecg_crc_group_kernel<crc64,alt>"},
 };
 constexpr uint32_t N_GROUP = sizeof(g_group) / sizeof(g_group[0]);
 
-/* the entry's table kind matches the request (adler32 has one kind; the
- * byte-granular kernels of unaligned extents have the 5-bit tables unless
- * the byte tables are asked for) */
+/* one table kind per kernel: the nibble tables for 16-byte aligned extents,
+ * the 5-bit tables for the byte-granular kernels (the byte and 5-bit aligned
+ * variants of rounds 1-3 were A/B builds, profiles/r03/crc_sq/) */
 __host__ inline bool kind_ok(const csum_entry &e, const ecg_csum_params_t *p)
 {
-	if (e.type == 7)
-		return true;
-	if (!e.aligned && p->byte_tables == TK_4)
-		return e.tk == TK_5;
-	return e.tk == (int)p->byte_tables;
+	(void)p;
+	return e.type == 7 || e.tk == (e.aligned ? TK_4 : TK_5);
 }
 
 } // namespace

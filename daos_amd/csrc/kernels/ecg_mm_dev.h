@@ -1,0 +1,439 @@
+// ecg_mm_dev.h -- device building blocks of the GF(2^8) product shared by
+// the product kernels (ecg_kernels.hip) and the fused product + checksum
+// kernels (ecg_fused_kernels.hip): lane layouts, cell loads and stores, the
+// v_perm_b32 multiply, ragged tails.  Design notes: ecg_kernels.hip header.
+#ifndef ECG_MM_DEV_H
+#define ECG_MM_DEV_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../ecg_kabi.h"
+
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#define CHUNK_BYTES 4096u	// 256 lanes x 16 B
+#define BLOCK 256
+#ifndef ECG_MM_WG_DEFAULT
+// per-shape default blocks per CU (mm_wg_cap) by the cell streams a block
+// keeps in flight (k + rows): none -- see mm_wg_cap
+#define ECG_MM_WG_DEFAULT(streams) 0u
+#endif
+
+template <bool B>
+struct ecg_bool {
+	static constexpr bool value = B;
+};
+
+__device__ __forceinline__ u32x4 ld_nt(const uint8_t *p)
+{
+	return __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+}
+
+__device__ __forceinline__ void st_nt(uint8_t *p, u32x4 v)
+{
+	__builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
+}
+
+// Lane access granule G (16, 8 or 4 bytes): the largest power of two that
+// divides every cell address of a launch (ecg_k_launch_matmul picks it).  A
+// wave always covers 1 KiB of each cell per column and a lane always owns 4
+// dwords of it; only how the dwords are fetched changes:
+//   G = 16: one dwordx4 at wave*1024 + lane*16
+//   G = 8 : two dwordx2 at wave*1024 + {0, 512} + lane*8
+//   G = 4 : four dwords at wave*1024 + {0, 256, 512, 768} + lane*4
+// so every wave-wide access is still one contiguous, naturally aligned
+// 1024 / 512 / 256-byte run.  GF arithmetic is per byte, so which bytes a
+// lane owns does not matter, only that loads and stores agree.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+template <int G>
+__device__ __forceinline__ uint32_t lane_off()
+{
+	return (threadIdx.x >> 6) * 1024u + (threadIdx.x & 63u) * (uint32_t)G;
+}
+
+// byte offset of dword i of the lane's piece from lane_off<G>()
+template <int G>
+__device__ __forceinline__ uint32_t elem_off(int i)
+{
+	return G == 16 ? 4u * i : G == 8 ? (uint32_t)(i >> 1) * 512u + (uint32_t)(i & 1) * 4u : (uint32_t)i * 256u;
+}
+
+template <int G>
+__device__ __forceinline__ u32x4 ld_g(const uint8_t *p)
+{
+	if constexpr (G == 16) {
+		return ld_nt(p);
+	} else if constexpr (G == 8) {
+		const u32x2 a = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(p));
+		const u32x2 b = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(p + 512));
+		return (u32x4){a[0], a[1], b[0], b[1]};
+	} else {
+		static_assert(G == 4, "granule");
+		const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
+		return (u32x4){__builtin_nontemporal_load(q), __builtin_nontemporal_load(q + 64),
+			       __builtin_nontemporal_load(q + 128), __builtin_nontemporal_load(q + 192)};
+	}
+}
+
+template <int G>
+__device__ __forceinline__ void st_g(uint8_t *p, u32x4 v)
+{
+	if constexpr (G == 16) {
+		st_nt(p, v);
+	} else if constexpr (G == 8) {
+		__builtin_nontemporal_store((u32x2){v[0], v[1]}, reinterpret_cast<u32x2 *>(p));
+		__builtin_nontemporal_store((u32x2){v[2], v[3]}, reinterpret_cast<u32x2 *>(p + 512));
+	} else {
+		uint32_t *q = reinterpret_cast<uint32_t *>(p);
+		__builtin_nontemporal_store(v[0], q);
+		__builtin_nontemporal_store(v[1], q + 64);
+		__builtin_nontemporal_store(v[2], q + 128);
+		__builtin_nontemporal_store(v[3], q + 192);
+	}
+}
+
+// c*x for the 4 bytes of one dword, given that dword's 3 selector words.
+__device__ __forceinline__ uint32_t gf_mul4(const ecg_ptbl_t &t, uint32_t s0, uint32_t s1, uint32_t s2)
+{
+	return __builtin_amdgcn_perm(t.t0hi, t.t0lo, s0) ^
+	       __builtin_amdgcn_perm(t.t1hi, t.t1lo, s1) ^
+	       __builtin_amdgcn_perm(t.t2, t.t2, s2);
+}
+
+// Byte-granular product for the < 16-byte tail of a cell (and the
+// misaligned fallback): same tables, one byte in the low lane of a dword.
+__device__ __forceinline__ uint8_t gf_mul1(const ecg_ptbl_t &t, uint32_t x)
+{
+	return (uint8_t)gf_mul4(t, x & 7u, (x >> 3) & 7u, x >> 6);
+}
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+	return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// One (stripe, 4 KiB column) item of the product.  Addresses are a
+// wave-uniform 64-bit base per cell (SGPRs) plus the lane's 32-bit offset.
+// The uniform cell offsets are passed through an empty asm per item so LICM
+// cannot hoist k+rows 64-bit pointers out of the stripe loop (they land in
+// VGPRs and spill at EC_8P2/EC_16P2).
+// JN, j0: load only cells [j0, j0 + JN) (phased loads of wide stripes; j0
+// is a constant once the caller's loop is unrolled).
+template <int KM, bool DIFF, int G = 16, int JN = KM>
+__device__ __forceinline__ void mm_load(const ecg_mm_params_t &P, int k, uint32_t s, uint64_t cbase,
+					uint32_t lo, u32x4 *x, int j0 = 0)
+{
+	const int64_t s_src = (int64_t)s * P.src_stripe_stride + (int64_t)cbase;
+	const int64_t s_src2 = DIFF ? (int64_t)s * P.src2_stripe_stride + (int64_t)cbase : 0;
+
+#pragma unroll
+	for (int j = j0; j < j0 + JN; j++) {
+		if (j < k) {
+			int64_t o = P.src_cell_off[j] + s_src;
+			asm volatile("" : "+s"(o));
+			x[j] = ld_g<G>(P.src + o + lo);
+			if (DIFF) {
+				int64_t o2 = P.src2_cell_off[j] + s_src2;
+				asm volatile("" : "+s"(o2));
+				x[j] ^= ld_g<G>(P.src2 + o2 + lo);
+			}
+		}
+	}
+}
+
+// mm_load with no branch: lanes whose 16 bytes would pass the cell end read
+// the column's first 16 bytes instead (C % 16 == 0; callers never use those
+// lanes' values)
+template <int KM>
+__device__ __forceinline__ void mm_load_any(const ecg_mm_params_t &P, int k, uint32_t s, uint64_t cbase,
+					    uint32_t lo, u32x4 *x)
+{
+	mm_load<KM, false>(P, k, s, cbase, cbase + lo + 16 <= P.cell_bytes ? lo : 0u, x);
+}
+
+// Cells loaded per phase of the product kernel for k = K and lane granule G
+// (0 = all k cells of a column before any arithmetic).  With PH > 0 a block
+// keeps PH x 4 KiB of loads in flight per column instead of k x 4 KiB, and
+// one phase's arithmetic overlaps the next phase's loads.  ECG_MM_WPE(K, G):
+// the waves per SIMD the register budget of those instantiations targets (0 =
+// the compiler's choice; a phased kernel needs a budget -- unconstrained, the
+// scheduler computes the selectors of a whole phase at once and spills to
+// AGPRs at 1 wave per SIMD).  Measured (tools/ec_ab.py, profiles/r04/ec_ab/,
+// ms, back-to-back launches): k = 8 in 2 phases of 4 at 4 waves --
+// EC_8P2 1 MiB x 512 decode 0.873 -> 0.836 (the best capped geometry before:
+// 0.859), encode 0.844 -> 0.831; the 8-byte-lane (G = 8) variant lost 3 %,
+// so phases apply to G = 16 and 4 only.  k = 16 in phases of 4 lost 5-20 %
+// at 4 or 5 waves (phases of 8 spill).
+#ifndef ECG_MM_PHASE
+#define ECG_MM_PHASE(K, G) ((K) == 8 && (G) != 8 ? 4 : 0)
+#endif
+#ifndef ECG_MM_WPE
+#define ECG_MM_WPE(K, G) ((K) == 8 && (G) != 8 ? 4 : 0)
+#endif
+
+// The product of one column: x[j] = the lane's 16 bytes of cell j.  STORE =
+// false leaves the stores to the caller (outputs returned in keep).  PH > 0:
+// only cells [0, PH) are loaded on entry, and cells [j, j + PH) are loaded
+// when the fold reaches j (DIFF: their src2 too).  (One function on purpose: the same loops split
+// into init / fold / store helpers made the register allocator keep EC_16P2
+// at 256 VGPRs + AGPRs, 1 wave per SIMD, instead of 114 / 4 waves.)
+template <int KM, int RM, bool ACC, bool KEEP, bool STORE = true, int G = 16, int PH = 0, bool DIFF = false>
+__device__ __forceinline__ void mm_compute(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
+					   uint32_t s, uint64_t cbase, uint32_t lo, u32x4 *x, u32x4 *keep)
+{
+	constexpr int T2V = (RM + 3) / 4;
+	constexpr int PER_J = RM + T2V;
+	const int64_t s_dst = (int64_t)s * P.dst_stripe_stride + (int64_t)cbase;
+
+	u32x4 acc[RM];
+#pragma unroll
+	for (int r = 0; r < RM; r++) {
+		if (r < rows) {
+			if (ACC) {
+				int64_t o = P.dst_cell_off[r] + s_dst;
+				asm volatile("" : "+s"(o));
+				acc[r] = ld_g<G>(P.dst + o + lo);
+			} else {
+				acc[r] = (u32x4){0u, 0u, 0u, 0u};
+			}
+		}
+	}
+#pragma unroll
+	for (int j = 0; j < KM; j++) {
+		if constexpr (PH > 0) {
+			if (j > 0 && j % PH == 0) {
+				// the next phase's loads and table reads depend (falsely)
+				// on every accumulator: none of them can be issued before
+				// this phase's arithmetic is done
+				uint32_t lo2 = lo, z2 = 0, dep = 0;
+#pragma unroll
+				for (int r = 0; r < RM; r++)
+					if (r < rows)
+						dep ^= acc[r][0] ^ acc[r][1] ^ acc[r][2] ^ acc[r][3];
+				asm volatile("" : "+v"(lo2), "+v"(z2) : "v"(dep));
+				tb += z2;
+				mm_load<KM, DIFF, G, PH>(P, k, s, cbase, lo2, x, j);
+			}
+		}
+		if (j < k) {
+			u32x4 sel0, sel1, sel2;
+#pragma unroll
+			for (int w = 0; w < 4; w++) {
+				const uint32_t v = x[j][w];
+				sel0[w] = v & 0x07070707u;
+				sel1[w] = (v >> 3) & 0x07070707u;
+				sel2[w] = (v >> 6) & 0x03030303u;
+			}
+			u32x4 t2v[T2V];
+#pragma unroll
+			for (int q = 0; q < T2V; q++)
+				t2v[q] = tb[j * PER_J + RM + q];
+#pragma unroll
+			for (int r = 0; r < RM; r++) {
+				if (r < rows) {
+					const u32x4 t = tb[j * PER_J + r];
+					const uint32_t t2 = t2v[r / 4][r % 4];
+#pragma unroll
+					for (int w = 0; w < 4; w++) {
+						const uint32_t p0 = __builtin_amdgcn_perm(t[1], t[0], sel0[w]);
+						const uint32_t p1 = __builtin_amdgcn_perm(t[3], t[2], sel1[w]);
+						const uint32_t p2 = __builtin_amdgcn_perm(t2, t2, sel2[w]);
+						acc[r][w] = xor3(acc[r][w], p0, xor3(p1, p2, 0u));
+					}
+				}
+			}
+		}
+	}
+#pragma unroll
+	for (int r = 0; r < RM; r++) {
+		if (r < rows) {
+			if (STORE) {
+				int64_t o = P.dst_cell_off[r] + s_dst;
+				asm volatile("" : "+s"(o));
+				st_g<G>(P.dst + o + lo, acc[r]);
+			}
+			if (KEEP)
+				keep[r] = acc[r];
+		}
+	}
+}
+
+template <int KM, int RM, bool ACC, bool DIFF, bool KEEP = false, int G = 16>
+__device__ __forceinline__ void mm_item(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
+					uint32_t s, uint64_t cbase, uint32_t lo, u32x4 *keep = nullptr)
+{
+	constexpr int PH = (ECG_MM_PHASE(KM, G) > 0 && ECG_MM_PHASE(KM, G) < KM && KM % ECG_MM_PHASE(KM, G) == 0)
+				   ? ECG_MM_PHASE(KM, G) : 0;
+	u32x4 x[KM];
+
+	mm_load<KM, DIFF, G, PH ? PH : KM>(P, k, s, cbase, lo, x);
+	mm_compute<KM, RM, ACC, KEEP, true, G, PH, DIFF>(P, tb, k, rows, s, cbase, lo, x, keep);
+}
+
+// One dword of every output row at byte offset `off` of the cells (the
+// partial last column of a G = 4 / 8 launch: off is a multiple of 4 and the
+// dword lies inside the cell).
+template <int RM, bool ACC, bool DIFF>
+__device__ __forceinline__ void mm_dword(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
+					 uint32_t s, uint64_t off)
+{
+	constexpr int T2V = (RM + 3) / 4;
+	constexpr int PER_J = RM + T2V;
+	const uint8_t *sb = P.src + (int64_t)s * P.src_stripe_stride + off;
+	const uint8_t *sb2 = DIFF ? P.src2 + (int64_t)s * P.src2_stripe_stride + off : nullptr;
+	uint8_t *db = P.dst + (int64_t)s * P.dst_stripe_stride + off;
+	uint32_t o[RM];
+
+#pragma unroll
+	for (int r = 0; r < RM; r++)
+		o[r] = 0;
+	for (int j = 0; j < k; j++) {
+		uint32_t v = *reinterpret_cast<const uint32_t *>(sb + P.src_cell_off[j]);
+		if (DIFF)
+			v ^= *reinterpret_cast<const uint32_t *>(sb2 + P.src2_cell_off[j]);
+		const uint32_t s0 = v & 0x07070707u, s1 = (v >> 3) & 0x07070707u, s2 = (v >> 6) & 0x03030303u;
+#pragma unroll
+		for (int r = 0; r < RM; r++) {
+			if (r < rows) {
+				const u32x4 t = tb[j * PER_J + r];
+				const uint32_t t2 = reinterpret_cast<const uint32_t *>(&tb[j * PER_J + RM])[r];
+				o[r] ^= __builtin_amdgcn_perm(t[1], t[0], s0) ^ __builtin_amdgcn_perm(t[3], t[2], s1) ^
+					__builtin_amdgcn_perm(t2, t2, s2);
+			}
+		}
+	}
+#pragma unroll
+	for (int r = 0; r < RM; r++) {
+		if (r < rows) {
+			uint32_t *d = reinterpret_cast<uint32_t *>(db + P.dst_cell_off[r]);
+			*d = ACC ? *d ^ o[r] : o[r];
+		}
+	}
+}
+
+// Ragged tail: fewer than 16 bytes of this lane's slot are inside the cell.
+template <int RM, bool ACC, bool DIFF>
+__device__ __forceinline__ void mm_tail(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
+				     uint32_t s, uint64_t off, int nb)
+{
+	constexpr int T2V = (RM + 3) / 4;
+	constexpr int PER_J = RM + T2V;
+	const uint8_t *sb = P.src + (int64_t)s * P.src_stripe_stride;
+	const uint8_t *sb2 = DIFF ? P.src2 + (int64_t)s * P.src2_stripe_stride : nullptr;
+	uint8_t *db = P.dst + (int64_t)s * P.dst_stripe_stride;
+
+	for (int b = 0; b < nb; b++) {
+		uint32_t o[RM];
+#pragma unroll
+		for (int r = 0; r < RM; r++)
+			o[r] = 0;
+		for (int j = 0; j < k; j++) {
+			uint32_t v = sb[P.src_cell_off[j] + off + b];
+			if (DIFF)
+				v ^= sb2[P.src2_cell_off[j] + off + b];
+			const uint32_t s0 = v & 7u, s1 = (v >> 3) & 7u, s2 = v >> 6;
+#pragma unroll
+			for (int r = 0; r < RM; r++) {
+				if (r < rows) {
+					const u32x4 t = tb[j * PER_J + r];
+					const uint32_t t2 = reinterpret_cast<const uint32_t *>(&tb[j * PER_J + RM])[r];
+					o[r] ^= __builtin_amdgcn_perm(t[1], t[0], s0) ^
+						__builtin_amdgcn_perm(t[3], t[2], s1) ^
+						__builtin_amdgcn_perm(t2, t2, s2);
+				}
+			}
+		}
+#pragma unroll
+		for (int r = 0; r < RM; r++) {
+			if (r < rows) {
+				uint8_t *d = db + P.dst_cell_off[r] + off + b;
+				*d = ACC ? (uint8_t)(*d ^ o[r]) : (uint8_t)o[r];
+			}
+		}
+	}
+}
+
+// The last, partial column of a cell (C % 4096 != 0): G = 16 as a full
+// lane piece where the lane's 16 bytes are inside the cell, else bytewise;
+// G = 4 / 8 dword by dword, the bytes after the cell's last whole dword
+// bytewise.
+template <int KM, int RM, bool ACC, bool DIFF, int G>
+__device__ __forceinline__ void mm_partial(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
+					   uint32_t s, uint64_t cbase, uint32_t lo)
+{
+	const uint64_t C = P.cell_bytes;
+
+	if constexpr (G == 16) {
+		if (cbase + lo + 16 <= C)
+			mm_item<KM, RM, ACC, DIFF>(P, tb, k, rows, s, cbase, lo);
+		else if (cbase + lo < C)
+			mm_tail<RM, ACC, DIFF>(P, tb, k, rows, s, cbase + lo, (int)(C - cbase - lo));
+	} else {
+#pragma unroll
+		for (int i = 0; i < 4; i++) {
+			const uint64_t off = cbase + lo + elem_off<G>(i);
+
+			if (off + 4 <= C)
+				mm_dword<RM, ACC, DIFF>(P, tb, k, rows, s, off);
+			else if (off < C)
+				mm_tail<RM, ACC, DIFF>(P, tb, k, rows, s, off, (int)(C - off));
+		}
+	}
+}
+
+// 1D item orders (P.order): which (stripe, 4 KiB column) block `it` of a
+// 1D grid works on.  The hardware dispatcher hands consecutive block ids to
+// the 8 XCDs round-robin, so `it & 7` is (nearly) the block's XCD.
+//   1  stripe-fastest: consecutive blocks touch the same column of
+//      consecutive stripes
+//   2  XCD-blocked, column-fastest: XCD x walks the x-th eighth of the
+//      column-fastest item list (each XCD streams its own stripe range)
+//   3  XCD-blocked, stripe-fastest
+__device__ __forceinline__ void item_map(uint32_t order, uint32_t it, uint32_t total, uint32_t nchunk,
+					 uint32_t S, uint32_t &s, uint32_t &ch)
+{
+	uint32_t g = it;
+
+	if (order >= 2) {
+		const uint32_t per = (total + 7) / 8;	// items per XCD slice
+		const uint32_t x = it & 7, j = it >> 3;
+
+		g = x * per + j;
+		if (g >= total)			// uneven tail: fall back to the plain id
+			g = it;
+	}
+	if (order == 1 || order == 3) {
+		s = g % S;
+		ch = g / S;
+	} else {
+		s = g / nchunk;
+		ch = g - s * nchunk;
+	}
+}
+
+// The common alignment of every cell address of a launch: 16, 8, 4 or 1.
+static inline uint32_t align_granule(const ecg_mm_params_t *p)
+{
+	uint64_t bits = (uint64_t)(uintptr_t)p->src | (uint64_t)(uintptr_t)p->dst |
+			(uint64_t)p->src_stripe_stride | (uint64_t)p->dst_stripe_stride;
+	for (uint32_t j = 0; j < p->k; j++) {
+		bits |= (uint64_t)p->src_cell_off[j];
+		if (p->diff)
+			bits |= (uint64_t)p->src2_cell_off[j];
+	}
+	if (p->diff)
+		bits |= (uint64_t)(uintptr_t)p->src2 | (uint64_t)p->src2_stripe_stride;
+	for (uint32_t r = 0; r < p->rows; r++)
+		bits |= (uint64_t)p->dst_cell_off[r];
+	return (bits & 15u) == 0 ? 16u : (bits & 7u) == 0 ? 8u : (bits & 3u) == 0 ? 4u : 1u;
+}
+
+static inline bool aligned16(const ecg_mm_params_t *p)
+{
+	return align_granule(p) == 16u;
+}
+
+#endif

@@ -90,6 +90,7 @@ _SIGS = [
     ("ecg_set_autotune", C.c_int, [vp, C.c_int]),
     ("ecg_tune_state", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, C.c_int64, C.c_int64, u32p,
                                  C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+    ("ecg_tune_counters", C.c_int, [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), u32p]),
     ("ecg_get_stats", C.c_int, [vp, vp, C.c_int]),
     # multi-device sharder (ecg_multi.h)
     ("ecg_multi_create", C.c_int, [C.POINTER(C.c_int), C.c_int, C.POINTER(vp)]),
@@ -171,7 +172,6 @@ _SIGS = [
     ("ecg_csum_extents", C.c_int, [vp, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, vp, C.c_int64,
                                    C.c_uint32, vp, vp]),
     ("ecg_set_csum_launch", C.c_int, [vp, C.c_uint32]),
-    ("ecg_set_csum_variant", C.c_int, [vp, C.c_uint32]),
     ("ecg_set_fused_cols", C.c_int, [vp, C.c_uint32]),
     ("ecg_encode_csum", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, vp, C.c_int64, vp, C.c_int64,
                                   C.c_int64, C.c_int, C.c_uint64, C.c_uint64, vp, vp]),
@@ -489,6 +489,12 @@ class Context:
     def set_autotune(self, on: int = 1):
         """Launch tuner (include/ecg.h ecg_set_autotune): 0 off, 1 on, 2 on and forget decisions."""
         _chk(lib().ecg_set_autotune(self.h, on), "set_autotune")
+
+    def tune_counters(self):
+        """(probe cycles started, launches run inside a probe, shapes held) -- ecg_tune_counters."""
+        cyc, lau, shp = C.c_uint64(), C.c_uint64(), C.c_uint32()
+        _chk(lib().ecg_tune_counters(self.h, C.byref(cyc), C.byref(lau), C.byref(shp)), "tune_counters")
+        return cyc.value, lau.value, shp.value
 
     def tune_state(self, k: int, rows: int, cell_bytes: int, nstripes: int, src_stride: int, dst_stride: int):
         """None while the shape is probing or unseen, else (cap, ms_uncapped, ms_capped);

@@ -270,22 +270,30 @@ int ecg_set_launch_order(ecg_ctx_t *ctx, uint32_t order);
  * with unused dynamic LDS.  Tuning only; results never depend on it. */
 int ecg_set_wg_per_cu(ecg_ctx_t *ctx, uint32_t wg_per_cu);
 /* Launch tuner (on by default; ECG_AUTOTUNE=0 in the environment turns it off
- * for new contexts): the first 23 product launches of each wide shape (k >= 8,
- * > 2048 blocks) in a context run 4 uncapped then 19 at the candidate cap (k = 16:
- * 2 blocks per CU, k = 8: 3), the last 3 of each arm timed with events on the
- * launch stream (a switch to a cap runs slow for its first ~10-20 launches); once the
- * timings have completed the faster is kept for the shape (the cap only when
- * it wins by > 1.5 %).  Skipped when ecg_set_wg_per_cu or ecg_set_launch /
- * _order set a geometry, and on streams under graph capture.  on: 0 off, 1 on,
- * 2 on and forget every decision.  Tuning only; results never depend on it. */
+ * for new contexts): the first 23 product launches of each wide shape (k >= 16,
+ * > 2048 blocks) in a context run 4 uncapped then 19 at the candidate cap (2
+ * blocks per CU), the last 3 of each arm timed with events on the
+ * stream of the launch that started the probe (a switch to a cap runs slow for
+ * its first ~10-20 launches); once every timing has completed the faster time
+ * per block is kept for the shape (the cap only when it wins by > 1.5 %).  A
+ * shape is (k, rows, acc/diff, cell bytes, lane granule, layout class:
+ * source and destination sharing one stripe stride or not) -- NOT the batch
+ * size, so batches of varying size share one probe and one decision.  Skipped
+ * when ecg_set_wg_per_cu or ecg_set_launch / _order set a geometry, and on
+ * streams under graph capture.  on: 0 off, 1 on, 2 on and forget every
+ * decision (and the counters).  Tuning only; results never depend on it. */
 int ecg_set_autotune(ecg_ctx_t *ctx, int on);
 /* The tuner's state of a shape (k inputs, rows outputs, acc/diff off, the
  * launch's source and destination stripe strides -- encode: k*C and the
  * parity stripe stride; in-place recovery: (k+p)*C both): 1 decided (*cap =
  * the cap, or 255 = none; the median launch times of both arms), 0 still
- * probing or not seen. */
+ * probing or not seen.  nstripes is not part of the shape (it only has to
+ * make the launch tunable, > 2048 blocks, to have been probed). */
 int ecg_tune_state(ecg_ctx_t *ctx, int k, int rows, uint64_t cell_bytes, uint32_t nstripes, int64_t sstride,
 		   int64_t dstride, uint32_t *cap, float *ms_uncapped, float *ms_capped);
+/* The tuner's counters since the context was created (or ecg_set_autotune(ctx,
+ * 2)): probe cycles started, launches that ran inside a probe, shapes held. */
+int ecg_tune_counters(ecg_ctx_t *ctx, uint64_t *probe_cycles, uint64_t *probe_launches, uint32_t *shapes);
 
 /* Pointer-table product: ISA-L's per-stripe pointer arrays
  * (ec_encode_data(len, k, rows, tbls, data[], coding[])) batched over

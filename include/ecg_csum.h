@@ -91,27 +91,11 @@ int ecg_recover_csum(ecg_ctx_t *ctx, int k, int p, uint64_t cell_bytes, uint32_t
  * stride beyond); 0 restores the default. */
 int ecg_set_csum_launch(ecg_ctx_t *ctx, uint32_t max_blocks);
 
-/* Launch tuning (A/B measurements; same results either way).  Bits 0-3, CRC
- * kernel shape for 16-byte aligned extents: 0 by shape (default: a workgroup
- * per chunk when chunks are long and few, a 16-lane group per chunk when
- * chunks are <= 8 KiB), 1 one wave per chunk, 2 one workgroup per chunk, 3 one
- * 16-lane group per chunk.  CRC lookup tables (default per hash: 5-bit for
- * crc16/crc32, byte tables for crc64): bit 4 forces the byte tables, bit 5 the
- * 5-bit tables, bit 6 the 16-slice byte tables in the fused kernels.  Fused
- * kernel shape (default: a wave per chunk for crc64 with k <= 4, else
- * workgroups over work items): bit 7 forces the wave per chunk, bit 8 the
- * workgroups.  Bit 9: the fused kernels' s16 byte tables with SDWA addresses
- * and the nibble column shift (TB 3).  Bit 10: the fused workgroup kernel's
- * positional nibble tables (TB 4; items of 4 columns unless set otherwise;
- * not combinable with bits 6, 7, 9).  Standalone CRC kernels default to the
- * nibble tables; bit 4 / bit 5 select the byte / 5-bit tables there too. */
-int ecg_set_csum_variant(ecg_ctx_t *ctx, uint32_t variant);
-
 /* Launch tuning: 4 KiB columns per work item of the fused product +
  * checksum kernels (ecg_encode_csum / ecg_recover_csum); 0 restores the
  * default (env ECG_FUSED_COLS, else by hash type, k and output rows: 2 for
- * crc32 with k = 8 and two rows, 4 for one row or k >= 8, else 8; 4 with the
- * TB 4 tables).  Same results either way. */
+ * crc32 with k = 8 and two rows, 4 for one row or k >= 8, else 8).  Same
+ * results either way. */
 int ecg_set_fused_cols(ecg_ctx_t *ctx, uint32_t ncols);
 
 #ifdef __cplusplus

@@ -106,6 +106,25 @@ def test_bench_gpus_n_spawns_ranks():
     assert sorted(x["rank"] for x in d["ranks"]) == [0, 1]
     assert len({x["pid"] for x in d["ranks"]}) == 2
     assert d["ms_per_step"] >= 2.0          # the slower rank (2 ms steps) sets the time
+    # the configs[3] / configs[4] legs ran on both ranks (split, timing, aggregation)
+    strong = d["detail"]["config3_EC_16P2_128KiB_x8192_strong"]
+    assert strong["scaling"] == "strong" and len(strong["ranks"]) == 2
+    assert sorted((r["first_stripe"], r["stripes"]) for r in strong["ranks"]) == [(0, 4096), (4096, 4096)]
+    stream = d["detail"]["config4_EC_8P2_1MiB_rebuild_stream"]
+    assert stream["scaling"] == "weak" and sorted(r["rank"] for r in stream["ranks"]) == [0, 1]
+
+
+def test_strong_split_ranges():
+    """configs[3]'s 8192 stripes cut into contiguous ranges that cover the
+    total exactly once for every world size, the first ranks one longer."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    for world in range(1, 17):
+        rs = [bench.split_range(8192 + 5, world, r) for r in range(world)]
+        assert rs[0][0] == 0 and sum(n for _, n in rs) == 8197
+        assert all(a + n == b for (a, n), (b, _) in zip(rs, rs[1:]))
+        assert max(n for _, n in rs) - min(n for _, n in rs) <= 1
 
 
 def test_bench_world_mismatch_refused():

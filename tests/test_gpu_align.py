@@ -1,0 +1,169 @@
+"""GPU parity of the product kernels at every operand alignment.
+
+The product kernels pick their lane access per launch from the common
+alignment of every cell address (ecg_kernels.hip align_granule): 16-byte
+dwordx4 lanes, 8-byte dwordx2 lanes (DAOS rounds its parity rows to 8 bytes,
+ref:src/object/cli_ec.c:86), 4-byte dword lanes, or the byte kernel (user sgl
+cells carry no alignment, ref:src/object/cli_ec.c:510-536).  Every case is
+compared byte for byte with the oracle, and the test asserts which kernel ran.
+Offsets 1, 4, 8 and 12 of the data and/or parity bases, cells whose last
+4 KiB column is partial, and cell sizes that are not multiples of 4 / 16.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def rand(shape, seed):
+    return np.random.default_rng(seed).integers(0, 256, shape, dtype=np.uint8)
+
+
+def granule(*vals):
+    bits = 0
+    for v in vals:
+        bits |= v
+    return 16 if bits % 16 == 0 else 8 if bits % 8 == 0 else 4 if bits % 4 == 0 else 1
+
+
+def expect_kernel(name, g, k, rows):
+    if g == 1:
+        assert name == "ecg_mm_byte_kernel", name
+    elif g == 16:
+        assert name.startswith("ecg_mm_kernel<") and ",g" not in name, name
+    else:
+        assert name.startswith("ecg_mm_kernel<") and name.endswith(f",g{g}>"), name
+
+
+def oracle_parity(oracle, k, p, data):
+    en = oracle.cauchy1(k, p)
+    return np.stack([oracle.encode_data(en[k:], data[s]) for s in range(data.shape[0])], axis=1)
+
+
+CELLS = [65536, 2 * 4096 + 1024 + 8, 3 * 4096 + 20, 4096 + 13]
+
+
+@pytest.mark.parametrize("C_", CELLS)
+@pytest.mark.parametrize("doff,poff", [(1, 0), (4, 0), (8, 0), (12, 0), (0, 1), (0, 4), (0, 8), (0, 12),
+                                       (8, 8), (4, 12), (12, 8)])
+def test_encode_offsets(ctx, oracle, ecglib, C_, doff, poff):
+    """Client-layout encode (data [S][k][C] -> parity [p][S][C]) with the data
+    and parity bases at byte offsets: the launch runs the g8 / g4 / byte
+    kernels as the addresses allow, with the oracle's parity."""
+    k, p, S = 8, 2, 3
+    data = rand((S, k, C_), C_ + doff * 16 + poff)
+    d = ctx.alloc(data.nbytes + 64)
+    d.upload(data.reshape(-1), offset=doff)
+    pitch = S * C_ + 8
+    par = ctx.alloc(p * pitch + 64)
+    par.fill(0xEE)
+    try:
+        ctx.encode(k, p, C_, S, d.ptr + doff, k * C_, par.ptr + poff, pitch, C_)
+        ctx.sync()
+        expect_kernel(ecglib.last_kernel(), granule(doff, poff, k * C_, C_, pitch), k, p)
+        raw = par.download()
+        got = np.stack([raw[poff + r * pitch: poff + r * pitch + S * C_].reshape(S, C_) for r in range(p)])
+        assert np.array_equal(got, oracle_parity(oracle, k, p, data))
+        # nothing written between or after the rows
+        assert (raw[:poff] == 0xEE).all()
+        for r in range(p):
+            assert (raw[poff + r * pitch + S * C_: poff + (r + 1) * pitch] == 0xEE).all()
+    finally:
+        d.free()
+        par.free()
+
+
+@pytest.mark.parametrize("k,p", [(2, 1), (4, 2), (8, 3), (16, 2), (16, 3)])
+@pytest.mark.parametrize("off", [4, 8])
+def test_encode_classes_at_offset(ctx, oracle, ecglib, k, p, off):
+    """Every specialised (k, p) has g8 and g4 instantiations."""
+    S, C_ = 4, 8192 + 4096
+    data = rand((S, k, C_), k * 10 + p + off)
+    d = ctx.alloc(data.nbytes + 64)
+    d.upload(data.reshape(-1), offset=off)
+    par = ctx.alloc(p * S * C_ + 64)
+    try:
+        ctx.encode(k, p, C_, S, d.ptr + off, k * C_, par.ptr + off, S * C_, C_)
+        ctx.sync()
+        name = ecglib.last_kernel()
+        assert name.startswith(f"ecg_mm_kernel<{k},{p},") and name.endswith(f",g{off}>"), name
+        got = par.download(p * S * C_, offset=off).reshape(p, S, C_)
+        assert np.array_equal(got, oracle_parity(oracle, k, p, data))
+    finally:
+        d.free()
+        par.free()
+
+
+@pytest.mark.parametrize("off", [1, 4, 8, 12])
+@pytest.mark.parametrize("C_", [32768, 4096 * 5 + 8, 4096 + 12])
+@pytest.mark.parametrize("errs", [[0, 1], [3, 9], [8]])
+def test_recover_in_place_at_offset(ctx, oracle, ecglib, off, C_, errs):
+    """Degraded-read recovery in place in [S][k+p][C] at an image offset."""
+    k, p, S = 8, 2, 3
+    data = rand((S, k, C_), off + C_ + len(errs))
+    stripes = np.concatenate([data, oracle_parity(oracle, k, p, data).transpose(1, 0, 2)], axis=1)
+    broken = stripes.copy()
+    broken[:, errs] = 0x5A
+    d = ctx.alloc(stripes.nbytes + 64)
+    d.upload(broken.reshape(-1), offset=off)
+    try:
+        ctx.recover(k, p, C_, S, d.ptr + off, (k + p) * C_, errs)
+        ctx.sync()
+        expect_kernel(ecglib.last_kernel(), granule(off, (k + p) * C_, C_), k, len(errs))
+        got = d.download(stripes.nbytes, offset=off).reshape(S, k + p, C_)
+        assert np.array_equal(got, stripes)
+    finally:
+        d.free()
+
+
+@pytest.mark.parametrize("off", [1, 4, 8, 12])
+def test_update_at_offset(ctx, oracle, ecglib, off):
+    """Delta parity update (ACC + DIFF, the runtime-shaped kernel) with the
+    old/new cells and the parity at an offset."""
+    k, p, C_, S = 8, 2, 6000 + 8, 3
+    cells = [0, 5]
+    en = oracle.cauchy1(k, p)
+    data = rand((S, k, C_), 31 + off)
+    par = oracle_parity(oracle, k, p, data)
+    new = rand((S, len(cells), C_), 32 + off)
+    old = data[:, cells].copy()
+    dold, dnew, dpar = ctx.alloc(old.nbytes + 64), ctx.alloc(new.nbytes + 64), ctx.alloc(par.nbytes + 64)
+    dold.upload(old.reshape(-1), offset=off)
+    dnew.upload(new.reshape(-1), offset=off)
+    dpar.upload(par.reshape(-1), offset=off)
+    try:
+        ctx.update(k, p, C_, S, cells, dold.ptr + off, dnew.ptr + off, len(cells) * C_, dpar.ptr + off, S * C_, C_)
+        ctx.sync()
+        got = dpar.download(par.nbytes, offset=off).reshape(p, S, C_)
+        data[:, cells] = new
+        assert np.array_equal(got, oracle_parity(oracle, k, p, data))
+        name = ecglib.last_kernel()
+        g = granule(off, C_, len(cells) * C_, S * C_)
+        assert name == "ecg_mm_byte_kernel" if g == 1 else name.endswith(f",1,1,g{g}>"), name
+    finally:
+        for b in (dold, dnew, dpar):
+            b.free()
+
+
+@pytest.mark.parametrize("off", [4, 8])
+@pytest.mark.parametrize("k,rows", [(5, 4), (12, 6), (33, 2)])
+def test_generic_shapes_at_offset(ctx, oracle, ecglib, off, k, rows):
+    """Runtime-shaped kernels (and k > 16 split into accumulating launches)
+    at 4 / 8-byte aligned operands."""
+    S, C_ = 3, 4096 + 512
+    coef = rand((rows, k), 77 + k)
+    data = rand((S, k, C_), 78 + rows)
+    d = ctx.alloc(data.nbytes + 64)
+    d.upload(data.reshape(-1), offset=off)
+    out = ctx.alloc(S * rows * C_ + 64)
+    try:
+        ctx.matmul(coef, C_, S, d.ptr + off, [j * C_ for j in range(k)], k * C_, out.ptr + off,
+                   [r * C_ for r in range(rows)], rows * C_, 0)
+        ctx.sync()
+        assert ecglib.last_kernel().endswith(f",g{off}>"), ecglib.last_kernel()
+        got = out.download(S * rows * C_, offset=off).reshape(S, rows, C_)
+        for s in range(S):
+            assert np.array_equal(got[s], oracle.encode_data(coef, data[s]))
+    finally:
+        d.free()
+        out.free()

@@ -64,32 +64,51 @@ def test_csum_parity(oracle, ecglib, ctx, htype, geom):
     assert np.array_equal(got, want), np.argwhere(got != want)[:5]
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3])
+SHAPE_GEOMS = GEOMS + [(1 << 20, 1, 0, 3 << 20), ((1 << 20) + 4096, 1, 5, 2 << 20),
+                       (65536, 16, 0, 70001), (2048, 1, 0, 100000),
+                       (4096, 1, 0, 4096 * 7 + 16 * 5), (8192, 8, 0, 3001),
+                       # step counts that are not multiples of the 4-piece Horner
+                       # step (zero prefix) in every shape
+                       ((1 << 20) + 5120 + 48, 1, 3, 3 << 20), (1040, 1, 0, 1040 * 9 + 7),
+                       (5 * 4096 + 1024, 1, 0, 7 * (5 * 4096 + 1024) - 16)]
+
+
+def _shape(cs, rb, nch, n_ext):
+    """The kernel shape ecg_csum_extents picks (ecg_csum.c): a workgroup per
+    chunk for fewer than 4096 chunks of >= 16 steps, a 16-lane group per
+    chunk of <= 8 steps, else a wave per chunk."""
+    rcs = cs - cs % rb if rb <= cs else rb
+    steps = (rcs // 16 + 63) // 64
+    if n_ext * nch < 4096 and steps >= 16:
+        return "split"
+    return "group" if steps <= 8 else "wave"
+
+
+@pytest.mark.parametrize("many", [False, True])
 @pytest.mark.parametrize("htype", (1, 2, 3, 7))
-@pytest.mark.parametrize("geom", GEOMS + [(1 << 20, 1, 0, 3 << 20), ((1 << 20) + 4096, 1, 5, 2 << 20),
-                                          (65536, 16, 0, 70001), (2048, 1, 0, 100000),
-                                          (4096, 1, 0, 4096 * 7 + 16 * 5), (8192, 8, 0, 3001)])
-def test_crc_kernel_shapes(oracle, ecglib, ctx, variant, htype, geom):
-    """Every kernel shape on every geometry: a wave per chunk (1), a
-    workgroup per chunk (2) -- CRC: the waves' slice CRCs shifted and
-    combined; adler32: the threads' position-weighted sums added; chunks
-    shorter than the workgroup's slices leave waves idle -- and, for CRC, a
-    16-lane group per chunk (3; 4 chunks per wave, the wave's last groups
-    idle past the final chunk)."""
+@pytest.mark.parametrize("geom", SHAPE_GEOMS)
+def test_crc_kernel_shapes(oracle, ecglib, ctx, many, htype, geom):
+    """Every kernel shape the geometry selects: a workgroup per chunk (few
+    long chunks -- CRC: the waves' slice CRCs shifted and combined; adler32:
+    the threads' position-weighted sums added; chunks shorter than the
+    workgroup's slices leave waves idle), a 16-lane group per short chunk
+    (4 chunks per wave, the wave's last groups idle past the final chunk),
+    and a wave per chunk.  `many` repeats the extent (stride 0) until there
+    are >= 4096 chunks, which turns the workgroup shape into the wave shape."""
     cs, rb, idx, nr = geom
     L = ecglib.lib()
     rng = np.random.default_rng((hash(geom) + htype) & 0xFFFFFFFF)
     host = rng.integers(0, 256, rb * nr, dtype=np.uint8)
-    assert L.ecg_set_csum_variant(ctx.h, variant) == 0
-    try:
-        got = _dev_csum(ecglib, ctx, htype, cs, rb, idx, nr, host)
-        kern = L.ecg_last_kernel().decode()
-    finally:
-        L.ecg_set_csum_variant(ctx.h, 0)
+    nch = L.ecg_csum_chunk_count(cs, rb, idx, nr)
+    n_ext = -(-4096 // nch) if many else 1
+    got = _dev_csum(ecglib, ctx, htype, cs, rb, idx, nr, host, ext_stride=0, n_ext=n_ext)
+    kern = L.ecg_last_kernel().decode()
     if "bytes" not in kern:
-        assert ("split" in kern) == (variant == 2), kern
-        assert ("group" in kern) == (variant == 3 and htype != 7), kern
-    assert np.array_equal(got, oracle.csum_extents(htype, cs, rb, idx, nr, host))
+        want_shape = _shape(cs, rb, nch, n_ext)
+        assert ("split" in kern) == (want_shape == "split"), kern
+        assert ("group" in kern) == (want_shape == "group" and htype != 7), kern
+    want = oracle.csum_extents(htype, cs, rb, idx, nr, host)
+    assert np.array_equal(got, np.tile(want, (n_ext, 1)))
 
 
 @pytest.mark.parametrize("htype", TYPES)
@@ -187,12 +206,10 @@ FUSED = [
 ]
 
 
-@pytest.mark.parametrize("wave", [0, 128])
 @pytest.mark.parametrize("case", FUSED)
-def test_encode_csum_fused(oracle, ecglib, ctx, case, wave):
+def test_encode_csum_fused(oracle, ecglib, ctx, case):
     k, p, C, S, cs, rb, htype = case
     L = ecglib.lib()
-    assert L.ecg_set_csum_variant(ctx.h, wave) == 0
     nch = L.ecg_csum_chunk_count(cs, rb, 0, C // rb)
     cl = L.ecg_csum_len(htype)
     rng = np.random.default_rng(sum(case))
@@ -211,7 +228,6 @@ def test_encode_csum_fused(oracle, ecglib, ctx, case, wave):
         want = _want_cell_csums(oracle, htype, cs, rb, want_par).reshape(p, S, nch)
         assert np.array_equal(got, want), np.argwhere(got != want)[:5]
     finally:
-        L.ecg_set_csum_variant(ctx.h, 0)
         d.free(); par.free(); out.free()
 
 
@@ -256,11 +272,9 @@ def test_encode_csum_fused_items(oracle, ecglib, ctx, case, cols):
 
 @pytest.mark.parametrize("errs", [[3, 9], [9, 3], [8, 9], [0], [0, 1], [5]])
 @pytest.mark.parametrize("htype", (2, 3))
-@pytest.mark.parametrize("wave", [0, 128])
-def test_recover_csum_fused(oracle, ecglib, ctx, errs, htype, wave):
+def test_recover_csum_fused(oracle, ecglib, ctx, errs, htype):
     k, p, C, S, cs = 8, 2, 256 << 10, 6, 32768
     L = ecglib.lib()
-    assert L.ecg_set_csum_variant(ctx.h, wave) == 0
     nch = C // cs
     cl = L.ecg_csum_len(htype)
     rng = np.random.default_rng(len(errs) * 10 + htype)
@@ -284,7 +298,6 @@ def test_recover_csum_fused(oracle, ecglib, ctx, errs, htype, wave):
             want = _want_cell_csums(oracle, htype, cs, 1, stripes[:, e])
             assert np.array_equal(got[i], want), (e, i)
     finally:
-        L.ecg_set_csum_variant(ctx.h, 0)
         d.free(); out.free()
 
 
@@ -352,112 +365,19 @@ def test_encode_csum_misaligned_csums(oracle, ecglib, ctx):
         d.free(); par.free(); out.free()
 
 
-@pytest.mark.parametrize("kind", [16, 32])          # byte tables / 5-bit tables forced
-@pytest.mark.parametrize("shape", [1, 2, 3])
-@pytest.mark.parametrize("htype", (1, 2, 3))
-@pytest.mark.parametrize("geom", [(32768, 1, 0, 200000), (4096, 1, 0, 4096 * 7 + 16 * 5),
-                                  ((1 << 20) + 4096, 1, 5, 2 << 20),
-                                  # step counts that are not multiples of the 5-bit path's
-                                  # 4-piece Horner step (zero prefix) in every shape
-                                  ((1 << 20) + 5120 + 48, 1, 3, 3 << 20), (1040, 1, 0, 1040 * 9 + 7),
-                                  (5 * 4096 + 1024, 1, 0, 7 * (5 * 4096 + 1024) - 16)])
-def test_crc_table_kinds(oracle, ecglib, ctx, kind, shape, htype, geom):
-    """Both CRC table kinds (conflict-free 5-bit tables, byte tables; the
-    default picks per hash) give the oracle's checksums on every kernel shape."""
-    cs, rb, idx, nr = geom
-    L = ecglib.lib()
-    host = np.random.default_rng(kind + shape + htype).integers(0, 256, rb * nr, dtype=np.uint8)
-    assert L.ecg_set_csum_variant(ctx.h, kind | shape) == 0
-    try:
-        got = _dev_csum(ecglib, ctx, htype, cs, rb, idx, nr, host)
-    finally:
-        L.ecg_set_csum_variant(ctx.h, 0)
-    assert np.array_equal(got, oracle.csum_extents(htype, cs, rb, idx, nr, host))
-
-
-@pytest.mark.parametrize("kind", [16, 32, 64, 128, 144, 160])   # fused TB 1 / 0 / 2; wave kernel
-@pytest.mark.parametrize("case", [(8, 2, 1 << 20, 3, 32768, 2), (8, 2, 1 << 20, 3, 32768, 3),
-                                  (4, 2, 256 << 10, 5, 32768, 2), (4, 2, 256 << 10, 5, 32768, 3),
-                                  (8, 1, 3 * 65536 + 48, 4, 65536, 2)])
-def test_encode_csum_fused_table_kinds(oracle, ecglib, ctx, kind, case):
-    """Every fused-kernel table kind (5-bit, slice-by-NB, s16) writes the
-    oracle's parity and checksums; a kind a shape does not instantiate runs
-    the two-pass path (product, then the checksum kernel) with the same
-    results."""
-    k, p, C, S, cs, htype = case
-    L = ecglib.lib()
-    nch = L.ecg_csum_chunk_count(cs, 1, 0, C)
-    cl = L.ecg_csum_len(htype)
-    data = np.random.default_rng(sum(case) + kind).integers(0, 256, S * k * C, dtype=np.uint8)
-    d = ctx.to_device(data)
-    par = ctx.alloc(p * S * C)
-    out = ctx.alloc(p * S * nch * cl)
-    assert L.ecg_set_csum_variant(ctx.h, kind) == 0
-    try:
-        ctx.encode_csum(k, p, C, S, d.ptr, k * C, par.ptr, S * C, C, htype, cs, 1, out.ptr)
-        ctx.sync()
-        want_par = oracle.encode_batch(k, p, C, S, data, nthreads=8, simd=True).reshape(p, S, C)
-        assert np.array_equal(par.download().reshape(p, S, C), want_par)
-        got = out.download().view(DT[cl]).reshape(p, S, nch)
-        want = _want_cell_csums(oracle, htype, cs, 1, want_par).reshape(p, S, nch)
-        assert np.array_equal(got, want), np.argwhere(got != want)[:5]
-    finally:
-        L.ecg_set_csum_variant(ctx.h, 0)
-        d.free(); par.free(); out.free()
-
-
-TB3 = [  # (k, p, htype): the fused kernels' s16 + SDWA + nibble-shift instantiations (csum_variant bit 9)
-    (8, 2, 2), (8, 2, 3), (4, 2, 2), (4, 2, 3), (8, 1, 2), (16, 2, 2), (8, 3, 2), (4, 1, 2), (16, 1, 2),
+DEFAULT_KINDS = [  # (k, p, htype): each fused instantiation's table kind (ecg_fused_kernels.hip CS_TB)
+    (8, 2, 2), (8, 2, 3), (8, 2, 1), (4, 2, 2), (4, 2, 3), (8, 1, 2), (8, 1, 3), (16, 2, 2), (16, 2, 3),
+    (8, 3, 2), (8, 3, 3), (4, 1, 2), (16, 1, 2), (2, 2, 3),
 ]
 
 
-@pytest.mark.parametrize("shape", [256, 0])          # workgroups over work items / the default shape
-@pytest.mark.parametrize("case", TB3)
-def test_encode_csum_tb3_tables(oracle, ecglib, ctx, case, shape):
-    """The TB 3 table kind (s16 byte tables addressed by SDWA byte selects,
-    column shift by nibble a4 tables) gives the oracle's parity and chunk
-    checksums -- ragged last chunk and 16-byte tail of the cell included."""
-    k, p, htype = case
-    C, S, cs = 3 * 32768 + 4096 + 16, 3, 32768
-    L = ecglib.lib()
-    nch = L.ecg_csum_chunk_count(cs, 1, 0, C)
-    cl = L.ecg_csum_len(htype)
-    rng = np.random.default_rng(k * 10 + p + htype)
-    data = rng.integers(0, 256, S * k * C, dtype=np.uint8)
-    d = ctx.to_device(data)
-    par = ctx.alloc(p * S * C)
-    out = ctx.alloc(p * S * nch * cl)
-    try:
-        var = 512 | shape
-        if htype == 3 and k <= 4:
-            var |= 256                                   # crc64 k <= 4 defaults to the wave kernel
-        assert L.ecg_set_csum_variant(ctx.h, var) == 0
-        ctx.encode_csum(k, p, C, S, d.ptr, k * C, par.ptr, S * C, C, htype, cs, 1, out.ptr)
-        ctx.sync()
-        assert L.ecg_last_kernel().decode().endswith(",tb3>"), L.ecg_last_kernel()
-        want_par = oracle.encode_batch(k, p, C, S, data, nthreads=8, simd=True).reshape(p, S, C)
-        assert np.array_equal(par.download().reshape(p, S, C), want_par)
-        got = out.download().view(DT[cl]).reshape(p, S, nch)
-        want = _want_cell_csums(oracle, htype, cs, 1, want_par).reshape(p, S, nch)
-        assert np.array_equal(got, want), np.argwhere(got != want)[:5]
-    finally:
-        L.ecg_set_csum_variant(ctx.h, 0)
-        d.free(); par.free(); out.free()
-
-
-TB4 = [  # (k, p, htype): the fused workgroup kernel's positional nibble instantiations (csum_variant bit 10)
-    (8, 2, 2), (8, 2, 3), (4, 2, 2), (4, 2, 3), (8, 1, 2), (8, 1, 3), (16, 2, 2), (16, 2, 3), (8, 3, 2), (8, 3, 3),
-]
-
-
-@pytest.mark.parametrize("cols", [0, 3, 8])        # 4-column items (the unrolled walk) / other items (the shift)
-@pytest.mark.parametrize("case", TB4)
-def test_encode_csum_tb4_tables(oracle, ecglib, ctx, case, cols):
-    """The TB 4 table kind (nibble tables of 4 column positions, one SDWA
-    address per lookup; items of exactly 4 full columns unrolled with constant
-    positions, other items Horner-folded with the nibble column shift) gives the
+@pytest.mark.parametrize("cols", [0, 3, 8])        # the default split of a chunk into work items / others
+@pytest.mark.parametrize("case", DEFAULT_KINDS)
+def test_encode_csum_fused_kinds(oracle, ecglib, ctx, case, cols):
+    """Every fused instantiation with its table kind (the byte tables for
+    crc64 and for crc32 at EC_8P2, the 5-bit tables elsewhere) gives the
     oracle's parity and chunk checksums -- ragged last chunk and 16-byte tail
-    of the cell included."""
+    of the cell included, items of the default and of other column counts."""
     k, p, htype = case
     C, S, cs = 3 * 32768 + 4096 + 16, 3, 32768
     L = ecglib.lib()
@@ -469,17 +389,15 @@ def test_encode_csum_tb4_tables(oracle, ecglib, ctx, case, cols):
     par = ctx.alloc(p * S * C)
     out = ctx.alloc(p * S * nch * cl)
     try:
-        assert L.ecg_set_csum_variant(ctx.h, 1024) == 0
         assert L.ecg_set_fused_cols(ctx.h, cols) == 0
         ctx.encode_csum(k, p, C, S, d.ptr, k * C, par.ptr, S * C, C, htype, cs, 1, out.ptr)
         ctx.sync()
-        assert L.ecg_last_kernel().decode().endswith(",tb4>"), L.ecg_last_kernel()
+        assert L.ecg_last_kernel().decode().startswith(f"ecg_mm_csum_kernel<{k},{p},"), L.ecg_last_kernel()
         want_par = oracle.encode_batch(k, p, C, S, data, nthreads=8, simd=True).reshape(p, S, C)
         assert np.array_equal(par.download().reshape(p, S, C), want_par)
         got = out.download().view(DT[cl]).reshape(p, S, nch)
         want = _want_cell_csums(oracle, htype, cs, 1, want_par).reshape(p, S, nch)
         assert np.array_equal(got, want), np.argwhere(got != want)[:5]
     finally:
-        L.ecg_set_csum_variant(ctx.h, 0)
         L.ecg_set_fused_cols(ctx.h, 0)
         d.free(); par.free(); out.free()

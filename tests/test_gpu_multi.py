@@ -197,6 +197,38 @@ def test_queue_updates_of_one_stripe_no_flush(ecglib, ctx, oracle):
     m.close()
 
 
+def test_queue_updates_overlapping_parity_ranges(ecglib, ctx, oracle):
+    """Updates whose parity cells overlap through DIFFERENT pointers into one
+    buffer (views at offsets of half a cell): the queue's locks
+    are striped over address regions, not keyed on the cell pointer, so every
+    delta lands.  Each update's parity rows are views into one shared buffer at
+    a per-request offset; the expected buffer is the XOR of every update's
+    delta at its offset."""
+    m = ecglib.Multi([0, 0])
+    q = ecglib.Queue(m, max_batch=4, max_wait_us=200)
+    k, p, C_ = 4, 2, 96 << 10
+    en = oracle.cauchy1(k, p)
+    NREQ = 24
+    buf = [rand(C_ * 4, 900 + r) for r in range(p)]          # one buffer per parity row
+    want = [b.copy() for b in buf]
+    rng = np.random.default_rng(5)
+    for rid in range(NREQ):
+        off = int(rng.integers(0, 6)) * (C_ // 2)             # overlapping windows of the buffers
+        j = rid % k
+        old, new = rand(C_, 2000 + rid), rand(C_, 3000 + rid)
+        views = [b[off:off + C_] for b in buf]
+        q.update(rid, k, p, j, old, new, views)
+        delta = oracle.encode_data_update(en[k:], j, old ^ new, np.zeros((p, C_), dtype=np.uint8))
+        for r in range(p):
+            want[r][off:off + C_] ^= delta[r]
+    q.flush()
+    assert all(rc == 0 for rc in q.done.values()) and len(q.done) == NREQ
+    for r in range(p):
+        assert np.array_equal(buf[r], want[r]), r
+    q.close()
+    m.close()
+
+
 def test_isal_dropin_over_device_list(oracle):
     """ECG_DEVICES=0,0,0 gives the synchronous ISA-L drop-in three contexts;
     threads are spread over them and every call stays bit-exact."""

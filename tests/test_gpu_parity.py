@@ -1,9 +1,11 @@
 """GPU parity tests: the HIP path (through the C-ABI) vs the CPU oracle.
 
-Bit-exact for every byte (integer GF(2^8) work).  Small sizes compare every
-output byte with the oracle; the BASELINE.json full-size configs are covered
-by size-independent properties (encode -> erase -> recover round trips,
-sampled stripes against the oracle).
+Bit-exact for every byte (integer GF(2^8) work): every case here compares
+every output byte with the oracle, at sizes the oracle finishes in seconds.
+The BASELINE.json configs are byte-compared at their full sizes in
+tests/test_gpu_configs.py (every parity byte and every recovered byte of
+configs 1-4, the rebuild-stream shape of config 5), and the product kernels'
+operand alignments (16 / 8 / 4 / 1 bytes) in tests/test_gpu_align.py.
 """
 import ctypes as C
 import itertools

@@ -144,3 +144,72 @@ def test_autotune_off_and_explicit_cap_skip_tuning(ctx):
         ctx.set_autotune(1)
         d.free()
         par.free()
+
+
+def test_autotune_varying_batches_one_probe(ctx, oracle):
+    """Batches of varying size (a queue's flushes, a rebuild's last batch,
+    per-shard counts) are one tuner shape: ten batch sizes of an EC_16P2
+    encode run ONE probe cycle (23 probing launches), not ten, and every
+    output -- probing or decided -- equals the oracle's."""
+    k, p, C_ = 16, 2, 65536                    # 16 columns per stripe
+    sizes = [130, 200, 131, 257, 140, 190, 300, 150, 170, 222] * 3   # 2080..4800 blocks (> 2048: tuned)
+    en = oracle.cauchy1(k, p)
+    data = rand((max(sizes), k, C_), 808)
+    want = np.stack([oracle.encode_data(en[k:], data[s]) for s in range(max(sizes))], axis=1)   # [p][S][C]
+    ctx.set_autotune(2)
+    try:
+        d = ctx.to_device(data)
+        par = ctx.alloc(p * max(sizes) * C_)
+        for i, S in enumerate(sizes):
+            par.fill(0)
+            ctx.encode(k, p, C_, S, d.ptr, k * C_, par.ptr, S * C_, C_)
+            ctx.sync()
+            got = par.download(p * S * C_).reshape(p, S, C_)
+            assert np.array_equal(got, want[:, :S]), (i, S)
+        cycles, launches, shapes = ctx.tune_counters()
+        assert cycles == 1 and shapes == 1, (cycles, launches, shapes)
+        assert launches == PROBE, launches
+        st = ctx.tune_state(k, p, C_, sizes[0], k * C_, C_)
+        assert st is not None and st[0] in (2, 255)
+        # the in-place recovery layout is a second shape, tuned on its own
+        img = np.concatenate([data[:150], want[:, :150].transpose(1, 0, 2)], axis=1)
+        stb = ctx.to_device(img)
+        for _ in range(3):
+            ctx.recover(k, p, C_, 150, stb.ptr, (k + p) * C_, [0, 1])
+        ctx.sync()
+        assert np.array_equal(stb.download().reshape(150, k + p, C_), img)
+        assert ctx.tune_counters()[0] == 2
+        for b in (d, par, stb):
+            b.free()
+    finally:
+        ctx.set_autotune(1)
+
+
+def test_autotune_probe_other_stream_not_timed(ctx, ecglib, oracle):
+    """Launches of a probing shape from another stream run uncapped and do not
+    count toward the probe (their events would time other work)."""
+    k, p, S, C_ = 16, 2, 300, 32768
+    data = rand((S, k, C_), 1602)
+    en = oracle.cauchy1(k, p)
+    want = np.stack([oracle.encode_data(en[k:], data[s]) for s in range(S)], axis=1)
+    ctx.set_autotune(2)
+    st2 = ctx.stream()
+    try:
+        d = ctx.to_device(data)
+        par = ctx.alloc(p * S * C_)
+        ctx.encode(k, p, C_, S, d.ptr, k * C_, par.ptr, S * C_, C_)          # starts the probe (default stream)
+        for _ in range(5):
+            ctx.encode(k, p, C_, S, d.ptr, k * C_, par.ptr, S * C_, C_, stream=st2)
+        ctx.sync()
+        assert ctx.tune_counters()[1] == 1
+        for _ in range(PROBE + 1):
+            ctx.encode(k, p, C_, S, d.ptr, k * C_, par.ptr, S * C_, C_)
+        ctx.sync()
+        assert ctx.tune_counters()[1] == PROBE
+        assert ctx.tune_state(k, p, C_, S, k * C_, C_) is not None
+        assert np.array_equal(par.download().reshape(p, S, C_), want)
+        d.free()
+        par.free()
+    finally:
+        ctx.destroy_stream(st2)
+        ctx.set_autotune(1)

@@ -44,17 +44,6 @@ def main():
                 res[f"{NAMES[htype]}_cs{cs >> 10}K_b{blocks}"] = {
                     "ms": round(ms, 4), "GBps": round(C * n / ms / 1e6, 1), "kernel": L.ecg_last_kernel().decode()}
         L.ecg_set_csum_launch(ctx.h, 0)
-    # CRC kernel shape: a wave per chunk (1) vs a workgroup per chunk (2), auto (0)
-    for htype in (1, 2, 3):
-        for cs in (32768, 131072, 1 << 20):
-            row = {}
-            for var in (1, 2, 0):
-                L.ecg_set_csum_variant(ctx.h, var)
-                ms = timed(lambda: ctx.csum_extents(htype, cs, 1, 0, C, buf.ptr, C, n, out.ptr))
-                row[f"v{var}_GBps"] = round(C * n / ms / 1e6, 1)
-                row[f"v{var}_kernel"] = L.ecg_last_kernel().decode()
-            res[f"shape_{NAMES[htype]}_cs{cs >> 10}K"] = row
-    L.ecg_set_csum_variant(ctx.h, 0)
     # rebuild pattern: encode alone / encode then checksum launches / fused
     for (k, p, C2, S, tag) in ((8, 2, 1 << 20, 256, "8p2_1M"), (4, 2, 1 << 20, 512, "4p2_1M"),
                                (16, 2, 128 << 10, 1024, "16p2_128K")):

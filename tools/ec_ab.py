@@ -1,0 +1,103 @@
+"""A/B of product-kernel builds (tools/build_exp.sh) on the device-resident
+EC shapes, timed as bench.py times its detail rows: launches back to back on
+one stream with an event at every boundary (no host wait between launches),
+the median of 30 after 40 warm-up launches.  One subprocess per library and
+round, libraries rotated every round (the box's clocks drift over a run).
+The launch tuner is off (ECG_AUTOTUNE=0); every shape is timed uncapped and
+at its candidate blocks-per-CU cap (k = 16: 2, k = 8: 3).
+usage: python tools/ec_ab.py NAME=lib.so ... -> gpurun_out/ec_ab.json.
+Bench infrastructure."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r'''
+import json, os, sys
+sys.path.insert(0, %r)
+from daos_amd import ecg
+ecg.LIB_PATH = sys.argv[1]
+ctx = ecg.Context(0)
+MiB = 1 << 20
+
+def timed(fn, iters=30, warm=40):
+    for _ in range(warm):
+        fn()
+    ctx.sync()
+    evs = [ctx.event() for _ in range(iters + 1)]
+    ctx.record(evs[0])
+    for i in range(iters):
+        fn()
+        ctx.record(evs[i + 1])
+    ms = sorted(ctx.elapsed_ms(evs[i], evs[i + 1]) for i in range(iters))
+    for e in evs:
+        ctx.destroy_event(e)
+    return ms[iters // 2]
+
+res = {}
+for k, p, C, S, op, off in ((16, 2, 128 << 10, 1024, "enc", 0), (16, 2, 128 << 10, 1024, "dec", 0),
+                            (16, 2, 128 << 10, 4096, "enc", 0), (8, 2, MiB, 512, "enc", 0),
+                            (8, 2, MiB, 512, "dec", 0), (4, 2, MiB, 1024, "enc", 0), (4, 2, MiB, 1024, "dec", 0),
+                            (8, 2, MiB, 512, "enc", 8), (8, 2, MiB, 512, "enc", 4)):
+    if op == "enc":
+        data = ctx.alloc(S * k * C + 64)
+        pitch = S * C + 4096
+        par = ctx.alloc(p * pitch + 64)
+        data.fill(0x3C)
+        fn = lambda: ctx.encode(k, p, C, S, data.ptr, k * C, par.ptr + off, pitch, C)
+        bufs = (data, par)
+        rows = p
+    else:
+        img = ctx.alloc(S * (k + p) * C)
+        img.fill(0x3C)
+        fn = lambda: ctx.recover(k, p, C, S, img.ptr, (k + p) * C, [0, 1])
+        bufs = (img,)
+        rows = 2
+    alg = (k + rows) * C * S
+    for cap in ((255, 2) if k >= 16 else (255, 3) if k >= 8 else (255,)):
+        if off and cap != 255:
+            continue
+        ctx.set_wg_per_cu(cap)
+        ms = timed(fn)
+        tag = "EC_%%dP%%d_%%dK_x%%d_%%s%%s_cap%%s" %% (k, p, C >> 10, S, op, "_off%%d" %% off if off else "", cap if cap != 255 else "none")
+        res[tag] = {"ms": round(ms, 4), "GBps": round(alg / ms / 1e6, 1), "kernel": ecg.last_kernel()}
+    ctx.set_wg_per_cu(0)
+    for b in bufs:
+        b.free()
+print(json.dumps(res))
+''' % ROOT
+
+
+def main():
+    libs = [a.split("=", 1) for a in sys.argv[1:]]
+    rounds = int(os.environ.get("EC_ROUNDS", "3"))
+    out = {name: [] for name, _ in libs}
+    env = dict(os.environ, ECG_AUTOTUNE="0")
+    for rnd in range(rounds):
+        order = libs[rnd % len(libs):] + libs[:rnd % len(libs)]
+        for name, lib in order:
+            r = subprocess.run([sys.executable, "-c", CHILD, os.path.abspath(lib)], capture_output=True, text=True,
+                               timeout=300, env=env)
+            if r.returncode != 0:
+                print(r.stdout, r.stderr, flush=True)
+                raise SystemExit(r.returncode)
+            row = json.loads(r.stdout.strip().splitlines()[-1])
+            out[name].append(row)
+            print(name, rnd, json.dumps({k: v["ms"] for k, v in row.items()}), flush=True)
+    summary = {}
+    for name, rows in out.items():
+        for tag in rows[0]:
+            ms = sorted(r[tag]["ms"] for r in rows)
+            summary.setdefault(tag, {})[name] = {"ms_median": ms[len(ms) // 2], "ms_all": ms,
+                                                 "kernel": rows[0][tag]["kernel"]}
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "ec_ab.json"), "w") as f:
+        json.dump({"runs": out, "summary": summary}, f, indent=1)
+    for tag, per in summary.items():
+        print(tag, {n: v["ms_median"] for n, v in per.items()})
+
+
+if __name__ == "__main__":
+    main()
