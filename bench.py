@@ -598,30 +598,34 @@ DETAIL_SHAPES = (("EC_8P2_1MiB_encode", 8, 2, 1 << 20, 512, "enc"),
 
 
 def offset_rows(ctx, aligned, iters=11):
-    """EC_8P2 1 MiB client-layout encode with the parity rows at a byte offset
-    of their allocation (DAOS rounds parity rows to 8 bytes only,
+    """EC_8P2 1 MiB client-layout encode with operands at a byte offset of
+    their allocation (DAOS rounds parity rows to 8 bytes only,
     ref:src/object/cli_ec.c:86; user cells carry no alignment,
-    ref:src/object/cli_ec.c:510-536): +8 runs the dwordx2-lane kernel, +4 the
-    dword-lane kernel, +1 the byte kernel (on 32 stripes: it is ~50x slower).
-    Each row's `of_aligned` = aligned ms / this ms."""
+    ref:src/object/cli_ec.c:510-536): parity rows at +8 run the dwordx2-lane
+    kernel, at +4 the dword-lane kernel; data cells at +1 (parity aligned) the
+    funnel-shift kernel; parity rows at +1 the byte kernel (on 32 stripes:
+    it is ~8x slower).  Each 512-stripe row's `of_aligned` = the aligned
+    row's ms / this ms."""
     from daos_amd import ecg
 
     k, p, C = 8, 2, 1 << 20
     rows = {}
-    for off, S, warm in ((8, 512, 40), (4, 512, 40), (1, 32, 2)):
-        data = ctx.alloc(S * k * C)
+    for what, off, S, warm in (("parity", 8, 512, 40), ("parity", 4, 512, 40), ("data", 1, 512, 40),
+                               ("parity", 1, 32, 2)):
+        data = ctx.alloc(S * k * C + 64)
         fill_device(ctx, data, S * k * C, 7)
         pitch = S * C + PARITY_ROW_PAD
         par = ctx.alloc(p * pitch + 64)
-        ms = time_kernel(ctx, lambda: ctx.encode(k, p, C, S, data.ptr, k * C, par.ptr + off, pitch, C), iters,
-                         warm=warm)
+        doff, poff = (off, 0) if what == "data" else (0, off)
+        ms = time_kernel(ctx, lambda: ctx.encode(k, p, C, S, data.ptr + doff, k * C, par.ptr + poff, pitch, C),
+                         iters, warm=warm)
         alg = (k + p) * C * S
-        row = {"parity_offset_bytes": off, "stripes": S, "ms": round(ms, 4),
+        row = {f"{what}_offset_bytes": off, "stripes": S, "ms": round(ms, 4),
                "GiBps_user": round(k * C * S / (ms / 1e3) / GIB, 1), "alg_GBps": round(alg / ms / 1e6, 1),
                "roofline_frac": round(alg / ms / 1e6 / HBM_PEAK_GBS, 4), "kernel": ecg.last_kernel()}
         if aligned and S == 512:
             row["of_aligned"] = round(aligned["ms"] / ms, 4)
-        rows[f"EC_8P2_1MiB_encode_parity_off{off}"] = row
+        rows[f"EC_8P2_1MiB_encode_{what}_off{off}"] = row
         data.free()
         par.free()
     return rows

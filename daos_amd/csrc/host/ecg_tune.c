@@ -66,7 +66,7 @@ struct ecg_tune_ent {
 	uint64_t stamp;
 	hipEvent_t ev[2][ECG_TUNE_T][2];
 	uint64_t blocks[2][ECG_TUNE_T];	/* blocks of each timed launch */
-	float ms[2];		/* decided: median per arm, scaled to the last timed launch */
+	float msb[2];		/* decided: median ms per block of each arm */
 };
 
 struct ecg_tuner {
@@ -227,7 +227,6 @@ static float median3(float a, float b, float c)
 static int try_decide(struct ecg_tune_ent *e)
 {
 	float per[2][ECG_TUNE_T], ms;
-	uint64_t ref = e->blocks[1][ECG_TUNE_T - 1];
 	int a, i, bad = 0;
 
 	for (a = 0; a < 2; a++)
@@ -249,14 +248,14 @@ static int try_decide(struct ecg_tune_ent *e)
 		}
 		e->decided = 1;
 		e->choice = ECG_WG_UNCAPPED;
-		e->ms[0] = e->ms[1] = 0.0f;
+		e->msb[0] = e->msb[1] = 0.0f;
 		return 1;
 	}
 	for (a = 0; a < 2; a++)
-		e->ms[a] = median3(per[a][0], per[a][1], per[a][2]) * (float)ref;
+		e->msb[a] = median3(per[a][0], per[a][1], per[a][2]);
 	e->decided = 1;
 	e->choice = ECG_WG_UNCAPPED;
-	if (e->ms[1] < e->ms[0] * (1.0f - (float)ECG_TUNE_MARGIN))
+	if (e->msb[1] < e->msb[0] * (1.0f - (float)ECG_TUNE_MARGIN))
 		e->choice = e->cand;
 	return 1;
 }
@@ -294,7 +293,7 @@ int ecg_tune_launch(ecg_ctx_t *ctx, const ecg_mm_params_t *p, hipStream_t st, ui
 	    cfg.grid_x != 0 || cfg.grid_y != 0)
 		return ecg_k_launch_matmul(p, &ctx->cfg, (void *)st, kid);
 	g = ecg_k_align_granule(p);
-	if (g == 1)			/* the byte kernel has no blocks-per-CU geometry */
+	if (g == 0)			/* the byte kernel has no blocks-per-CU geometry */
 		return ecg_k_launch_matmul(p, &ctx->cfg, (void *)st, kid);
 	if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
 		return ecg_k_launch_matmul(p, &ctx->cfg, (void *)st, kid);
@@ -382,10 +381,11 @@ int ecg_tune_state(ecg_ctx_t *ctx, int k, int rows, uint64_t cell_bytes, uint32_
 	rc = e && e->decided ? 1 : 0;
 	if (cap)
 		*cap = e && e->decided ? e->choice : 0;
+	/* the arms' medians per block, scaled to a launch of nstripes */
 	if (ms_uncapped)
-		*ms_uncapped = e && e->decided ? e->ms[0] : 0.0f;
+		*ms_uncapped = e && e->decided ? e->msb[0] * (float)mm_blocks(p) : 0.0f;
 	if (ms_capped)
-		*ms_capped = e && e->decided ? e->ms[1] : 0.0f;
+		*ms_capped = e && e->decided ? e->msb[1] * (float)mm_blocks(p) : 0.0f;
 	pthread_mutex_unlock(&t->lock);
 	free(p);
 	return rc;

@@ -376,7 +376,7 @@ static const kentry g_kernels[] = {
 	KE(8, 1, 0, 0), KE(8, 2, 0, 0), KE(8, 3, 0, 0),
 	KE(16, 1, 0, 0), KE(16, 2, 0, 0), KE(16, 3, 0, 0),
 	KE(0, 0, 0, 0), KE(0, 0, 1, 0), KE(0, 0, 0, 1), KE(0, 0, 1, 1),
-	KEG_SET(8), KEG_SET(4),
+	KEG_SET(4), KEG_SET(1),
 };
 #define N_KERNELS ((uint32_t)(sizeof(g_kernels) / sizeof(g_kernels[0])))
 
@@ -494,10 +494,11 @@ extern "C" int ecg_k_launch_matmul(const ecg_mm_params_t *p, const ecg_launch_cf
 	if (p->nstripes == 0 || p->cell_bytes == 0 || p->rows == 0)
 		return (int)hipSuccess;
 
-	// the widest lane access every operand's alignment allows (16 / 8 / 4 B);
-	// byte-aligned operands take the byte kernel
+	// the widest lane access every operand's alignment allows (16 / 8 / 4 B;
+	// 1: sources at any byte, destinations dword-aligned); a destination off
+	// a dword boundary takes the byte kernel
 	const int g = (int)align_granule(p);
-	if (variant == 2 || g == 1) {
+	if (variant == 2 || g == 0) {
 		uint64_t total = p->cell_bytes * p->nstripes;
 		uint64_t blocks = (total + BLOCK - 1) / BLOCK;
 		if (blocks > 8192)

@@ -51,7 +51,8 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 template <int G>
 __device__ __forceinline__ uint32_t lane_off()
 {
-	return (threadIdx.x >> 6) * 1024u + (threadIdx.x & 63u) * (uint32_t)G;
+	constexpr uint32_t GL = G == 1 ? 4u : (uint32_t)G;	// G = 1: the dword layout
+	return (threadIdx.x >> 6) * 1024u + (threadIdx.x & 63u) * GL;
 }
 
 // byte offset of dword i of the lane's piece from lane_off<G>()
@@ -61,10 +62,19 @@ __device__ __forceinline__ uint32_t elem_off(int i)
 	return G == 16 ? 4u * i : G == 8 ? (uint32_t)(i >> 1) * 512u + (uint32_t)(i & 1) * 4u : (uint32_t)i * 256u;
 }
 
+// G = 1 (sources at any byte alignment, destinations dword-aligned): the
+// dword layout of G = 4 for the lanes and every store; a source dword at
+// byte address a is funnel-shifted out of the aligned dwords around it,
+// v_alignbyte_b32(hi, lo, a & 3).  hi holds byte a + 3, so it never leaves
+// the cell's pages; when a is aligned hi is read from lo's own address
+// (no branch: the shift is then 0).  m = a & 3 is wave-uniform per cell.
+
 template <int G>
 __device__ __forceinline__ u32x4 ld_g(const uint8_t *p)
 {
-	if constexpr (G == 16) {
+	if constexpr (G == 1) {
+		return ld_g<4>(p);	// destinations (ACC reads) are dword-aligned
+	} else if constexpr (G == 16) {
 		return ld_nt(p);
 	} else if constexpr (G == 8) {
 		const u32x2 a = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(p));
@@ -81,7 +91,9 @@ __device__ __forceinline__ u32x4 ld_g(const uint8_t *p)
 template <int G>
 __device__ __forceinline__ void st_g(uint8_t *p, u32x4 v)
 {
-	if constexpr (G == 16) {
+	if constexpr (G == 1) {
+		st_g<4>(p, v);
+	} else if constexpr (G == 16) {
 		st_nt(p, v);
 	} else if constexpr (G == 8) {
 		__builtin_nontemporal_store((u32x2){v[0], v[1]}, reinterpret_cast<u32x2 *>(p));
@@ -92,6 +104,43 @@ __device__ __forceinline__ void st_g(uint8_t *p, u32x4 v)
 		__builtin_nontemporal_store(v[1], q + 64);
 		__builtin_nontemporal_store(v[2], q + 128);
 		__builtin_nontemporal_store(v[3], q + 192);
+	}
+}
+
+// The lane's 4 dwords of a source cell at (wave-uniform) address `cell`.
+// G = 1: the cell's dwords at lane offsets lo + 256 i, funnel-shifted out of
+// the aligned dwords a_i (one load each, as G = 4) and the next aligned dword
+// b_i, which is lane l+1's a_i -- a DPP wave rotate, no second load -- except
+// for lane 63, whose b_i is lane 0's a_(i+1), and for b_3 of lane 63, the
+// aligned dword after the wave's 1 KiB (one wave-uniform load).  When the
+// cell is aligned (m = 0) the shift is 0 and b is never used; the uniform
+// load then reads the wave's own last dword, so nothing past the column is
+// ever read.
+template <int G>
+__device__ __forceinline__ u32x4 ld_src(const uint8_t *cell, uint32_t lo)
+{
+	if constexpr (G == 1) {
+		const uint32_t m = (uint32_t)(uintptr_t)cell & 3u;
+		const uint8_t *base = cell - m;
+		const u32x4 a = ld_g<4>(base + lo);
+		const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+		const uint32_t e = __builtin_nontemporal_load(
+			reinterpret_cast<const uint32_t *>(base + wv * 1024u + (m ? 1024u : 1020u)));
+		const bool last = (threadIdx.x & 63u) == 63u;
+		uint32_t r[4];
+		u32x4 x;
+
+#pragma unroll
+		for (int w = 0; w < 4; w++)	// lane l <- lane l+1 (wave_rol:1)
+			r[w] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a[w], 0x134, 0xf, 0xf, false);
+#pragma unroll
+		for (int w = 0; w < 4; w++) {
+			const uint32_t b = last ? (w < 3 ? r[w + 1] : e) : r[w];
+			x[w] = __builtin_amdgcn_alignbyte(b, a[w], m);
+		}
+		return x;
+	} else {
+		return ld_g<G>(cell + lo);
 	}
 }
 
@@ -134,11 +183,11 @@ __device__ __forceinline__ void mm_load(const ecg_mm_params_t &P, int k, uint32_
 		if (j < k) {
 			int64_t o = P.src_cell_off[j] + s_src;
 			asm volatile("" : "+s"(o));
-			x[j] = ld_g<G>(P.src + o + lo);
+			x[j] = ld_src<G>(P.src + o, lo);
 			if (DIFF) {
 				int64_t o2 = P.src2_cell_off[j] + s_src2;
 				asm volatile("" : "+s"(o2));
-				x[j] ^= ld_g<G>(P.src2 + o2 + lo);
+				x[j] ^= ld_src<G>(P.src2 + o2, lo);
 			}
 		}
 	}
@@ -164,14 +213,14 @@ __device__ __forceinline__ void mm_load_any(const ecg_mm_params_t &P, int k, uin
 // AGPRs at 1 wave per SIMD).  Measured (tools/ec_ab.py, profiles/r04/ec_ab/,
 // ms, back-to-back launches): k = 8 in 2 phases of 4 at 4 waves --
 // EC_8P2 1 MiB x 512 decode 0.873 -> 0.836 (the best capped geometry before:
-// 0.859), encode 0.844 -> 0.831; the 8-byte-lane (G = 8) variant lost 3 %,
-// so phases apply to G = 16 and 4 only.  k = 16 in phases of 4 lost 5-20 %
-// at 4 or 5 waves (phases of 8 spill).
+// 0.859), encode 0.844 -> 0.831, the dword-lane (G = 4) variant 0.895 ->
+// 0.887.  The funnel-shift kernels (G = 1) spill when phased.  k = 16 in
+// phases of 4 lost 5-20 % at 4 or 5 waves (phases of 8 spill).
 #ifndef ECG_MM_PHASE
-#define ECG_MM_PHASE(K, G) ((K) == 8 && (G) != 8 ? 4 : 0)
+#define ECG_MM_PHASE(K, G) ((K) == 8 && ((G) == 16 || (G) == 4) ? 4 : 0)
 #endif
 #ifndef ECG_MM_WPE
-#define ECG_MM_WPE(K, G) ((K) == 8 && (G) != 8 ? 4 : 0)
+#define ECG_MM_WPE(K, G) ((K) == 8 && ((G) == 16 || (G) == 4) ? 4 : 0)
 #endif
 
 // The product of one column: x[j] = the lane's 16 bytes of cell j.  STORE =
@@ -372,14 +421,17 @@ __device__ __forceinline__ void mm_partial(const ecg_mm_params_t &P, const u32x4
 		else if (cbase + lo < C)
 			mm_tail<RM, ACC, DIFF>(P, tb, k, rows, s, cbase + lo, (int)(C - cbase - lo));
 	} else {
-#pragma unroll
+		// not unrolled: four inlined copies of the byte loop cost ~70 VGPRs
+		// in every instantiation (this path runs once per cell at most)
+#pragma nounroll
 		for (int i = 0; i < 4; i++) {
 			const uint64_t off = cbase + lo + elem_off<G>(i);
 
-			if (off + 4 <= C)
+			// G = 1: the sources are not dword-aligned, so bytewise
+			if (G != 1 && off + 4 <= C)
 				mm_dword<RM, ACC, DIFF>(P, tb, k, rows, s, off);
 			else if (off < C)
-				mm_tail<RM, ACC, DIFF>(P, tb, k, rows, s, off, (int)(C - off));
+				mm_tail<RM, ACC, DIFF>(P, tb, k, rows, s, off, (int)(C - off < 4 ? C - off : 4));
 		}
 	}
 }
@@ -414,21 +466,40 @@ __device__ __forceinline__ void item_map(uint32_t order, uint32_t it, uint32_t t
 	}
 }
 
-// The common alignment of every cell address of a launch: 16, 8, 4 or 1.
+static inline uint32_t granule_of(uint64_t bits)
+{
+	return (bits & 15u) == 0 ? 16u : (bits & 7u) == 0 ? 8u : (bits & 3u) == 0 ? 4u : 1u;
+}
+
+// The lane access a launch can use: 16 when every cell address is 16-byte
+// aligned, 4 when all are dword-aligned; 1 when only the sources are off a
+// dword boundary (the funnel-shifted loads of ld_src<1>, destinations
+// dword-aligned); 0 when a destination is not dword-aligned (the byte kernel).
+// (ld_g / st_g also implement an 8-byte lane layout, G = 8, which no launch
+// selects.)
 static inline uint32_t align_granule(const ecg_mm_params_t *p)
 {
-	uint64_t bits = (uint64_t)(uintptr_t)p->src | (uint64_t)(uintptr_t)p->dst |
-			(uint64_t)p->src_stripe_stride | (uint64_t)p->dst_stripe_stride;
+	uint64_t sb = (uint64_t)(uintptr_t)p->src | (uint64_t)p->src_stripe_stride;
+	uint64_t db = (uint64_t)(uintptr_t)p->dst | (uint64_t)p->dst_stripe_stride;
 	for (uint32_t j = 0; j < p->k; j++) {
-		bits |= (uint64_t)p->src_cell_off[j];
+		sb |= (uint64_t)p->src_cell_off[j];
 		if (p->diff)
-			bits |= (uint64_t)p->src2_cell_off[j];
+			sb |= (uint64_t)p->src2_cell_off[j];
 	}
 	if (p->diff)
-		bits |= (uint64_t)(uintptr_t)p->src2 | (uint64_t)p->src2_stripe_stride;
+		sb |= (uint64_t)(uintptr_t)p->src2 | (uint64_t)p->src2_stripe_stride;
 	for (uint32_t r = 0; r < p->rows; r++)
-		bits |= (uint64_t)p->dst_cell_off[r];
-	return (bits & 15u) == 0 ? 16u : (bits & 7u) == 0 ? 8u : (bits & 3u) == 0 ? 4u : 1u;
+		db |= (uint64_t)p->dst_cell_off[r];
+	const uint32_t gs = granule_of(sb), gd = granule_of(db);
+
+	if (gd < 4)
+		return 0;
+	if (gs < 4)
+		return 1;
+	/* 8-byte alignment takes the dword lanes too: the dwordx2-lane variant
+	 * ran 0.84-0.94 of the aligned kernel on different boxes, the dword one
+	 * (two-phase at k = 8) 0.94-0.98 (profiles/r04/run2/) */
+	return gs == 16 && gd == 16 ? 16 : 4;
 }
 
 static inline bool aligned16(const ecg_mm_params_t *p)

@@ -286,8 +286,8 @@ int ecg_set_autotune(ecg_ctx_t *ctx, int on);
 /* The tuner's state of a shape (k inputs, rows outputs, acc/diff off, the
  * launch's source and destination stripe strides -- encode: k*C and the
  * parity stripe stride; in-place recovery: (k+p)*C both): 1 decided (*cap =
- * the cap, or 255 = none; the median launch times of both arms), 0 still
- * probing or not seen.  nstripes is not part of the shape (it only has to
+ * the cap, or 255 = none; both arms' median times per block, scaled to a
+ * launch of nstripes stripes), 0 still probing or not seen.  nstripes is not part of the shape (it only has to
  * make the launch tunable, > 2048 blocks, to have been probed). */
 int ecg_tune_state(ecg_ctx_t *ctx, int k, int rows, uint64_t cell_bytes, uint32_t nstripes, int64_t sstride,
 		   int64_t dstride, uint32_t *cap, float *ms_uncapped, float *ms_capped);

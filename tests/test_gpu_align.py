@@ -1,12 +1,14 @@
 """GPU parity of the product kernels at every operand alignment.
 
 The product kernels pick their lane access per launch from the common
-alignment of every cell address (ecg_kernels.hip align_granule): 16-byte
-dwordx4 lanes, 8-byte dwordx2 lanes (DAOS rounds its parity rows to 8 bytes,
-ref:src/object/cli_ec.c:86), 4-byte dword lanes, or the byte kernel (user sgl
-cells carry no alignment, ref:src/object/cli_ec.c:510-536).  Every case is
-compared byte for byte with the oracle, and the test asserts which kernel ran.
-Offsets 1, 4, 8 and 12 of the data and/or parity bases, cells whose last
+alignment of every cell address (ecg_mm_dev.h align_granule): dwordx4 lanes
+when all are 16-byte aligned; dword lanes (g4) for 8- and 4-byte alignment
+(DAOS rounds its parity rows to 8 bytes, ref:src/object/cli_ec.c:86); dword
+lanes whose source dwords are funnel-shifted out of aligned loads (g1: user
+sgl cells carry no alignment, ref:src/object/cli_ec.c:510-536, while DAOS
+allocates the parity aligned); the byte kernel when a destination is off a
+dword boundary.  Every case is compared byte for byte with the oracle, and
+the test asserts which kernel ran.  Offsets 1, 4, 8 and 12 of the data and/or parity bases, cells whose last
 4 KiB column is partial, and cell sizes that are not multiples of 4 / 16.
 """
 import numpy as np
@@ -26,8 +28,18 @@ def granule(*vals):
     return 16 if bits % 16 == 0 else 8 if bits % 8 == 0 else 4 if bits % 4 == 0 else 1
 
 
+def launch_granule(src_vals, dst_vals):
+    """ecg_kernels.hip align_granule: the common alignment of all cell
+    addresses; 1 = sources at any byte with dword-aligned destinations (the
+    funnel-shift kernel); 0 = a destination off a dword boundary (byte kernel)."""
+    gs, gd = granule(*src_vals), granule(*dst_vals)
+    if gd < 4:
+        return 0
+    return 1 if gs < 4 else 16 if gs == gd == 16 else 4     # 8-byte alignment runs the dword lanes
+
+
 def expect_kernel(name, g, k, rows):
-    if g == 1:
+    if g == 0:
         assert name == "ecg_mm_byte_kernel", name
     elif g == 16:
         assert name.startswith("ecg_mm_kernel<") and ",g" not in name, name
@@ -48,7 +60,7 @@ CELLS = [65536, 2 * 4096 + 1024 + 8, 3 * 4096 + 20, 4096 + 13]
                                        (8, 8), (4, 12), (12, 8)])
 def test_encode_offsets(ctx, oracle, ecglib, C_, doff, poff):
     """Client-layout encode (data [S][k][C] -> parity [p][S][C]) with the data
-    and parity bases at byte offsets: the launch runs the g8 / g4 / byte
+    and parity bases at byte offsets: the launch runs the g4 / g1 / byte
     kernels as the addresses allow, with the oracle's parity."""
     k, p, S = 8, 2, 3
     data = rand((S, k, C_), C_ + doff * 16 + poff)
@@ -60,7 +72,7 @@ def test_encode_offsets(ctx, oracle, ecglib, C_, doff, poff):
     try:
         ctx.encode(k, p, C_, S, d.ptr + doff, k * C_, par.ptr + poff, pitch, C_)
         ctx.sync()
-        expect_kernel(ecglib.last_kernel(), granule(doff, poff, k * C_, C_, pitch), k, p)
+        expect_kernel(ecglib.last_kernel(), launch_granule((doff, k * C_, C_), (poff, pitch, C_)), k, p)
         raw = par.download()
         got = np.stack([raw[poff + r * pitch: poff + r * pitch + S * C_].reshape(S, C_) for r in range(p)])
         assert np.array_equal(got, oracle_parity(oracle, k, p, data))
@@ -73,21 +85,24 @@ def test_encode_offsets(ctx, oracle, ecglib, C_, doff, poff):
         par.free()
 
 
-@pytest.mark.parametrize("k,p", [(2, 1), (4, 2), (8, 3), (16, 2), (16, 3)])
-@pytest.mark.parametrize("off", [4, 8])
+@pytest.mark.parametrize("k,p", [(2, 1), (4, 2), (8, 2), (8, 3), (16, 2), (16, 3)])
+@pytest.mark.parametrize("off", [4, 8, 1])
 def test_encode_classes_at_offset(ctx, oracle, ecglib, k, p, off):
-    """Every specialised (k, p) has g8 and g4 instantiations."""
+    """Every specialised (k, p) has g4 (4- or 8-byte aligned operands) and g1
+    instantiations (g1: the data cells at a byte offset, the parity
+    dword-aligned)."""
     S, C_ = 4, 8192 + 4096
     data = rand((S, k, C_), k * 10 + p + off)
     d = ctx.alloc(data.nbytes + 64)
     d.upload(data.reshape(-1), offset=off)
     par = ctx.alloc(p * S * C_ + 64)
+    poff = 0 if off == 1 else off
     try:
-        ctx.encode(k, p, C_, S, d.ptr + off, k * C_, par.ptr + off, S * C_, C_)
+        ctx.encode(k, p, C_, S, d.ptr + off, k * C_, par.ptr + poff, S * C_, C_)
         ctx.sync()
         name = ecglib.last_kernel()
-        assert name.startswith(f"ecg_mm_kernel<{k},{p},") and name.endswith(f",g{off}>"), name
-        got = par.download(p * S * C_, offset=off).reshape(p, S, C_)
+        assert name.startswith(f"ecg_mm_kernel<{k},{p},") and name.endswith(f",g{min(off, 4)}>"), name
+        got = par.download(p * S * C_, offset=poff).reshape(p, S, C_)
         assert np.array_equal(got, oracle_parity(oracle, k, p, data))
     finally:
         d.free()
@@ -109,7 +124,8 @@ def test_recover_in_place_at_offset(ctx, oracle, ecglib, off, C_, errs):
     try:
         ctx.recover(k, p, C_, S, d.ptr + off, (k + p) * C_, errs)
         ctx.sync()
-        expect_kernel(ecglib.last_kernel(), granule(off, (k + p) * C_, C_), k, len(errs))
+        g = granule(off, (k + p) * C_, C_)         # in place: sources and destinations alike
+        expect_kernel(ecglib.last_kernel(), 0 if g < 4 else 16 if g == 16 else 4, k, len(errs))
         got = d.download(stripes.nbytes, offset=off).reshape(S, k + p, C_)
         assert np.array_equal(got, stripes)
     finally:
@@ -138,8 +154,8 @@ def test_update_at_offset(ctx, oracle, ecglib, off):
         data[:, cells] = new
         assert np.array_equal(got, oracle_parity(oracle, k, p, data))
         name = ecglib.last_kernel()
-        g = granule(off, C_, len(cells) * C_, S * C_)
-        assert name == "ecg_mm_byte_kernel" if g == 1 else name.endswith(f",1,1,g{g}>"), name
+        g = granule(off, C_, len(cells) * C_, S * C_)       # the parity is read and written (ACC)
+        assert name == "ecg_mm_byte_kernel" if g == 1 else name.endswith(",1,1,g4>"), name
     finally:
         for b in (dold, dnew, dpar):
             b.free()
@@ -160,7 +176,7 @@ def test_generic_shapes_at_offset(ctx, oracle, ecglib, off, k, rows):
         ctx.matmul(coef, C_, S, d.ptr + off, [j * C_ for j in range(k)], k * C_, out.ptr + off,
                    [r * C_ for r in range(rows)], rows * C_, 0)
         ctx.sync()
-        assert ecglib.last_kernel().endswith(f",g{off}>"), ecglib.last_kernel()
+        assert ecglib.last_kernel().endswith(",g4>"), ecglib.last_kernel()
         got = out.download(S * rows * C_, offset=off).reshape(S, rows, C_)
         for s in range(S):
             assert np.array_equal(got[s], oracle.encode_data(coef, data[s]))
