@@ -977,7 +977,9 @@ def leg_stream(args, ctx, world, rank, steps, numa_info):
     else:
         wl = HostWorkload(ctx, k, p, C, S, chunk=args.host_chunk)
         step, sync = wl.step, ctx.sync
-    mine, tmax = timed_leg(world, steps, 0 if args.rehearse else 2, step, sync)
+    # 8 warm-up steps: the first batches of a process's host pipeline ran 42 instead of 50 GiB/s
+    # after 2 warm-up steps, steady from 4 on (tools/hoststream_probe.py, profiles/r04/hoststream_probe/)
+    mine, tmax = timed_leg(world, steps, 0 if args.rehearse else 8, step, sync)
     row = {"rank": rank, "ms_per_step": round(mine / steps * 1e3, 4),
            "numa_node": (numa_info or {}).get("numa_node"), "pinned_cpus": (numa_info or {}).get("pinned_cpus")}
     user = 2 * k * C * S
