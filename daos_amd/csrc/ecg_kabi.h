@@ -274,11 +274,14 @@ const char *ecg_k_fused_kernel_name(uint32_t kernel_id);
 /* The common alignment (16, 8, 4 or 1 bytes) of every cell address of a
  * product launch: the lane access granule the product kernels use. */
 uint32_t ecg_k_align_granule(const ecg_mm_params_t *p);
-/* Pointer-table product (kernels/ecg_kernels.hip): cells_dev[s*(k+rows)+j] =
- * device address of input cell j / output cell j-k of stripe s.  aligned = all
- * addresses 16-byte aligned (else the byte-granular kernel). */
-int ecg_k_launch_matmul_ptrs(const ecg_mm_params_t *p, const uint64_t *cells_dev, int aligned,
+/* Pointer-table product (kernels/ecg_ptr_kernels.hip): cells_dev[s*(k+rows)+j]
+ * = device address of input cell j / output cell j-k of stripe s.  granule:
+ * 16 = every address 16-byte aligned, 4 = all dword-aligned, 1 = outputs
+ * dword-aligned and inputs at any byte, 0 = the byte-granular kernel. */
+int ecg_k_launch_matmul_ptrs(const ecg_mm_params_t *p, const uint64_t *cells_dev, int granule,
 			     const ecg_launch_cfg_t *cfg, void *stream, uint32_t *kernel_id);
+#define ECG_KID_PTR 600u	/* pointer-table kernel ids start here */
+const char *ecg_k_ptr_kernel_name(uint32_t kernel_id);
 /* Chunked checksums (kernels/ecg_csum_kernels.hip). max_blocks 0 = default. */
 int ecg_k_launch_csum(const ecg_csum_params_t *p, void *stream, uint32_t max_blocks,
 		      uint32_t *kernel_id);

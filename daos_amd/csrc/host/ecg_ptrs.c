@@ -81,14 +81,36 @@ void ecg_scratch_free(ecg_ctx_t *ctx)
 	memset(&ctx->scratch, 0, sizeof(ctx->scratch));
 }
 
+/* Lane access of a pointer table (ecg_k_launch_matmul_ptrs): from the OR of
+ * the input and of the output cell addresses. */
+static int ptr_granule(const uint64_t *tab, uint32_t S, int k, int rows)
+{
+	uint64_t in = 0, out = 0;
+
+	for (uint64_t s = 0; s < S; s++) {
+		const uint64_t *t = tab + s * (uint64_t)(k + rows);
+
+		for (int j = 0; j < k; j++)
+			in |= t[j];
+		for (int r = 0; r < rows; r++)
+			out |= t[k + r];
+	}
+	if (out & 3u)
+		return 0;
+	if (in & 3u)
+		return 1;
+	return ((in | out) & 15u) == 0 ? 16 : 4;
+}
+
 /* Table already in sc->pin (S x (k+rows) entries); copy, launch, record
  * (ctx->lock held).  With `gather`, its segment table follows the pointer
  * table at byte seg_off of the slot (pinned and device alike): both travel in
  * one H2D and the gather copies run before the product. */
 static int launch_table(ecg_ctx_t *ctx, struct ecg_scratch_slot *sc, int k, int rows,
-			const unsigned char *coef, uint64_t C, uint32_t S, int aligned, hipStream_t st,
+			const unsigned char *coef, uint64_t C, uint32_t S, hipStream_t st,
 			const struct ecg_segs *gather, size_t seg_off)
 {
+	const int granule = ptr_granule((const uint64_t *)sc->pin, S, k, rows);
 	size_t tbytes = (size_t)S * (size_t)(k + rows) * sizeof(uint64_t);
 	ecg_mm_params_t *prm;
 	uint32_t kid = 0;
@@ -116,7 +138,7 @@ static int launch_table(ecg_ctx_t *ctx, struct ecg_scratch_slot *sc, int k, int 
 	for (r = 0; r < rows; r++)
 		for (j = 0; j < k; j++)
 			ecg_build_ptbl(coef[(size_t)r * k + j], &prm->tbl[r][j]);
-	ke = ecg_k_launch_matmul_ptrs(prm, (const uint64_t *)sc->dev, aligned, &ctx->cfg, (void *)st,
+	ke = ecg_k_launch_matmul_ptrs(prm, (const uint64_t *)sc->dev, granule, &ctx->cfg, (void *)st,
 				      &kid);
 	free(prm);
 	if (ke != 0)
@@ -134,7 +156,6 @@ int ecg_matmul_ptrs(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, 
 {
 	const size_t n = (size_t)nstripes * (size_t)(k + rows);
 	struct ecg_scratch_slot *sc = NULL;
-	uint64_t bits = cell_bytes;
 	hipStream_t st;
 	int rc;
 
@@ -148,7 +169,6 @@ int ecg_matmul_ptrs(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, 
 	for (size_t i = 0; i < n; i++) {
 		if (cells[i] == NULL)
 			return ecg_fail(-ECG_DER_INVAL, "matmul_ptrs: NULL cell %zu", i);
-		bits |= (uint64_t)(uintptr_t)cells[i];
 	}
 	rc = ecg_ctx_enter(ctx);
 	if (rc)
@@ -158,7 +178,7 @@ int ecg_matmul_ptrs(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, 
 	rc = ecg_scratch_reserve(ctx, n * sizeof(uint64_t), n * sizeof(uint64_t), &sc);
 	if (rc == 0) {
 		memcpy(sc->pin, cells, n * sizeof(uint64_t));
-		rc = launch_table(ctx, sc, k, rows, coef, cell_bytes, nstripes, (bits & 15u) == 0, st, NULL, 0);
+		rc = launch_table(ctx, sc, k, rows, coef, cell_bytes, nstripes, st, NULL, 0);
 	}
 	pthread_mutex_unlock(&ctx->lock);
 	return rc;
@@ -314,8 +334,7 @@ int ecg_obj_ec_recx_encode(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_bytes,
 		rc = sgl_walk(iovs, iov_nr, recxs, recx_nr, k, p, cell_bytes, pbufs, (uint64_t *)sc->pin,
 			      (unsigned char *)sc->dev + tbytes + sbytes, &segs, &ngather, &npieces, &bits);
 		if (rc == 0)	/* one H2D of both tables, gather launch, product launch */
-			rc = launch_table(ctx, sc, k, p, &en[k * k], cell_bytes, (uint32_t)S,
-					  (bits & 15u) == 0, st, &segs, tbytes);
+			rc = launch_table(ctx, sc, k, p, &en[k * k], cell_bytes, (uint32_t)S, st, &segs, tbytes);
 	}
 	pthread_mutex_unlock(&ctx->lock);
 	return rc;

@@ -158,110 +158,6 @@ ecg_mm_sel_kernel(const ecg_mm_params_t P, const uint8_t *__restrict__ sel, uint
 	}
 }
 
-template <int KM, int RM>
-__device__ __forceinline__ void mm_ptr_item(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
-					    uint32_t s, uint64_t cbase, uint32_t lo, const uint64_t *a)
-{
-	u32x4 x[KM], outv[RM];
-
-#pragma unroll
-	for (int j = 0; j < KM; j++)
-		if (j < k)
-			x[j] = ld_nt(reinterpret_cast<const uint8_t *>(a[j]) + lo);
-	mm_compute<KM, RM, false, true, false>(P, tb, k, rows, s, cbase, lo, x, outv);
-#pragma unroll
-	for (int r = 0; r < RM; r++)
-		if (r < rows)
-			st_nt(reinterpret_cast<uint8_t *>(a[KM + r]) + lo, outv[r]);
-}
-
-// Pointer-table product (ISA-L's data[]/coding[] convention batched over
-// stripes): cells[s*(k+rows) + j] is the device address of input cell j (j < k)
-// or output cell j-k of stripe s.  Same columns, tables and arithmetic as
-// ecg_mm_kernel; a stripe's k+rows addresses are wave-uniform (scalar loads).
-template <int K, int R>
-__global__ void __launch_bounds__(BLOCK)
-ecg_mm_ptr_kernel(const ecg_mm_params_t P, const uint64_t *__restrict__ cells)
-{
-	constexpr int KM = K ? K : ECG_KMAX_K;
-	constexpr int RM = R ? R : ECG_KMAX_R;
-	constexpr int T2V = (RM + 3) / 4;
-	constexpr int PER_J = RM + T2V;
-	__shared__ u32x4 s_tbl[KM * PER_J];
-	const int k = K ? K : (int)P.k;
-	const int rows = R ? R : (int)P.rows;
-	const uint64_t C = P.cell_bytes;
-	const uint32_t nchunk = (uint32_t)((C + CHUNK_BYTES - 1) / CHUNK_BYTES);
-	const uint32_t lo = threadIdx.x * 16u;
-
-	for (int i = threadIdx.x; i < KM * RM; i += BLOCK) {
-		const int j = i / RM, r = i % RM;
-		if (j < k && r < rows) {
-			const ecg_ptbl_t &t = P.tbl[r][j];
-			s_tbl[j * PER_J + r] = (u32x4){t.t0lo, t.t0hi, t.t1lo, t.t1hi};
-			reinterpret_cast<uint32_t *>(&s_tbl[j * PER_J + RM])[r] = t.t2;
-		}
-	}
-	__syncthreads();
-
-	for (uint32_t s = blockIdx.y; s < P.nstripes; s += gridDim.y) {
-		const uint64_t *pt = cells + (uint64_t)s * (uint32_t)(k + rows);
-		uint64_t base[KM + RM];
-
-		// the stripe's addresses: one dependent (scalar) load per stripe, not
-		// per column -- the workgroup then walks several columns
-#pragma unroll
-		for (int j = 0; j < KM + RM; j++)
-			if (j < k || (j >= KM && j - KM < rows))
-				base[j] = pt[j < KM ? j : k + (j - KM)];
-		for (uint32_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
-			const uint64_t cbase = (uint64_t)ch * CHUNK_BYTES;
-			uint64_t a[KM + RM];
-			uint32_t z = 0;
-
-#pragma unroll
-			for (int j = 0; j < KM + RM; j++) {
-				if (j < k || (j >= KM && j - KM < rows)) {
-					a[j] = base[j] + cbase;
-					asm volatile("" : "+s"(a[j]));
-				}
-			}
-			asm volatile("" : "+v"(z));
-			const u32x4 *tb = s_tbl + z;
-			if (cbase + CHUNK_BYTES <= C)
-				mm_ptr_item<KM, RM>(P, tb, k, rows, s, cbase, lo, a);
-			else if (cbase + lo + 16 <= C)	// C % 16 == 0 on this path
-				mm_ptr_item<KM, RM>(P, tb, k, rows, s, cbase, lo, a);
-		}
-	}
-}
-
-// Pointer-table product, any alignment and length: one byte per lane.
-__global__ void __launch_bounds__(BLOCK)
-ecg_mm_ptr_byte_kernel(const ecg_mm_params_t P, const uint64_t *cells)
-{
-	const uint64_t C = P.cell_bytes;
-	const uint64_t total = C * P.nstripes;
-	const int k = (int)P.k, rows = (int)P.rows;
-
-	for (uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; e < total;
-	     e += (uint64_t)gridDim.x * BLOCK) {
-		const uint64_t s = e / C, i = e % C;
-		const uint64_t *pt = cells + s * (uint64_t)(k + rows);
-		uint8_t o[ECG_KMAX_R];
-
-		for (int r = 0; r < ECG_KMAX_R; r++)
-			o[r] = 0;
-		for (int j = 0; j < k; j++) {
-			const uint32_t v = reinterpret_cast<const uint8_t *>(pt[j])[i];
-			for (int r = 0; r < rows; r++)
-				o[r] ^= gf_mul1(P.tbl[r][j], v);
-		}
-		for (int r = 0; r < rows; r++)
-			reinterpret_cast<uint8_t *>(pt[k + r])[i] = o[r];
-	}
-}
-
 // Any alignment, any length: one byte per lane-iteration.  Used only when a
 // caller hands cell bases/strides that are not 16-byte aligned.
 __global__ void __launch_bounds__(BLOCK)
@@ -383,24 +279,6 @@ static const kentry g_kernels[] = {
 
 
 
-typedef void (*mmptr_fn_t)(const ecg_mm_params_t, const uint64_t *);
-
-struct pentry {
-	int k, r;
-	mmptr_fn_t fn;
-	const char *name;
-};
-
-#define PE(K_, R_) {K_, R_, ecg_mm_ptr_kernel<K_, R_>, "ecg_mm_ptr_kernel<" #K_ "," #R_ ">"}
-
-static const pentry g_pkernels[] = {
-	PE(2, 1), PE(2, 2), PE(2, 3), PE(4, 1), PE(4, 2), PE(4, 3),
-	PE(8, 1), PE(8, 2), PE(8, 3), PE(16, 1), PE(16, 2), PE(16, 3), PE(0, 0),
-};
-#define N_PKERNELS ((uint32_t)(sizeof(g_pkernels) / sizeof(g_pkernels[0])))
-#define KID_PTR 600u		/* pointer-table kernel ids: KID_PTR + index */
-#define KID_PTR_BYTE (KID_PTR + N_PKERNELS)
-
 #define KID_SEL 700u		/* per-stripe column kernels: <1>, <2>, <0> */
 
 #define KID_BYTE N_KERNELS
@@ -429,10 +307,8 @@ extern "C" const char *ecg_k_kernel_name(uint32_t id)
 		return ecg_k_csum_kernel_name(id);
 	if (id >= ECG_KID_FUSED && id < ECG_KID_FUSED + 100u)	/* below KID_PTR */
 		return ecg_k_fused_kernel_name(id);
-	if (id >= KID_PTR && id < KID_PTR + N_PKERNELS)
-		return g_pkernels[id - KID_PTR].name;
-	if (id == KID_PTR_BYTE)
-		return "ecg_mm_ptr_byte_kernel";
+	if (id >= ECG_KID_PTR && id < ECG_KID_PTR + 100u)
+		return ecg_k_ptr_kernel_name(id);
 	if (id == ECG_KID_COPY_SEGS)
 		return "ecg_copy_segs_kernel";
 	if (id == KID_SEL)
@@ -616,40 +492,5 @@ extern "C" int ecg_k_launch_matmul_sel(const ecg_mm_params_t *p, const uint8_t *
 				   sel_dev, ncols);
 	if (kernel_id)
 		*kernel_id = KID_SEL + v;
-	return (int)hipGetLastError();
-}
-
-extern "C" int ecg_k_launch_matmul_ptrs(const ecg_mm_params_t *p, const uint64_t *cells_dev,
-				       int aligned, const ecg_launch_cfg_t *cfg, void *stream,
-				       uint32_t *kernel_id)
-{
-	hipStream_t st = (hipStream_t)stream;
-	const uint64_t nchunk = (p->cell_bytes + CHUNK_BYTES - 1) / CHUNK_BYTES;
-	uint32_t id = N_PKERNELS;
-
-	if (p->nstripes == 0 || p->cell_bytes == 0 || p->rows == 0)
-		return (int)hipSuccess;
-	if (!aligned || (p->cell_bytes & 15u) || (cfg && cfg->variant == 2)) {
-		uint64_t blocks = (p->cell_bytes * p->nstripes + BLOCK - 1) / BLOCK;
-		if (blocks > 8192)
-			blocks = 8192;
-		hipLaunchKernelGGL(ecg_mm_ptr_byte_kernel, dim3((uint32_t)blocks), dim3(BLOCK), 0, st, *p,
-				   cells_dev);
-		if (kernel_id)
-			*kernel_id = KID_PTR_BYTE;
-		return (int)hipGetLastError();
-	}
-	for (uint32_t i = 0; i < N_PKERNELS && (!cfg || cfg->variant != 1); i++)
-		if (g_pkernels[i].k == (int)p->k && g_pkernels[i].r == (int)p->rows) {
-			id = i;
-			break;
-		}
-	if (id == N_PKERNELS)
-		id = N_PKERNELS - 1;	/* runtime-shaped */
-	uint32_t gx = cfg && cfg->grid_x ? cfg->grid_x : (uint32_t)(nchunk < 65535 ? nchunk : 65535);
-	uint32_t gy = cfg && cfg->grid_y ? cfg->grid_y : (p->nstripes < 65535 ? p->nstripes : 65535);
-	hipLaunchKernelGGL(g_pkernels[id].fn, dim3(gx, gy), dim3(BLOCK), 0, st, *p, cells_dev);
-	if (kernel_id)
-		*kernel_id = KID_PTR + id;
 	return (int)hipGetLastError();
 }

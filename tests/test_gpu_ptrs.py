@@ -10,33 +10,79 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("k,rows,C,S,aligned", [(8, 2, 65536, 12, True), (4, 3, 4096 * 3 + 48, 7, True),
-                                                 (16, 2, 8192, 5, True), (6, 5, 1000, 9, False),
-                                                 (2, 1, 4097, 4, False)])
-def test_matmul_ptrs(oracle, ecglib, ctx, k, rows, C, S, aligned):
-    """Cells scattered at random (disjoint, shuffled) offsets of one buffer."""
-    rng = np.random.default_rng(k * 100 + rows)
-    slot = (C + 15) // 16 * 16 + (0 if aligned else 16)
+def _ptr_granule(in_skews, out_skews, C):
+    """ecg_ptrs.c ptr_granule + ecg_k_launch_matmul_ptrs: 0 byte kernel,
+    1 funnel-shifted inputs, 4 dword lanes, 16 dwordx4 lanes."""
+    ib = 0
+    for x in in_skews:
+        ib |= x
+    ob = 0
+    for x in out_skews:
+        ob |= x
+    if ob & 3:
+        return 0
+    if ib & 3:
+        return 1
+    return 16 if ((ib | ob) & 15) == 0 and C % 16 == 0 else 4
+
+
+@pytest.mark.parametrize("k,rows,C,S,iskew,oskew", [
+    (8, 2, 65536, 12, 0, 0), (4, 3, 4096 * 3 + 48, 7, 0, 0), (16, 2, 8192, 5, 0, 0),
+    (6, 5, 1000, 9, 3, 3),                      # outputs off a dword: byte kernel
+    (2, 1, 4097, 4, 3, 3),
+    (8, 2, 65536 + 4096 + 20, 6, 0, 0),         # cell size not a multiple of 16: dword lanes
+    (8, 2, 65536, 6, 8, 4),                     # 8- / 4-byte aligned cells: dword lanes
+    (8, 2, 65536 + 1000, 6, "rand", 0),         # inputs at random byte offsets: funnel-shifted dwords
+    (16, 3, 12288 + 5, 4, "rand", 8),
+    (4, 2, 4096, 9, 1, 0), (5, 3, 5000, 4, "rand", 4),
+])
+def test_matmul_ptrs(oracle, ecglib, ctx, k, rows, C, S, iskew, oskew):
+    """Cells scattered at random (disjoint, shuffled) offsets of one buffer,
+    inputs and outputs at the given byte skews within their slots ("rand":
+    each input cell at its own random skew, as in-place sgl cells are)."""
+    rng = np.random.default_rng(k * 100 + rows + C)
+    slot = (C + 15) // 16 * 16 + 32
     nslots = S * (k + rows) + 8
     buf = ctx.alloc(nslots * slot)
     order = rng.permutation(nslots)[: S * (k + rows)]
-    skew = 0 if aligned else 3
     host = rng.integers(0, 256, nslots * slot, dtype=np.uint8)
+    skews = []
+    for s in range(S):
+        for j in range(k + rows):
+            if j < k:
+                skews.append(int(rng.integers(0, 16)) if iskew == "rand" else iskew)
+            else:
+                skews.append(oskew)
     try:
         buf.upload(host)
-        addrs = [buf.ptr + int(o) * slot + skew for o in order]
+        addrs = [buf.ptr + int(o) * slot + sk for o, sk in zip(order, skews)]
         coef = rng.integers(0, 256, (rows, k), dtype=np.uint8)
         ctx.matmul_ptrs(k, rows, coef, C, S, addrs)
         ctx.sync()
         kern = ecglib.last_kernel()
-        assert ("ptr_byte" in kern) == (not aligned or C % 16 != 0), kern
+        g = _ptr_granule([a for i, a in enumerate(addrs) if i % (k + rows) < k],
+                         [a for i, a in enumerate(addrs) if i % (k + rows) >= k], C)
+        if g == 0:
+            assert kern == "ecg_mm_ptr_byte_kernel", kern
+        elif g == 16:
+            assert kern.startswith("ecg_mm_ptr_kernel<") and ",g" not in kern, kern
+        else:
+            assert kern.startswith("ecg_mm_ptr_kernel<") and kern.endswith(f",g{g}>"), kern
         dev = buf.download()
         for s in range(S):
-            cells = np.stack([host[int(order[s * (k + rows) + j]) * slot + skew:][:C] for j in range(k)])
+            cells = np.stack([host[int(order[s * (k + rows) + j]) * slot + skews[s * (k + rows) + j]:][:C]
+                              for j in range(k)])
             want = oracle.encode_data(coef, cells)
             for r in range(rows):
-                o = int(order[s * (k + rows) + k + r]) * slot + skew
+                i = s * (k + rows) + k + r
+                o = int(order[i]) * slot + skews[i]
                 assert np.array_equal(dev[o:o + C], want[r]), (s, r)
+            # bytes around the outputs untouched
+            for r in range(rows):
+                i = s * (k + rows) + k + r
+                o = int(order[i]) * slot
+                assert np.array_equal(dev[o:o + skews[i]], host[o:o + skews[i]])
+                assert np.array_equal(dev[o + skews[i] + C:o + slot], host[o + skews[i] + C:o + slot])
     finally:
         buf.free()
 
@@ -56,14 +102,16 @@ def _split_sgl(rng, total, C, n_iov, zero_iovs):
     return lens
 
 
-@pytest.mark.parametrize("k,p,C,recx_plan,n_iov,zeros", [
-    (4, 2, 8192, [(0, 3), (131072, 2)], 1, 0),             # one iov: every cell in place
-    (8, 2, 4096, [(0, 4), (4096 * 8 * 6, 3)], 7, 2),        # cells cut across iovs, empty iovs
-    (2, 1, 1000, [(0, 5), (30000, 4), (60000, 1)], 23, 3),  # unaligned cells
-    (16, 2, 16384, [(16384 * 16, 3)], 5, 1),                # leading gap
-    (4, 3, 4096, [(0, 2), (32768, 2)], 64, 0),               # many small iovs
+@pytest.mark.parametrize("k,p,C,recx_plan,n_iov,zeros,shift", [
+    (4, 2, 8192, [(0, 3), (131072, 2)], 1, 0, 0),             # one iov: every cell in place
+    (8, 2, 4096, [(0, 4), (4096 * 8 * 6, 3)], 7, 2, 0),        # cells cut across iovs, empty iovs
+    (2, 1, 1000, [(0, 5), (30000, 4), (60000, 1)], 23, 3, 0),  # cell size not a multiple of 16
+    (16, 2, 16384, [(16384 * 16, 3)], 5, 1, 0),                # leading gap
+    (4, 3, 4096, [(0, 2), (32768, 2)], 64, 0, 0),               # many small iovs
+    (8, 2, 65536, [(0, 6)], 1, 0, 3),                           # one iov at an odd address: cells in place, unaligned
+    (8, 2, 65536 + 12, [(0, 3), (8 * 65548 * 5, 2)], 4, 1, 5),  # odd iovs, cells cut and in place
 ])
-def test_recx_encode_sgl(oracle, ecglib, ctx, k, p, C, recx_plan, n_iov, zeros):
+def test_recx_encode_sgl(oracle, ecglib, ctx, k, p, C, recx_plan, n_iov, zeros, shift):
     L = ecglib.lib()
     rng = np.random.default_rng(n_iov * 31 + k)
     stripe = k * C
@@ -74,8 +122,8 @@ def test_recx_encode_sgl(oracle, ecglib, ctx, k, p, C, recx_plan, n_iov, zeros):
     nstripes = sum(n for _, n in recx_plan)
     pbufs = [ctx.alloc(nstripes * C) for _ in range(p)]
     try:
-        # iovs placed with gaps between them in device memory
-        iovs, pos, dev_off = [], 0, 0
+        # iovs placed with gaps between them in device memory (the first at byte `shift`)
+        iovs, pos, dev_off = [], 0, shift
         for ln in lens:
             buf.upload(stream[pos:pos + ln], offset=dev_off) if ln else None
             iovs.append(ecglib.Iov(buf.ptr + dev_off, ln))
@@ -87,6 +135,9 @@ def test_recx_encode_sgl(oracle, ecglib, ctx, k, p, C, recx_plan, n_iov, zeros):
         rc = L.ecg_obj_ec_recx_encode(ctx.h, _oc(k, p), C, iov_arr, len(iovs), rx, len(recx_plan), pb, None)
         assert rc == 0, ecglib.lib().ecg_strerror()
         ctx.sync()
+        if shift % 4:       # in-place cells at odd addresses, parity aligned: funnel-shifted inputs
+            assert ecglib.last_kernel().startswith("ecg_mm_ptr_kernel<") and \
+                ecglib.last_kernel().endswith(",g1>"), ecglib.last_kernel()
         en = oracle.cauchy1(k, p)
         n = 0
         got = [b.download() for b in pbufs]

@@ -59,6 +59,12 @@ for what in "$@"; do
 			step rocprof_${w}_w 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv \
 				-d "$O/pmc_${w}_w" -o run -- python3 tools/ec_pmc.py $w || exit $?
 		done
+		python tools/pmc_traffic.py "$O/pmc_dec_8p2_f" "$O/pmc_dec_8p2_w" "ecg_mm_kernel<8, 2" 5368709120 \
+			"$O/pmc_traffic_dec_8p2.json" || exit $?
+		python tools/pmc_traffic.py "$O/pmc_enc_16p2_f" "$O/pmc_enc_16p2_w" "ecg_mm_kernel<16, 2" 2415919104 \
+			"$O/pmc_traffic_enc_16p2.json" || exit $?
+		python tools/pmc_traffic.py "$O/pmc_dec_16p2_f" "$O/pmc_dec_16p2_w" "ecg_mm_kernel<16, 2" 2415919104 \
+			"$O/pmc_traffic_dec_16p2.json" || exit $?
 		;;
 	rehearse8)        # 8 ranks on this one GPU: rendezvous, NUMA pinning, legs, accounting (no scaling)
 		step bench_rehearse8 900 python bench.py --gpus 8 --allow-shared-device --steps 10 --warmup 2 --no-cpu \
