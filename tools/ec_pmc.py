@@ -4,8 +4,11 @@ launches after 2 warm-up launches, seeded random cells:
   dec_8p2     EC_8P2 1 MiB x 512, {d0,d1} regenerated in [S][k+p][C]
   enc_16p2    EC_16P2 128 KiB x 1024, data [S][k][C] -> parity [p][S][C] (padded pitch)
   dec_16p2    EC_16P2 128 KiB x 1024, {d0,d1} regenerated in [S][k+p][C]
+  enc_4p2 / enc_8p2 / enc_16p2_cap2 (2 blocks per CU) / enc_16p2_x4096, and the
+  streaming read / write kernels (4 GiB) as references for the memory-side counters
 Run as  rocprofv3 --pmc FETCH_SIZE -- python3 tools/ec_pmc.py dec_8p2  and summarise
-with tools/pmc_traffic.py (algorithmic bytes printed here).  Bench infrastructure."""
+with tools/pmc_traffic.py (algorithmic bytes printed here) or tools/pmc_summary.py.
+The launch tuner is off: every launch runs the geometry named.  Bench infrastructure."""
 import os
 import sys
 
@@ -15,12 +18,37 @@ from daos_amd import ecg  # noqa: E402
 from tools.datagen import stripe_bytes  # noqa: E402
 
 SHAPES = {"dec_8p2": (8, 2, 1 << 20, 512, "dec"), "enc_16p2": (16, 2, 128 << 10, 1024, "enc"),
-          "dec_16p2": (16, 2, 128 << 10, 1024, "dec")}
+          "dec_16p2": (16, 2, 128 << 10, 1024, "dec"), "enc_4p2": (4, 2, 1 << 20, 1024, "enc"),
+          "enc_8p2": (8, 2, 1 << 20, 512, "enc"), "enc_16p2_cap2": (16, 2, 128 << 10, 1024, "enc"),
+          "enc_16p2_x4096": (16, 2, 128 << 10, 4096, "enc"), "read": (0, 0, 0, 0, "read"),
+          "write": (0, 0, 0, 0, "write")}
+
+
+def stream(ctx, mode):
+    """The box's streaming read (mode 1) / write (mode 2) kernel over 4 GiB,
+    at the geometry bench.py measures its ceilings with."""
+    n = 4 << 30
+    a, b = ctx.alloc(n), ctx.alloc(n)
+    a.fill(0x3C)
+    ctx.set_launch(512 if mode == 1 else 0, 0, 0)
+    for _ in range(7):
+        ctx.copy_kernel(b.ptr, a.ptr, n, mode)
+    ctx.sync()
+    print(f"ec_pmc stream mode {mode} kernel {ecg.last_kernel()} bytes_per_launch {n}", flush=True)
+    a.free()
+    b.free()
 
 
 def main():
     k, p, C, S, op = SHAPES[sys.argv[1]]
     ctx = ecg.Context(0)
+    ctx.set_autotune(0)
+    if op in ("read", "write"):
+        stream(ctx, 1 if op == "read" else 2)
+        ctx.close()
+        return
+    if sys.argv[1].endswith("_cap2"):
+        ctx.set_wg_per_cu(2)
     st = (k + p) * C
     buf = ctx.alloc(S * st)
     blk = stripe_bytes(256 << 20, 5)

@@ -66,6 +66,20 @@ for what in "$@"; do
 		python tools/pmc_traffic.py "$O/pmc_dec_16p2_f" "$O/pmc_dec_16p2_w" "ecg_mm_kernel<16, 2" 2415919104 \
 			"$O/pmc_traffic_dec_16p2.json" || exit $?
 		;;
+	ecdram)           # memory-side queueing of the EC shapes vs the streaming kernels: outstanding
+	                  # requests per cycle (LEVEL), requests, DRAM-credit stall cycles, GRBM cycles
+		for w in ${ECDRAM_SHAPES:-read write enc_4p2 enc_8p2 dec_8p2 enc_16p2 enc_16p2_cap2}; do
+			rm -rf "$O/dram_${w}_r" "$O/dram_${w}_w"
+			step dram_${w}_r 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ \
+				TCC_EA0_RDREQ_LEVEL TCC_EA0_RDREQ_DRAM_CREDIT_STALL GRBM_GUI_ACTIVE --output-format csv \
+				-d "$O/dram_${w}_r" -o run -- python3 tools/ec_pmc.py $w || exit $?
+			step dram_${w}_w 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc TCC_EA0_WRREQ \
+				TCC_EA0_WRREQ_LEVEL TCC_EA0_WRREQ_DRAM_CREDIT_STALL GRBM_GUI_ACTIVE --output-format csv \
+				-d "$O/dram_${w}_w" -o run -- python3 tools/ec_pmc.py $w || exit $?
+			python tools/pmc_summary.py --skip 2 "$O/dram_${w}_r/run_counter_collection.csv" \
+				"$O/dram_${w}_w/run_counter_collection.csv" > "$O/dram_${w}.jsonl" || exit $?
+		done
+		;;
 	rehearse8)        # 8 ranks on this one GPU: rendezvous, NUMA pinning, legs, accounting (no scaling)
 		step bench_rehearse8 900 python bench.py --gpus 8 --allow-shared-device --steps 10 --warmup 2 --no-cpu \
 			|| exit $?
