@@ -903,7 +903,8 @@ def pmc_traffic():
 # them after the headline, each with its own barrier / max-over-ranks timing:
 #   configs[3]: EC_16P2, 128 KiB cells, 8192 stripes in total, split over the
 #     N ranks by contiguous stripe ranges (strong scaling; the reference's
-#     per-stripe loop ref:src/object/cli_ec.c:627-659 is what the ranges cut);
+#     per-stripe loop ref:src/object/cli_ec.c:627-659 is what the ranges cut),
+#     and its weak form, 1024 stripes per rank;
 #   configs[4]: the EC_8P2 rebuild stream -- per rank one encode batch and one
 #     {d0,d1} recovery batch of 64 stripes, stripes in pinned host memory
 #     allocated after the rank pinned itself to its GPU's NUMA node, so the
@@ -911,8 +912,10 @@ def pmc_traffic():
 #     ref:src/object/srv_obj_migrate.c:1116-1177 is per object, so objects
 #     partition across GPUs).
 LEG_STRONG = "config3_EC_16P2_128KiB_x8192_strong"
+LEG_WEAK = "config3_EC_16P2_128KiB_x1024_per_gpu_weak"
 LEG_STREAM = "config4_EC_8P2_1MiB_rebuild_stream"
 STRONG_TOTAL = 8192
+WEAK_PER_GPU = 1024
 
 
 def split_range(total, world, rank):
@@ -938,10 +941,13 @@ def timed_leg(world, steps, warm, step, sync):
     return mine, max_over_ranks(world, mine)
 
 
-def leg_strong(args, ctx, world, rank, steps):
-    """configs[3] on this rank's contiguous share of the 8192 stripes."""
+def leg_strong(args, ctx, world, rank, steps, weak=False):
+    """configs[3] on this rank's contiguous share of the 8192 stripes (weak:
+    1024 stripes per rank, the per-GPU shard of the 8-GPU split, SURVEY §8(d)
+    config 4's weak-scaling form)."""
     k, p, C = 16, 2, 128 << 10
-    first, S = split_range(STRONG_TOTAL, world, rank)
+    total = WEAK_PER_GPU * world if weak else STRONG_TOTAL
+    first, S = split_range(total, world, rank)
     if args.rehearse:
         wl = None
         step, sync = (lambda timed: time.sleep(1e-4 * S / 1024)), (lambda: None)
@@ -960,10 +966,11 @@ def leg_strong(args, ctx, world, rank, steps):
         row["verified"] = all(wl.verify().values())      # after reading the timed launches' kernel
         wl.free()
     rows = gather(world, row)
-    return {"config": f"EC_{k}P{p} {C >> 10} KiB cells, {STRONG_TOTAL} stripes in total split over {world} "
+    return {"config": f"EC_{k}P{p} {C >> 10} KiB cells, {total} stripes in total split over {world} "
                       "rank(s) by contiguous ranges, client-layout encode, device-resident",
-            "value_GiBps": None if args.rehearse else round(STRONG_TOTAL * k * C * steps / tmax / GIB, 2),
-            "unit": "GiB/s", "scaling": "strong", "steps": steps, "ms_per_step": round(tmax / steps * 1e3, 4),
+            "value_GiBps": None if args.rehearse else round(total * k * C * steps / tmax / GIB, 2),
+            "unit": "GiB/s", "scaling": "weak" if weak else "strong", "steps": steps,
+            "ms_per_step": round(tmax / steps * 1e3, 4),
             "ranks": rows, "verified": all(r.get("verified", True) for r in rows),
             **({"rehearsal": True} if args.rehearse else {})}
 
@@ -1004,6 +1011,7 @@ def leg_stream(args, ctx, world, rank, steps, numa_info):
 def config_legs(args, ctx, world, rank, numa_info):
     steps = max(5, args.steps)
     return {LEG_STRONG: leg_strong(args, ctx, world, rank, steps),
+            LEG_WEAK: leg_strong(args, ctx, world, rank, steps, weak=True),
             LEG_STREAM: leg_stream(args, ctx, world, rank, min(steps, 10), numa_info)}
 
 

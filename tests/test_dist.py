@@ -110,6 +110,8 @@ def test_bench_gpus_n_spawns_ranks():
     strong = d["detail"]["config3_EC_16P2_128KiB_x8192_strong"]
     assert strong["scaling"] == "strong" and len(strong["ranks"]) == 2
     assert sorted((r["first_stripe"], r["stripes"]) for r in strong["ranks"]) == [(0, 4096), (4096, 4096)]
+    weak = d["detail"]["config3_EC_16P2_128KiB_x1024_per_gpu_weak"]
+    assert weak["scaling"] == "weak" and sorted(r["stripes"] for r in weak["ranks"]) == [1024, 1024]
     stream = d["detail"]["config4_EC_8P2_1MiB_rebuild_stream"]
     assert stream["scaling"] == "weak" and sorted(r["rank"] for r in stream["ranks"]) == [0, 1]
 

@@ -183,3 +183,31 @@ def test_generic_shapes_at_offset(ctx, oracle, ecglib, off, k, rows):
     finally:
         d.free()
         out.free()
+
+
+@pytest.mark.parametrize("off", [1, 2, 3, 5])
+def test_update_unaligned_cells_aligned_parity(ctx, oracle, ecglib, off):
+    """Aggregation delta update with the old / new cells at a byte offset and
+    the parity dword-aligned: the ACC + DIFF runtime kernel with
+    funnel-shifted loads of both sources (g1)."""
+    k, p, C_, S = 8, 2, 3 * 4096 + 44, 3
+    cells = [1, 6]
+    data = rand((S, k, C_), 41 + off)
+    par = oracle_parity(oracle, k, p, data)
+    new = rand((S, len(cells), C_), 42 + off)
+    old = data[:, cells].copy()
+    dold, dnew = ctx.alloc(old.nbytes + 64), ctx.alloc(new.nbytes + 64)
+    dold.upload(old.reshape(-1), offset=off)
+    dnew.upload(new.reshape(-1), offset=(off * 3) % 7)
+    dpar = ctx.to_device(par)
+    try:
+        ctx.update(k, p, C_, S, cells, dold.ptr + off, dnew.ptr + (off * 3) % 7, len(cells) * C_, dpar.ptr,
+                   S * C_, C_)
+        ctx.sync()
+        assert ecglib.last_kernel().endswith(",1,1,g1>"), ecglib.last_kernel()
+        got = dpar.download().reshape(p, S, C_)
+        data[:, cells] = new
+        assert np.array_equal(got, oracle_parity(oracle, k, p, data))
+    finally:
+        for b in (dold, dnew, dpar):
+            b.free()
