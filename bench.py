@@ -603,18 +603,20 @@ def offset_rows(ctx, aligned, iters=11):
     ref:src/object/cli_ec.c:86; user cells carry no alignment,
     ref:src/object/cli_ec.c:510-536): parity rows at +8 run the dwordx2-lane
     kernel, at +4 the dword-lane kernel; data cells at +1 (parity aligned) the
-    funnel-shift kernel; parity rows at +1 the byte kernel (on 32 stripes:
-    it is ~8x slower).  Each 512-stripe row's `of_aligned` = the aligned
-    row's ms / this ms."""
+    funnel-shift kernel; parity rows at +1 a 3-byte head per cell bytewise and
+    the rest shifted onto the funnel-shift kernel (both launches timed); parity
+    rows misaligned by different amounts (row pitch +1) the byte kernel (on 32
+    stripes: it is ~8x slower).  Each 512-stripe row's `of_aligned` = the
+    aligned row's ms / this ms."""
     from daos_amd import ecg
 
     k, p, C = 8, 2, 1 << 20
     rows = {}
     for what, off, S, warm in (("parity", 8, 512, 40), ("parity", 4, 512, 40), ("data", 1, 512, 40),
-                               ("parity", 1, 32, 2)):
+                               ("parity", 1, 512, 40), ("parity_unequal", 1, 32, 2)):
         data = ctx.alloc(S * k * C + 64)
         fill_device(ctx, data, S * k * C, 7)
-        pitch = S * C + PARITY_ROW_PAD
+        pitch = S * C + PARITY_ROW_PAD + (what == "parity_unequal")
         par = ctx.alloc(p * pitch + 64)
         doff, poff = (off, 0) if what == "data" else (0, off)
         ms = time_kernel(ctx, lambda: ctx.encode(k, p, C, S, data.ptr + doff, k * C, par.ptr + poff, pitch, C),

@@ -286,6 +286,21 @@ static const kentry g_kernels[] = {
 #define KID_READ (N_KERNELS + 2)
 #define KID_WRITE (N_KERNELS + 3)
 
+// All output cells equally far (md bytes) past a dword boundary: *head = the
+// 4 - md bytes before their first aligned dword (1).  0 if they differ.
+static bool dst_head_bytes(const ecg_mm_params_t *p, uint32_t *head)
+{
+	const uint64_t a0 = (uint64_t)(uintptr_t)p->dst + (uint64_t)p->dst_cell_off[0];
+	uint64_t diff = (uint64_t)p->dst_stripe_stride;
+
+	for (uint32_t r = 1; r < p->rows; r++)
+		diff |= (uint64_t)(p->dst_cell_off[r] - p->dst_cell_off[0]);
+	if ((diff & 3u) || (a0 & 3u) == 0)
+		return false;
+	*head = 4u - (uint32_t)(a0 & 3u);
+	return true;
+}
+
 extern "C" uint32_t ecg_k_align_granule(const ecg_mm_params_t *p)
 {
 	return align_granule(p);
@@ -374,6 +389,29 @@ extern "C" int ecg_k_launch_matmul(const ecg_mm_params_t *p, const ecg_launch_cf
 	// 1: sources at any byte, destinations dword-aligned); a destination off
 	// a dword boundary takes the byte kernel
 	const int g = (int)align_granule(p);
+	uint32_t head = 0;
+	if (variant != 2 && g == 0 && dst_head_bytes(p, &head) && p->cell_bytes > head) {
+		// every output cell starts the same md bytes past a dword boundary:
+		// the first head = 4 - md bytes of every cell bytewise, the rest as
+		// cells shifted by head bytes -- whose outputs are dword-aligned
+		// (sources at any byte: the funnel-shift kernel)
+		ecg_mm_params_t hd = *p, body = *p;
+		int e;
+
+		hd.cell_bytes = head;
+		hipLaunchKernelGGL(ecg_mm_byte_kernel, dim3((uint32_t)((head * p->nstripes + BLOCK - 1) / BLOCK < 8192
+								? (head * p->nstripes + BLOCK - 1) / BLOCK : 8192)),
+				   dim3(BLOCK), 0, st, hd);
+		e = (int)hipGetLastError();
+		if (e != (int)hipSuccess)
+			return e;
+		body.src = p->src + head;
+		if (p->diff)
+			body.src2 = p->src2 + head;
+		body.dst = p->dst + head;
+		body.cell_bytes = p->cell_bytes - head;
+		return ecg_k_launch_matmul(&body, cfg, stream, kernel_id);
+	}
 	if (variant == 2 || g == 0) {
 		uint64_t total = p->cell_bytes * p->nstripes;
 		uint64_t blocks = (total + BLOCK - 1) / BLOCK;

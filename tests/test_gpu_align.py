@@ -6,8 +6,9 @@ when all are 16-byte aligned; dword lanes (g4) for 8- and 4-byte alignment
 (DAOS rounds its parity rows to 8 bytes, ref:src/object/cli_ec.c:86); dword
 lanes whose source dwords are funnel-shifted out of aligned loads (g1: user
 sgl cells carry no alignment, ref:src/object/cli_ec.c:510-536, while DAOS
-allocates the parity aligned); the byte kernel when a destination is off a
-dword boundary.  Every case is compared byte for byte with the oracle, and
+allocates the parity aligned); destinations all equally far off a dword
+boundary run their first bytes bytewise and the rest shifted onto the vector
+paths; the byte kernel only when they are misaligned unequally.  Every case is compared byte for byte with the oracle, and
 the test asserts which kernel ran.  Offsets 1, 4, 8 and 12 of the data and/or parity bases, cells whose last
 4 KiB column is partial, and cell sizes that are not multiples of 4 / 16.
 """
@@ -29,13 +30,22 @@ def granule(*vals):
 
 
 def launch_granule(src_vals, dst_vals):
-    """ecg_kernels.hip align_granule: the common alignment of all cell
-    addresses; 1 = sources at any byte with dword-aligned destinations (the
-    funnel-shift kernel); 0 = a destination off a dword boundary (byte kernel)."""
+    """ecg_mm_dev.h align_granule + ecg_k_launch_matmul: the kernel a launch
+    runs, from its source / destination base offsets (first value) and the
+    cell offsets and strides (the rest).  16 / 4: dwordx4 / dword lanes (8-byte
+    alignment runs the dword lanes); 1: sources at any byte with dword-aligned
+    destinations (funnel shift); when every destination cell is the same
+    md bytes past a dword boundary, the launch runs the first 4 - md bytes of
+    each cell bytewise and the rest as cells shifted by that much -- the kernel
+    reported is the shifted launch's; 0: the byte kernel (destinations
+    misaligned unequally)."""
     gs, gd = granule(*src_vals), granule(*dst_vals)
-    if gd < 4:
+    if gd >= 4:
+        return 1 if gs < 4 else 16 if gs == gd == 16 else 4
+    if granule(*dst_vals[1:]) < 4:          # cells misaligned by different amounts
         return 0
-    return 1 if gs < 4 else 16 if gs == gd == 16 else 4     # 8-byte alignment runs the dword lanes
+    head = 4 - dst_vals[0] % 4
+    return launch_granule((src_vals[0] + head,) + tuple(src_vals[1:]), (dst_vals[0] + head,) + tuple(dst_vals[1:]))
 
 
 def expect_kernel(name, g, k, rows):
@@ -124,8 +134,8 @@ def test_recover_in_place_at_offset(ctx, oracle, ecglib, off, C_, errs):
     try:
         ctx.recover(k, p, C_, S, d.ptr + off, (k + p) * C_, errs)
         ctx.sync()
-        g = granule(off, (k + p) * C_, C_)         # in place: sources and destinations alike
-        expect_kernel(ecglib.last_kernel(), 0 if g < 4 else 16 if g == 16 else 4, k, len(errs))
+        vals = (off, (k + p) * C_, C_)             # in place: sources and destinations alike
+        expect_kernel(ecglib.last_kernel(), launch_granule(vals, vals), k, len(errs))
         got = d.download(stripes.nbytes, offset=off).reshape(S, k + p, C_)
         assert np.array_equal(got, stripes)
     finally:
@@ -154,8 +164,8 @@ def test_update_at_offset(ctx, oracle, ecglib, off):
         data[:, cells] = new
         assert np.array_equal(got, oracle_parity(oracle, k, p, data))
         name = ecglib.last_kernel()
-        g = granule(off, C_, len(cells) * C_, S * C_)       # the parity is read and written (ACC)
-        assert name == "ecg_mm_byte_kernel" if g == 1 else name.endswith(",1,1,g4>"), name
+        g = launch_granule((off, C_, len(cells) * C_), (off, S * C_, C_))   # the parity is read and written (ACC)
+        assert name == "ecg_mm_byte_kernel" if g == 0 else name.endswith(f",1,1,g{g}>"), name
     finally:
         for b in (dold, dnew, dpar):
             b.free()
