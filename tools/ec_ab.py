@@ -3,9 +3,11 @@ EC shapes, timed as bench.py times its detail rows: launches back to back on
 one stream with an event at every boundary (no host wait between launches),
 the median of 30 after 40 warm-up launches.  One subprocess per library and
 round, libraries rotated every round (the box's clocks drift over a run).
-The launch tuner is off (ECG_AUTOTUNE=0); every shape is timed uncapped and
-at its candidate blocks-per-CU cap (k = 16: 2, k = 8: 3).
-usage: python tools/ec_ab.py NAME=lib.so ... -> gpurun_out/ec_ab.json.
+The launch tuner is off (ECG_AUTOTUNE=0); every plain shape is timed
+uncapped and at its candidate blocks-per-CU cap (k = 16: 2, k = 8: 3).
+EC_OPS (default "enc,dec") picks the shapes: enc, dec, crc32, crc64 (the
+fused encode + parity checksums).
+usage: [EC_OPS=...] python tools/ec_ab.py NAME=lib.so ... -> gpurun_out/ec_ab.json.
 Bench infrastructure."""
 import json
 import os
@@ -36,12 +38,26 @@ def timed(fn, iters=30, warm=40):
         ctx.destroy_event(e)
     return ms[iters // 2]
 
+SHAPES = ((16, 2, 128 << 10, 1024, "enc", 0), (16, 2, 128 << 10, 1024, "dec", 0),
+          (16, 2, 128 << 10, 4096, "enc", 0), (8, 2, MiB, 512, "enc", 0),
+          (8, 2, MiB, 512, "dec", 0), (4, 2, MiB, 1024, "enc", 0), (4, 2, MiB, 1024, "dec", 0),
+          (8, 2, MiB, 512, "enc", 8), (8, 2, MiB, 512, "enc", 4),
+          (8, 2, MiB, 512, "crc32", 0), (8, 2, MiB, 512, "crc64", 0), (4, 2, MiB, 1024, "crc64", 0))
+ops = os.environ.get("EC_OPS", "enc,dec").split(",")
 res = {}
-for k, p, C, S, op, off in ((16, 2, 128 << 10, 1024, "enc", 0), (16, 2, 128 << 10, 1024, "dec", 0),
-                            (16, 2, 128 << 10, 4096, "enc", 0), (8, 2, MiB, 512, "enc", 0),
-                            (8, 2, MiB, 512, "dec", 0), (4, 2, MiB, 1024, "enc", 0), (4, 2, MiB, 1024, "dec", 0),
-                            (8, 2, MiB, 512, "enc", 8), (8, 2, MiB, 512, "enc", 4)):
-    if op == "enc":
+for k, p, C, S, op, off in (s for s in SHAPES if s[4] in ops):
+    if op.startswith("crc"):
+        # encode + checksums of the parity over 32 KiB chunks (the fused kernel), back to back
+        data = ctx.alloc(S * k * C + 64)
+        pitch = S * C + 4096
+        par = ctx.alloc(p * pitch + 64)
+        out = ctx.alloc(p * S * (C // 32768) * 8)
+        data.fill(0x3C)
+        ht = ecg.HASH_CRC32 if op == "crc32" else ecg.HASH_CRC64
+        fn = lambda: ctx.encode_csum(k, p, C, S, data.ptr, k * C, par.ptr, pitch, C, ht, 32768, 1, out.ptr)
+        bufs = (data, par, out)
+        rows = p
+    elif op == "enc":
         data = ctx.alloc(S * k * C + 64)
         pitch = S * C + 4096
         par = ctx.alloc(p * pitch + 64)
@@ -57,7 +73,7 @@ for k, p, C, S, op, off in ((16, 2, 128 << 10, 1024, "enc", 0), (16, 2, 128 << 1
         rows = 2
     alg = (k + rows) * C * S
     for cap in ((255, 2) if k >= 16 else (255, 3) if k >= 8 else (255,)):
-        if off and cap != 255:
+        if (off or op.startswith("crc")) and cap != 255:
             continue
         ctx.set_wg_per_cu(cap)
         ms = timed(fn)
