@@ -1,0 +1,163 @@
+"""Seeded random layouts through ecg_matmul, byte for byte against the oracle.
+
+The product picks its kernel per launch from the operands (ecg_kernels.hip
+ecg_k_launch_matmul: dwordx4 / dword / funnel-shift lanes, a bytewise head per
+cell when every output cell is equally far off a dword boundary, the byte
+kernel otherwise; k > 16 split into accumulating launches).  The fixed cases in
+test_gpu_align.py pin each choice; these cases draw the layout at random --
+base offsets, cell pitches, stripe strides, cell order, in-place recovery-style
+layouts where sources and outputs share one buffer, accumulate or overwrite --
+so combinations nobody wrote down still meet the oracle (the reference's
+ec_encode_data takes arbitrary pointers per cell, ref:src/object/cli_ec.c:540,
+2641).  Bytes outside the output cells must be untouched, and the kernel that
+ran must be the one `predict` (a restatement of the launch rules) names.
+"""
+import numpy as np
+import pytest
+
+N_CASES = 96
+CELLS = [1, 3, 4, 17, 255, 1000, 1024, 4095, 4096, 4097, 6000, 8192, 12288 + 20, 20000 + 3]
+CELLS16 = [16, 1024, 4096, 8192, 12288 + 16]
+
+
+def gran(bits):
+    return 16 if bits % 16 == 0 else 8 if bits % 8 == 0 else 4 if bits % 4 == 0 else 1
+
+
+def predict(C, sbase, soff, sstride, dbase, doff, dstride):
+    """The kernel class of one launch (ecg_mm_dev.h align_granule, then
+    ecg_k_launch_matmul's head split); bases are byte offsets from a
+    256-byte-aligned allocation."""
+    sb = sbase | sstride
+    for o in soff:
+        sb |= o
+    db = dbase | dstride
+    for o in doff:
+        db |= o
+    gs, gd = gran(sb), gran(db)
+    if gd >= 4:
+        return "g1" if gs < 4 else "g16" if gs == gd == 16 else "g4"
+    a0 = dbase + doff[0]
+    diff = dstride
+    for o in doff:
+        diff |= o - doff[0]
+    if diff % 4 or a0 % 4 == 0 or C <= 4 - a0 % 4:
+        return "byte"
+    h = 4 - a0 % 4
+    return predict(C - h, sbase + h, soff, sstride, dbase + h, doff, dstride)
+
+
+def draw(rng, mode):
+    """mode 0: everything 16-byte aligned; 1: dword-aligned; 2: outputs all
+    equally off a dword boundary; 3: sources at any byte; 4: anything."""
+    k = int(rng.choice([1, 2, 3, 4, 5, 8, 12, 16, 17, 24]))
+    rows = int(rng.integers(1, 7))
+    S = int(rng.integers(1, 5))
+    inplace = bool(rng.integers(0, 2)) and mode != 3
+    acc = bool(rng.integers(0, 2))
+    unit = 16 if mode == 0 else 4 if mode in (1, 2, 3) else int(rng.choice([1, 4, 16]))
+    C = int(rng.choice(CELLS16 if mode == 0 else CELLS))
+    if mode in (1, 2) and C % 4:
+        C += 4 - C % 4                      # the output stripe stride of the separate layout is C
+    pitch = -(-(C + unit * int(rng.integers(0, 3))) // unit) * unit if unit > 1 else C + int(rng.integers(0, 5))
+    pad = unit * int(rng.integers(0, 5))
+    if mode == 4:
+        sbase, dbase = int(rng.integers(0, 20)), int(rng.integers(0, 20))
+    else:
+        sbase, dbase = unit * int(rng.integers(0, 3)), unit * int(rng.integers(0, 3))
+        if mode == 2:
+            dbase += int(rng.integers(1, 4))
+            sbase = dbase if inplace else sbase
+        if mode == 3:
+            sbase += int(rng.integers(1, 4))
+    return k, rows, C, S, inplace, acc, pitch, pad, sbase, dbase
+
+
+def run_case(ctx, oracle, ecglib, seed):
+    rng = np.random.default_rng(1000 + seed)
+    k, rows, C, S, inplace, acc, pitch, pad, sbase, dbase = draw(rng, seed % 5)
+    coef = rng.integers(0, 256, (rows, k), dtype=np.uint8)
+    if inplace:
+        # one [S][k + rows][pitch] image: a random choice of cells are the sources,
+        # the rest the outputs (a degraded read's survivors and erased cells)
+        order = rng.permutation(k + rows)
+        stride = (k + rows) * pitch + pad
+        src_off = [int(c) * pitch for c in order[:k]]
+        dst_off = [int(c) * pitch for c in order[k:]]
+        img = rng.integers(0, 256, sbase + S * stride + 64, dtype=np.uint8)
+        bufs = (ctx.to_device(img),)
+        src_stride = dst_stride = stride
+        dbase = sbase
+        before = img
+    else:
+        # separate source [S][k][pitch] and output rows [rows][S][C] (+ row padding), cells in random order
+        src_stride = k * pitch + pad
+        img = rng.integers(0, 256, sbase + S * src_stride + 64, dtype=np.uint8)
+        src_off = [int(c) * pitch for c in rng.permutation(k)]
+        drow = S * C + pad
+        dst_off = [int(r) * drow for r in rng.permutation(rows)]
+        dst_stride = C
+        before = rng.integers(0, 256, dbase + rows * drow + 64, dtype=np.uint8)
+        bufs = (ctx.to_device(img), ctx.to_device(before))
+    last = src_off[(k - 1) // 16 * 16:]           # k > 16: the last launch takes the last <= 16 cells
+    want = predict(C, sbase, last, src_stride, dbase, dst_off, dst_stride)
+    try:
+        ctx.matmul(coef, C, S, bufs[0].ptr + sbase, src_off, src_stride, bufs[-1].ptr + dbase, dst_off,
+                   dst_stride, 1 if acc else 0)
+        ctx.sync()
+        kern = ecglib.last_kernel()
+        after = bufs[-1].download()
+    finally:
+        for b in bufs:
+            b.free()
+    expect = before.copy()
+    for s in range(S):
+        cells = np.stack([img[sbase + s * src_stride + o: sbase + s * src_stride + o + C] for o in src_off])
+        prod = oracle.encode_data(coef, cells)
+        for r, o in enumerate(dst_off):
+            at = dbase + s * dst_stride + o
+            expect[at: at + C] = (expect[at: at + C] ^ prod[r]) if acc else prod[r]
+    what = (f"seed {seed}: k={k} rows={rows} C={C} S={S} inplace={inplace} acc={acc} pitch={pitch} pad={pad} "
+            f"bases={sbase},{dbase} kernel={kern} predicted={want}")
+    bad = np.flatnonzero(after != expect)
+    assert bad.size == 0, f"{what}: {bad.size} bytes differ, first at {bad[0]}"
+    got = "byte" if kern == "ecg_mm_byte_kernel" else kern.rsplit(",", 1)[-1].rstrip(">") if ",g" in kern \
+        else "g16"
+    assert got == want, what
+    return got
+
+
+def test_predict_covers_every_class():
+    """The draw reaches every lane-access class (host-only check of the draw)."""
+    seen = {}
+    for seed in range(N_CASES):
+        rng = np.random.default_rng(1000 + seed)
+        k, rows, C, S, inplace, acc, pitch, pad, sbase, dbase = draw(rng, seed % 5)
+        rng.integers(0, 256, (rows, k), dtype=np.uint8)
+        if inplace:
+            order = rng.permutation(k + rows)
+            stride = (k + rows) * pitch + pad
+            cls = predict(C, sbase, [int(c) * pitch for c in order[:k]][(k - 1) // 16 * 16:], stride, sbase,
+                          [int(c) * pitch for c in order[k:]], stride)
+        else:
+            rng.integers(0, 256, sbase + S * (k * pitch + pad) + 64, dtype=np.uint8)
+            soff = [int(c) * pitch for c in rng.permutation(k)]
+            cls = predict(C, sbase, soff[(k - 1) // 16 * 16:], k * pitch + pad, dbase,
+                          [int(r) * (S * C + pad) for r in rng.permutation(rows)], C)
+        seen[cls] = seen.get(cls, 0) + 1
+    assert {"byte", "g1", "g4", "g16"} <= set(seen), seen
+    # the head split's predicted outcome differs from the plain rule for some draws
+    assert predict(4096, 0, [0], 4096, 1, [0, 8192], 4096) == "g1"
+    assert predict(4096, 0, [0], 4096, 1, [0, 8193], 4096) == "byte"
+    assert predict(4096, 1, [0], 4096, 1, [0, 8192], 4096) == "g4"
+    assert predict(2, 0, [0], 4096, 1, [0], 4096) == "byte"
+
+
+@pytest.mark.gpu
+def test_random_layouts(ctx, oracle, ecglib):
+    kernels = {}
+    for seed in range(N_CASES):
+        got = run_case(ctx, oracle, ecglib, seed)
+        kernels[got] = kernels.get(got, 0) + 1
+    print("kernels:", kernels)
+    assert {"byte", "g1", "g4", "g16"} <= set(kernels), kernels
