@@ -474,7 +474,8 @@ static inline uint32_t granule_of(uint64_t bits)
 // The lane access a launch can use: 16 when every cell address is 16-byte
 // aligned, 4 when all are dword-aligned; 1 when only the sources are off a
 // dword boundary (the funnel-shifted loads of ld_src<1>, destinations
-// dword-aligned); 0 when a destination is not dword-aligned (the byte kernel).
+// dword-aligned); 0 when a destination is not dword-aligned (ecg_k_launch_matmul
+// then runs a bytewise head and the rest shifted, or the byte kernel).
 // (ld_g / st_g also implement an 8-byte lane layout, G = 8, which no launch
 // selects.)
 static inline uint32_t align_granule(const ecg_mm_params_t *p)
