@@ -388,8 +388,10 @@ extern "C" int ecg_k_launch_matmul(const ecg_mm_params_t *p, const ecg_launch_cf
 	// the widest lane access every operand's alignment allows (16 / 8 / 4 B;
 	// 1: sources at any byte, destinations dword-aligned); a destination off
 	// a dword boundary takes the byte kernel
-	const int g = (int)align_granule(p);
+	int g = (int)align_granule(p);
 	uint32_t head = 0;
+	if (variant == 3 && g < 4)
+		g = 4;		// dword lanes at any address (the hardware's unaligned access mode)
 	if (variant != 2 && g == 0 && dst_head_bytes(p, &head) && p->cell_bytes > head) {
 		// every output cell starts the same md bytes past a dword boundary:
 		// the first head = 4 - md bytes of every cell bytewise, the rest as

@@ -102,6 +102,9 @@ for what in "$@"; do
 			rc=$?; [ $rc -eq 0 ] || exit $rc
 		done
 		;;
+	unaligned)        # dword lanes at misaligned addresses vs the launch's own choice (tools/unaligned_ab.py)
+		step unaligned_ab 300 python tools/unaligned_ab.py || exit $?
+		;;
 	csum)
 		step bench_csum 600 python tools/bench_csum.py || exit $?
 		;;

@@ -1,0 +1,76 @@
+"""Misaligned operands: the launch's own choice (variant 0: funnel-shifted
+dword lanes, bytewise head + shifted body, byte kernel) against dword lanes
+issued at the misaligned addresses themselves (variant 3: the hardware's
+unaligned access mode serves them).  EC_8P2 1 MiB client-layout encode;
+median of 20 back-to-back launches after 10; both variants' parity compared
+byte for byte.  usage: python tools/unaligned_ab.py -> gpurun_out/unaligned_ab.json.
+Bench infrastructure."""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("ECG_AUTOTUNE", "0")
+from daos_amd import ecg  # noqa: E402
+
+MiB = 1 << 20
+
+
+def timed(ctx, fn, iters=20, warm=10):
+    for _ in range(warm):
+        fn()
+    ctx.sync()
+    evs = [ctx.event() for _ in range(iters + 1)]
+    ctx.record(evs[0])
+    for i in range(iters):
+        fn()
+        ctx.record(evs[i + 1])
+    ms = sorted(ctx.elapsed_ms(evs[i], evs[i + 1]) for i in range(iters))
+    for e in evs:
+        ctx.destroy_event(e)
+    return ms[iters // 2]
+
+
+def main():
+    ctx = ecg.Context(0)
+    k, p, C = 8, 2, MiB
+    res = {}
+    # name, stripes, data offset, parity offset, extra parity row pitch
+    cases = (("aligned", 512, 0, 0, 0), ("data_off1", 512, 1, 0, 0), ("parity_off1", 512, 0, 1, 0),
+             ("parity_off2_data_off1", 512, 1, 2, 0), ("parity_off1_unequal", 64, 0, 1, 1),
+             ("data_off3_parity_off1_unequal", 64, 3, 1, 1))
+    for name, S, doff, poff, extra in cases:
+        data = ctx.alloc(S * k * C + 64)
+        data.fill(0x3C)
+        data.upload(np.random.default_rng(S + doff).integers(0, 256, 64 * MiB, dtype=np.uint8))
+        pitch = S * C + 4096 + extra
+        par = ctx.alloc(p * pitch + 64)
+        row = {"stripes": S}
+        outs = {}
+        for variant in (0, 3):
+            ctx.set_launch(0, 0, variant)
+            fn = lambda: ctx.encode(k, p, C, S, data.ptr + doff, k * C, par.ptr + poff, pitch, C)
+            par.fill(0)
+            ms = timed(ctx, fn)
+            alg = (k + p) * C * S
+            row[f"v{variant}"] = {"ms": round(ms, 4), "alg_GBps": round(alg / ms / 1e6, 1),
+                                  "kernel": ecg.last_kernel()}
+            outs[variant] = par.download()
+        ctx.set_launch(0, 0, 0)
+        row["v3_over_v0"] = round(row["v0"]["ms"] / row["v3"]["ms"], 4)
+        row["equal"] = bool(np.array_equal(outs[0], outs[3]))
+        res[name] = row
+        print(name, json.dumps(row), flush=True)
+        data.free()
+        par.free()
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "unaligned_ab.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    assert all(r["equal"] for r in res.values()), "variant 3 parity differs"
+
+
+if __name__ == "__main__":
+    main()
