@@ -601,26 +601,31 @@ def offset_rows(ctx, aligned, iters=11):
     """EC_8P2 1 MiB client-layout encode with operands at a byte offset of
     their allocation (DAOS rounds parity rows to 8 bytes only,
     ref:src/object/cli_ec.c:86; user cells carry no alignment,
-    ref:src/object/cli_ec.c:510-536): parity rows at +8 run the dwordx2-lane
-    kernel, at +4 the dword-lane kernel; data cells at +1 (parity aligned) the
-    funnel-shift kernel; parity rows at +1 a 3-byte head per cell bytewise and
-    the rest shifted onto the funnel-shift kernel (both launches timed); parity
-    rows misaligned by different amounts (row pitch +1) the byte kernel (on 32
-    stripes: it is ~8x slower).  Each 512-stripe row's `of_aligned` = the
+    ref:src/object/cli_ec.c:510-536): parity rows at +8 or +4 run the
+    dword-lane kernel, at +1 (and at +1 with rows misaligned by different
+    amounts: row pitch +1) the same lanes with misaligned dword stores; data
+    cells at +1 the funnel-shift kernel.  The byte kernel, which the launcher
+    no longer picks (launch variant 2 forces it), is timed on 32 stripes for
+    the record: it is ~8x slower.  Each 512-stripe row's `of_aligned` = the
     aligned row's ms / this ms."""
     from daos_amd import ecg
 
     k, p, C = 8, 2, 1 << 20
     rows = {}
     for what, off, S, warm in (("parity", 8, 512, 40), ("parity", 4, 512, 40), ("data", 1, 512, 40),
-                               ("parity", 1, 512, 40), ("parity_unequal", 1, 32, 2)):
+                               ("parity", 1, 512, 40), ("parity_unequal", 1, 512, 40),
+                               ("parity_byte_kernel", 1, 32, 2)):
         data = ctx.alloc(S * k * C + 64)
         fill_device(ctx, data, S * k * C, 7)
         pitch = S * C + PARITY_ROW_PAD + (what == "parity_unequal")
         par = ctx.alloc(p * pitch + 64)
         doff, poff = (off, 0) if what == "data" else (0, off)
-        ms = time_kernel(ctx, lambda: ctx.encode(k, p, C, S, data.ptr + doff, k * C, par.ptr + poff, pitch, C),
-                         iters, warm=warm)
+        ctx.set_launch(0, 0, 2 if what == "parity_byte_kernel" else 0)
+        try:
+            ms = time_kernel(ctx, lambda: ctx.encode(k, p, C, S, data.ptr + doff, k * C, par.ptr + poff, pitch,
+                                                     C), iters, warm=warm)
+        finally:
+            ctx.set_launch(0, 0, 0)
         alg = (k + p) * C * S
         row = {f"{what}_offset_bytes": off, "stripes": S, "ms": round(ms, 4),
                "GiBps_user": round(k * C * S / (ms / 1e3) / GIB, 1), "alg_GBps": round(alg / ms / 1e6, 1),

@@ -95,10 +95,8 @@ static int ptr_granule(const uint64_t *tab, uint32_t S, int k, int rows)
 		for (int r = 0; r < rows; r++)
 			out |= t[k + r];
 	}
-	if (out & 3u)
-		return 0;
 	if (in & 3u)
-		return 1;
+		return 1;	/* outputs at any byte: misaligned dword stores */
 	return ((in | out) & 15u) == 0 ? 16 : 4;
 }
 

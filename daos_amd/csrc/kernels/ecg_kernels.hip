@@ -153,13 +153,14 @@ ecg_mm_sel_kernel(const ecg_mm_params_t P, const uint8_t *__restrict__ sel, uint
 			else if (cbase + lo + 16 <= C)
 				mm_item<1, RM, false, false>(P, tb, 1, rows, s, cbase, lo);
 			else if (cbase + lo < C)
-				mm_tail<RM, false, false>(P, tb, 1, rows, s, cbase + lo, (int)(C - cbase - lo));
+				mm_tail<1, RM, false, false>(P, tb, 1, rows, s, cbase + lo, (int)(C - cbase - lo));
 		}
 	}
 }
 
-// Any alignment, any length: one byte per lane-iteration.  Used only when a
-// caller hands cell bases/strides that are not 16-byte aligned.
+// Any alignment, any length: one byte per lane-iteration.  Not chosen by the
+// launcher (the lane kernels take every alignment); forced by launch variant
+// 2 as a second, independent implementation for tests and A/B runs.
 __global__ void __launch_bounds__(BLOCK)
 ecg_mm_byte_kernel(const ecg_mm_params_t P)
 {
@@ -288,19 +289,6 @@ static const kentry g_kernels[] = {
 
 // All output cells equally far (md bytes) past a dword boundary: *head = the
 // 4 - md bytes before their first aligned dword (1).  0 if they differ.
-static bool dst_head_bytes(const ecg_mm_params_t *p, uint32_t *head)
-{
-	const uint64_t a0 = (uint64_t)(uintptr_t)p->dst + (uint64_t)p->dst_cell_off[0];
-	uint64_t diff = (uint64_t)p->dst_stripe_stride;
-
-	for (uint32_t r = 1; r < p->rows; r++)
-		diff |= (uint64_t)(p->dst_cell_off[r] - p->dst_cell_off[0]);
-	if ((diff & 3u) || (a0 & 3u) == 0)
-		return false;
-	*head = 4u - (uint32_t)(a0 & 3u);
-	return true;
-}
-
 extern "C" uint32_t ecg_k_align_granule(const ecg_mm_params_t *p)
 {
 	return align_granule(p);
@@ -385,36 +373,13 @@ extern "C" int ecg_k_launch_matmul(const ecg_mm_params_t *p, const ecg_launch_cf
 	if (p->nstripes == 0 || p->cell_bytes == 0 || p->rows == 0)
 		return (int)hipSuccess;
 
-	// the widest lane access every operand's alignment allows (16 / 8 / 4 B;
-	// 1: sources at any byte, destinations dword-aligned); a destination off
-	// a dword boundary takes the byte kernel
+	// the widest lane access every operand's alignment allows (16 / 4 B;
+	// 1: a source at any byte -- funnel-shifted loads); destinations at any
+	// byte take the dword lanes' (misaligned) stores
 	int g = (int)align_granule(p);
-	uint32_t head = 0;
 	if (variant == 3 && g < 4)
-		g = 4;		// dword lanes at any address (the hardware's unaligned access mode)
-	if (variant != 2 && g == 0 && dst_head_bytes(p, &head) && p->cell_bytes > head) {
-		// every output cell starts the same md bytes past a dword boundary:
-		// the first head = 4 - md bytes of every cell bytewise, the rest as
-		// cells shifted by head bytes -- whose outputs are dword-aligned
-		// (sources at any byte: the funnel-shift kernel)
-		ecg_mm_params_t hd = *p, body = *p;
-		int e;
-
-		hd.cell_bytes = head;
-		hipLaunchKernelGGL(ecg_mm_byte_kernel, dim3((uint32_t)((head * p->nstripes + BLOCK - 1) / BLOCK < 8192
-								? (head * p->nstripes + BLOCK - 1) / BLOCK : 8192)),
-				   dim3(BLOCK), 0, st, hd);
-		e = (int)hipGetLastError();
-		if (e != (int)hipSuccess)
-			return e;
-		body.src = p->src + head;
-		if (p->diff)
-			body.src2 = p->src2 + head;
-		body.dst = p->dst + head;
-		body.cell_bytes = p->cell_bytes - head;
-		return ecg_k_launch_matmul(&body, cfg, stream, kernel_id);
-	}
-	if (variant == 2 || g == 0) {
+		g = 4;		// A/B: misaligned source dwords loaded as they are
+	if (variant == 2) {
 		uint64_t total = p->cell_bytes * p->nstripes;
 		uint64_t blocks = (total + BLOCK - 1) / BLOCK;
 		if (blocks > 8192)

@@ -62,8 +62,8 @@ __device__ __forceinline__ uint32_t elem_off(int i)
 	return G == 16 ? 4u * i : G == 8 ? (uint32_t)(i >> 1) * 512u + (uint32_t)(i & 1) * 4u : (uint32_t)i * 256u;
 }
 
-// G = 1 (sources at any byte alignment, destinations dword-aligned): the
-// dword layout of G = 4 for the lanes and every store; a source dword at
+// G = 1 (sources at any byte alignment): the dword layout of G = 4 for the
+// lanes and every store (and ACC read) of the destinations; a source dword at
 // byte address a is funnel-shifted out of the aligned dwords around it,
 // v_alignbyte_b32(hi, lo, a & 3).  hi holds byte a + 3, so it never leaves
 // the cell's pages; when a is aligned hi is read from lo's own address
@@ -73,7 +73,7 @@ template <int G>
 __device__ __forceinline__ u32x4 ld_g(const uint8_t *p)
 {
 	if constexpr (G == 1) {
-		return ld_g<4>(p);	// destinations (ACC reads) are dword-aligned
+		return ld_g<4>(p);	// destinations (ACC reads)
 	} else if constexpr (G == 16) {
 		return ld_nt(p);
 	} else if constexpr (G == 8) {
@@ -323,14 +323,19 @@ __device__ __forceinline__ void mm_item(const ecg_mm_params_t &P, const u32x4 *t
 }
 
 // One dword of every output row at byte offset `off` of the cells (the
-// partial last column of a G = 4 / 8 launch: off is a multiple of 4 and the
-// dword lies inside the cell).
-template <int RM, bool ACC, bool DIFF>
+// partial last column of a G = 4 / 1 launch: the dword lies inside the cell).
+// The k loads are issued together.  Cells off a dword boundary (G = 1, and
+// destinations at any byte) are read and written with misaligned dword
+// accesses, which the hardware's unaligned access mode serves (the ROCm
+// default on gfx9+; the compiler itself emits such accesses for byte-aligned
+// data).
+template <int KM, int RM, bool ACC, bool DIFF>
 __device__ __forceinline__ void mm_dword(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
 					 uint32_t s, uint64_t off)
 {
 	constexpr int T2V = (RM + 3) / 4;
 	constexpr int PER_J = RM + T2V;
+	constexpr int JB = KM < 4 ? KM : 4;	// loads in flight (more cost k = 16 a wave per SIMD)
 	const uint8_t *sb = P.src + (int64_t)s * P.src_stripe_stride + off;
 	const uint8_t *sb2 = DIFF ? P.src2 + (int64_t)s * P.src2_stripe_stride + off : nullptr;
 	uint8_t *db = P.dst + (int64_t)s * P.dst_stripe_stride + off;
@@ -339,18 +344,41 @@ __device__ __forceinline__ void mm_dword(const ecg_mm_params_t &P, const u32x4 *
 #pragma unroll
 	for (int r = 0; r < RM; r++)
 		o[r] = 0;
-	for (int j = 0; j < k; j++) {
-		uint32_t v = *reinterpret_cast<const uint32_t *>(sb + P.src_cell_off[j]);
-		if (DIFF)
-			v ^= *reinterpret_cast<const uint32_t *>(sb2 + P.src2_cell_off[j]);
-		const uint32_t s0 = v & 0x07070707u, s1 = (v >> 3) & 0x07070707u, s2 = (v >> 6) & 0x03030303u;
+#pragma nounroll
+	for (int j0 = 0; j0 < k; j0 += JB) {
+		uint32_t x[JB];
+
 #pragma unroll
-		for (int r = 0; r < RM; r++) {
-			if (r < rows) {
-				const u32x4 t = tb[j * PER_J + r];
-				const uint32_t t2 = reinterpret_cast<const uint32_t *>(&tb[j * PER_J + RM])[r];
-				o[r] ^= __builtin_amdgcn_perm(t[1], t[0], s0) ^ __builtin_amdgcn_perm(t[3], t[2], s1) ^
-					__builtin_amdgcn_perm(t2, t2, s2);
+		for (int i = 0; i < JB; i++) {
+			if (j0 + i < k) {
+				// laundered like mm_load's: LICM would hoist the unrolled
+				// cell offsets out of the stripe loop into VGPRs
+				int64_t o1 = P.src_cell_off[j0 + i];
+				asm volatile("" : "+s"(o1));
+				x[i] = *reinterpret_cast<const uint32_t *>(sb + o1);
+				if (DIFF) {
+					int64_t o2 = P.src2_cell_off[j0 + i];
+					asm volatile("" : "+s"(o2));
+					x[i] ^= *reinterpret_cast<const uint32_t *>(sb2 + o2);
+				}
+			}
+		}
+#pragma unroll
+		for (int i = 0; i < JB; i++) {
+			const int j = j0 + i;
+
+			if (j >= k)
+				continue;
+			const uint32_t v = x[i];
+			const uint32_t s0 = v & 0x07070707u, s1 = (v >> 3) & 0x07070707u, s2 = (v >> 6) & 0x03030303u;
+#pragma unroll
+			for (int r = 0; r < RM; r++) {
+				if (r < rows) {
+					const u32x4 t = tb[j * PER_J + r];
+					const uint32_t t2 = reinterpret_cast<const uint32_t *>(&tb[j * PER_J + RM])[r];
+					o[r] ^= __builtin_amdgcn_perm(t[1], t[0], s0) ^ __builtin_amdgcn_perm(t[3], t[2], s1) ^
+						__builtin_amdgcn_perm(t2, t2, s2);
+				}
 			}
 		}
 	}
@@ -363,13 +391,15 @@ __device__ __forceinline__ void mm_dword(const ecg_mm_params_t &P, const u32x4 *
 	}
 }
 
-// Ragged tail: fewer than 16 bytes of this lane's slot are inside the cell.
-template <int RM, bool ACC, bool DIFF>
+// Ragged tail: fewer than 16 bytes of this lane's slot are inside the cell;
+// bytewise, up to 8 of a byte's k loads issued together.
+template <int KM, int RM, bool ACC, bool DIFF>
 __device__ __forceinline__ void mm_tail(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
 				     uint32_t s, uint64_t off, int nb)
 {
 	constexpr int T2V = (RM + 3) / 4;
 	constexpr int PER_J = RM + T2V;
+	constexpr int JB = KM < 4 ? KM : 4;
 	const uint8_t *sb = P.src + (int64_t)s * P.src_stripe_stride;
 	const uint8_t *sb2 = DIFF ? P.src2 + (int64_t)s * P.src2_stripe_stride : nullptr;
 	uint8_t *db = P.dst + (int64_t)s * P.dst_stripe_stride;
@@ -379,19 +409,40 @@ __device__ __forceinline__ void mm_tail(const ecg_mm_params_t &P, const u32x4 *t
 #pragma unroll
 		for (int r = 0; r < RM; r++)
 			o[r] = 0;
-		for (int j = 0; j < k; j++) {
-			uint32_t v = sb[P.src_cell_off[j] + off + b];
-			if (DIFF)
-				v ^= sb2[P.src2_cell_off[j] + off + b];
-			const uint32_t s0 = v & 7u, s1 = (v >> 3) & 7u, s2 = v >> 6;
+#pragma nounroll
+		for (int j0 = 0; j0 < k; j0 += JB) {
+			uint32_t x[JB];
+
 #pragma unroll
-			for (int r = 0; r < RM; r++) {
-				if (r < rows) {
-					const u32x4 t = tb[j * PER_J + r];
-					const uint32_t t2 = reinterpret_cast<const uint32_t *>(&tb[j * PER_J + RM])[r];
-					o[r] ^= __builtin_amdgcn_perm(t[1], t[0], s0) ^
-						__builtin_amdgcn_perm(t[3], t[2], s1) ^
-						__builtin_amdgcn_perm(t2, t2, s2);
+			for (int i = 0; i < JB; i++) {
+				if (j0 + i < k) {
+					int64_t o1 = P.src_cell_off[j0 + i];
+					asm volatile("" : "+s"(o1));
+					x[i] = sb[o1 + off + b];
+					if (DIFF) {
+						int64_t o2 = P.src2_cell_off[j0 + i];
+						asm volatile("" : "+s"(o2));
+						x[i] ^= sb2[o2 + off + b];
+					}
+				}
+			}
+#pragma unroll
+			for (int i = 0; i < JB; i++) {
+				const int j = j0 + i;
+
+				if (j >= k)
+					continue;
+				const uint32_t v = x[i];
+				const uint32_t s0 = v & 7u, s1 = (v >> 3) & 7u, s2 = v >> 6;
+#pragma unroll
+				for (int r = 0; r < RM; r++) {
+					if (r < rows) {
+						const u32x4 t = tb[j * PER_J + r];
+						const uint32_t t2 = reinterpret_cast<const uint32_t *>(&tb[j * PER_J + RM])[r];
+						o[r] ^= __builtin_amdgcn_perm(t[1], t[0], s0) ^
+							__builtin_amdgcn_perm(t[3], t[2], s1) ^
+							__builtin_amdgcn_perm(t2, t2, s2);
+					}
 				}
 			}
 		}
@@ -407,8 +458,8 @@ __device__ __forceinline__ void mm_tail(const ecg_mm_params_t &P, const u32x4 *t
 
 // The last, partial column of a cell (C % 4096 != 0): G = 16 as a full
 // lane piece where the lane's 16 bytes are inside the cell, else bytewise;
-// G = 4 / 8 dword by dword, the bytes after the cell's last whole dword
-// bytewise.
+// G = 4 / 1 dword by dword (G = 1: misaligned source dwords), the bytes
+// after the cell's last whole dword bytewise.
 template <int KM, int RM, bool ACC, bool DIFF, int G>
 __device__ __forceinline__ void mm_partial(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
 					   uint32_t s, uint64_t cbase, uint32_t lo)
@@ -419,7 +470,7 @@ __device__ __forceinline__ void mm_partial(const ecg_mm_params_t &P, const u32x4
 		if (cbase + lo + 16 <= C)
 			mm_item<KM, RM, ACC, DIFF>(P, tb, k, rows, s, cbase, lo);
 		else if (cbase + lo < C)
-			mm_tail<RM, ACC, DIFF>(P, tb, k, rows, s, cbase + lo, (int)(C - cbase - lo));
+			mm_tail<KM, RM, ACC, DIFF>(P, tb, k, rows, s, cbase + lo, (int)(C - cbase - lo));
 	} else {
 		// not unrolled: four inlined copies of the byte loop cost ~70 VGPRs
 		// in every instantiation (this path runs once per cell at most)
@@ -427,11 +478,10 @@ __device__ __forceinline__ void mm_partial(const ecg_mm_params_t &P, const u32x4
 		for (int i = 0; i < 4; i++) {
 			const uint64_t off = cbase + lo + elem_off<G>(i);
 
-			// G = 1: the sources are not dword-aligned, so bytewise
-			if (G != 1 && off + 4 <= C)
-				mm_dword<RM, ACC, DIFF>(P, tb, k, rows, s, off);
+			if (off + 4 <= C)
+				mm_dword<KM, RM, ACC, DIFF>(P, tb, k, rows, s, off);
 			else if (off < C)
-				mm_tail<RM, ACC, DIFF>(P, tb, k, rows, s, off, (int)(C - off < 4 ? C - off : 4));
+				mm_tail<KM, RM, ACC, DIFF>(P, tb, k, rows, s, off, (int)(C - off));
 		}
 	}
 }
@@ -471,11 +521,13 @@ static inline uint32_t granule_of(uint64_t bits)
 	return (bits & 15u) == 0 ? 16u : (bits & 7u) == 0 ? 8u : (bits & 3u) == 0 ? 4u : 1u;
 }
 
-// The lane access a launch can use: 16 when every cell address is 16-byte
-// aligned, 4 when all are dword-aligned; 1 when only the sources are off a
-// dword boundary (the funnel-shifted loads of ld_src<1>, destinations
-// dword-aligned); 0 when a destination is not dword-aligned (ecg_k_launch_matmul
-// then runs a bytewise head and the rest shifted, or the byte kernel).
+// The lane access a launch uses: 16 when every cell address is 16-byte
+// aligned, 4 when every source is dword-aligned; 1 when a source is off a
+// dword boundary (the funnel-shifted loads of ld_src<1>).  Destinations off a
+// dword boundary take the dword lanes' stores as they are: misaligned dword
+// stores (and ACC loads), served by the hardware's unaligned access mode,
+// ran 0.96 of the aligned kernel where the byte kernel ran 0.13
+// (tools/unaligned_ab.py, profiles/r04/unaligned_ab/).
 // (ld_g / st_g also implement an 8-byte lane layout, G = 8, which no launch
 // selects.)
 static inline uint32_t align_granule(const ecg_mm_params_t *p)
@@ -493,8 +545,6 @@ static inline uint32_t align_granule(const ecg_mm_params_t *p)
 		db |= (uint64_t)p->dst_cell_off[r];
 	const uint32_t gs = granule_of(sb), gd = granule_of(db);
 
-	if (gd < 4)
-		return 0;
 	if (gs < 4)
 		return 1;
 	/* 8-byte alignment takes the dword lanes too: the dwordx2-lane variant

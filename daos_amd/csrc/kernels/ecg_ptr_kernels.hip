@@ -9,10 +9,10 @@
 // cell j-k of stripe s.  Same columns, tables and arithmetic as ecg_mm_kernel
 // (ecg_mm_dev.h); a stripe's k+rows addresses are wave-uniform (scalar loads).
 // The lane access G follows the cells' alignment exactly as the offset kernel:
-// 16 (every address and the cell size 16-byte aligned), 4 (all dword-aligned),
-// 1 (outputs dword-aligned, inputs at any byte: each input dword funnel-shifted
-// out of aligned loads, ld_src<1>); outputs off a dword boundary take the
-// byte kernel.
+// 16 (every address and the cell size 16-byte aligned), 4 (every input
+// dword-aligned), 1 (an input at any byte: each input dword funnel-shifted out
+// of aligned loads, ld_src<1>); outputs at any byte take misaligned dword
+// stores (the hardware's unaligned access mode, ecg_mm_dev.h mm_dword).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -36,37 +36,65 @@ __device__ __forceinline__ void mm_ptr_item(const ecg_mm_params_t &P, const u32x
 			st_g<G>(reinterpret_cast<uint8_t *>(a[KM + r]) + lo, outv[r]);
 }
 
-// nb (< 4 or one dword read bytewise) bytes at column offset `off` of every
-// cell: the partial last column of the G = 4 / 1 kernels
+// The partial last column of the G = 4 / 1 kernels, at column offset `off`
+// of every cell: one dword (nb = 4; misaligned cells read and written as they
+// are) or the nb < 4 bytes after the cell's last whole dword.  The cell
+// addresses come from the stripe's table row `pt` (scalar loads), up to 8
+// cells' loads in flight.
 template <int KM, int RM>
-__device__ __forceinline__ void mm_ptr_bytes(const u32x4 *tb, int k, int rows, const uint64_t *a, uint64_t off,
+__device__ __forceinline__ void mm_ptr_bytes(const u32x4 *tb, int k, int rows, const uint64_t *pt, uint64_t off,
 					     int nb)
 {
 	constexpr int T2V = (RM + 3) / 4;
 	constexpr int PER_J = RM + T2V;
+	constexpr int JB = KM < 4 ? KM : 4;
+	const bool dw = nb == 4;
 
-	for (int b = 0; b < nb; b++) {
+	for (int b = 0; b < (dw ? 1 : nb); b++) {
 		uint32_t o[RM];
 #pragma unroll
 		for (int r = 0; r < RM; r++)
 			o[r] = 0;
-		for (int j = 0; j < k; j++) {
-			const uint32_t v = reinterpret_cast<const uint8_t *>(a[j])[off + b];
-			const uint32_t s0 = v & 7u, s1 = (v >> 3) & 7u, s2 = v >> 6;
+#pragma nounroll
+		for (int j0 = 0; j0 < k; j0 += JB) {
+			uint32_t x[JB];
+
 #pragma unroll
-			for (int r = 0; r < RM; r++) {
-				if (r < rows) {
-					const u32x4 t = tb[j * PER_J + r];
-					const uint32_t t2 = reinterpret_cast<const uint32_t *>(&tb[j * PER_J + RM])[r];
-					o[r] ^= __builtin_amdgcn_perm(t[1], t[0], s0) ^ __builtin_amdgcn_perm(t[3], t[2], s1) ^
-						__builtin_amdgcn_perm(t2, t2, s2);
+			for (int i = 0; i < JB; i++) {
+				if (j0 + i < k) {
+					const uint8_t *c = reinterpret_cast<const uint8_t *>(pt[j0 + i]) + off;
+					x[i] = dw ? *reinterpret_cast<const uint32_t *>(c) : (uint32_t)c[b];
+				}
+			}
+#pragma unroll
+			for (int i = 0; i < JB; i++) {
+				const int j = j0 + i;
+
+				if (j >= k)
+					continue;
+				const uint32_t v = x[i];
+				const uint32_t s0 = v & 0x07070707u, s1 = (v >> 3) & 0x07070707u, s2 = (v >> 6) & 0x03030303u;
+#pragma unroll
+				for (int r = 0; r < RM; r++) {
+					if (r < rows) {
+						const u32x4 t = tb[j * PER_J + r];
+						const uint32_t t2 = reinterpret_cast<const uint32_t *>(&tb[j * PER_J + RM])[r];
+						o[r] ^= __builtin_amdgcn_perm(t[1], t[0], s0) ^
+							__builtin_amdgcn_perm(t[3], t[2], s1) ^ __builtin_amdgcn_perm(t2, t2, s2);
+					}
 				}
 			}
 		}
 #pragma unroll
-		for (int r = 0; r < RM; r++)
-			if (r < rows)
-				reinterpret_cast<uint8_t *>(a[KM + r])[off + b] = (uint8_t)o[r];
+		for (int r = 0; r < RM; r++) {
+			if (r < rows) {
+				uint8_t *d = reinterpret_cast<uint8_t *>(pt[k + r]) + off;
+				if (dw)
+					*reinterpret_cast<uint32_t *>(d) = o[r];
+				else
+					d[b] = (uint8_t)o[r];
+			}
+		}
 	}
 }
 
@@ -125,25 +153,22 @@ ecg_mm_ptr_kernel(const ecg_mm_params_t P, const uint64_t *__restrict__ cells)
 				if (cbase + lo + 16 <= C)	// C % 16 == 0 on this path
 					mm_ptr_item<KM, RM, G>(P, tb, k, rows, s, cbase, lo, a);
 			} else {
-				// the partial last column, bytewise per dword of the lane
+				// the partial last column, dword by dword of the lane
 				// (once per cell; a loop, not four inlined copies)
-				uint64_t ab[KM + RM];
-#pragma unroll
-				for (int j = 0; j < KM + RM; j++)
-					ab[j] = (j < k || (j >= KM && j - KM < rows)) ? base[j] : 0;
 #pragma nounroll
 				for (int i = 0; i < 4; i++) {
 					const uint64_t off = cbase + lo + elem_off<G>(i);
 
 					if (off < C)
-						mm_ptr_bytes<KM, RM>(tb, k, rows, ab, off, (int)(C - off < 4 ? C - off : 4));
+						mm_ptr_bytes<KM, RM>(tb, k, rows, pt, off, (int)(C - off < 4 ? C - off : 4));
 				}
 			}
 		}
 	}
 }
 
-// Pointer-table product, any alignment and length: one byte per lane.
+// Pointer-table product, any alignment and length: one byte per lane (launch
+// variant 2 only: a second implementation for tests and A/B runs).
 __global__ void __launch_bounds__(BLOCK)
 ecg_mm_ptr_byte_kernel(const ecg_mm_params_t P, const uint64_t *cells)
 {
@@ -213,7 +238,7 @@ extern "C" int ecg_k_launch_matmul_ptrs(const ecg_mm_params_t *p, const uint64_t
 		return (int)hipSuccess;
 	if (g == 16 && (p->cell_bytes & 15u))	// the 16-byte lanes need whole 16-byte pieces
 		g = 4;
-	if (g == 0 || (cfg && cfg->variant == 2)) {
+	if (cfg && cfg->variant == 2) {
 		uint64_t blocks = (p->cell_bytes * p->nstripes + BLOCK - 1) / BLOCK;
 		if (blocks > 8192)
 			blocks = 8192;

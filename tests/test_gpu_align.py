@@ -6,9 +6,9 @@ when all are 16-byte aligned; dword lanes (g4) for 8- and 4-byte alignment
 (DAOS rounds its parity rows to 8 bytes, ref:src/object/cli_ec.c:86); dword
 lanes whose source dwords are funnel-shifted out of aligned loads (g1: user
 sgl cells carry no alignment, ref:src/object/cli_ec.c:510-536, while DAOS
-allocates the parity aligned); destinations all equally far off a dword
-boundary run their first bytes bytewise and the rest shifted onto the vector
-paths; the byte kernel only when they are misaligned unequally.  Every case is compared byte for byte with the oracle, and
+allocates the parity aligned); destinations at any byte take the
+same lanes' stores as misaligned dwords (the hardware's unaligned access
+mode).  Every case is compared byte for byte with the oracle, and
 the test asserts which kernel ran.  Offsets 1, 4, 8 and 12 of the data and/or parity bases, cells whose last
 4 KiB column is partial, and cell sizes that are not multiples of 4 / 16.
 """
@@ -30,22 +30,13 @@ def granule(*vals):
 
 
 def launch_granule(src_vals, dst_vals):
-    """ecg_mm_dev.h align_granule + ecg_k_launch_matmul: the kernel a launch
-    runs, from its source / destination base offsets (first value) and the
-    cell offsets and strides (the rest).  16 / 4: dwordx4 / dword lanes (8-byte
-    alignment runs the dword lanes); 1: sources at any byte with dword-aligned
-    destinations (funnel shift); when every destination cell is the same
-    md bytes past a dword boundary, the launch runs the first 4 - md bytes of
-    each cell bytewise and the rest as cells shifted by that much -- the kernel
-    reported is the shifted launch's; 0: the byte kernel (destinations
-    misaligned unequally)."""
+    """ecg_mm_dev.h align_granule: the lanes a launch runs, from its source /
+    destination base offsets, cell offsets and strides.  16 / 4: dwordx4 /
+    dword lanes (8-byte alignment runs the dword lanes); 1: a source at any
+    byte (funnel-shifted loads).  Destinations at any byte take the lanes'
+    stores as misaligned dwords; the byte kernel (0) is never chosen."""
     gs, gd = granule(*src_vals), granule(*dst_vals)
-    if gd >= 4:
-        return 1 if gs < 4 else 16 if gs == gd == 16 else 4
-    if granule(*dst_vals[1:]) < 4:          # cells misaligned by different amounts
-        return 0
-    head = 4 - dst_vals[0] % 4
-    return launch_granule((src_vals[0] + head,) + tuple(src_vals[1:]), (dst_vals[0] + head,) + tuple(dst_vals[1:]))
+    return 1 if gs < 4 else 16 if gs == gd == 16 else 4
 
 
 def expect_kernel(name, g, k, rows):
@@ -70,8 +61,8 @@ CELLS = [65536, 2 * 4096 + 1024 + 8, 3 * 4096 + 20, 4096 + 13]
                                        (8, 8), (4, 12), (12, 8)])
 def test_encode_offsets(ctx, oracle, ecglib, C_, doff, poff):
     """Client-layout encode (data [S][k][C] -> parity [p][S][C]) with the data
-    and parity bases at byte offsets: the launch runs the g4 / g1 / byte
-    kernels as the addresses allow, with the oracle's parity."""
+    and parity bases at byte offsets: the launch runs the 16 / g4 / g1 lanes
+    as the addresses allow, with the oracle's parity."""
     k, p, S = 8, 2, 3
     data = rand((S, k, C_), C_ + doff * 16 + poff)
     d = ctx.alloc(data.nbytes + 64)
@@ -165,7 +156,7 @@ def test_update_at_offset(ctx, oracle, ecglib, off):
         assert np.array_equal(got, oracle_parity(oracle, k, p, data))
         name = ecglib.last_kernel()
         g = launch_granule((off, C_, len(cells) * C_), (off, S * C_, C_))   # the parity is read and written (ACC)
-        assert name == "ecg_mm_byte_kernel" if g == 0 else name.endswith(f",1,1,g{g}>"), name
+        assert name.endswith(f",1,1,g{g}>") if g < 16 else name.endswith(",1,1>"), name
     finally:
         for b in (dold, dnew, dpar):
             b.free()

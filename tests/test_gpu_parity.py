@@ -109,21 +109,33 @@ def test_accumulate_flag(ctx, oracle):
         assert np.array_equal(got[s], base[s] ^ oracle.encode_data(coef, data[s]))
 
 
-def test_misaligned_cells_byte_kernel(ctx, oracle, ecglib):
-    """Cells at odd byte offsets (user sgl offsets carry no alignment,
-    SURVEY §8b) take the byte kernel; same bytes."""
+@pytest.mark.parametrize("variant,kernel", [(0, "ecg_mm_kernel<4,2,0,0,g1>"), (2, "ecg_mm_byte_kernel")])
+def test_misaligned_cells(ctx, oracle, ecglib, variant, kernel):
+    """Cells at odd byte offsets and an odd cell size (user sgl offsets carry
+    no alignment): the funnel-shift lanes with misaligned dword
+    stores, and the byte kernel (launch variant 2, the independent second
+    implementation); same bytes."""
     k, p, C_, S = 4, 2, 1001, 3
     data = rand((S, k, C_), 11)
     buf = np.zeros(S * k * C_ + 64, dtype=np.uint8)
     buf[3:3 + data.size] = data.reshape(-1)
     d = ctx.to_device(buf)
     par = ctx.alloc(p * S * C_ + 64)
+    par.fill(0xEE)
     coef = oracle.cauchy1(k, p)[k:]
-    ctx.matmul(coef, C_, S, d.ptr + 3, [j * C_ for j in range(k)], k * C_, par.ptr + 5,
-               [r * S * C_ for r in range(p)], C_, 0)
-    assert ecglib.last_kernel() == "ecg_mm_byte_kernel"
-    got = par.download()[5:5 + p * S * C_].reshape(p, S, C_)
-    assert np.array_equal(got, oracle_parity(oracle, k, p, data))
+    ctx.set_launch(0, 0, variant)
+    try:
+        ctx.matmul(coef, C_, S, d.ptr + 3, [j * C_ for j in range(k)], k * C_, par.ptr + 5,
+                   [r * S * C_ for r in range(p)], C_, 0)
+        ctx.sync()
+    finally:
+        ctx.set_launch(0, 0, 0)
+    assert ecglib.last_kernel() == kernel
+    raw = par.download()
+    assert np.array_equal(raw[5:5 + p * S * C_].reshape(p, S, C_), oracle_parity(oracle, k, p, data))
+    assert (raw[:5] == 0xEE).all() and (raw[5 + p * S * C_:] == 0xEE).all()
+    d.free()
+    par.free()
 
 
 def test_golden_fixtures(ctx):

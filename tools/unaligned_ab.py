@@ -38,11 +38,14 @@ def main():
     ctx = ecg.Context(0)
     k, p, C = 8, 2, MiB
     res = {}
-    # name, stripes, data offset, parity offset, extra parity row pitch
-    cases = (("aligned", 512, 0, 0, 0), ("data_off1", 512, 1, 0, 0), ("parity_off1", 512, 0, 1, 0),
-             ("parity_off2_data_off1", 512, 1, 2, 0), ("parity_off1_unequal", 64, 0, 1, 1),
-             ("data_off3_parity_off1_unequal", 64, 3, 1, 1))
-    for name, S, doff, poff, extra in cases:
+    # name, stripes, data offset, parity offset, extra parity row pitch, cell bytes
+    # (cells short of 1 MiB: every cell ends in a partial 4 KiB column)
+    cases = (("aligned", 512, 0, 0, 0, C), ("data_off1", 512, 1, 0, 0, C), ("parity_off1", 512, 0, 1, 0, C),
+             ("parity_off2_data_off1", 512, 1, 2, 0, C), ("parity_off1_unequal", 64, 0, 1, 1, C),
+             ("data_off3_parity_off1_unequal", 64, 3, 1, 1, C),
+             ("aligned_C-16", 512, 0, 0, 0, C - 16), ("aligned_C-4", 512, 0, 0, 0, C - 4),
+             ("data_off1_C-4", 512, 1, 0, 0, C - 4), ("C-3", 512, 0, 0, 0, C - 3))
+    for name, S, doff, poff, extra, C in cases:
         data = ctx.alloc(S * k * C + 64)
         data.fill(0x3C)
         data.upload(np.random.default_rng(S + doff).integers(0, 256, 64 * MiB, dtype=np.uint8))
