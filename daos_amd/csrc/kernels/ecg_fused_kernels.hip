@@ -29,9 +29,13 @@
 // scheduler can interleave with the lookup chains).  Bit 0: crc16/crc32,
 // bit 1: crc64.  Measured (tools/fused_libs.py, 3 interleaved rounds,
 // profiles/r03/defer/): EC_8P2 x 512 crc64 0.906 -> 0.886 ms (encode 0.838),
-// crc32 and EC_4P2 unchanged within +-0.5 %.
+// crc32 and EC_4P2 unchanged within +-0.5 %.  Timed as back-to-back blocks
+// (round 4, tools/ec_ab.py EC_OPS=crc32,crc64, 3 rotated rounds,
+// profiles/r04/ec_ab/ec_ab_fused_defer.json, ms): EC_8P2 crc32 0.903 deferred
+// vs 0.891 immediate, crc64 0.920 vs 0.912, EC_4P2 x 1024 crc64 1.077 vs
+// 1.110 -- so crc32 folds immediately, crc64 one column late.
 #ifndef ECG_FUSED_DEFER
-#define ECG_FUSED_DEFER 3
+#define ECG_FUSED_DEFER 2
 #endif
 
 // Work item `it` of the fused kernel -> chunk c, sub-chunk h, its columns
