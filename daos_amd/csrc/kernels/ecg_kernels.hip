@@ -153,7 +153,7 @@ ecg_mm_sel_kernel(const ecg_mm_params_t P, const uint8_t *__restrict__ sel, uint
 			else if (cbase + lo + 16 <= C)
 				mm_item<1, RM, false, false>(P, tb, 1, rows, s, cbase, lo);
 			else if (cbase + lo < C)
-				mm_tail<1, RM, false, false>(P, tb, 1, rows, s, cbase + lo, (int)(C - cbase - lo));
+				mm_tail<RM, false, false>(P, tb, 1, rows, s, cbase + lo, (int)(C - cbase - lo));
 		}
 	}
 }

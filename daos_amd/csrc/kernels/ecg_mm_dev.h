@@ -391,10 +391,55 @@ __device__ __forceinline__ void mm_dword(const ecg_mm_params_t &P, const u32x4 *
 	}
 }
 
-// Ragged tail: fewer than 16 bytes of this lane's slot are inside the cell;
-// bytewise, up to 8 of a byte's k loads issued together.
-template <int KM, int RM, bool ACC, bool DIFF>
+// Ragged tail: fewer than 16 bytes of this lane's slot are inside the cell
+// (G = 16: the lane straddling the cell's end).  A plain loop: inlined into
+// every kernel, a batched version changed the register allocation of the
+// main path (EC_4P2 76 -> 61 VGPRs and 2 % slower, profiles/r04/unaligned_ab/).
+template <int RM, bool ACC, bool DIFF>
 __device__ __forceinline__ void mm_tail(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
+				     uint32_t s, uint64_t off, int nb)
+{
+	constexpr int T2V = (RM + 3) / 4;
+	constexpr int PER_J = RM + T2V;
+	const uint8_t *sb = P.src + (int64_t)s * P.src_stripe_stride;
+	const uint8_t *sb2 = DIFF ? P.src2 + (int64_t)s * P.src2_stripe_stride : nullptr;
+	uint8_t *db = P.dst + (int64_t)s * P.dst_stripe_stride;
+
+	for (int b = 0; b < nb; b++) {
+		uint32_t o[RM];
+#pragma unroll
+		for (int r = 0; r < RM; r++)
+			o[r] = 0;
+		for (int j = 0; j < k; j++) {
+			uint32_t v = sb[P.src_cell_off[j] + off + b];
+			if (DIFF)
+				v ^= sb2[P.src2_cell_off[j] + off + b];
+			const uint32_t s0 = v & 7u, s1 = (v >> 3) & 7u, s2 = v >> 6;
+#pragma unroll
+			for (int r = 0; r < RM; r++) {
+				if (r < rows) {
+					const u32x4 t = tb[j * PER_J + r];
+					const uint32_t t2 = reinterpret_cast<const uint32_t *>(&tb[j * PER_J + RM])[r];
+					o[r] ^= __builtin_amdgcn_perm(t[1], t[0], s0) ^
+						__builtin_amdgcn_perm(t[3], t[2], s1) ^
+						__builtin_amdgcn_perm(t2, t2, s2);
+				}
+			}
+		}
+#pragma unroll
+		for (int r = 0; r < RM; r++) {
+			if (r < rows) {
+				uint8_t *d = db + P.dst_cell_off[r] + off + b;
+				*d = ACC ? (uint8_t)(*d ^ o[r]) : (uint8_t)o[r];
+			}
+		}
+	}
+}
+
+// The < 4 bytes after a cell's last whole dword (G = 4 / 1 partial
+// columns): bytewise, up to 4 of a byte's k loads issued together.
+template <int KM, int RM, bool ACC, bool DIFF>
+__device__ __forceinline__ void mm_tail_b(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
 				     uint32_t s, uint64_t off, int nb)
 {
 	constexpr int T2V = (RM + 3) / 4;
@@ -470,7 +515,7 @@ __device__ __forceinline__ void mm_partial(const ecg_mm_params_t &P, const u32x4
 		if (cbase + lo + 16 <= C)
 			mm_item<KM, RM, ACC, DIFF>(P, tb, k, rows, s, cbase, lo);
 		else if (cbase + lo < C)
-			mm_tail<KM, RM, ACC, DIFF>(P, tb, k, rows, s, cbase + lo, (int)(C - cbase - lo));
+			mm_tail<RM, ACC, DIFF>(P, tb, k, rows, s, cbase + lo, (int)(C - cbase - lo));
 	} else {
 		// not unrolled: four inlined copies of the byte loop cost ~70 VGPRs
 		// in every instantiation (this path runs once per cell at most)
@@ -481,7 +526,7 @@ __device__ __forceinline__ void mm_partial(const ecg_mm_params_t &P, const u32x4
 			if (off + 4 <= C)
 				mm_dword<KM, RM, ACC, DIFF>(P, tb, k, rows, s, off);
 			else if (off < C)
-				mm_tail<KM, RM, ACC, DIFF>(P, tb, k, rows, s, off, (int)(C - off));
+				mm_tail_b<KM, RM, ACC, DIFF>(P, tb, k, rows, s, off, (int)(C - off));
 		}
 	}
 }
