@@ -42,7 +42,7 @@
 // G: lane access granule (lane_off / ld_g), 16 unless an operand is only 4-
 // or 8-byte aligned.
 template <int K, int R, bool ACC, bool DIFF, int G = 16>
-__global__ void __launch_bounds__(BLOCK, ECG_MM_WPE(K, G) ? ECG_MM_WPE(K, G) : 1)
+__global__ void __launch_bounds__(BLOCK, ECG_MM_WPE(K, R, G) ? ECG_MM_WPE(K, R, G) : 1)
 ecg_mm_kernel(const ecg_mm_params_t P)
 {
 	constexpr int KM = K ? K : ECG_KMAX_K;

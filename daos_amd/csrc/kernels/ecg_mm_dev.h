@@ -206,11 +206,12 @@ __device__ __forceinline__ void mm_load_any(const ecg_mm_params_t &P, int k, uin
 // Cells loaded per phase of the product kernel for k = K and lane granule G
 // (0 = all k cells of a column before any arithmetic).  With PH > 0 a block
 // keeps PH x 4 KiB of loads in flight per column instead of k x 4 KiB, and
-// one phase's arithmetic overlaps the next phase's loads.  ECG_MM_WPE(K, G):
+// one phase's arithmetic overlaps the next phase's loads.  ECG_MM_WPE(K, R, G):
 // the waves per SIMD the register budget of those instantiations targets (0 =
 // the compiler's choice; a phased kernel needs a budget -- unconstrained, the
 // scheduler computes the selectors of a whole phase at once and spills to
-// AGPRs at 1 wave per SIMD).  Measured (tools/ec_ab.py, profiles/r04/ec_ab/,
+// AGPRs at 1 wave per SIMD; with three output rows the 4-wave budget spilled
+// 84 bytes per lane to scratch, so R = 3 gets 3 waves).  Measured (tools/ec_ab.py, profiles/r04/ec_ab/,
 // ms, back-to-back launches): k = 8 in 2 phases of 4 at 4 waves --
 // EC_8P2 1 MiB x 512 decode 0.873 -> 0.836 (the best capped geometry before:
 // 0.859), encode 0.844 -> 0.831, the dword-lane (G = 4) variant 0.895 ->
@@ -220,7 +221,7 @@ __device__ __forceinline__ void mm_load_any(const ecg_mm_params_t &P, int k, uin
 #define ECG_MM_PHASE(K, G) ((K) == 8 && ((G) == 16 || (G) == 4) ? 4 : 0)
 #endif
 #ifndef ECG_MM_WPE
-#define ECG_MM_WPE(K, G) ((K) == 8 && ((G) == 16 || (G) == 4) ? 4 : 0)
+#define ECG_MM_WPE(K, R, G) ((K) == 8 && ((G) == 16 || (G) == 4) ? ((R) <= 2 ? 4 : 3) : 0)
 #endif
 
 // The product of one column: x[j] = the lane's 16 bytes of cell j.  STORE =
@@ -391,6 +392,48 @@ __device__ __forceinline__ void mm_dword(const ecg_mm_params_t &P, const u32x4 *
 	}
 }
 
+// The same dword, the k loads one after another: the G = 4 partial column
+// (the batched form above changed the G = 4 main path's register
+// allocation, and 8-byte-aligned parity rows ran 1-2 % slower,
+// profiles/r04/ec_ab/).
+template <int RM, bool ACC, bool DIFF>
+__device__ __forceinline__ void mm_dword_plain(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
+					 uint32_t s, uint64_t off)
+{
+	constexpr int T2V = (RM + 3) / 4;
+	constexpr int PER_J = RM + T2V;
+	const uint8_t *sb = P.src + (int64_t)s * P.src_stripe_stride + off;
+	const uint8_t *sb2 = DIFF ? P.src2 + (int64_t)s * P.src2_stripe_stride + off : nullptr;
+	uint8_t *db = P.dst + (int64_t)s * P.dst_stripe_stride + off;
+	uint32_t o[RM];
+
+#pragma unroll
+	for (int r = 0; r < RM; r++)
+		o[r] = 0;
+	for (int j = 0; j < k; j++) {
+		uint32_t v = *reinterpret_cast<const uint32_t *>(sb + P.src_cell_off[j]);
+		if (DIFF)
+			v ^= *reinterpret_cast<const uint32_t *>(sb2 + P.src2_cell_off[j]);
+		const uint32_t s0 = v & 0x07070707u, s1 = (v >> 3) & 0x07070707u, s2 = (v >> 6) & 0x03030303u;
+#pragma unroll
+		for (int r = 0; r < RM; r++) {
+			if (r < rows) {
+				const u32x4 t = tb[j * PER_J + r];
+				const uint32_t t2 = reinterpret_cast<const uint32_t *>(&tb[j * PER_J + RM])[r];
+				o[r] ^= __builtin_amdgcn_perm(t[1], t[0], s0) ^ __builtin_amdgcn_perm(t[3], t[2], s1) ^
+					__builtin_amdgcn_perm(t2, t2, s2);
+			}
+		}
+	}
+#pragma unroll
+	for (int r = 0; r < RM; r++) {
+		if (r < rows) {
+			uint32_t *d = reinterpret_cast<uint32_t *>(db + P.dst_cell_off[r]);
+			*d = ACC ? *d ^ o[r] : o[r];
+		}
+	}
+}
+
 // Ragged tail: fewer than 16 bytes of this lane's slot are inside the cell
 // (G = 16: the lane straddling the cell's end).  A plain loop: inlined into
 // every kernel, a batched version changed the register allocation of the
@@ -523,10 +566,17 @@ __device__ __forceinline__ void mm_partial(const ecg_mm_params_t &P, const u32x4
 		for (int i = 0; i < 4; i++) {
 			const uint64_t off = cbase + lo + elem_off<G>(i);
 
-			if (off + 4 <= C)
-				mm_dword<KM, RM, ACC, DIFF>(P, tb, k, rows, s, off);
-			else if (off < C)
-				mm_tail_b<KM, RM, ACC, DIFF>(P, tb, k, rows, s, off, (int)(C - off));
+			if constexpr (G == 1) {
+				if (off + 4 <= C)
+					mm_dword<KM, RM, ACC, DIFF>(P, tb, k, rows, s, off);
+				else if (off < C)
+					mm_tail_b<KM, RM, ACC, DIFF>(P, tb, k, rows, s, off, (int)(C - off));
+			} else {
+				if (off + 4 <= C)
+					mm_dword_plain<RM, ACC, DIFF>(P, tb, k, rows, s, off);
+				else if (off < C)
+					mm_tail<RM, ACC, DIFF>(P, tb, k, rows, s, off, (int)(C - off));
+			}
 		}
 	}
 }

@@ -6,7 +6,7 @@ round, libraries rotated every round (the box's clocks drift over a run).
 The launch tuner is off (ECG_AUTOTUNE=0); every plain shape is timed
 uncapped and at its candidate blocks-per-CU cap (k = 16: 2, k = 8: 3).
 EC_OPS (default "enc,dec") picks the shapes: enc, dec, crc32, crc64 (the
-fused encode + parity checksums).
+fused encode + parity checksums), enc3 / dec3 (three parity rows / erasures).
 usage: [EC_OPS=...] python tools/ec_ab.py NAME=lib.so ... -> gpurun_out/ec_ab.json.
 Bench infrastructure."""
 import json
@@ -42,7 +42,9 @@ SHAPES = ((16, 2, 128 << 10, 1024, "enc", 0), (16, 2, 128 << 10, 1024, "dec", 0)
           (16, 2, 128 << 10, 4096, "enc", 0), (8, 2, MiB, 512, "enc", 0),
           (8, 2, MiB, 512, "dec", 0), (4, 2, MiB, 1024, "enc", 0), (4, 2, MiB, 1024, "dec", 0),
           (8, 2, MiB, 512, "enc", 8), (8, 2, MiB, 512, "enc", 4),
-          (8, 2, MiB, 512, "crc32", 0), (8, 2, MiB, 512, "crc64", 0), (4, 2, MiB, 1024, "crc64", 0))
+          (8, 2, MiB, 512, "crc32", 0), (8, 2, MiB, 512, "crc64", 0), (4, 2, MiB, 1024, "crc64", 0),
+          (8, 3, MiB, 512, "enc3", 0), (8, 3, MiB, 512, "dec3", 0), (4, 3, MiB, 1024, "enc3", 0),
+          (16, 3, 128 << 10, 1024, "enc3", 0))
 ops = os.environ.get("EC_OPS", "enc,dec").split(",")
 res = {}
 for k, p, C, S, op, off in (s for s in SHAPES if s[4] in ops):
@@ -57,7 +59,7 @@ for k, p, C, S, op, off in (s for s in SHAPES if s[4] in ops):
         fn = lambda: ctx.encode_csum(k, p, C, S, data.ptr, k * C, par.ptr, pitch, C, ht, 32768, 1, out.ptr)
         bufs = (data, par, out)
         rows = p
-    elif op == "enc":
+    elif op in ("enc", "enc3"):
         data = ctx.alloc(S * k * C + 64)
         pitch = S * C + 4096
         par = ctx.alloc(p * pitch + 64)
@@ -68,9 +70,10 @@ for k, p, C, S, op, off in (s for s in SHAPES if s[4] in ops):
     else:
         img = ctx.alloc(S * (k + p) * C)
         img.fill(0x3C)
-        fn = lambda: ctx.recover(k, p, C, S, img.ptr, (k + p) * C, [0, 1])
+        errs = [0, 1, 2] if op == "dec3" else [0, 1]
+        fn = lambda: ctx.recover(k, p, C, S, img.ptr, (k + p) * C, errs)
         bufs = (img,)
-        rows = 2
+        rows = len(errs)
     alg = (k + rows) * C * S
     for cap in ((255, 2) if k >= 16 else (255, 3) if k >= 8 else (255,)):
         if (off or op.startswith("crc")) and cap != 255:
