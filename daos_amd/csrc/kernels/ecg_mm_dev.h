@@ -210,8 +210,11 @@ __device__ __forceinline__ void mm_load_any(const ecg_mm_params_t &P, int k, uin
 // the waves per SIMD the register budget of those instantiations targets (0 =
 // the compiler's choice; a phased kernel needs a budget -- unconstrained, the
 // scheduler computes the selectors of a whole phase at once and spills to
-// AGPRs at 1 wave per SIMD; with three output rows the 4-wave budget spilled
-// 84 bytes per lane to scratch, so R = 3 gets 3 waves).  Measured (tools/ec_ab.py, profiles/r04/ec_ab/,
+// AGPRs at 1 wave per SIMD).  With three output rows the 4-wave budget
+// spills 84 bytes per lane to scratch; a 3-wave budget (141 VGPRs, no
+// spill) measured the same (EC_8P3 1 MiB x 512 encode 0.982-0.988 vs
+// 0.971-0.985 ms, decode 0.984-0.986 vs 0.981-0.984, profiles/r04/ec_ab/
+// ec_ab_8p3_budget.json), so every R keeps 4.  Measured (tools/ec_ab.py, profiles/r04/ec_ab/,
 // ms, back-to-back launches): k = 8 in 2 phases of 4 at 4 waves --
 // EC_8P2 1 MiB x 512 decode 0.873 -> 0.836 (the best capped geometry before:
 // 0.859), encode 0.844 -> 0.831, the dword-lane (G = 4) variant 0.895 ->
@@ -221,7 +224,7 @@ __device__ __forceinline__ void mm_load_any(const ecg_mm_params_t &P, int k, uin
 #define ECG_MM_PHASE(K, G) ((K) == 8 && ((G) == 16 || (G) == 4) ? 4 : 0)
 #endif
 #ifndef ECG_MM_WPE
-#define ECG_MM_WPE(K, R, G) ((K) == 8 && ((G) == 16 || (G) == 4) ? ((R) <= 2 ? 4 : 3) : 0)
+#define ECG_MM_WPE(K, R, G) ((K) == 8 && ((G) == 16 || (G) == 4) ? 4 : 0)
 #endif
 
 // The product of one column: x[j] = the lane's 16 bytes of cell j.  STORE =

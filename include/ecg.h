@@ -100,11 +100,9 @@ int ecg_recov_matrix(int k, int p, const unsigned char *en_matrix,
  *   dst cell r of s = dst + s*dst_stripe_stride + dst_cell_off[r]
  * All pointers are device pointers.  k <= 64, rows <= 8 (larger k is split
  * into accumulating launches).  Any alignment: 16-byte aligned cells run
- * 16-byte lanes, dword-aligned ones dword lanes, sources at any byte with
- * dword-aligned outputs funnel-shifted dword lanes; outputs all equally far
- * off a dword boundary run their first 1-3 bytes bytewise and the rest on
- * those lanes; outputs misaligned by different amounts run a byte kernel
- * (same results, ~8x slower).
+ * 16-byte lanes, dword-aligned sources dword lanes, sources at any byte
+ * funnel-shifted dword lanes; outputs at any byte are stored as misaligned
+ * dwords by the same lanes.
  * Asynchronous on `stream`.
  */
 int ecg_matmul(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef,
