@@ -293,8 +293,6 @@ int ecg_tune_launch(ecg_ctx_t *ctx, const ecg_mm_params_t *p, hipStream_t st, ui
 	    cfg.grid_x != 0 || cfg.grid_y != 0)
 		return ecg_k_launch_matmul(p, &ctx->cfg, (void *)st, kid);
 	g = ecg_k_align_granule(p);
-	if (g == 0)			/* the byte kernel has no blocks-per-CU geometry */
-		return ecg_k_launch_matmul(p, &ctx->cfg, (void *)st, kid);
 	if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
 		return ecg_k_launch_matmul(p, &ctx->cfg, (void *)st, kid);
 

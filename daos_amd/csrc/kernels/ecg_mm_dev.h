@@ -36,17 +36,15 @@ __device__ __forceinline__ void st_nt(uint8_t *p, u32x4 v)
 	__builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
 }
 
-// Lane access granule G (16, 8 or 4 bytes): the largest power of two that
-// divides every cell address of a launch (ecg_k_launch_matmul picks it).  A
-// wave always covers 1 KiB of each cell per column and a lane always owns 4
-// dwords of it; only how the dwords are fetched changes:
+// Lane access granule G (16, 4 or 1; align_granule below picks it per
+// launch).  A wave always covers 1 KiB of each cell per column and a lane
+// always owns 4 dwords of it; only how the dwords are fetched changes:
 //   G = 16: one dwordx4 at wave*1024 + lane*16
-//   G = 8 : two dwordx2 at wave*1024 + {0, 512} + lane*8
 //   G = 4 : four dwords at wave*1024 + {0, 256, 512, 768} + lane*4
-// so every wave-wide access is still one contiguous, naturally aligned
-// 1024 / 512 / 256-byte run.  GF arithmetic is per byte, so which bytes a
-// lane owns does not matter, only that loads and stores agree.
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+//   G = 1 : the G = 4 layout, source dwords funnel-shifted (ld_src below)
+// so every wave-wide access is one contiguous 1024- or 256-byte run.  GF
+// arithmetic is per byte, so which bytes a lane owns does not matter, only
+// that loads and stores agree.
 
 template <int G>
 __device__ __forceinline__ uint32_t lane_off()
@@ -59,7 +57,7 @@ __device__ __forceinline__ uint32_t lane_off()
 template <int G>
 __device__ __forceinline__ uint32_t elem_off(int i)
 {
-	return G == 16 ? 4u * i : G == 8 ? (uint32_t)(i >> 1) * 512u + (uint32_t)(i & 1) * 4u : (uint32_t)i * 256u;
+	return G == 16 ? 4u * i : (uint32_t)i * 256u;
 }
 
 // G = 1 (sources at any byte alignment): the dword layout of G = 4 for the
@@ -76,10 +74,6 @@ __device__ __forceinline__ u32x4 ld_g(const uint8_t *p)
 		return ld_g<4>(p);	// destinations (ACC reads)
 	} else if constexpr (G == 16) {
 		return ld_nt(p);
-	} else if constexpr (G == 8) {
-		const u32x2 a = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(p));
-		const u32x2 b = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(p + 512));
-		return (u32x4){a[0], a[1], b[0], b[1]};
 	} else {
 		static_assert(G == 4, "granule");
 		const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
@@ -95,9 +89,6 @@ __device__ __forceinline__ void st_g(uint8_t *p, u32x4 v)
 		st_g<4>(p, v);
 	} else if constexpr (G == 16) {
 		st_nt(p, v);
-	} else if constexpr (G == 8) {
-		__builtin_nontemporal_store((u32x2){v[0], v[1]}, reinterpret_cast<u32x2 *>(p));
-		__builtin_nontemporal_store((u32x2){v[2], v[3]}, reinterpret_cast<u32x2 *>(p + 512));
 	} else {
 		uint32_t *q = reinterpret_cast<uint32_t *>(p);
 		__builtin_nontemporal_store(v[0], q);
@@ -624,10 +615,8 @@ static inline uint32_t granule_of(uint64_t bits)
 // dword boundary (the funnel-shifted loads of ld_src<1>).  Destinations off a
 // dword boundary take the dword lanes' stores as they are: misaligned dword
 // stores (and ACC loads), served by the hardware's unaligned access mode,
-// ran 0.96 of the aligned kernel where the byte kernel ran 0.13
-// (tools/unaligned_ab.py, profiles/r04/unaligned_ab/).
-// (ld_g / st_g also implement an 8-byte lane layout, G = 8, which no launch
-// selects.)
+// ran 0.93-0.96 of the aligned kernel where the byte kernel ran 0.10 of the
+// HBM spec (tools/unaligned_ab.py, profiles/r04/unaligned_ab/).
 static inline uint32_t align_granule(const ecg_mm_params_t *p)
 {
 	uint64_t sb = (uint64_t)(uintptr_t)p->src | (uint64_t)p->src_stripe_stride;

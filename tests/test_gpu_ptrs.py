@@ -27,7 +27,7 @@ def _ptr_granule(in_skews, out_skews, C):
 
 @pytest.mark.parametrize("k,rows,C,S,iskew,oskew", [
     (8, 2, 65536, 12, 0, 0), (4, 3, 4096 * 3 + 48, 7, 0, 0), (16, 2, 8192, 5, 0, 0),
-    (6, 5, 1000, 9, 3, 3),                      # outputs off a dword: byte kernel
+    (6, 5, 1000, 9, 3, 3),                      # outputs off a dword: misaligned dword stores
     (2, 1, 4097, 4, 3, 3),
     (8, 2, 65536 + 4096 + 20, 6, 0, 0),         # cell size not a multiple of 16: dword lanes
     (8, 2, 65536, 6, 8, 4),                     # 8- / 4-byte aligned cells: dword lanes
