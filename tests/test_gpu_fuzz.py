@@ -150,3 +150,67 @@ def test_random_layouts(ctx, oracle, ecglib):
         kernels[got] = kernels.get(got, 0) + 1
     print("kernels:", kernels)
     assert {"g1", "g4", "g16"} <= set(kernels), kernels
+
+
+def ptr_predict(ins, outs, C):
+    """ecg_ptrs.c ptr_granule + ecg_k_launch_matmul_ptrs (addresses as offsets
+    from a 256-byte-aligned allocation)."""
+    ib = 0
+    for a in ins:
+        ib |= a
+    ob = 0
+    for a in outs:
+        ob |= a
+    if ib & 3:
+        return "g1"
+    return "g16" if ((ib | ob) & 15) == 0 and C % 16 == 0 else "g4"
+
+
+@pytest.mark.gpu
+def test_random_pointer_tables(ctx, oracle, ecglib):
+    """The pointer-table product (ISA-L's data[] / coding[] per stripe,
+    ref:src/object/cli_ec.c:476-546) over seeded random cells: every cell in
+    its own slot of one buffer at a drawn skew (all 0, all dword multiples, or
+    any byte, for inputs and outputs separately), slots shuffled, random
+    k <= 16, rows <= 6, cell sizes and stripe counts."""
+    seen = {}
+    for seed in range(48):
+        rng = np.random.default_rng(5000 + seed)
+        k, rows = int(rng.integers(1, 17)), int(rng.integers(1, 7))
+        C = int(rng.choice(CELLS16 if seed % 4 == 0 else CELLS))
+        S = int(rng.integers(1, 5))
+        n = S * (k + rows)
+        slot = (C + 15) // 16 * 16 + 32
+        unit_in, unit_out = (16, 16) if seed % 4 == 0 else (int(rng.choice([16, 4, 1])), int(rng.choice([16, 4, 1])))
+        order = rng.permutation(n + 3)[:n]
+        skews = [int(rng.integers(0, 16 // u)) * u if u > 1 else int(rng.integers(0, 16))
+                 for u in [unit_in if i % (k + rows) < k else unit_out for i in range(n)]]
+        host = rng.integers(0, 256, (n + 3) * slot, dtype=np.uint8)
+        coef = rng.integers(0, 256, (rows, k), dtype=np.uint8)
+        offs = [int(o) * slot + sk for o, sk in zip(order, skews)]
+        want = ptr_predict([o for i, o in enumerate(offs) if i % (k + rows) < k],
+                           [o for i, o in enumerate(offs) if i % (k + rows) >= k], C)
+        buf = ctx.to_device(host)
+        try:
+            ctx.matmul_ptrs(k, rows, coef, C, S, [buf.ptr + o for o in offs])
+            ctx.sync()
+            kern = ecglib.last_kernel()
+            dev = buf.download()
+        finally:
+            buf.free()
+        expect = host.copy()
+        for s in range(S):
+            base = s * (k + rows)
+            cells = np.stack([host[offs[base + j]: offs[base + j] + C] for j in range(k)])
+            prod = oracle.encode_data(coef, cells)
+            for r in range(rows):
+                o = offs[base + k + r]
+                expect[o: o + C] = prod[r]
+        what = f"seed {seed}: k={k} rows={rows} C={C} S={S} units={unit_in},{unit_out} kernel={kern} want={want}"
+        bad = np.flatnonzero(dev != expect)
+        assert bad.size == 0, f"{what}: {bad.size} bytes differ, first at {bad[0]}"
+        got = kern.rsplit(",", 1)[-1].rstrip(">") if ",g" in kern else "g16"
+        assert kern.startswith("ecg_mm_ptr_kernel<") and got == want, what
+        seen[got] = seen.get(got, 0) + 1
+    print("kernels:", seen)
+    assert {"g1", "g4", "g16"} <= set(seen), seen
