@@ -7,6 +7,8 @@ The launch tuner is off (ECG_AUTOTUNE=0); every plain shape is timed
 uncapped and at its candidate blocks-per-CU cap (k = 16: 2, k = 8: 3).
 EC_OPS (default "enc,dec") picks the shapes: enc, dec, crc32, crc64 (the
 fused encode + parity checksums), enc3 / dec3 (three parity rows / erasures).
+EC_ORDERS (default "0") times each shape under the listed 1D item orders
+(ecg_set_launch_order: 1 stripe-fastest, 2 / 3 XCD-blocked).
 usage: [EC_OPS=...] python tools/ec_ab.py NAME=lib.so ... -> gpurun_out/ec_ab.json.
 Bench infrastructure."""
 import json
@@ -46,6 +48,7 @@ SHAPES = ((16, 2, 128 << 10, 1024, "enc", 0), (16, 2, 128 << 10, 1024, "dec", 0)
           (8, 3, MiB, 512, "enc3", 0), (8, 3, MiB, 512, "dec3", 0), (4, 3, MiB, 1024, "enc3", 0),
           (16, 3, 128 << 10, 1024, "enc3", 0))
 ops = os.environ.get("EC_OPS", "enc,dec").split(",")
+orders = [int(o) for o in os.environ.get("EC_ORDERS", "0").split(",")]
 res = {}
 for k, p, C, S, op, off in (s for s in SHAPES if s[4] in ops):
     if op.startswith("crc"):
@@ -78,11 +81,15 @@ for k, p, C, S, op, off in (s for s in SHAPES if s[4] in ops):
     for cap in ((255, 2) if k >= 16 else (255, 3) if k >= 8 else (255,)):
         if (off or op.startswith("crc")) and cap != 255:
             continue
-        ctx.set_wg_per_cu(cap)
-        ms = timed(fn)
-        tag = "EC_%%dP%%d_%%dK_x%%d_%%s%%s_cap%%s" %% (k, p, C >> 10, S, op, "_off%%d" %% off if off else "", cap if cap != 255 else "none")
-        res[tag] = {"ms": round(ms, 4), "GBps": round(alg / ms / 1e6, 1), "kernel": ecg.last_kernel()}
+        for order in orders:
+            ctx.set_wg_per_cu(cap)
+            ctx.set_order(order)
+            ms = timed(fn)
+            tag = "EC_%%dP%%d_%%dK_x%%d_%%s%%s_cap%%s%%s" %% (k, p, C >> 10, S, op, "_off%%d" %% off if off else "",
+                                                  cap if cap != 255 else "none", "_o%%d" %% order if order else "")
+            res[tag] = {"ms": round(ms, 4), "GBps": round(alg / ms / 1e6, 1), "kernel": ecg.last_kernel()}
     ctx.set_wg_per_cu(0)
+    ctx.set_order(0)
     for b in bufs:
         b.free()
 print(json.dumps(res))
