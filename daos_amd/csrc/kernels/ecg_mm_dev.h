@@ -605,6 +605,46 @@ __device__ __forceinline__ void item_map(uint32_t order, uint32_t it, uint32_t t
 	}
 }
 
+// Blocks per CU of the product kernel's 2D grid (ecg_set_wg_per_cu; 0 =
+// none).  A block streams k + rows cells at once (one 4 KiB column of each);
+// with every block the registers allow resident, wide stripes keep so many
+// cell streams in flight that HBM efficiency drops.  Swept over the EC
+// classes (tools/wg_cap_sweep.py, profiles/r02/wg_cap/, caps interleaved
+// launch by launch): k = 16 best at 2 blocks per CU (encode +3-10 %, decode
+// +2-7 % over the register limit of 4), k = 8 at 3 (+1-5 %), k <= 4 uncapped
+// (any cap <= 4 loses).  Timed back to back as bench.py does, the gain does
+// not hold: k = 16 at 2 blocks per CU +2 % on one box and -4..-6 % on
+// another, k = 8 at 3 -2..-4 % (bench_wg*.log), so no shape is capped by
+// default; the knob stays for A/B runs.  A default cap would apply only to
+// launches of more than 2048 blocks (a smaller grid is latency-bound).
+__host__ static inline uint32_t mm_wg_cap(const ecg_mm_params_t *p, const ecg_launch_cfg_t *cfg, uint64_t blocks)
+{
+	const uint32_t c = cfg ? cfg->wg_per_cu : 0;
+
+	if (c == ECG_WG_UNCAPPED)
+		return 0;
+	if (c)
+		return c < 2 ? 2 : c;
+	return blocks > 2048 ? ECG_MM_WG_DEFAULT(p->k + p->rows) : 0u;
+}
+
+// Unused dynamic LDS that leaves room for exactly `cap` blocks per CU (160 KiB
+// of LDS; a block may take at most 64 KiB, so cap >= 2); k, r: the
+// instantiation's (0 = runtime-shaped), whose static table takes the rest.
+__host__ static inline size_t mm_dyn_lds(uint32_t cap, int k, int r)
+{
+	const int km = k ? k : ECG_KMAX_K, rm = r ? r : ECG_KMAX_R;
+	const size_t stat = (size_t)km * (rm + (rm + 3) / 4) * 16;	// ecg_mm_kernel's s_tbl
+	size_t d;
+
+	if (cap == 0)
+		return 0;
+	d = (size_t)(163840.0 / (cap + 0.5));
+	if (d > 65536)
+		d = 65536;
+	return d > stat ? (d - stat) & ~(size_t)255 : 0;
+}
+
 static inline uint32_t granule_of(uint64_t bits)
 {
 	return (bits & 15u) == 0 ? 16u : (bits & 7u) == 0 ? 8u : (bits & 3u) == 0 ? 4u : 1u;

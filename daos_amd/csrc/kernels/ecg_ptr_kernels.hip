@@ -262,7 +262,9 @@ extern "C" int ecg_k_launch_matmul_ptrs(const ecg_mm_params_t *p, const uint64_t
 		return (int)hipErrorInvalidDeviceFunction;
 	uint32_t gx = cfg && cfg->grid_x ? cfg->grid_x : (uint32_t)(nchunk < 65535 ? nchunk : 65535);
 	uint32_t gy = cfg && cfg->grid_y ? cfg->grid_y : (p->nstripes < 65535 ? p->nstripes : 65535);
-	hipLaunchKernelGGL(g_pkernels[id].fn, dim3(gx, gy), dim3(BLOCK), 0, st, *p, cells_dev);
+	// blocks per CU as the offset kernel's (ecg_set_wg_per_cu): unused dynamic LDS
+	const size_t lds = mm_dyn_lds(mm_wg_cap(p, cfg, (uint64_t)gx * gy), g_pkernels[id].k, g_pkernels[id].r);
+	hipLaunchKernelGGL(g_pkernels[id].fn, dim3(gx, gy), dim3(BLOCK), lds, st, *p, cells_dev);
 	if (kernel_id)
 		*kernel_id = KID_PTR + id;
 	return (int)hipGetLastError();
