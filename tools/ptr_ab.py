@@ -18,6 +18,9 @@ os.environ.setdefault("ECG_AUTOTUNE", "0")
 from daos_amd import ecg  # noqa: E402
 
 MiB = 1 << 20
+# PTR_GX_DIVS: the pointer-table grid's x dimension = columns / d, so each
+# block walks d columns of its stripe (the stripe's table row loaded once)
+GX_DIVS = [int(d) for d in os.environ.get("PTR_GX_DIVS", "1").split(",")]
 
 
 def timed(ctx, fn, iters=30, warm=40):
@@ -60,14 +63,19 @@ def main():
             ctx.encode(k, p, Cb, S, data.ptr, k * Cb, par.ptr, pitch, Cb)
 
         alg = (k + p) * Cb * S
+        nchunk = Cb // 4096
         for cap in ((0, 2) if k >= 8 else (0,)):
-            for name, fn in (("offset", off_call), ("ptr", ptr_call)):
-                ctx.set_wg_per_cu(cap)
-                ms = timed(ctx, fn)
-                tag = f"EC_{k}P{p}_{Cb >> 10}K_x{S}_{name}_cap{cap}"
-                res[tag] = {"ms": round(ms, 4), "alg_GBps": round(alg / ms / 1e6, 1), "kernel": ecg.last_kernel()}
-                print(tag, res[tag], flush=True)
+            for name, fn, divs in (("offset", off_call, (1,)), ("ptr", ptr_call, GX_DIVS)):
+                for dv in divs:
+                    ctx.set_wg_per_cu(cap)
+                    ctx.set_launch(nchunk // dv if dv > 1 else 0, 0, 0)
+                    ms = timed(ctx, fn)
+                    tag = f"EC_{k}P{p}_{Cb >> 10}K_x{S}_{name}_cap{cap}" + (f"_cols{dv}" if dv > 1 else "")
+                    res[tag] = {"ms": round(ms, 4), "alg_GBps": round(alg / ms / 1e6, 1),
+                                "kernel": ecg.last_kernel()}
+                    print(tag, res[tag], flush=True)
         ctx.set_wg_per_cu(0)
+        ctx.set_launch(0, 0, 0)
         data.free()
         par.free()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
