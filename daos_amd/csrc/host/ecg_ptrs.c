@@ -100,6 +100,48 @@ static int ptr_granule(const uint64_t *tab, uint32_t S, int k, int rows)
 	return ((in | out) & 15u) == 0 ? 16 : 4;
 }
 
+/* A table whose every cell sits at a fixed offset from a per-stripe base --
+ * cell j of stripe s at tab[j] + s * stride, one stride for the inputs and
+ * one for the outputs -- is the offset kernel's layout: the client's encode
+ * over one contiguous iov (data [S][k][C] in place, ref:src/object/cli_ec.c:
+ * 510-536) and parity of stripe n at pbufs[m] + n*C (:638-640).  That launch
+ * needs no table upload and no dependent address load per block (the
+ * pointer-table kernel ran 4-15 % behind it on the same layout, and a
+ * 128 KiB-cell call paid ~25 us of table staging; profiles/r04/ptr_ab/). */
+static int table_affine(const uint64_t *tab, uint32_t S, int k, int rows, int64_t *soff, int64_t *sstride,
+			int64_t *doff, int64_t *dstride)
+{
+	const uint64_t n = (uint64_t)(k + rows);
+	const uint64_t bs = S > 1 ? tab[n] - tab[0] : 0, bd = S > 1 ? tab[n + (uint64_t)k] - tab[k] : 0;
+
+	for (uint64_t s = 1; s < S; s++)
+		for (uint64_t j = 0; j < n; j++)
+			if (tab[s * n + j] != tab[j] + s * (j < (uint64_t)k ? bs : bd))
+				return 0;
+	for (int j = 0; j < k; j++)
+		soff[j] = (int64_t)(tab[j] - tab[0]);
+	for (int r = 0; r < rows; r++)
+		doff[r] = (int64_t)(tab[k + r] - tab[k]);
+	*sstride = (int64_t)bs;
+	*dstride = (int64_t)bd;
+	return 1;
+}
+
+/* The offset-kernel launch of an affine table (ecg_matmul: lane choice,
+ * launch tuner and last-kernel report as for any strided call). */
+static int launch_affine(ecg_ctx_t *ctx, const uint64_t *tab, int k, int rows, const unsigned char *coef,
+			 uint64_t C, uint32_t S, hipStream_t st, int *done)
+{
+	int64_t soff[ECG_KMAX_K], doff[ECG_KMAX_R], ss, ds;
+
+	*done = 0;
+	if (k > ECG_KMAX_K || rows > ECG_KMAX_R || !table_affine(tab, S, k, rows, soff, &ss, doff, &ds))
+		return 0;
+	*done = 1;
+	return ecg_matmul(ctx, k, rows, coef, C, S, (const void *)(uintptr_t)tab[0], soff, ss,
+			  (void *)(uintptr_t)tab[k], doff, ds, 0, (void *)st);
+}
+
 /* Table already in sc->pin (S x (k+rows) entries); copy, launch, record
  * (ctx->lock held).  With `gather`, its segment table follows the pointer
  * table at byte seg_off of the slot (pinned and device alike): both travel in
@@ -113,8 +155,13 @@ static int launch_table(ecg_ctx_t *ctx, struct ecg_scratch_slot *sc, int k, int 
 	ecg_mm_params_t *prm;
 	uint32_t kid = 0;
 	hipError_t e;
-	int r, j, ke;
+	int r, j, ke, done;
 
+	if (!(gather && gather->n)) {	/* no gather copies: maybe the offset kernel's layout */
+		r = launch_affine(ctx, (const uint64_t *)sc->pin, k, rows, coef, C, S, st, &done);
+		if (done)
+			return r;
+	}
 	if (gather && gather->n)
 		tbytes = seg_off + gather->n * sizeof(ecg_copy_seg_t);
 	e = hipMemcpyAsync(sc->dev, sc->pin, tbytes, hipMemcpyHostToDevice, st);
@@ -172,6 +219,13 @@ int ecg_matmul_ptrs(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, 
 	if (rc)
 		return rc;
 	st = ecg_pick_stream(ctx, stream);
+	{
+		int done;
+
+		rc = launch_affine(ctx, (const uint64_t *)cells, k, rows, coef, cell_bytes, nstripes, st, &done);
+		if (done)
+			return rc;
+	}
 	pthread_mutex_lock(&ctx->lock);
 	rc = ecg_scratch_reserve(ctx, n * sizeof(uint64_t), n * sizeof(uint64_t), &sc);
 	if (rc == 0) {

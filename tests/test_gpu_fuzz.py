@@ -152,6 +152,16 @@ def test_random_layouts(ctx, oracle, ecglib):
     assert {"g1", "g4", "g16"} <= set(kernels), kernels
 
 
+def table_affine(offs, S, k, rows):
+    """ecg_ptrs.c table_affine: every cell at a fixed offset from a per-stripe
+    base (one stride for the inputs, one for the outputs)."""
+    n = k + rows
+    if S == 1:
+        return True
+    bs, bd = offs[n] - offs[0], offs[n + k] - offs[k]
+    return all(offs[s * n + j] == offs[j] + s * (bs if j < k else bd) for s in range(S) for j in range(n))
+
+
 def ptr_predict(ins, outs, C):
     """ecg_ptrs.c ptr_granule + ecg_k_launch_matmul_ptrs (addresses as offsets
     from a 256-byte-aligned allocation)."""
@@ -206,11 +216,22 @@ def test_random_pointer_tables(ctx, oracle, ecglib):
             for r in range(rows):
                 o = offs[base + k + r]
                 expect[o: o + C] = prod[r]
-        what = f"seed {seed}: k={k} rows={rows} C={C} S={S} units={unit_in},{unit_out} kernel={kern} want={want}"
+        affine = table_affine(offs, S, k, rows)
+        what = (f"seed {seed}: k={k} rows={rows} C={C} S={S} units={unit_in},{unit_out} affine={affine} "
+                f"kernel={kern} want={want}")
         bad = np.flatnonzero(dev != expect)
         assert bad.size == 0, f"{what}: {bad.size} bytes differ, first at {bad[0]}"
         got = kern.rsplit(",", 1)[-1].rstrip(">") if ",g" in kern else "g16"
-        assert kern.startswith("ecg_mm_ptr_kernel<") and got == want, what
+        if affine:      # the offset kernel, its lanes by its own rule
+            n = k + rows
+            bs, bd = (offs[n] - offs[0], offs[n + k] - offs[k]) if S > 1 else (0, 0)
+            want = predict(offs[0], [offs[j] - offs[0] for j in range(k)], bs, offs[k],
+                           [offs[k + r] - offs[k] for r in range(rows)], bd)
+            what += f" -> offset kernel {want}"
+            assert kern.startswith("ecg_mm_kernel<"), what
+        else:
+            assert kern.startswith("ecg_mm_ptr_kernel<"), what
+        assert got == want, what
         seen[got] = seen.get(got, 0) + 1
     print("kernels:", seen)
     assert {"g1", "g4", "g16"} <= set(seen), seen

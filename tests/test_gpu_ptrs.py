@@ -167,3 +167,40 @@ def test_recx_encode_rec2big(ecglib, ctx):
         buf.free()
         for b in pb_bufs:
             b.free()
+
+
+@pytest.mark.parametrize("k,p,C,S,moved", [(8, 2, 65536, 6, False), (4, 2, 4096 * 3 + 40, 5, False),
+                                           (16, 3, 8192, 3, False), (8, 2, 65536, 6, True)])
+def test_matmul_ptrs_affine_table(ctx, oracle, ecglib, k, p, C, S, moved):
+    """A pointer table of the client's contiguous layout -- data cell j of
+    stripe s at base + (s*k + j)*C, parity of stripe s at pbuf[m] + s*C
+    (ref:src/object/cli_ec.c:510-536, 638-640) -- runs the offset kernel
+    (no table upload); one cell moved elsewhere keeps the pointer-table
+    kernel.  Same bytes either way."""
+    rng = np.random.default_rng(k * 7 + C + S + moved)
+    data = rng.integers(0, 256, (S, k, C), dtype=np.uint8)
+    d = ctx.to_device(data)
+    spare = ctx.alloc(C + 64)
+    spare.upload(data[S - 1, 1])
+    par = ctx.alloc(p * (S * C + 4096))
+    try:
+        cells = []
+        for s in range(S):
+            cells += [d.ptr + (s * k + j) * C for j in range(k)]
+            cells += [par.ptr + r * (S * C + 4096) + s * C for r in range(p)]
+        if moved:
+            cells[(S - 1) * (k + p) + 1] = spare.ptr
+        coef = oracle.cauchy1(k, p)[k:]
+        ctx.matmul_ptrs(k, p, coef, C, S, cells)
+        ctx.sync()
+        kern = ecglib.last_kernel()
+        assert kern.startswith("ecg_mm_ptr_kernel<" if moved else f"ecg_mm_kernel<{k},{p},"), kern
+        raw = par.download()
+        for r in range(p):
+            got = raw[r * (S * C + 4096): r * (S * C + 4096) + S * C].reshape(S, C)
+            for s in range(S):
+                assert np.array_equal(got[s], oracle.encode_data(coef, data[s])[r]), (r, s)
+    finally:
+        d.free()
+        spare.free()
+        par.free()
