@@ -304,8 +304,11 @@ int ecg_tune_counters(ecg_ctx_t *ctx, uint64_t *probe_cycles, uint64_t *probe_la
  * nstripes.  cells[s*(k+rows) + j] is the DEVICE address of input cell j
  * (j < k) or output cell j-k of stripe s; the table itself is a host array
  * (copied before return is not required: it is staged internally).  k <= 16,
- * rows <= 8; any alignment (16-byte aligned cells take the vector kernel).
- * Asynchronous on `stream`. */
+ * rows <= 8; any alignment.  A table whose cells sit at fixed offsets from a
+ * per-stripe base (cell j of stripe s at cells[j] + s*stride, one stride for
+ * the inputs, one for the outputs -- a contiguous client buffer) runs as the
+ * strided product (ecg_matmul) with no table upload.  Asynchronous on
+ * `stream`. */
 int ecg_matmul_ptrs(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef,
 		    uint64_t cell_bytes, uint32_t nstripes, void *const *cells, void *stream);
 
