@@ -109,10 +109,56 @@ static int tstage_get(ecg_ctx_t *ctx, size_t bytes, struct tstage **out)
 	return 0;
 }
 
+/* 1 when p is device memory of this process (hipMalloc'd), 0 for host
+ * memory.  A query of unregistered host memory may fail: its error is
+ * cleared here so a later launch check does not report it. */
+static int is_device_ptr(const void *p)
+{
+	hipPointerAttribute_t a;
+
+	memset(&a, 0, sizeof(a));
+	if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+		(void)hipGetLastError();
+		return 0;
+	}
+	return a.type == hipMemoryTypeDevice;
+}
+
+/* The ISA-L data-plane calls with DEVICE cells (an engine whose bio buffers
+ * live in HBM keeps its ec_encode_data call sites): one strided launch, cell
+ * offsets relative to the first source / output, then the stream is drained
+ * (ISA-L's calls are synchronous). */
+static int matmul_device(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
+			 unsigned char *const *src, unsigned char *const *dst, unsigned flags)
+{
+	int64_t soff[ECG_MAX_K], doff[256];
+	hipError_t e;
+	int j, r, rc;
+
+	if (k > ECG_MAX_K)
+		return ecg_fail(-ECG_DER_INVAL, "matmul_host: k=%d device cells (max %d)", k, ECG_MAX_K);
+	for (j = 0; j < k; j++) {
+		if (!is_device_ptr(src[j]))
+			return ecg_fail(-ECG_DER_INVAL, "matmul_host: source %d is host memory, source 0 device", j);
+		soff[j] = (int64_t)((uintptr_t)src[j] - (uintptr_t)src[0]);
+	}
+	for (r = 0; r < rows; r++) {
+		if (!is_device_ptr(dst[r]))
+			return ecg_fail(-ECG_DER_INVAL, "matmul_host: output %d is host memory, sources device", r);
+		doff[r] = (int64_t)((uintptr_t)dst[r] - (uintptr_t)dst[0]);
+	}
+	rc = ecg_matmul(ctx, k, rows, coef, (uint64_t)len, 1, src[0], soff, 0, dst[0], doff, 0, flags, NULL);
+	if (rc)
+		return rc;
+	e = hipStreamSynchronize(ctx->stream);
+	return e == hipSuccess ? 0 : ecg_hip_fail(e, "matmul_host: device cells sync");
+}
+
 /*
- * dst[r][i] (^)= XOR_j coef[r*k + j] * src[j][i], i < len, host pointers.
- * With ECG_F_ACCUMULATE the current dst bytes travel to the device first
- * (ec_encode_data_update semantics).
+ * dst[r][i] (^)= XOR_j coef[r*k + j] * src[j][i], i < len.  Host cells are
+ * staged through pinned memory; device cells (every cell hipMalloc'd) run
+ * in place.  With ECG_F_ACCUMULATE the current dst bytes travel to the
+ * device first (ec_encode_data_update semantics).
  */
 int ecg_matmul_host(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
 		    unsigned char *const *src, unsigned char *const *dst, unsigned flags)
@@ -134,6 +180,8 @@ int ecg_matmul_host(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned cha
 	rc = ecg_ctx_enter(ctx);
 	if (rc)
 		return rc;
+	if (is_device_ptr(src[0]))
+		return matmul_device(ctx, len, k, rows, coef, src, dst, flags);
 	pitch = ((size_t)len + 255) & ~(size_t)255;
 	bytes = pitch * (size_t)(k + rows);
 	rc = tstage_get(ctx, bytes, &t);

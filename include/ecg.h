@@ -147,10 +147,12 @@ int ecg_update(ecg_ctx_t *ctx, int k, int p, uint64_t cell_bytes, uint32_t nstri
 	       void *stream);
 
 /* ---- host-resident pipeline (PCIe-inclusive) ---------------------------- */
-/* One stripe, ISA-L ec_encode_data calling convention: host pointers
- * src[k], dst[rows] (any alignment), `len` bytes each;
- * dst[r] (^)= XOR_j coef[r*k+j] * src[j].  Executed on the GPU through
- * per-thread pinned staging; synchronous.  k may exceed ECG_MAX_K (xor_gen). */
+/* One stripe, ISA-L ec_encode_data calling convention: pointers src[k],
+ * dst[rows] (any alignment), `len` bytes each;
+ * dst[r] (^)= XOR_j coef[r*k+j] * src[j].  Host cells run on the GPU
+ * through per-thread pinned staging; device cells (src[0] hipMalloc'd: then
+ * every cell must be) run in place as one strided launch.  Synchronous.  k
+ * may exceed ECG_MAX_K for host cells (xor_gen). */
 int ecg_matmul_host(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
 		    unsigned char *const *src, unsigned char *const *dst, unsigned flags);
 /* Encode host-resident stripes (data [S][k][C], parity [p][S][C] in host

@@ -27,7 +27,9 @@
  *
  * Data-plane calls (ec_encode_data, ec_encode_data_update, xor_gen) run on
  * the GPU: a process-wide context on device $ECG_DEVICE (default 0), with
- * per-thread pinned staging.  There is no CPU fallback: if no gfx950 device
+ * per-thread pinned staging for host cells; cells in device memory (every
+ * pointer of the call hipMalloc'd -- an engine whose buffers live in HBM)
+ * are used in place, no staging.  There is no CPU fallback: if no gfx950 device
  * is usable these `void` functions print the reason and abort().
  */
 #ifndef ECG_ISAL_H

@@ -252,6 +252,51 @@ def test_isal_drop_in(ecglib, oracle, ctx):
     assert ecglib.isal_xor_gen([a, c]) != 0
 
 
+def test_isal_drop_in_device_cells(ecglib, oracle, ctx):
+    """The ISA-L data-plane calls with cells in device memory (an engine whose
+    buffers live in HBM keeps its ec_encode_data call sites,
+    ref:src/object/cli_ec.c:540): scattered cells at odd offsets of
+    hipMalloc'd buffers, used in place -- ec_encode_data, then
+    ec_encode_data_update of one cell, then xor_gen."""
+    L = ecglib.lib()
+    k, p, n = 8, 3, 32768 + 5
+    en = np.zeros((k + p) * k, dtype=np.uint8)
+    L.gf_gen_cauchy1_matrix(en.ctypes.data_as(ecglib.u8p), k + p, k)
+    en = en.reshape(k + p, k)
+    tbls = ecglib.isal_init_tables(en[k:])
+    data = np.stack([rand(n, 140 + j) for j in range(k)])
+    slot = n + 64
+    dbuf, pbuf = ctx.alloc((k + 2) * slot), ctx.alloc((p + 1) * slot)
+    order = [5, 0, 9, 2, 7, 1, 3, 8]                # cells scattered over the slots, odd offsets
+    dofs = [order[j] * slot + 2 * j + 1 for j in range(k)]
+    pofs = [r * slot + 3 for r in range(p)]
+    try:
+        for j in range(k):
+            dbuf.upload(data[j], offset=dofs[j])
+        pbuf.fill(0xEE)
+        dp = (ecglib.u8p * k)(*[C.cast(C.c_void_p(dbuf.ptr + o), ecglib.u8p) for o in dofs])
+        cp = (ecglib.u8p * p)(*[C.cast(C.c_void_p(pbuf.ptr + o), ecglib.u8p) for o in pofs])
+        L.ec_encode_data(n, k, p, tbls.ctypes.data_as(ecglib.u8p), dp, cp)
+        want = oracle.encode_data(en[k:], data)
+        raw = pbuf.download()
+        assert all(np.array_equal(raw[pofs[r]: pofs[r] + n], want[r]) for r in range(p))
+        assert (raw[:3] == 0xEE).all() and (raw[pofs[0] + n: pofs[1]] == 0xEE).all()
+        # one cell updated: parity ^= coef * delta
+        delta = rand(n, 150)
+        dbuf.upload(delta, offset=dofs[0])
+        L.ec_encode_data_update(n, k, p, 3, tbls.ctypes.data_as(ecglib.u8p), dp[0], cp)
+        want2 = oracle.encode_data_update(en[k:], 3, delta, want)
+        raw = pbuf.download()
+        assert all(np.array_equal(raw[pofs[r]: pofs[r] + n], want2[r]) for r in range(p))
+        # xor_gen: the last pointer is the destination
+        v = (C.c_void_p * 3)(dbuf.ptr + dofs[1], dbuf.ptr + dofs[2], pbuf.ptr + pofs[0])
+        assert L.xor_gen(3, n, v) == 0
+        assert np.array_equal(pbuf.download(n, offset=pofs[0]), data[1] ^ data[2])
+    finally:
+        dbuf.free()
+        pbuf.free()
+
+
 def test_isal_reference_aggregate_pattern(ecglib, oracle, ctx):
     """The reference's only byte-level parity test
     (ref:src/tests/suite/daos_aggregate_ec.c:371-395): cell j filled with j
