@@ -3,7 +3,8 @@ stripe per call, host buffers) by cell size -- what an unbatched DAOS caller
 linked against libecg sees.  Run once per staging mode (env
 ECG_ZERO_COPY_MAX: 0 = always DMA copies, large = kernel on the pinned
 staging in place); appends one JSON line to gpurun_out/bench_dropin.jsonl.
-Bench infrastructure (no oracle)."""
+DROPIN_DEVICE=1: the cells live in device memory instead (the drop-in then
+launches on them in place).  Bench infrastructure (no oracle)."""
 import json
 import os
 import sys
@@ -19,19 +20,37 @@ def main():
     k, p = 8, 2
     tbls = ecg.isal_init_tables(ecg.cauchy1(k, p)[k:])
     rng = np.random.default_rng(5)
-    res = {"zero_copy_max": os.environ.get("ECG_ZERO_COPY_MAX", "default")}
+    device = os.environ.get("DROPIN_DEVICE") == "1"
+    res = {"zero_copy_max": os.environ.get("ECG_ZERO_COPY_MAX", "default"), "cells": "device" if device else "host"}
+    ctx = ecg.Context(0) if device else None
+    L = ecg.lib()
     for C in (4096, 16384, 32768, 65536, 131072, 262144, 1 << 20):
-        cells = [rng.integers(0, 256, C, dtype=np.uint8) for _ in range(k)]
-        coding = [np.zeros(C, dtype=np.uint8) for _ in range(p)]
+        if device:
+            buf = ctx.alloc((k + p) * C)
+            buf.fill(0x5A)
+            dp = (ecg.u8p * k)(*[ecg.C.cast(ecg.C.c_void_p(buf.ptr + j * C), ecg.u8p) for j in range(k)])
+            cp = (ecg.u8p * p)(*[ecg.C.cast(ecg.C.c_void_p(buf.ptr + (k + r) * C), ecg.u8p) for r in range(p)])
+            tp = tbls.ctypes.data_as(ecg.u8p)
+
+            def call():
+                L.ec_encode_data(C, k, p, tp, dp, cp)
+        else:
+            cells = [rng.integers(0, 256, C, dtype=np.uint8) for _ in range(k)]
+            coding = [np.zeros(C, dtype=np.uint8) for _ in range(p)]
+
+            def call():
+                ecg.isal_encode_data(tbls, k, p, cells, coding)
         for _ in range(5):
-            ecg.isal_encode_data(tbls, k, p, cells, coding)
+            call()
         it = 200 if C <= 65536 else 40
         t0 = time.perf_counter()
         for _ in range(it):
-            ecg.isal_encode_data(tbls, k, p, cells, coding)
+            call()
         us = (time.perf_counter() - t0) / it * 1e6
         res[f"{C >> 10}KiB_us"] = round(us, 1)
         res[f"{C >> 10}KiB_GiBps"] = round(k * C / (us / 1e6) / (1 << 30), 2)
+        if device:
+            buf.free()
     print(json.dumps(res), flush=True)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "bench_dropin.jsonl"), "a") as f:
