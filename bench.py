@@ -638,6 +638,59 @@ def offset_rows(ctx, aligned, iters=11):
     return rows
 
 
+def sgl_rows(ctx, aligned, iters=11):
+    """The client's full-stripe encode over a device-resident sgl
+    (ecg_obj_ec_recx_encode, restating obj_ec_recx_encode /
+    obj_ec_stripe_encode, ref:src/object/cli_ec.c:476-546, 593-663): EC_8P2
+    1 MiB x 512 stripes of one recx, parity into p separate buffers (the
+    oer_pbufs layout, :75-97).  One iov: every cell used in place at an
+    affine address, so the call runs the strided product kernel; 64 iovs of
+    random lengths with gaps between them: cells cut across iovs are gathered
+    into device scratch, the rest used in place, one pointer-table launch.
+    Timed per call (host walk, table upload, gathers and product included);
+    `of_aligned` = the plain encode row's ms / this ms."""
+    import ctypes
+
+    import numpy as np
+    from daos_amd import ecg
+
+    k, p, C, S = 8, 2, 1 << 20, 512
+    total = S * k * C
+    rng = np.random.default_rng(11)
+    rows = {}
+    L = ecg.lib()
+    for name, n_iov in (("one_iov", 1), ("64_iovs", 64)):
+        cuts = sorted(set(int(x) for x in rng.integers(1, total, n_iov - 1))) if n_iov > 1 else []
+        lens = np.diff([0] + cuts + [total]).tolist()
+        buf = ctx.alloc(total + 256 * n_iov)
+        fill_device(ctx, buf, total + 256 * n_iov, 9)
+        iovs, off = [], 0
+        for ln in lens:
+            iovs.append(ecg.Iov(buf.ptr + off, ln, ln))
+            off += ln + (256 if n_iov > 1 else 0)
+        iov_arr = (ecg.Iov * len(iovs))(*iovs)
+        rx = (ecg.EcRecx * 1)(ecg.EcRecx(0, S, 0))
+        pbufs = [ctx.alloc(S * C) for _ in range(p)]
+        pb = (ctypes.c_void_p * p)(*[b.ptr for b in pbufs])
+        oc = (37 << 24) | 1                         # OC_EC_8P2G1
+
+        def fn():
+            ecg._chk(L.ecg_obj_ec_recx_encode(ctx.h, oc, C, iov_arr, len(iovs), rx, 1, pb, None), "recx_encode")
+
+        ms = time_kernel(ctx, fn, iters, warm=40)
+        alg = (k + p) * C * S
+        row = {"iovs": n_iov, "stripes": S, "ms": round(ms, 4), "GiBps_user": round(k * C * S / (ms / 1e3) / GIB, 1),
+               "alg_GBps": round(alg / ms / 1e6, 1), "roofline_frac": round(alg / ms / 1e6 / HBM_PEAK_GBS, 4),
+               "kernel": ecg.last_kernel()}
+        if aligned:
+            row["of_aligned"] = round(aligned["ms"] / ms, 4)
+        rows[f"EC_8P2_1MiB_recx_encode_sgl_{name}"] = row
+        buf.free()
+        for b in pbufs:
+            b.free()
+    return rows
+
+
 def detail_rows(ctx, ceil, iters=11, shapes=DETAIL_SHAPES, csum=True):
     """Extra device-resident rows (per GPU): the north-star EC_8P2 encode,
     EC_8P2 2-erasure decode, EC_16P2 128 KiB encode, EC_2P1 128 KiB encode.
@@ -691,6 +744,7 @@ def detail_rows(ctx, ceil, iters=11, shapes=DETAIL_SHAPES, csum=True):
         if buf2 is not None:
             buf2.free()
     rows.update(offset_rows(ctx, rows.get("EC_8P2_1MiB_encode"), iters))
+    rows.update(sgl_rows(ctx, rows.get("EC_8P2_1MiB_encode"), iters))
     if not csum:
         return rows
     # checksums of regenerated cells (include/ecg_csum.h): EC_8P2 encode with
