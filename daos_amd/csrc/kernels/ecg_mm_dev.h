@@ -224,9 +224,13 @@ __device__ __forceinline__ void mm_load_any(const ecg_mm_params_t &P, int k, uin
 // when the fold reaches j (DIFF: their src2 too).  (One function on purpose: the same loops split
 // into init / fold / store helpers made the register allocator keep EC_16P2
 // at 256 VGPRs + AGPRs, 1 wave per SIMD, instead of 114 / 4 waves.)
-template <int KM, int RM, bool ACC, bool KEEP, bool STORE = true, int G = 16, int PH = 0, bool DIFF = false>
+// PA (the pointer-table kernel): the phase loads read cell j at the
+// wave-uniform address pa[j] (+ lo) instead of P's offsets.
+template <int KM, int RM, bool ACC, bool KEEP, bool STORE = true, int G = 16, int PH = 0, bool DIFF = false,
+	  bool PA = false>
 __device__ __forceinline__ void mm_compute(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
-					   uint32_t s, uint64_t cbase, uint32_t lo, u32x4 *x, u32x4 *keep)
+					   uint32_t s, uint64_t cbase, uint32_t lo, u32x4 *x, u32x4 *keep,
+					   const uint64_t *pa = nullptr)
 {
 	constexpr int T2V = (RM + 3) / 4;
 	constexpr int PER_J = RM + T2V;
@@ -259,7 +263,14 @@ __device__ __forceinline__ void mm_compute(const ecg_mm_params_t &P, const u32x4
 						dep ^= acc[r][0] ^ acc[r][1] ^ acc[r][2] ^ acc[r][3];
 				asm volatile("" : "+v"(lo2), "+v"(z2) : "v"(dep));
 				tb += z2;
-				mm_load<KM, DIFF, G, PH>(P, k, s, cbase, lo2, x, j);
+				if constexpr (PA) {
+#pragma unroll
+					for (int i = j; i < j + PH && i < KM; i++)
+						if (i < k)
+							x[i] = ld_src<G>(reinterpret_cast<const uint8_t *>(pa[i]), lo2);
+				} else {
+					mm_load<KM, DIFF, G, PH>(P, k, s, cbase, lo2, x, j);
+				}
 			}
 		}
 		if (j < k) {

@@ -23,13 +23,17 @@ template <int KM, int RM, int G>
 __device__ __forceinline__ void mm_ptr_item(const ecg_mm_params_t &P, const u32x4 *tb, int k, int rows,
 					    uint32_t s, uint64_t cbase, uint32_t lo, const uint64_t *a)
 {
+	// phased loads as the offset kernel's (ECG_MM_PHASE): the first PH cells
+	// now, the rest as the fold reaches them
+	constexpr int PH = (ECG_MM_PHASE(KM, G) > 0 && ECG_MM_PHASE(KM, G) < KM && KM % ECG_MM_PHASE(KM, G) == 0)
+				   ? ECG_MM_PHASE(KM, G) : 0;
 	u32x4 x[KM], outv[RM];
 
 #pragma unroll
-	for (int j = 0; j < KM; j++)
+	for (int j = 0; j < (PH ? PH : KM); j++)
 		if (j < k)
 			x[j] = ld_src<G>(reinterpret_cast<const uint8_t *>(a[j]), lo);
-	mm_compute<KM, RM, false, true, false>(P, tb, k, rows, s, cbase, lo, x, outv);
+	mm_compute<KM, RM, false, true, false, G, PH, false, true>(P, tb, k, rows, s, cbase, lo, x, outv, a);
 #pragma unroll
 	for (int r = 0; r < RM; r++)
 		if (r < rows)
@@ -99,7 +103,7 @@ __device__ __forceinline__ void mm_ptr_bytes(const u32x4 *tb, int k, int rows, c
 }
 
 template <int K, int R, int G>
-__global__ void __launch_bounds__(BLOCK)
+__global__ void __launch_bounds__(BLOCK, ECG_MM_WPE(K, R, G) ? ECG_MM_WPE(K, R, G) : 1)
 ecg_mm_ptr_kernel(const ecg_mm_params_t P, const uint64_t *__restrict__ cells)
 {
 	constexpr int KM = K ? K : ECG_KMAX_K;

@@ -21,6 +21,11 @@ MiB = 1 << 20
 # PTR_GX_DIVS: the pointer-table grid's x dimension = columns / d, so each
 # block walks d columns of its stripe (the stripe's table row loaded once)
 GX_DIVS = [int(d) for d in os.environ.get("PTR_GX_DIVS", "1").split(",")]
+# PTR_SHUFFLE=1: the table lists the stripes in a shuffled order -- the same
+# cells, no longer an affine table, so the pointer-table kernel runs
+SHUFFLE = os.environ.get("PTR_SHUFFLE") == "1"
+if os.environ.get("ECG_TEST_LIB"):
+    ecg.LIB_PATH = os.path.abspath(os.environ["ECG_TEST_LIB"])
 
 
 def timed(ctx, fn, iters=30, warm=40):
@@ -50,9 +55,10 @@ def main():
         pitch = S * Cb + 4096
         par = ctx.alloc(p * pitch)
         cells = []
-        for s in range(S):
-            cells += [data.ptr + (s * k + j) * Cb for j in range(k)]
-            cells += [par.ptr + r * pitch + s * Cb for r in range(p)]
+        order = np.random.default_rng(S).permutation(S) if SHUFFLE else range(S)
+        for s in order:
+            cells += [data.ptr + (int(s) * k + j) * Cb for j in range(k)]
+            cells += [par.ptr + r * pitch + int(s) * Cb for r in range(p)]
         arr = (C.c_void_p * len(cells))(*cells)
         h = ctx.h
 
