@@ -691,6 +691,37 @@ def sgl_rows(ctx, aligned, iters=11):
     return rows
 
 
+def update_rows(ctx, iters=11):
+    """Aggregation's delta parity update (agg_update_parity: xor_gen of old and
+    new, then ec_encode_data_update per updated cell,
+    ref:src/object/srv_ec_aggregate.c:1062-1105) batched over stripes:
+    parity[r] ^= sum_i coef[r][cell_i] * (old_i ^ new_i), one fused launch
+    reading old, new and the parity and writing the parity -- (2n + 2p) * C
+    algorithmic bytes per stripe for n updated cells."""
+    from daos_amd import ecg
+
+    k, p, C, S = 8, 2, 1 << 20, 512
+    rows = {}
+    for cells in ([3], [1, 6]):
+        n = len(cells)
+        old, new = ctx.alloc(S * n * C), ctx.alloc(S * n * C)
+        fill_device(ctx, old, S * n * C, 12)
+        fill_device(ctx, new, S * n * C, 13)
+        pitch = S * C + PARITY_ROW_PAD
+        par = ctx.alloc(p * pitch)
+        fill_device(ctx, par, p * pitch, 14)
+        ms = time_kernel(ctx, lambda: ctx.update(k, p, C, S, cells, old.ptr, new.ptr, n * C, par.ptr, pitch, C),
+                         iters, warm=40)
+        alg = (2 * n + 2 * p) * C * S
+        rows[f"EC_8P2_1MiB_update_{n}cell"] = {
+            "cells_per_stripe": n, "stripes": S, "ms": round(ms, 4),
+            "GiBps_updated": round(n * C * S / (ms / 1e3) / GIB, 1), "alg_GBps": round(alg / ms / 1e6, 1),
+            "roofline_frac": round(alg / ms / 1e6 / HBM_PEAK_GBS, 4), "kernel": ecg.last_kernel()}
+        for b in (old, new, par):
+            b.free()
+    return rows
+
+
 def detail_rows(ctx, ceil, iters=11, shapes=DETAIL_SHAPES, csum=True):
     """Extra device-resident rows (per GPU): the north-star EC_8P2 encode,
     EC_8P2 2-erasure decode, EC_16P2 128 KiB encode, EC_2P1 128 KiB encode.
@@ -745,6 +776,7 @@ def detail_rows(ctx, ceil, iters=11, shapes=DETAIL_SHAPES, csum=True):
             buf2.free()
     rows.update(offset_rows(ctx, rows.get("EC_8P2_1MiB_encode"), iters))
     rows.update(sgl_rows(ctx, rows.get("EC_8P2_1MiB_encode"), iters))
+    rows.update(update_rows(ctx, iters))
     if not csum:
         return rows
     # checksums of regenerated cells (include/ecg_csum.h): EC_8P2 encode with

@@ -272,6 +272,9 @@ static const kentry g_kernels[] = {
 	KE(4, 1, 0, 0), KE(4, 2, 0, 0), KE(4, 3, 0, 0),
 	KE(8, 1, 0, 0), KE(8, 2, 0, 0), KE(8, 3, 0, 0),
 	KE(16, 1, 0, 0), KE(16, 2, 0, 0), KE(16, 3, 0, 0),
+	// aggregation's delta update of one cell per stripe (ACC + DIFF, rows = p),
+	// ref:src/object/srv_ec_aggregate.c:1099-1101
+	KE(1, 1, 1, 1), KE(1, 2, 1, 1), KE(1, 3, 1, 1),
 	KE(0, 0, 0, 0), KE(0, 0, 1, 0), KE(0, 0, 0, 1), KE(0, 0, 1, 1),
 	KEG_SET(4), KEG_SET(1),
 };
@@ -352,10 +355,10 @@ extern "C" int ecg_k_launch_matmul(const ecg_mm_params_t *p, const ecg_launch_cf
 	}
 
 	uint32_t id = N_KERNELS;
-	if (variant != 1 && !p->accumulate && !p->diff) {
+	if (variant != 1) {
 		for (uint32_t i = 0; i < N_KERNELS; i++)
 			if (g_kernels[i].g == g && g_kernels[i].k == (int)p->k && g_kernels[i].r == (int)p->rows &&
-			    !g_kernels[i].acc && !g_kernels[i].diff) {
+			    g_kernels[i].acc == (int)(p->accumulate != 0) && g_kernels[i].diff == (int)(p->diff != 0)) {
 				id = i;
 				break;
 			}

@@ -6,7 +6,8 @@ round, libraries rotated every round (the box's clocks drift over a run).
 The launch tuner is off (ECG_AUTOTUNE=0); every plain shape is timed
 uncapped and at its candidate blocks-per-CU cap (k = 16: 2, k = 8: 3).
 EC_OPS (default "enc,dec") picks the shapes: enc, dec, crc32, crc64 (the
-fused encode + parity checksums), enc3 / dec3 (three parity rows / erasures).
+fused encode + parity checksums), enc3 / dec3 (three parity rows / erasures),
+upd1 / upd2 (delta parity update of 1 / 2 cells per stripe).
 EC_ORDERS (default "0") times each shape under the listed 1D item orders
 (ecg_set_launch_order: 1 stripe-fastest, 2 / 3 XCD-blocked).
 usage: [EC_OPS=...] python tools/ec_ab.py NAME=lib.so ... -> gpurun_out/ec_ab.json.
@@ -46,12 +47,27 @@ SHAPES = ((16, 2, 128 << 10, 1024, "enc", 0), (16, 2, 128 << 10, 1024, "dec", 0)
           (8, 2, MiB, 512, "enc", 8), (8, 2, MiB, 512, "enc", 4),
           (8, 2, MiB, 512, "crc32", 0), (8, 2, MiB, 512, "crc64", 0), (4, 2, MiB, 1024, "crc64", 0),
           (8, 3, MiB, 512, "enc3", 0), (8, 3, MiB, 512, "dec3", 0), (4, 3, MiB, 1024, "enc3", 0),
-          (16, 3, 128 << 10, 1024, "enc3", 0))
+          (16, 3, 128 << 10, 1024, "enc3", 0),
+          (8, 2, MiB, 512, "upd1", 0), (8, 2, MiB, 512, "upd2", 0), (4, 2, MiB, 1024, "upd1", 0),
+          (16, 2, 128 << 10, 1024, "upd1", 0))
 ops = os.environ.get("EC_OPS", "enc,dec").split(",")
 orders = [int(o) for o in os.environ.get("EC_ORDERS", "0").split(",")]
 res = {}
 for k, p, C, S, op, off in (s for s in SHAPES if s[4] in ops):
-    if op.startswith("crc"):
+    if op.startswith("upd"):
+        # delta parity update of n cells per stripe: parity ^= coef * (old ^ new)
+        n = int(op[3:])
+        cells = [3, 6][:n] if k > 6 else [0, 1][:n]
+        old, new = ctx.alloc(S * n * C), ctx.alloc(S * n * C)
+        old.fill(0x11)
+        new.fill(0x5E)
+        pitch = S * C + 4096
+        par = ctx.alloc(p * pitch + 64)
+        fn = lambda: ctx.update(k, p, C, S, cells, old.ptr, new.ptr, n * C, par.ptr, pitch, C)
+        bufs = (old, new, par)
+        rows = p
+        alg_over = (2 * n + 2 * p) * C * S
+    elif op.startswith("crc"):
         # encode + checksums of the parity over 32 KiB chunks (the fused kernel), back to back
         data = ctx.alloc(S * k * C + 64)
         pitch = S * C + 4096
@@ -77,9 +93,9 @@ for k, p, C, S, op, off in (s for s in SHAPES if s[4] in ops):
         fn = lambda: ctx.recover(k, p, C, S, img.ptr, (k + p) * C, errs)
         bufs = (img,)
         rows = len(errs)
-    alg = (k + rows) * C * S
+    alg = alg_over if op.startswith("upd") else (k + rows) * C * S
     for cap in ((255, 2) if k >= 16 else (255, 3) if k >= 8 else (255,)):
-        if (off or op.startswith("crc")) and cap != 255:
+        if (off or op.startswith("crc") or op.startswith("upd")) and cap != 255:
             continue
         for order in orders:
             ctx.set_wg_per_cu(cap)
