@@ -272,12 +272,15 @@ static const kentry g_kernels[] = {
 	KE(4, 1, 0, 0), KE(4, 2, 0, 0), KE(4, 3, 0, 0),
 	KE(8, 1, 0, 0), KE(8, 2, 0, 0), KE(8, 3, 0, 0),
 	KE(16, 1, 0, 0), KE(16, 2, 0, 0), KE(16, 3, 0, 0),
-	// aggregation's delta update of one or two cells per stripe (ACC + DIFF,
-	// rows = p), ref:src/object/srv_ec_aggregate.c:1099-1101: the runtime-
+	// aggregation's delta update of 1-4 cells per stripe (ACC + DIFF, rows =
+	// p), ref:src/object/srv_ec_aggregate.c:1099-1101 -- DAOS re-encodes the
+	// stripe instead when more of it changed (agg_recalc_parity): the runtime-
 	// shaped ACC + DIFF kernel holds 189 VGPRs (2 waves per SIMD) and ran these
-	// at half the rate (profiles/r04/ec_ab/ec_ab_update.json)
+	// at half the rate (profiles/r04/ec_ab/ec_ab_update*.json)
 	KE(1, 1, 1, 1), KE(1, 2, 1, 1), KE(1, 3, 1, 1),
 	KE(2, 1, 1, 1), KE(2, 2, 1, 1), KE(2, 3, 1, 1),
+	KE(3, 1, 1, 1), KE(3, 2, 1, 1), KE(3, 3, 1, 1),
+	KE(4, 1, 1, 1), KE(4, 2, 1, 1), KE(4, 3, 1, 1),
 	KE(0, 0, 0, 0), KE(0, 0, 1, 0), KE(0, 0, 0, 1), KE(0, 0, 1, 1),
 	KEG_SET(4), KEG_SET(1),
 };

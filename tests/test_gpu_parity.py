@@ -205,8 +205,12 @@ def test_recover_data_loss(ctx, ecglib):
 
 
 # --------------------------------------------------------------- update
-@pytest.mark.parametrize("k,p,cells", [(4, 2, [1]), (8, 2, [0, 5]), (8, 3, [2, 3, 7]), (16, 2, list(range(16)))])
-def test_update_matches_oracle(ctx, oracle, k, p, cells):
+@pytest.mark.parametrize("k,p,cells", [(4, 2, [1]), (8, 2, [0, 5]), (8, 3, [2, 3, 7]), (16, 2, list(range(16))),
+                                     (4, 1, [2]), (8, 1, [0, 1, 2, 3]), (16, 3, [4, 9]), (4, 3, [0, 1, 2, 3]),
+                                     (8, 2, [1, 2, 4, 6, 7])])
+def test_update_matches_oracle(ctx, oracle, ecglib, k, p, cells):
+    """Delta parity update (ACC + DIFF): 1-4 cells per stripe on their own
+    instantiations, more on the runtime-shaped kernel."""
     C_, S = 6000, 3
     en = oracle.cauchy1(k, p)
     data = rand((S, k, C_), 21)
@@ -216,6 +220,10 @@ def test_update_matches_oracle(ctx, oracle, k, p, cells):
     dold, dnew = ctx.to_device(old), ctx.to_device(new)
     dpar = ctx.to_device(par)
     ctx.update(k, p, C_, S, cells, dold.ptr, dnew.ptr, len(cells) * C_, dpar.ptr, S * C_, C_)
+    ctx.sync()
+    n = len(cells)
+    assert ecglib.last_kernel() == (f"ecg_mm_kernel<{n},{p},1,1>" if n <= 4 else "ecg_mm_kernel<0,0,1,1>"), \
+        ecglib.last_kernel()
     got = dpar.download().reshape(p, S, C_)
     for s in range(S):
         want = par[:, s].copy()

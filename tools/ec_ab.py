@@ -7,7 +7,7 @@ The launch tuner is off (ECG_AUTOTUNE=0); every plain shape is timed
 uncapped and at its candidate blocks-per-CU cap (k = 16: 2, k = 8: 3).
 EC_OPS (default "enc,dec") picks the shapes: enc, dec, crc32, crc64 (the
 fused encode + parity checksums), enc3 / dec3 (three parity rows / erasures),
-upd1 / upd2 (delta parity update of 1 / 2 cells per stripe).
+upd1 .. upd4 (delta parity update of 1-4 cells per stripe).
 EC_ORDERS (default "0") times each shape under the listed 1D item orders
 (ecg_set_launch_order: 1 stripe-fastest, 2 / 3 XCD-blocked).
 usage: [EC_OPS=...] python tools/ec_ab.py NAME=lib.so ... -> gpurun_out/ec_ab.json.
@@ -48,7 +48,8 @@ SHAPES = ((16, 2, 128 << 10, 1024, "enc", 0), (16, 2, 128 << 10, 1024, "dec", 0)
           (8, 2, MiB, 512, "crc32", 0), (8, 2, MiB, 512, "crc64", 0), (4, 2, MiB, 1024, "crc64", 0),
           (8, 3, MiB, 512, "enc3", 0), (8, 3, MiB, 512, "dec3", 0), (4, 3, MiB, 1024, "enc3", 0),
           (16, 3, 128 << 10, 1024, "enc3", 0),
-          (8, 2, MiB, 512, "upd1", 0), (8, 2, MiB, 512, "upd2", 0), (4, 2, MiB, 1024, "upd1", 0),
+          (8, 2, MiB, 512, "upd1", 0), (8, 2, MiB, 512, "upd2", 0), (8, 2, MiB, 512, "upd3", 0),
+          (8, 2, MiB, 512, "upd4", 0), (4, 2, MiB, 1024, "upd1", 0),
           (16, 2, 128 << 10, 1024, "upd1", 0))
 ops = os.environ.get("EC_OPS", "enc,dec").split(",")
 orders = [int(o) for o in os.environ.get("EC_ORDERS", "0").split(",")]
@@ -57,7 +58,7 @@ for k, p, C, S, op, off in (s for s in SHAPES if s[4] in ops):
     if op.startswith("upd"):
         # delta parity update of n cells per stripe: parity ^= coef * (old ^ new)
         n = int(op[3:])
-        cells = [3, 6][:n] if k > 6 else [0, 1][:n]
+        cells = [3, 6, 0, 5][:n] if k > 6 else [0, 1, 2, 3][:n]
         old, new = ctx.alloc(S * n * C), ctx.alloc(S * n * C)
         old.fill(0x11)
         new.fill(0x5E)
