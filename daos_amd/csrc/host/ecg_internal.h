@@ -163,6 +163,16 @@ struct ecg_tuner;
 int ecg_tune_init(ecg_ctx_t *ctx);
 void ecg_tune_fini(ecg_ctx_t *ctx);
 int ecg_tune_launch(ecg_ctx_t *ctx, const ecg_mm_params_t *p, hipStream_t st, uint32_t *kid);
+/* The same for any launcher of the product (the pointer-table kernel): `g`
+ * its lane granule, `layout` its layout class (ECG_TUNE_LAYOUT_*), `fn(p,
+ * cfg, stream, kid, arg)` the launch under a given geometry. */
+typedef int (*ecg_mm_launch_fn)(const ecg_mm_params_t *p, const ecg_launch_cfg_t *cfg, void *stream,
+				uint32_t *kid, const void *arg);
+#define ECG_TUNE_LAYOUT_SEPARATE 0u	/* source and destination stripe strides differ */
+#define ECG_TUNE_LAYOUT_INTERLEAVED 1u	/* one stripe stride: in-place recovery */
+#define ECG_TUNE_LAYOUT_PTRS 2u		/* per-stripe pointer table */
+int ecg_tune_launch_fn(ecg_ctx_t *ctx, const ecg_mm_params_t *p, uint32_t g, uint32_t layout,
+		       ecg_mm_launch_fn fn, const void *arg, hipStream_t st, uint32_t *kid);
 
 /* context helpers (ecg_core.c) */
 int ecg_ctx_enter(ecg_ctx_t *ctx);

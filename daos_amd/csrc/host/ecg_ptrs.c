@@ -142,6 +142,19 @@ static int launch_affine(ecg_ctx_t *ctx, const uint64_t *tab, int k, int rows, c
 			  (void *)(uintptr_t)tab[k], doff, ds, 0, (void *)st);
 }
 
+struct ptr_launch_arg {
+	const uint64_t *cells_dev;
+	int granule;
+};
+
+static int launch_ptrs(const ecg_mm_params_t *p, const ecg_launch_cfg_t *cfg, void *stream, uint32_t *kid,
+		       const void *arg)
+{
+	const struct ptr_launch_arg *a = arg;
+
+	return ecg_k_launch_matmul_ptrs(p, a->cells_dev, a->granule, cfg, stream, kid);
+}
+
 /* Table already in sc->pin (S x (k+rows) entries); copy, launch, record
  * (ctx->lock held).  With `gather`, its segment table follows the pointer
  * table at byte seg_off of the slot (pinned and device alike): both travel in
@@ -183,8 +196,13 @@ static int launch_table(ecg_ctx_t *ctx, struct ecg_scratch_slot *sc, int k, int 
 	for (r = 0; r < rows; r++)
 		for (j = 0; j < k; j++)
 			ecg_build_ptbl(coef[(size_t)r * k + j], &prm->tbl[r][j]);
-	ke = ecg_k_launch_matmul_ptrs(prm, (const uint64_t *)sc->dev, granule, &ctx->cfg, (void *)st,
-				      &kid);
+	{
+		/* through the launch tuner like the strided product: wide stripes
+		 * probe the blocks-per-CU cap per (shape, pointer-table layout) */
+		const struct ptr_launch_arg a = {(const uint64_t *)sc->dev, granule};
+
+		ke = ecg_tune_launch_fn(ctx, prm, (uint32_t)granule, ECG_TUNE_LAYOUT_PTRS, launch_ptrs, &a, st, &kid);
+	}
 	free(prm);
 	if (ke != 0)
 		return ecg_hip_fail((hipError_t)ke, "pointer-table kernel launch");

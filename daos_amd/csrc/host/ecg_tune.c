@@ -96,7 +96,7 @@ static uint32_t candidate_cap(const ecg_mm_params_t *p)
 
 static uint32_t layout_class(const ecg_mm_params_t *p)
 {
-	return p->src_stripe_stride == p->dst_stripe_stride;	/* 1: interleaved, 0: separate */
+	return p->src_stripe_stride == p->dst_stripe_stride ? ECG_TUNE_LAYOUT_INTERLEAVED : ECG_TUNE_LAYOUT_SEPARATE;
 }
 
 int ecg_tune_init(ecg_ctx_t *ctx)
@@ -167,20 +167,21 @@ int ecg_set_autotune(ecg_ctx_t *ctx, int on)
 	return 0;
 }
 
-static int same_shape(const struct ecg_tune_ent *e, const ecg_mm_params_t *p, uint32_t g)
+static int same_shape(const struct ecg_tune_ent *e, const ecg_mm_params_t *p, uint32_t g, uint32_t layout)
 {
 	return e->valid && e->k == p->k && e->rows == p->rows && e->acc == p->accumulate && e->diff == p->diff &&
-	       e->C == p->cell_bytes && e->layout == layout_class(p) && (g == 0 || e->g == g);
+	       e->C == p->cell_bytes && e->layout == layout && (g == 0 || e->g == g);
 }
 
 /* g = 0 matches any lane granule (ecg_tune_state) */
-static struct ecg_tune_ent *lookup(struct ecg_tuner *t, const ecg_mm_params_t *p, uint32_t g, int create)
+static struct ecg_tune_ent *lookup(struct ecg_tuner *t, const ecg_mm_params_t *p, uint32_t g, uint32_t layout,
+				   int create)
 {
 	struct ecg_tune_ent *old = NULL;
 	int i;
 
 	for (i = 0; i < ECG_NTUNE; i++) {
-		if (same_shape(&t->ent[i], p, g)) {
+		if (same_shape(&t->ent[i], p, g, layout)) {
 			t->ent[i].stamp = ++t->clock;
 			return &t->ent[i];
 		}
@@ -208,7 +209,7 @@ static struct ecg_tune_ent *lookup(struct ecg_tuner *t, const ecg_mm_params_t *p
 	old->diff = p->diff;
 	old->C = p->cell_bytes;
 	old->g = g;
-	old->layout = layout_class(p);
+	old->layout = layout;
 	old->stamp = ++t->clock;
 	t->cycles++;
 	return old;
@@ -279,33 +280,45 @@ static int make_events(struct ecg_tune_ent *e)
 	return 0;
 }
 
+static int launch_offsets(const ecg_mm_params_t *p, const ecg_launch_cfg_t *cfg, void *stream, uint32_t *kid,
+			  const void *arg)
+{
+	(void)arg;
+	return ecg_k_launch_matmul(p, cfg, stream, kid);
+}
+
 int ecg_tune_launch(ecg_ctx_t *ctx, const ecg_mm_params_t *p, hipStream_t st, uint32_t *kid)
+{
+	return ecg_tune_launch_fn(ctx, p, ecg_k_align_granule(p), layout_class(p), launch_offsets, NULL, st, kid);
+}
+
+int ecg_tune_launch_fn(ecg_ctx_t *ctx, const ecg_mm_params_t *p, uint32_t g, uint32_t layout,
+		       ecg_mm_launch_fn fn, const void *arg, hipStream_t st, uint32_t *kid)
 {
 	struct ecg_tuner *t = ctx->tuner;
 	ecg_launch_cfg_t cfg = ctx->cfg;
 	struct ecg_tune_ent *e;
 	hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-	uint32_t cand, g;
+	uint32_t cand;
 	int arm, idx, timed = 0, rc;
 
 	cand = candidate_cap(p);
 	if (t == NULL || cand == 0 || cfg.wg_per_cu != 0 || cfg.variant != 0 || cfg.order != 0 ||
 	    cfg.grid_x != 0 || cfg.grid_y != 0)
-		return ecg_k_launch_matmul(p, &ctx->cfg, (void *)st, kid);
-	g = ecg_k_align_granule(p);
+		return fn(p, &ctx->cfg, (void *)st, kid, arg);
 	if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
-		return ecg_k_launch_matmul(p, &ctx->cfg, (void *)st, kid);
+		return fn(p, &ctx->cfg, (void *)st, kid, arg);
 
 	pthread_mutex_lock(&t->lock);
 	if (!enabled(t)) {
 		pthread_mutex_unlock(&t->lock);
-		return ecg_k_launch_matmul(p, &ctx->cfg, (void *)st, kid);
+		return fn(p, &ctx->cfg, (void *)st, kid, arg);
 	}
-	e = lookup(t, p, g, 1);
+	e = lookup(t, p, g, layout, 1);
 	if (e == NULL) {		/* probe budget spent: untuned shapes run uncapped */
 		cfg.wg_per_cu = ECG_WG_UNCAPPED;
 		pthread_mutex_unlock(&t->lock);
-		return ecg_k_launch_matmul(p, &cfg, (void *)st, kid);
+		return fn(p, &cfg, (void *)st, kid, arg);
 	}
 	if (e->n == 0 && !e->decided) {
 		e->stream = st;		/* the probe runs on the stream that starts it */
@@ -316,20 +329,20 @@ int ecg_tune_launch(ecg_ctx_t *ctx, const ecg_mm_params_t *p, hipStream_t st, ui
 	if (e->decided) {
 		cfg.wg_per_cu = e->choice;
 		pthread_mutex_unlock(&t->lock);
-		return ecg_k_launch_matmul(p, &cfg, (void *)st, kid);
+		return fn(p, &cfg, (void *)st, kid, arg);
 	}
 	if (e->n >= ECG_TUNE_PROBE || st != e->stream) {
 		/* timings still in flight, or another stream: run uncapped */
 		cfg.wg_per_cu = ECG_WG_UNCAPPED;
 		pthread_mutex_unlock(&t->lock);
-		return ecg_k_launch_matmul(p, &cfg, (void *)st, kid);
+		return fn(p, &cfg, (void *)st, kid, arg);
 	}
 	if (!e->events && make_events(e)) {
 		e->decided = 1;
 		e->choice = ECG_WG_UNCAPPED;
 		cfg.wg_per_cu = ECG_WG_UNCAPPED;
 		pthread_mutex_unlock(&t->lock);
-		return ecg_k_launch_matmul(p, &cfg, (void *)st, kid);
+		return fn(p, &cfg, (void *)st, kid, arg);
 	}
 	/* probing: arm 0 uncapped, arm 1 capped, each W untimed + T timed, back
 	 * to back; the lock is held across the timed launch so concurrent callers
@@ -343,7 +356,7 @@ int ecg_tune_launch(ecg_ctx_t *ctx, const ecg_mm_params_t *p, hipStream_t st, ui
 		timed = hipEventRecord(e->ev[arm][idx][0], st) == hipSuccess;
 		e->blocks[arm][idx] = mm_blocks(p);
 	}
-	rc = ecg_k_launch_matmul(p, &cfg, (void *)st, kid);
+	rc = fn(p, &cfg, (void *)st, kid, arg);
 	if (timed && (rc != 0 || hipEventRecord(e->ev[arm][idx][1], st) != hipSuccess)) {
 		e->decided = 1;		/* give up on this shape: uncapped */
 		e->choice = ECG_WG_UNCAPPED;
@@ -373,7 +386,7 @@ int ecg_tune_state(ecg_ctx_t *ctx, int k, int rows, uint64_t cell_bytes, uint32_
 	p->src_stripe_stride = sstride;
 	p->dst_stripe_stride = dstride;
 	pthread_mutex_lock(&t->lock);
-	e = lookup(t, p, 0, 0);
+	e = lookup(t, p, 0, layout_class(p), 0);
 	if (e && !e->decided && e->n >= ECG_TUNE_PROBE)
 		(void)try_decide(e);
 	rc = e && e->decided ? 1 : 0;

@@ -213,3 +213,40 @@ def test_autotune_probe_other_stream_not_timed(ctx, ecglib, oracle):
     finally:
         ctx.destroy_stream(st2)
         ctx.set_autotune(1)
+
+
+def test_autotune_pointer_tables(ctx, oracle, ecglib):
+    """Pointer-table launches (ecg_matmul_ptrs with a table that is not affine:
+    the stripes listed in shuffled order) go through the launch tuner as
+    their own layout class: one probe of PROBE launches for the wide shape,
+    kept apart from the strided encode of the same (k, rows, C), and every
+    launch writes the oracle's parity."""
+    k, p, S, C_ = 16, 2, 300, 32768          # 2400 blocks: tuned
+    data = rand((S, k, C_), 1701)
+    en = oracle.cauchy1(k, p)
+    want = np.stack([oracle.encode_data(en[k:], data[s]) for s in range(S)], axis=1)   # [p][S][C]
+    order = np.random.default_rng(3).permutation(S)
+    ctx.set_autotune(2)
+    try:
+        d = ctx.to_device(data)
+        pars = [ctx.alloc(p * S * C_) for _ in range(PROBE + 2)]
+        for par in pars:
+            cells = []
+            for s in order:
+                cells += [d.ptr + (int(s) * k + j) * C_ for j in range(k)]
+                cells += [par.ptr + r * S * C_ + int(s) * C_ for r in range(p)]
+            ctx.matmul_ptrs(k, p, en[k:], C_, S, cells)
+            assert ecglib.last_kernel().startswith("ecg_mm_ptr_kernel<16,2"), ecglib.last_kernel()
+        ctx.sync()
+        cycles, launches, shapes = ctx.tune_counters()
+        assert cycles == 1 and launches == PROBE and shapes == 1, (cycles, launches, shapes)
+        for par in pars:
+            assert np.array_equal(par.download().reshape(p, S, C_), want)
+        # the strided encode of the same shape is a different layout class: a probe of its own
+        ctx.encode(k, p, C_, S, d.ptr, k * C_, pars[0].ptr, S * C_, C_)
+        ctx.sync()
+        assert ctx.tune_counters()[0] == 2
+        for b in pars + [d]:
+            b.free()
+    finally:
+        ctx.set_autotune(1)
