@@ -26,8 +26,10 @@
  * Shapes are keyed coarsely (round 4): by (k, rows,
  * acc, diff, cell bytes, lane granule, layout class) where the layout class
  * is "interleaved" (source and destination share one stripe stride: in-place
- * recovery, the recovery-layout encode) or "separate" (the client write
- * layout).  The batch size is not part of the key: callers whose batches
+ * recovery, the recovery-layout encode), "separate" (the client write
+ * layout) or "pointer table" (ecg_matmul_ptrs / recx_encode launches of the
+ * pointer-table kernel, which come in through ecg_tune_launch_fn with their
+ * own launcher).  The batch size is not part of the key: callers whose batches
  * vary (queue flushes, the last batch of a rebuild, per-shard counts) share
  * one decision, and the arms compare the median time PER BLOCK, so a probe
  * stays valid when batch sizes change under it.  A probe runs on the stream
