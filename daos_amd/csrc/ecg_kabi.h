@@ -66,8 +66,12 @@ typedef struct ecg_launch_cfg {
 	uint32_t order;		/* 0 = 2D grid x columns / y stripes; 1-3 1D orders (ecg_kernels.hip) */
 	uint32_t wg_per_cu;	/* product kernel blocks per CU: 0 = per-shape default, 1..16 = cap,
 				 * ECG_WG_UNCAPPED = none (ecg_kernels.hip mm_wg_cap) */
+	uint32_t no_unaligned;	/* the device did not serve misaligned dword accesses at context
+				 * creation (ecg_k_unaligned_check): operands that need them take
+				 * the byte kernels */
 } ecg_launch_cfg_t;
 #define ECG_WG_UNCAPPED 255u
+
 
 /*
  * Chunked checksums (DAOS csummer semantics, ref:src/common/checksum.c:467-497):
@@ -249,6 +253,13 @@ typedef struct ecg_copy_seg {
 #ifdef __cplusplus
 extern "C" {
 #endif
+/* Whether the device serves misaligned dword loads and stores (the unaligned
+ * access mode the ROCm driver enables on gfx9+), which the product kernels
+ * use for destinations off a dword boundary and for partial columns of
+ * unaligned sources: 4 lanes copy dwords from src+1+4i to dst+3+4i of small
+ * scratch buffers and the bytes are compared.  *ok = 1 when they arrived
+ * intact.  Synchronous on `stream`. */
+int ecg_k_unaligned_check(void *stream, int *ok);
 /* Tiles one segment occupies (0 when len == 0). */
 uint64_t ecg_k_copy_tiles(uint64_t dst, uint64_t len);
 /* One launch of ntiles workgroups over nseg segments (segs_dev in device memory). */

@@ -116,8 +116,28 @@ int ecg_ctx_create(int device, ecg_ctx_t **out)
 		free(ctx);
 		return -ECG_DER_NOMEM;
 	}
+	{
+		/* misaligned dword accesses served? (destinations off a dword, partial
+		 * columns of unaligned sources); ECG_UNALIGNED=0 forces the byte
+		 * kernels for those operands, as a device without them would get */
+		const char *env = getenv("ECG_UNALIGNED");
+		int ok = 0;
+
+		if (env && env[0] == '0')
+			ok = 0;
+		else if (ecg_k_unaligned_check((void *)ctx->stream, &ok) != 0)
+			ok = 0;
+		ctx->cfg.no_unaligned = ok ? 0u : 1u;
+	}
 	*out = ctx;
 	return 0;
+}
+
+int ecg_ctx_unaligned_ok(ecg_ctx_t *ctx)
+{
+	if (ctx == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "NULL context");
+	return ctx->cfg.no_unaligned ? 0 : 1;
 }
 
 static void stage_free(ecg_ctx_t *ctx)

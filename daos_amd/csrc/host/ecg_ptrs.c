@@ -82,8 +82,9 @@ void ecg_scratch_free(ecg_ctx_t *ctx)
 }
 
 /* Lane access of a pointer table (ecg_k_launch_matmul_ptrs): from the OR of
- * the input and of the output cell addresses. */
-static int ptr_granule(const uint64_t *tab, uint32_t S, int k, int rows)
+ * the input and of the output cell addresses; 0 (the byte kernel) when the
+ * device serves no misaligned dwords and an address is off a dword. */
+static int ptr_granule(const uint64_t *tab, uint32_t S, int k, int rows, int no_unaligned)
 {
 	uint64_t in = 0, out = 0;
 
@@ -95,6 +96,8 @@ static int ptr_granule(const uint64_t *tab, uint32_t S, int k, int rows)
 		for (int r = 0; r < rows; r++)
 			out |= t[k + r];
 	}
+	if (no_unaligned && ((in | out) & 3u))
+		return 0;
 	if (in & 3u)
 		return 1;	/* outputs at any byte: misaligned dword stores */
 	return ((in | out) & 15u) == 0 ? 16 : 4;
@@ -163,7 +166,7 @@ static int launch_table(ecg_ctx_t *ctx, struct ecg_scratch_slot *sc, int k, int 
 			const unsigned char *coef, uint64_t C, uint32_t S, hipStream_t st,
 			const struct ecg_segs *gather, size_t seg_off)
 {
-	const int granule = ptr_granule((const uint64_t *)sc->pin, S, k, rows);
+	const int granule = ptr_granule((const uint64_t *)sc->pin, S, k, rows, (int)ctx->cfg.no_unaligned);
 	size_t tbytes = (size_t)S * (size_t)(k + rows) * sizeof(uint64_t);
 	ecg_mm_params_t *prm;
 	uint32_t kid = 0;

@@ -24,6 +24,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 #include "../ecg_kabi.h"
 #include "ecg_mm_dev.h"
@@ -298,6 +299,65 @@ static const kentry g_kernels[] = {
 
 // All output cells equally far (md bytes) past a dword boundary: *head = the
 // 4 - md bytes before their first aligned dword (1).  0 if they differ.
+// 4 lanes copy a dword from in + 1 + 4i to out + 3 + 4i: misaligned vector
+// loads and stores exactly as the product's lanes issue them (per-lane
+// addresses, so never scalar-memory accesses)
+__global__ void ecg_unaligned_probe_kernel(const uint8_t *in, uint8_t *out)
+{
+	const uint32_t i = threadIdx.x;
+
+	if (i < 4) {
+		const uint32_t v = *reinterpret_cast<const uint32_t *>(in + 1 + 4 * i);
+		*reinterpret_cast<uint32_t *>(out + 3 + 4 * i) = v;
+	}
+}
+
+extern "C" int ecg_k_unaligned_check(void *stream, int *ok)
+{
+	hipStream_t st = (hipStream_t)stream;
+	uint8_t h[64], *d = nullptr;
+	hipError_t e;
+
+	*ok = 0;
+	for (int i = 0; i < 32; i++)
+		h[i] = (uint8_t)(0x40 + i);
+	memset(h + 32, 0xEE, 32);
+	e = hipMalloc(&d, 64);
+	if (e != hipSuccess)
+		return (int)e;
+	e = hipMemcpyAsync(d, h, 64, hipMemcpyHostToDevice, st);
+	if (e == hipSuccess) {
+		hipLaunchKernelGGL(ecg_unaligned_probe_kernel, dim3(1), dim3(64), 0, st, d, d + 32);
+		e = hipGetLastError();
+	}
+	if (e == hipSuccess)
+		e = hipMemcpyAsync(h, d, 64, hipMemcpyDeviceToHost, st);
+	if (e == hipSuccess)
+		e = hipStreamSynchronize(st);
+	(void)hipFree(d);
+	if (e != hipSuccess)
+		return (int)e;
+	*ok = 1;
+	for (int i = 0; i < 32; i++) {
+		const uint8_t want = i >= 3 && i < 19 ? (uint8_t)(0x40 + i - 2) : 0xEE;
+
+		if (h[32 + i] != want)
+			*ok = 0;
+	}
+	return 0;
+}
+
+// destinations off a dword boundary (their stores, and ACC loads, are
+// misaligned dword accesses)
+static bool dst_misaligned(const ecg_mm_params_t *p)
+{
+	uint64_t db = (uint64_t)(uintptr_t)p->dst | (uint64_t)p->dst_stripe_stride;
+
+	for (uint32_t r = 0; r < p->rows; r++)
+		db |= (uint64_t)p->dst_cell_off[r];
+	return (db & 3u) != 0;
+}
+
 extern "C" uint32_t ecg_k_align_granule(const ecg_mm_params_t *p)
 {
 	return align_granule(p);
@@ -347,9 +407,11 @@ extern "C" int ecg_k_launch_matmul(const ecg_mm_params_t *p, const ecg_launch_cf
 	// 1: a source at any byte -- funnel-shifted loads); destinations at any
 	// byte take the dword lanes' (misaligned) stores
 	int g = (int)align_granule(p);
-	if (variant == 3 && g < 4)
+	if (cfg && cfg->no_unaligned && (g == 1 || dst_misaligned(p)))
+		g = 0;		// the device serves no misaligned dwords: bytewise
+	else if (variant == 3 && g < 4)
 		g = 4;		// A/B: misaligned source dwords loaded as they are
-	if (variant == 2) {
+	if (variant == 2 || g == 0) {
 		uint64_t total = p->cell_bytes * p->nstripes;
 		uint64_t blocks = (total + BLOCK - 1) / BLOCK;
 		if (blocks > 8192)

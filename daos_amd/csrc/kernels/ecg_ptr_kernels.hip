@@ -242,7 +242,8 @@ extern "C" int ecg_k_launch_matmul_ptrs(const ecg_mm_params_t *p, const uint64_t
 		return (int)hipSuccess;
 	if (g == 16 && (p->cell_bytes & 15u))	// the 16-byte lanes need whole 16-byte pieces
 		g = 4;
-	if (cfg && cfg->variant == 2) {
+	if (g == 0 || (cfg && cfg->variant == 2)) {	/* 0: the host found operands the
+							 * device cannot serve as dwords */
 		uint64_t blocks = (p->cell_bytes * p->nstripes + BLOCK - 1) / BLOCK;
 		if (blocks > 8192)
 			blocks = 8192;

@@ -37,6 +37,7 @@ _SIGS = [
     ("ecg_device_count", C.c_int, []),
     ("ecg_ctx_create", C.c_int, [C.c_int, C.POINTER(vp)]),
     ("ecg_ctx_destroy", None, [vp]),
+    ("ecg_ctx_unaligned_ok", C.c_int, [vp]),
     ("ecg_ctx_device", C.c_int, [vp]),
     ("ecg_ctx_stream", vp, [vp]),
     ("ecg_device_pci_bus_id", C.c_int, [C.c_int, C.c_char_p, C.c_int]),
@@ -485,6 +486,12 @@ class Context:
     def set_wg_per_cu(self, wg_per_cu: int = 0):
         """Product-kernel blocks per CU: 0 per-shape default, 1..16 cap, 255 none."""
         _chk(lib().ecg_set_wg_per_cu(self.h, wg_per_cu), "set_wg_per_cu")
+
+    def unaligned_ok(self) -> bool:
+        """include/ecg.h ecg_ctx_unaligned_ok: misaligned dword accesses served."""
+        r = lib().ecg_ctx_unaligned_ok(self.h)
+        _chk(min(r, 0), "ctx_unaligned_ok")
+        return r == 1
 
     def set_autotune(self, on: int = 1):
         """Launch tuner (include/ecg.h ecg_set_autotune): 0 off, 1 on, 2 on and forget decisions."""

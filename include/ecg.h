@@ -55,6 +55,12 @@ int ecg_device_count(void);
 int ecg_ctx_create(int device, ecg_ctx_t **ctx);
 void ecg_ctx_destroy(ecg_ctx_t *ctx);
 int ecg_ctx_device(const ecg_ctx_t *ctx);
+/* 1 when the context's device served misaligned dword loads and stores at
+ * creation (the unaligned access mode ROCm enables on gfx9+): destinations
+ * off a dword boundary then run on the vector lanes; 0 when it did not (or
+ * ECG_UNALIGNED=0 was set): such launches run the byte kernels, same
+ * results, ~8x slower. */
+int ecg_ctx_unaligned_ok(ecg_ctx_t *ctx);
 /* PCI bus id ("0000:c1:00.0") of a visible device: tells ranks or shards
  * that landed on the same physical GPU apart. */
 int ecg_device_pci_bus_id(int device, char *buf, int len);

@@ -212,3 +212,66 @@ def test_update_unaligned_cells_aligned_parity(ctx, oracle, ecglib, off):
     finally:
         for b in (dold, dnew, dpar):
             b.free()
+
+
+def test_unaligned_access_served(ctx):
+    """The context's start-up probe (ecg_k_unaligned_check: misaligned dword
+    loads and stores by 4 lanes) found them served on this MI355X, so
+    misaligned destinations run on the vector lanes."""
+    assert ctx.unaligned_ok()
+
+
+CHILD_NO_UNALIGNED = r'''
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from daos_amd import ecg
+from oracle import ref as oracle
+ctx = ecg.Context(0)
+assert not ctx.unaligned_ok()
+k, p, C, S = 8, 2, 3 * 4096 + 20, 3
+rng = np.random.default_rng(9)
+data = rng.integers(0, 256, (S, k, C), dtype=np.uint8)
+en = oracle.cauchy1(k, p)
+want = np.stack([oracle.encode_data(en[k:], data[s]) for s in range(S)])      # [S][p][C]
+for doff, poff, kern in ((0, 0, "ecg_mm_kernel<8,2,0,0,g4>"), (0, 1, "ecg_mm_byte_kernel"),
+                         (1, 0, "ecg_mm_byte_kernel"), (4, 8, "ecg_mm_kernel<8,2,0,0,g4>")):
+    d = ctx.alloc(data.nbytes + 64)
+    d.upload(data.reshape(-1), offset=doff)
+    par = ctx.alloc(p * S * C + 64)
+    ctx.encode(k, p, C, S, d.ptr + doff, k * C, par.ptr + poff, S * C, C)
+    ctx.sync()
+    assert ecg.last_kernel() == kern, (doff, poff, ecg.last_kernel())
+    got = par.download(p * S * C, offset=poff).reshape(p, S, C).transpose(1, 0, 2)
+    assert np.array_equal(got, want), (doff, poff)
+    # the pointer-table path: stripes listed in reverse (not an affine table)
+    cells = []
+    for s in reversed(range(S)):
+        cells += [d.ptr + doff + (s * k + j) * C for j in range(k)]
+        cells += [par.ptr + poff + r * S * C + s * C for r in range(p)]
+    ctx.matmul_ptrs(k, p, en[k:], C, S, cells)
+    ctx.sync()
+    assert (ecg.last_kernel() == "ecg_mm_ptr_byte_kernel") == (doff % 4 != 0 or poff % 4 != 0), ecg.last_kernel()
+    got = par.download(p * S * C, offset=poff).reshape(p, S, C).transpose(1, 0, 2)
+    assert np.array_equal(got, want), ("ptr", doff, poff)
+    d.free()
+    par.free()
+print("OK")
+'''
+
+
+def test_no_unaligned_access_takes_byte_kernels():
+    """A device that does not serve misaligned dwords (forced with
+    ECG_UNALIGNED=0): launches whose sources or destinations are off a dword
+    boundary run the byte kernels, the rest the vector lanes; every output
+    equals the oracle's.  In a child process (the flag is read at context
+    creation)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ECG_UNALIGNED="0")
+    r = subprocess.run([sys.executable, "-c", CHILD_NO_UNALIGNED, root], capture_output=True, text=True, env=env,
+                       timeout=110)
+    assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout + r.stderr
