@@ -244,9 +244,9 @@ for doff, poff, kern in ((0, 0, "ecg_mm_kernel<8,2,0,0,g4>"), (0, 1, "ecg_mm_byt
     assert ecg.last_kernel() == kern, (doff, poff, ecg.last_kernel())
     got = par.download(p * S * C, offset=poff).reshape(p, S, C).transpose(1, 0, 2)
     assert np.array_equal(got, want), (doff, poff)
-    # the pointer-table path: stripes listed in reverse (not an affine table)
+    # the pointer-table path: stripes listed as 1, 0, 2 (not an affine table)
     cells = []
-    for s in reversed(range(S)):
+    for s in (1, 0, 2):
         cells += [d.ptr + doff + (s * k + j) * C for j in range(k)]
         cells += [par.ptr + poff + r * S * C + s * C for r in range(p)]
     ctx.matmul_ptrs(k, p, en[k:], C, S, cells)
