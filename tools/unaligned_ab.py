@@ -1,7 +1,8 @@
 """Misaligned operands: the launch's own choice (variant 0: funnel-shifted
-dword lanes, bytewise head + shifted body, byte kernel) against dword lanes
-issued at the misaligned addresses themselves (variant 3: the hardware's
-unaligned access mode serves them).  EC_8P2 1 MiB client-layout encode;
+source dwords for sources at any byte, misaligned dword stores for
+destinations at any byte; before round 4's change, a bytewise head + shifted
+body or the byte kernel) against dword lanes issued at the misaligned
+addresses themselves for the sources too (variant 3).  EC_8P2 1 MiB client-layout encode;
 median of 20 back-to-back launches after 10; both variants' parity compared
 byte for byte.  usage: python tools/unaligned_ab.py -> gpurun_out/unaligned_ab.json.
 Bench infrastructure."""
