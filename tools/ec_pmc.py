@@ -5,7 +5,9 @@ launches after 2 warm-up launches, seeded random cells:
   enc_16p2    EC_16P2 128 KiB x 1024, data [S][k][C] -> parity [p][S][C] (padded pitch)
   dec_16p2    EC_16P2 128 KiB x 1024, {d0,d1} regenerated in [S][k+p][C]
   enc_4p2 / enc_8p2 / enc_16p2_cap2 (2 blocks per CU) / enc_16p2_x4096, and the
-  streaming read / write kernels (4 GiB) as references for the memory-side counters
+  streaming read / write kernels (4 GiB) as references for the memory-side counters,
+  upd1_8p2    EC_8P2 1 MiB x 512, delta update of one cell per stripe (old, new
+              [S][1][C], parity [p][S][C] read and written)
 Run as  rocprofv3 --pmc FETCH_SIZE -- python3 tools/ec_pmc.py dec_8p2  and summarise
 with tools/pmc_traffic.py (algorithmic bytes printed here) or tools/pmc_summary.py.
 The launch tuner is off: every launch runs the geometry named.  Bench infrastructure."""
@@ -21,7 +23,7 @@ SHAPES = {"dec_8p2": (8, 2, 1 << 20, 512, "dec"), "enc_16p2": (16, 2, 128 << 10,
           "dec_16p2": (16, 2, 128 << 10, 1024, "dec"), "enc_4p2": (4, 2, 1 << 20, 1024, "enc"),
           "enc_8p2": (8, 2, 1 << 20, 512, "enc"), "enc_16p2_cap2": (16, 2, 128 << 10, 1024, "enc"),
           "enc_16p2_x4096": (16, 2, 128 << 10, 4096, "enc"), "read": (0, 0, 0, 0, "read"),
-          "write": (0, 0, 0, 0, "write")}
+          "write": (0, 0, 0, 0, "write"), "upd1_8p2": (8, 2, 1 << 20, 512, "upd")}
 
 
 def stream(ctx, mode):
@@ -54,7 +56,13 @@ def main():
     blk = stripe_bytes(256 << 20, 5)
     for off in range(0, buf.nbytes, blk.size):
         buf.upload(blk[: min(blk.size, buf.nbytes - off)], offset=off)
-    if op == "enc":
+    if op == "upd":
+        # old / new cells in the first 2*S*C bytes of buf, parity rows after them
+        pitch = S * C + 4096
+        par = ctx.alloc(p * pitch)
+        fn = lambda: ctx.update(k, p, C, S, [3], buf.ptr, buf.ptr + S * C, C, par.ptr, pitch, C)  # noqa: E731
+        alg = (2 + 2 * p) * C * S
+    elif op == "enc":
         pitch = S * C + 4096
         par = ctx.alloc(p * pitch)
         fn = lambda: ctx.encode(k, p, C, S, buf.ptr, k * C, par.ptr, pitch, C)  # noqa: E731

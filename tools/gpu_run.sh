@@ -66,6 +66,15 @@ for what in "$@"; do
 		python tools/pmc_traffic.py "$O/pmc_dec_16p2_f" "$O/pmc_dec_16p2_w" "ecg_mm_kernel<16, 2" 2415919104 \
 			"$O/pmc_traffic_dec_16p2.json" || exit $?
 		;;
+	updpmc)           # HBM bytes of the one-cell delta update kernel
+		rm -rf "$O/pmc_upd_f" "$O/pmc_upd_w"
+		step rocprof_upd_f 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv \
+			-d "$O/pmc_upd_f" -o run -- python3 tools/ec_pmc.py upd1_8p2 || exit $?
+		step rocprof_upd_w 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv \
+			-d "$O/pmc_upd_w" -o run -- python3 tools/ec_pmc.py upd1_8p2 || exit $?
+		python tools/pmc_traffic.py "$O/pmc_upd_f" "$O/pmc_upd_w" "ecg_mm_kernel<1, 2" 3221225472 \
+			"$O/pmc_traffic_upd1_8p2.json" || exit $?
+		;;
 	ecdram)           # memory-side queueing of the EC shapes vs the streaming kernels: outstanding
 	                  # requests per cycle (LEVEL), requests, DRAM-credit stall cycles, GRBM cycles
 		for w in ${ECDRAM_SHAPES:-read write enc_4p2 enc_8p2 dec_8p2 enc_16p2 enc_16p2_cap2}; do
