@@ -289,7 +289,8 @@ int ecg_set_wg_per_cu(ecg_ctx_t *ctx, uint32_t wg_per_cu);
  * its first ~10-20 launches); once every timing has completed the faster time
  * per block is kept for the shape (the cap only when it wins by > 1.5 %).  A
  * shape is (k, rows, acc/diff, cell bytes, lane granule, layout class:
- * source and destination sharing one stripe stride or not) -- NOT the batch
+ * source and destination sharing one stripe stride or not, or a pointer
+ * table from ecg_matmul_ptrs / ecg_obj_ec_recx_encode) -- NOT the batch
  * size, so batches of varying size share one probe and one decision.  Skipped
  * when ecg_set_wg_per_cu or ecg_set_launch / _order set a geometry, and on
  * streams under graph capture.  on: 0 off, 1 on, 2 on and forget every
