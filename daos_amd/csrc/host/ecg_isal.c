@@ -67,6 +67,24 @@ static ecg_ctx_t *default_ctx(const char *fn)
 	return t_ctx;
 }
 
+/* The context for a call's cells: the thread's for host cells (staged), the
+ * one on the cells' own device for device cells (used in place; a device not
+ * in $ECG_DEVICES is an error, not a silent peer access). */
+static ecg_ctx_t *ctx_for(const char *fn, const void *cell)
+{
+	ecg_ctx_t *c = default_ctx(fn);
+	const int dev = ecg_ptr_device(cell);
+	int i;
+
+	if (dev < 0 || ecg_ctx_device(c) == dev)
+		return c;
+	for (i = 0; i < g_nctx; i++)
+		if (ecg_ctx_device(g_ctx[i]) == dev)
+			return g_ctx[i];
+	fprintf(stderr, "ecg: %s: cells in memory of device %d, which $ECG_DEVICES does not list\n", fn, dev);
+	abort();
+}
+
 void gf_vect_mul_init(unsigned char c, unsigned char *tbl)
 {
 	int n;
@@ -124,7 +142,7 @@ void ec_encode_data(int len, int k, int rows, unsigned char *gftbls, unsigned ch
 	if (k > ECG_MAX_K || rows > 256)
 		die("ec_encode_data (k/rows out of range)", -ECG_DER_INVAL);
 	coef_from_tables("ec_encode_data", k, rows, gftbls, coef);
-	rc = ecg_matmul_host(default_ctx("ec_encode_data"), len, k, rows, coef, data, coding, 0);
+	rc = ecg_matmul_host(ctx_for("ec_encode_data", data[0]), len, k, rows, coef, data, coding, 0);
 	if (rc)
 		die("ec_encode_data", rc);
 }
@@ -143,7 +161,7 @@ void ec_encode_data_update(int len, int k, int rows, int vec_i, unsigned char *g
 	for (r = 0; r < rows; r++)
 		coef[r] = table_coef("ec_encode_data_update", gftbls + 32 * (r * k + vec_i));
 	src[0] = data;
-	rc = ecg_matmul_host(default_ctx("ec_encode_data_update"), len, 1, rows, coef, src, coding,
+	rc = ecg_matmul_host(ctx_for("ec_encode_data_update", data), len, 1, rows, coef, src, coding,
 			     ECG_F_ACCUMULATE);
 	if (rc)
 		die("ec_encode_data_update", rc);
@@ -204,7 +222,7 @@ int xor_gen(int vects, int len, void **array)
 	if (vects - 1 > ECG_MAX_K + 256)
 		return 1;
 	memset(ones, 1, sizeof(ones));
-	rc = ecg_matmul_host(default_ctx("xor_gen"), len, vects - 1, 1, ones, v, &v[vects - 1], 0);
+	rc = ecg_matmul_host(ctx_for("xor_gen", v[0]), len, vects - 1, 1, ones, v, &v[vects - 1], 0);
 	if (rc)
 		die("xor_gen", rc);
 	return 0;

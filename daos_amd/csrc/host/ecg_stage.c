@@ -109,19 +109,19 @@ static int tstage_get(ecg_ctx_t *ctx, size_t bytes, struct tstage **out)
 	return 0;
 }
 
-/* 1 when p is device memory of this process (hipMalloc'd), 0 for host
- * memory.  A query of unregistered host memory may fail: its error is
- * cleared here so a later launch check does not report it. */
-static int is_device_ptr(const void *p)
+/* The device whose memory p is (hipMalloc'd), -1 for host memory.  A query
+ * of unregistered host memory may fail: its error is cleared here so a later
+ * launch check does not report it. */
+int ecg_ptr_device(const void *p)
 {
 	hipPointerAttribute_t a;
 
 	memset(&a, 0, sizeof(a));
 	if (hipPointerGetAttributes(&a, p) != hipSuccess) {
 		(void)hipGetLastError();
-		return 0;
+		return -1;
 	}
-	return a.type == hipMemoryTypeDevice;
+	return a.type == hipMemoryTypeDevice ? a.device : -1;
 }
 
 /* The ISA-L data-plane calls with DEVICE cells (an engine whose bio buffers
@@ -138,13 +138,15 @@ static int matmul_device(ecg_ctx_t *ctx, int len, int k, int rows, const unsigne
 	if (k > ECG_MAX_K)
 		return ecg_fail(-ECG_DER_INVAL, "matmul_host: k=%d device cells (max %d)", k, ECG_MAX_K);
 	for (j = 0; j < k; j++) {
-		if (!is_device_ptr(src[j]))
-			return ecg_fail(-ECG_DER_INVAL, "matmul_host: source %d is host memory, source 0 device", j);
+		if (ecg_ptr_device(src[j]) != ctx->device)
+			return ecg_fail(-ECG_DER_INVAL, "matmul_host: source %d is not memory of device %d "
+					"(every cell of a call must be)", j, ctx->device);
 		soff[j] = (int64_t)((uintptr_t)src[j] - (uintptr_t)src[0]);
 	}
 	for (r = 0; r < rows; r++) {
-		if (!is_device_ptr(dst[r]))
-			return ecg_fail(-ECG_DER_INVAL, "matmul_host: output %d is host memory, sources device", r);
+		if (ecg_ptr_device(dst[r]) != ctx->device)
+			return ecg_fail(-ECG_DER_INVAL, "matmul_host: output %d is not memory of device %d "
+					"(every cell of a call must be)", r, ctx->device);
 		doff[r] = (int64_t)((uintptr_t)dst[r] - (uintptr_t)dst[0]);
 	}
 	rc = ecg_matmul(ctx, k, rows, coef, (uint64_t)len, 1, src[0], soff, 0, dst[0], doff, 0, flags, NULL);
@@ -180,7 +182,7 @@ int ecg_matmul_host(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned cha
 	rc = ecg_ctx_enter(ctx);
 	if (rc)
 		return rc;
-	if (is_device_ptr(src[0]))
+	if (ecg_ptr_device(src[0]) >= 0)
 		return matmul_device(ctx, len, k, rows, coef, src, dst, flags);
 	pitch = ((size_t)len + 255) & ~(size_t)255;
 	bytes = pitch * (size_t)(k + rows);
