@@ -209,6 +209,67 @@ static void *isal_thread(void *arg)
 	return NULL;
 }
 
+/* ec_encode_data on DEVICE cells (an engine whose buffers live in HBM keeps
+ * its ISA-L call sites): the drop-in launches on them in place */
+struct djob {
+	ecg_ctx_t *ctx;
+	int k, p, len, iters, id;
+	int fails;
+};
+
+static void *isal_device_thread(void *arg)
+{
+	struct djob *j = arg;
+	unsigned char en[(16 + 4) * 16], tb[16 * 4 * 32], rtb[16 * 4 * 32];
+	unsigned char *hdata[16], *want[4], *got, *data[16], *par[4];
+	void *dbuf = NULL;
+	const size_t slot = ((size_t)j->len + 64) & ~(size_t)15;
+	uint64_t st = 0xC2B2AE3D27D4EB4Full * (uint64_t)(j->id + 1);
+
+	gf_gen_cauchy1_matrix(en, j->k + j->p, j->k);
+	ec_init_tables(j->k, j->p, &en[j->k * j->k], tb);
+	ref_ec_init_tables(j->k, j->p, &en[j->k * j->k], rtb);
+	if (ecg_dev_alloc(j->ctx, slot * (size_t)(j->k + j->p) + 64, &dbuf) != 0) {
+		j->fails++;
+		return NULL;
+	}
+	got = malloc(j->len);
+	for (int c = 0; c < j->k; c++) {
+		hdata[c] = malloc(j->len);
+		data[c] = (unsigned char *)dbuf + c * slot + (c & 3);	/* odd offsets */
+	}
+	for (int r = 0; r < j->p; r++) {
+		want[r] = malloc(j->len);
+		par[r] = (unsigned char *)dbuf + (j->k + r) * slot + 1;
+	}
+	for (int it = 0; it < j->iters; it++) {
+		for (int c = 0; c < j->k; c++) {
+			for (int i = 0; i < j->len; i++) {
+				st ^= st << 13;
+				st ^= st >> 7;
+				st ^= st << 17;
+				hdata[c][i] = (unsigned char)st;
+			}
+			j->fails += ecg_memcpy(j->ctx, data[c], hdata[c], j->len, 0, NULL) != 0;
+		}
+		j->fails += ecg_stream_sync(j->ctx, NULL) != 0;
+		ec_encode_data(j->len, j->k, j->p, tb, data, par);
+		ref_ec_encode_data(j->len, j->k, j->p, rtb, hdata, want);
+		for (int r = 0; r < j->p; r++) {
+			j->fails += ecg_memcpy(j->ctx, got, par[r], j->len, 1, NULL) != 0 ||
+				    ecg_stream_sync(j->ctx, NULL) != 0;
+			j->fails += memcmp(got, want[r], j->len) != 0;
+		}
+	}
+	for (int c = 0; c < j->k; c++)
+		free(hdata[c]);
+	for (int r = 0; r < j->p; r++)
+		free(want[r]);
+	free(got);
+	ecg_dev_free(j->ctx, dbuf);
+	return NULL;
+}
+
 struct qdone {
 	pthread_mutex_t lock;
 	int done, bad;
@@ -248,6 +309,23 @@ static void device_checks(void)
 	CHECK(ecg_ctx_create(0, &ctx) == 0, "ctx_create: %s", ecg_strerror());
 	if (ctx == NULL)
 		return;
+	/* concurrent ISA-L-convention calls on device cells */
+	{
+		enum { ND = 8 };
+		pthread_t dth[ND];
+		struct djob djobs[ND];
+
+		for (t = 0; t < ND; t++) {
+			static const int shapes[][3] = {{4, 2, 4096}, {8, 2, 933}, {16, 3, 8569}, {2, 1, 37}};
+
+			djobs[t] = (struct djob){ctx, shapes[t % 4][0], shapes[t % 4][1], shapes[t % 4][2], 10, t, 0};
+			pthread_create(&dth[t], NULL, isal_device_thread, &djobs[t]);
+		}
+		for (t = 0; t < ND; t++) {
+			pthread_join(dth[t], NULL);
+			CHECK(djobs[t].fails == 0, "device-cell thread %d: %d failures", t, djobs[t].fails);
+		}
+	}
 	{
 		const int k = 8, p = 2, S = 6;
 		const uint64_t C = 65536 + 16;
