@@ -13,7 +13,9 @@
  *   queue: ecg_queue_update()
  *   cpu  : diff loop + ref_simd_encode_data(k = 1, the vec_i column) XORed
  *          into the parity (ISA-L-equivalent CPU restatement)
- * and GiB/s counts the updated cell bytes.  Bench infrastructure.
+ * and GiB/s counts the updated cell bytes.  With "device" the cells live in
+ * device memory and only the drop-in runs (ec_encode_data on device cells,
+ * in place, each thread on its own stream).  Bench infrastructure.
  */
 #include <pthread.h>
 #include <stdio.h>
@@ -28,6 +30,7 @@
 static int K = 8, P = 2, T = 8, N = 64;
 static uint64_t CB = 128 << 10;
 static unsigned char *g_cells;		/* T * N stripes of (K + P) cells */
+static unsigned char *g_dcells;		/* the same in device memory ("device") */
 static unsigned char g_tbls[64 * 8 * 32];
 static ecg_queue_t *g_q;
 static int g_mode;			/* 0 isal, 1 queue, 2 cpu */
@@ -117,7 +120,7 @@ static void *worker(void *arg)
 			update_one(t, i);
 			continue;
 		}
-		unsigned char *s = g_cells + ((size_t)t * N + i) * (K + P) * CB;
+		unsigned char *s = (g_dcells ? g_dcells : g_cells) + ((size_t)t * N + i) * (K + P) * CB;
 		unsigned char *data[64], *par[8];
 
 		for (int c = 0; c < K; c++)
@@ -169,6 +172,7 @@ int main(int argc, char **argv)
 	if (argc > 2)
 		T = atoi(argv[2]);
 	g_update = argc > 3 && strcmp(argv[3], "update") == 0;
+	const int device = argc > 3 && strcmp(argv[3], "device") == 0;
 	g_cells = malloc((size_t)T * N * (K + P) * CB);
 	g_new = malloc((size_t)T * N * CB);
 	for (size_t i = 0; i < (size_t)T * N * (K + P) * CB; i++)
@@ -183,6 +187,28 @@ int main(int argc, char **argv)
 	if (ecg_ctx_create(0, &ctx) || ecg_queue_create(ctx, &qa, &g_q)) {
 		fprintf(stderr, "no device: %s\n", ecg_strerror());
 		return 1;
+	}
+	if (device) {
+		void *d = NULL;
+		const size_t nb = (size_t)T * N * (K + P) * CB;
+
+		if (ecg_dev_alloc(ctx, nb, &d) || ecg_memcpy(ctx, d, g_cells, nb, 0, NULL) ||
+		    ecg_stream_sync(ctx, NULL)) {
+			fprintf(stderr, "device cells: %s\n", ecg_strerror());
+			return 1;
+		}
+		g_dcells = d;
+		run(0);
+		isal = run(0);
+		printf("{\"op\": \"encode\", \"cells\": \"device\", \"k\": %d, \"p\": %d, \"cell_bytes\": %llu, "
+		       "\"threads\": %d, \"stripes_per_thread\": %d, \"isal_one_stripe_GiBps\": %.2f}\n", K, P,
+		       (unsigned long long)CB, T, N, isal);
+		ecg_dev_free(ctx, d);
+		ecg_queue_destroy(g_q);
+		ecg_ctx_destroy(ctx);
+		free(g_cells);
+		free(g_new);
+		return 0;
 	}
 	run(0);			/* warm up staging / code objects */
 	isal = run(0);
