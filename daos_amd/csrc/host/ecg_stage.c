@@ -126,14 +126,12 @@ int ecg_ptr_device(const void *p)
 
 /* The ISA-L data-plane calls with DEVICE cells (an engine whose bio buffers
  * live in HBM keeps its ec_encode_data call sites): one strided launch, cell
- * offsets relative to the first source / output, on the calling thread's own
- * stream (so concurrent callers' launches overlap), then that stream is
- * drained (ISA-L's calls are synchronous). */
+ * offsets relative to the first source / output, then the stream is drained
+ * (ISA-L's calls are synchronous). */
 static int matmul_device(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
 			 unsigned char *const *src, unsigned char *const *dst, unsigned flags)
 {
 	int64_t soff[ECG_MAX_K], doff[256];
-	struct tstage *t = NULL;
 	hipError_t e;
 	int j, r, rc;
 
@@ -151,13 +149,10 @@ static int matmul_device(ecg_ctx_t *ctx, int len, int k, int rows, const unsigne
 					"(every cell of a call must be)", r, ctx->device);
 		doff[r] = (int64_t)((uintptr_t)dst[r] - (uintptr_t)dst[0]);
 	}
-	rc = tstage_get(ctx, 0, &t);
+	rc = ecg_matmul(ctx, k, rows, coef, (uint64_t)len, 1, src[0], soff, 0, dst[0], doff, 0, flags, NULL);
 	if (rc)
 		return rc;
-	rc = ecg_matmul(ctx, k, rows, coef, (uint64_t)len, 1, src[0], soff, 0, dst[0], doff, 0, flags, (void *)t->st);
-	if (rc)
-		return rc;
-	e = hipStreamSynchronize(t->st);
+	e = hipStreamSynchronize(ctx->stream);
 	return e == hipSuccess ? 0 : ecg_hip_fail(e, "matmul_host: device cells sync");
 }
 

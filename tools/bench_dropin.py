@@ -4,8 +4,7 @@ linked against libecg sees.  Run once per staging mode (env
 ECG_ZERO_COPY_MAX: 0 = always DMA copies, large = kernel on the pinned
 staging in place); appends one JSON line to gpurun_out/bench_dropin.jsonl.
 DROPIN_DEVICE=1: the cells live in device memory instead (the drop-in then
-launches on them in place); DROPIN_THREADS=n (device cells) runs n threads
-of calls at once and reports the aggregate.  Bench infrastructure (no oracle)."""
+launches on them in place).  Bench infrastructure (no oracle)."""
 import json
 import os
 import sys
@@ -58,49 +57,5 @@ def main():
         f.write(json.dumps(res) + "\n")
 
 
-def threaded(nthreads):
-    """n threads, each with its own device cells, calling ec_encode_data on
-    EC_8P2 1 MiB / 128 KiB cells; aggregate user-data GiB/s."""
-    import threading
-
-    k, p = 8, 2
-    tbls = ecg.isal_init_tables(ecg.cauchy1(k, p)[k:])
-    tp = tbls.ctypes.data_as(ecg.u8p)
-    ctx = ecg.Context(0)
-    L = ecg.lib()
-    res = {"cells": "device", "threads": nthreads}
-    for C, it in ((1 << 20, 200), (128 << 10, 400)):
-        bufs, args = [], []
-        for _ in range(nthreads):
-            buf = ctx.alloc((k + p) * C)
-            buf.fill(0x5A)
-            dp = (ecg.u8p * k)(*[ecg.C.cast(ecg.C.c_void_p(buf.ptr + j * C), ecg.u8p) for j in range(k)])
-            cp = (ecg.u8p * p)(*[ecg.C.cast(ecg.C.c_void_p(buf.ptr + (k + r) * C), ecg.u8p) for r in range(p)])
-            bufs.append(buf)
-            args.append((dp, cp))
-
-        def worker(i, n):
-            dp, cp = args[i]
-            for _ in range(n):
-                L.ec_encode_data(C, k, p, tp, dp, cp)
-
-        ths = [threading.Thread(target=worker, args=(i, 5)) for i in range(nthreads)]
-        [t.start() for t in ths]
-        [t.join() for t in ths]
-        ths = [threading.Thread(target=worker, args=(i, it)) for i in range(nthreads)]
-        t0 = time.perf_counter()
-        [t.start() for t in ths]
-        [t.join() for t in ths]
-        dt = time.perf_counter() - t0
-        res[f"{C >> 10}KiB_GiBps"] = round(nthreads * it * k * C / dt / (1 << 30), 1)
-        res[f"{C >> 10}KiB_us_per_call"] = round(dt / it * 1e6, 1)
-        for b in bufs:
-            b.free()
-    print(json.dumps(res), flush=True)
-
-
 if __name__ == "__main__":
-    if os.environ.get("DROPIN_THREADS"):
-        threaded(int(os.environ["DROPIN_THREADS"]))
-    else:
-        main()
+    main()
