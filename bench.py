@@ -1068,8 +1068,61 @@ def leg_strong(args, ctx, world, rank, steps, weak=False):
             **({"rehearsal": True} if args.rehearse else {})}
 
 
+def concurrent_copy_rates(world, ctx, host, nbytes, reps=3):
+    """This rank's pinned H2D / D2H GB/s while EVERY rank copies at once
+    (barrier-aligned start of each copy), over `host` -- the leg's own pinned
+    buffer -- and one device buffer of its size: the per-rank PCIe / host
+    memory ceiling at this N.  Without a context (CPU rehearsal) the "copy" is
+    a host memcpy of the buffer, so the plumbing and keys are the same."""
+    import numpy as np
+
+    dev = ctx.alloc(nbytes) if ctx is not None else None
+    scratch = None if ctx is not None else np.empty_like(host)
+    out = {}
+    try:
+        for name in ("h2d", "d2h"):
+            ts = []
+            for _ in range(reps):
+                barrier(world)
+                t0 = time.perf_counter()
+                if ctx is None:
+                    np.copyto(scratch, host) if name == "h2d" else np.copyto(host, scratch)
+                else:
+                    from daos_amd import ecg
+
+                    src, dst = (host.ctypes.data, dev.ptr) if name == "h2d" else (dev.ptr, host.ctypes.data)
+                    ecg._chk(ecg.lib().ecg_memcpy(ctx.h, dst, src, nbytes, 0 if name == "h2d" else 1, None),
+                             name)
+                    ctx.sync()
+                ts.append(time.perf_counter() - t0)
+            out[name] = round(nbytes / sorted(ts)[len(ts) // 2] / 1e9, 2)
+    finally:
+        if dev is not None:
+            dev.free()
+        barrier(world)
+    return out
+
+
+def solo_copy_rates(world, rank, ctx, nbytes):
+    """This rank's pinned copy rates with the other ranks idle (ranks take
+    turns): the denominator a rank alone would see."""
+    out = None
+    for r in range(world):
+        barrier(world)
+        if r == rank and ctx is not None:
+            out = pinned_copy_rates(ctx, n=nbytes)
+    barrier(world)
+    return out
+
+
 def leg_stream(args, ctx, world, rank, steps, numa_info):
-    """configs[4] per rank from node-local pinned buffers."""
+    """configs[4] per rank from node-local pinned buffers.  Its denominator at
+    N > 1 is the pinned copy rate each rank reaches while all ranks copy at
+    once (`concurrent_pinned_GBps`, the same pinned buffers the leg streams
+    from); the solo rate (ranks in turn) is reported beside it, and the node's
+    host-memory / PCIe ceiling is the concurrent rates summed over ranks."""
+    import numpy as np
+
     k, p, C, S = 8, 2, 1 << 20, 64
     if args.rehearse:
         wl = None
@@ -1083,20 +1136,33 @@ def leg_stream(args, ctx, world, rank, steps, numa_info):
     row = {"rank": rank, "ms_per_step": round(mine / steps * 1e3, 4),
            "numa_node": (numa_info or {}).get("numa_node"), "pinned_cpus": (numa_info or {}).get("pinned_cpus")}
     user = 2 * k * C * S
+    h2d_bytes = 2 * k * C * S if wl is None else wl.h2d_bytes_per_step()
+    h2d = h2d_bytes * steps / mine / 1e9
+    host = wl.data.array if wl is not None else np.ones(64 << 20, dtype=np.uint8)
+    conc = concurrent_copy_rates(world, ctx if wl is not None else None, host, host.size)
+    solo = solo_copy_rates(world, rank, ctx if wl is not None else None, 256 << 20)
+    row.update({"h2d_GBps": round(h2d, 2), "concurrent_pinned_GBps": conc,
+                "frac_of_h2d": round(h2d / conc["h2d"], 4),
+                "denominator": "pinned H2D rate of this rank with all ranks copying at once"})
+    if solo is not None:
+        row.update({"measured_pinned_GBps": solo, "frac_of_solo_h2d": round(h2d / solo["h2d"], 4)})
     if wl is not None:
-        h2d = wl.h2d_bytes_per_step() * steps / mine / 1e9
-        raw = pinned_copy_rates(ctx, n=256 << 20)
-        row.update({"h2d_GBps": round(h2d, 2), "d2h_GBps": round(wl.d2h_bytes_per_step() * steps / mine / 1e9, 2),
-                    "measured_pinned_GBps": raw, "frac_of_h2d": round(h2d / raw["h2d"], 4),
+        row.update({"d2h_GBps": round(wl.d2h_bytes_per_step() * steps / mine / 1e9, 2),
                     "verified": all(wl.verify().values())})
         wl.free()
     rows = gather(world, row)
+    node = {"h2d_GBps": round(sum(r["concurrent_pinned_GBps"]["h2d"] for r in rows), 2),
+            "d2h_GBps": round(sum(r["concurrent_pinned_GBps"]["d2h"] for r in rows), 2),
+            "what": "concurrent pinned copies summed over ranks: the node's host-memory / PCIe ceiling at this N"}
     return {"config": f"EC_{k}P{p} {C >> 20} MiB cells: per rank one encode batch + one {{d0,d1}} recovery "
                       f"batch of {S} stripes per step, stripes in NUMA-local pinned host memory, "
                       f"host<->device copies included ({args.host_chunk or HOST_CHUNK}-stripe staging chunks)",
             "value_GiBps": None if args.rehearse else round(world * user * steps / tmax / GIB, 2),
             "unit": "GiB/s", "scaling": "weak", "bound": "pcie", "steps": steps,
             "ms_per_step": round(tmax / steps * 1e3, 4), "ranks": rows,
+            "node_concurrent_copy_ceiling": node,
+            "frac_of_node_ceiling": None if args.rehearse else
+            round(world * h2d_bytes * steps / tmax / 1e9 / node["h2d_GBps"], 4),
             "verified": all(r.get("verified", True) for r in rows),
             **({"rehearsal": True} if args.rehearse else {})}
 

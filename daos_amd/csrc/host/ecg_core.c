@@ -165,6 +165,10 @@ void ecg_ctx_destroy(ecg_ctx_t *ctx)
 	ecg_scratch_free(ctx);
 	ecg_csum_ctx_fini(ctx);
 	ecg_tune_fini(ctx);
+	for (int i = 0; i < ctx->ndpool; i++) {
+		(void)hipStreamSynchronize(ctx->dpool[i]);
+		(void)hipStreamDestroy(ctx->dpool[i]);
+	}
 	(void)hipStreamDestroy(ctx->stream);
 	pthread_mutex_destroy(&ctx->lock);
 	free(ctx);

@@ -9,9 +9,6 @@
 #include "../../../include/ecg_isal.h"
 #include "ecg_internal.h"
 
-int ecg_matmul_host(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
-		    unsigned char *const *src, unsigned char *const *dst, unsigned flags);
-
 /* OR_RS_* order of ref:src/include/daos_obj_class.h:70-80 */
 static const int g_rs_kp[ECG_OR_RS_LAST - ECG_OR_RS_FIRST + 1][2] = {
 	{2, 1}, {2, 2}, {4, 1}, {4, 2}, {8, 1}, {8, 2}, {16, 1}, {16, 2}, {4, 3}, {8, 3}, {16, 3},
@@ -22,26 +19,11 @@ static struct ecg_obj_ec_codec g_codecs[N_RS];
 static int g_codecs_ready;
 static pthread_mutex_t g_codec_lock = PTHREAD_MUTEX_INITIALIZER;
 
-static ecg_ctx_t *g_ctx;
-static int g_ctx_rc;
-static pthread_once_t g_ctx_once = PTHREAD_ONCE_INIT;
-
-static void ctx_init(void)
+/* The batched host entry points with ctx == NULL: the calling thread's
+ * default device (ecg_dropin.c), or the CPU path when the process has none. */
+static ecg_ctx_t *default_ctx(ecg_ctx_t *ctx)
 {
-	const char *env = getenv("ECG_DEVICE");
-
-	g_ctx_rc = ecg_ctx_create(env ? atoi(env) : 0, &g_ctx);
-}
-
-static int pick_ctx(ecg_ctx_t **ctx)
-{
-	if (*ctx)
-		return 0;
-	pthread_once(&g_ctx_once, ctx_init);
-	if (g_ctx_rc)
-		return g_ctx_rc;
-	*ctx = g_ctx;
-	return 0;
+	return ctx ? ctx : ecg_dropin_ctx();
 }
 
 int ecg_obj_ec_class_kp(uint32_t oc_id, int *k, int *p)
@@ -117,7 +99,6 @@ int ecg_obj_ec_encode_buf(uint32_t oc_id, uint64_t cell_bytes, unsigned char *bu
 {
 	unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
 	unsigned char *data[ECG_MAX_K];
-	ecg_ctx_t *ctx = NULL;
 	int k, p, i, rc;
 
 	rc = ecg_obj_ec_class_kp(oc_id, &k, &p);
@@ -134,11 +115,8 @@ int ecg_obj_ec_encode_buf(uint32_t oc_id, uint64_t cell_bytes, unsigned char *bu
 	}
 	for (i = 0; i < k; i++)
 		data[i] = buffer + (size_t)i * cell_bytes;
-	rc = pick_ctx(&ctx);
-	if (rc)
-		return rc;
 	ecg_gen_cauchy1(k, p, en);
-	return ecg_matmul_host(ctx, (int)cell_bytes, k, p, &en[k * k], data, p_bufs, 0);
+	return ecg_dropin_product("obj_ec_encode_buf", NULL, (int)cell_bytes, k, p, &en[k * k], data, p_bufs, 0);
 }
 
 struct ecg_obj_ec_recov_codec *ecg_obj_ec_recov_codec_alloc(void)
@@ -187,15 +165,34 @@ int ecg_obj_ec_recov_codec_init(uint32_t oc_id, const uint32_t *err_list, uint32
 int ecg_obj_ec_recov_data(ecg_ctx_t *ctx, const struct ecg_obj_ec_recov_codec *rv,
 			  uint64_t cell_sz, unsigned char *buf_stripes, uint32_t nstripes)
 {
-	int rc;
+	unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K], rows[ECG_MAX_P * ECG_MAX_K];
+	uint32_t out_idx[ECG_MAX_P], dec_idx[ECG_MAX_K];
+	unsigned char *src[ECG_MAX_K], *dst[ECG_MAX_P];
+	int rc, reused, i;
+	uint32_t s;
 
 	if (rv == NULL || buf_stripes == NULL)
 		return ecg_fail(-ECG_DER_INVAL, "recov_data: NULL argument");
-	rc = pick_ctx(&ctx);
-	if (rc)
-		return rc;
-	return ecg_recover_host(ctx, rv->k, rv->p, cell_sz, nstripes, buf_stripes,
-				rv->er_err_list, (int)rv->er_nerrs, 0);
+	ctx = default_ctx(ctx);
+	if (ctx)
+		return ecg_recover_host(ctx, rv->k, rv->p, cell_sz, nstripes, buf_stripes,
+					rv->er_err_list, (int)rv->er_nerrs, 0);
+	/* no usable device: obj_ec_recov_stripe's loop on the CPU path */
+	if (cell_sz > 0x7fffffffULL)
+		return ecg_fail(-ECG_DER_INVAL, "recov_data: cell %llu too large", (unsigned long long)cell_sz);
+	ecg_gen_cauchy1(rv->k, rv->p, en);
+	rc = ecg_recov_rows(rv->k, rv->p, en, rv->er_err_list, (int)rv->er_nerrs, rows, out_idx, dec_idx,
+			    &reused);
+	for (s = 0; rc == 0 && s < nstripes; s++) {
+		unsigned char *st = buf_stripes + (size_t)s * (size_t)(rv->k + rv->p) * cell_sz;
+
+		for (i = 0; i < rv->k; i++)
+			src[i] = st + (size_t)dec_idx[i] * cell_sz;
+		for (i = 0; i < (int)rv->er_nerrs; i++)
+			dst[i] = st + (size_t)out_idx[i] * cell_sz;
+		rc = ecg_cpu_matmul((int)cell_sz, rv->k, (int)rv->er_nerrs, rows, src, dst, 0);
+	}
+	return rc;
 }
 
 int ecg_obj_ec_encode_stripes(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_bytes,
@@ -203,13 +200,30 @@ int ecg_obj_ec_encode_stripes(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_byte
 {
 	int k, p, rc;
 
+	unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
+	unsigned char *src[ECG_MAX_K], *dst[ECG_MAX_P];
+	uint32_t s;
+	int i;
+
 	rc = ecg_obj_ec_class_kp(oc_id, &k, &p);
 	if (rc)
 		return rc;
-	rc = pick_ctx(&ctx);
-	if (rc)
-		return rc;
-	return ecg_encode_host(ctx, k, p, cell_bytes, nstripes, data, parity, 0);
+	ctx = default_ctx(ctx);
+	if (ctx)
+		return ecg_encode_host(ctx, k, p, cell_bytes, nstripes, data, parity, 0);
+	/* no usable device: obj_ec_recx_encode's stripe loop on the CPU path */
+	if (cell_bytes > 0x7fffffffULL)
+		return ecg_fail(-ECG_DER_INVAL, "encode_stripes: cell %llu too large",
+				(unsigned long long)cell_bytes);
+	ecg_gen_cauchy1(k, p, en);
+	for (s = 0; rc == 0 && s < nstripes; s++) {
+		for (i = 0; i < k; i++)
+			src[i] = (unsigned char *)data + ((size_t)s * k + i) * cell_bytes;
+		for (i = 0; i < p; i++)
+			dst[i] = parity + ((size_t)i * nstripes + s) * cell_bytes;
+		rc = ecg_cpu_matmul((int)cell_bytes, k, p, &en[k * k], src, dst, 0);
+	}
+	return rc;
 }
 
 static int bit_isset(const uint8_t *bm, uint32_t j)
@@ -272,9 +286,6 @@ int ecg_agg_update_parity(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_recs, ui
 	if (cell_cnt > (uint32_t)k || cb == 0 || cb > 0x7fffffffULL || bit_map == NULL ||
 	    (n_ext && (ext_start == NULL || ext_nr == NULL)))
 		return ecg_fail(-ECG_DER_INVAL, "agg_update_parity: bad arguments");
-	rc = pick_ctx(&ctx);
-	if (rc)
-		return rc;
 	if (n_ext) {
 		masked = malloc((size_t)cb * cell_cnt);
 		if (masked == NULL)
@@ -307,7 +318,8 @@ int ecg_agg_update_parity(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_recs, ui
 	}
 	for (r = 0; r < p; r++)
 		dst[r] = parity + (size_t)r * cb;
-	rc = ecg_matmul_host(ctx, (int)cb, (int)(2 * cell_cnt), p, coef, src, dst, ECG_F_ACCUMULATE);
+	rc = ecg_dropin_product("agg_update_parity", ctx, (int)cb, (int)(2 * cell_cnt), p, coef, src, dst,
+				ECG_F_ACCUMULATE);
 	free(masked);
 	return rc;
 }
@@ -335,13 +347,10 @@ int ecg_agg_recalc_parity(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cb, const uin
 	if (rr != cell_cnt)	/* D_ASSERT(r == cell_cnt) in the reference */
 		return ecg_fail(-ECG_DER_INVAL, "agg_recalc_parity: bitmap has %u cells, not %u", rr,
 				cell_cnt);
-	rc = pick_ctx(&ctx);
-	if (rc)
-		return rc;
 	for (i = 0; i < p; i++)
 		dst[i] = parity + (size_t)i * cb;
 	ecg_gen_cauchy1(k, p, en);
-	return ecg_matmul_host(ctx, (int)cb, k, p, &en[k * k], data, dst, 0);
+	return ecg_dropin_product("agg_recalc_parity", ctx, (int)cb, k, p, &en[k * k], data, dst, 0);
 }
 
 uint64_t ecg_obj_ec_singv_cell_bytes(uint32_t oc_id, uint64_t iod_size)
@@ -361,7 +370,6 @@ int ecg_obj_ec_singv_encode(uint32_t oc_id, uint64_t iod_size, const unsigned ch
 	unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
 	unsigned char *data[ECG_MAX_K];
 	unsigned char *cells;
-	ecg_ctx_t *ctx = NULL;
 	uint64_t cb;
 	int k, p, i, rc;
 
@@ -383,11 +391,8 @@ int ecg_obj_ec_singv_encode(uint32_t oc_id, uint64_t iod_size, const unsigned ch
 	memcpy(cells, value, iod_size);
 	for (i = 0; i < k; i++)
 		data[i] = cells + (size_t)i * cb;
-	rc = pick_ctx(&ctx);
-	if (rc == 0) {
-		ecg_gen_cauchy1(k, p, en);
-		rc = ecg_matmul_host(ctx, (int)cb, k, p, &en[k * k], data, p_bufs, 0);
-	}
+	ecg_gen_cauchy1(k, p, en);
+	rc = ecg_dropin_product("obj_ec_singv_encode", NULL, (int)cb, k, p, &en[k * k], data, p_bufs, 0);
 	free(cells);
 	return rc;
 }

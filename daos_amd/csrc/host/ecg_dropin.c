@@ -1,0 +1,177 @@
+/*
+ * ecg_dropin.c -- where a synchronous one-stripe product of the drop-in
+ * surfaces runs (ISA-L ec_encode_data / ec_encode_data_update / xor_gen in
+ * ecg_isal.c; obj_ec_encode_buf, agg_* and singv in ecg_daos.c).
+ *
+ * The rule ("CPU for small len, GPU via staging above a
+ * threshold"):
+ *   - device cells (src[0] is hipMalloc'd memory)   -> HIP kernels, in place;
+ *   - host cells, len * (k + rows) >= crossover       -> HIP kernels through
+ *                                                       pinned staging;
+ *   - host cells below the crossover, every call in a process without a
+ *     usable gfx950 device, and ECG_FORCE_CPU=1       -> the CPU path
+ *                                                       (ecg_cpu.c).
+ * The default crossover is the measured one (on the MI355X box
+ * one EPYC core with GFNI beats the PCIe round trip of a synchronous call at
+ * every size up to the largest measured, so host cells stay on the CPU);
+ * ECG_DROPIN_CROSSOVER=<bytes> or ecg_set_dropin_crossover() move it.
+ *
+ * Contexts: one per device of $ECG_DEVICES ("0,1,2,3" / "all"; default
+ * $ECG_DEVICE, else device 0), created on the first call that needs the GPU;
+ * calling threads are spread over them round-robin on their first such call,
+ * so an engine's xstreams use every listed GPU.  Device cells run on the
+ * context of their own device.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "ecg_internal.h"
+
+#define DROPIN_MAXDEV 64
+
+/* Measured crossover in bytes of len * (k + rows): DESIGN.md §7,
+ * profiles/r05/dropin/.  UINT64_MAX = host cells never take the GPU. */
+#define DROPIN_CROSSOVER_DEFAULT UINT64_MAX
+
+static pthread_once_t g_once = PTHREAD_ONCE_INIT;
+static int g_gpu;		/* a gfx950 device is visible and usable */
+static uint64_t g_crossover = DROPIN_CROSSOVER_DEFAULT;
+
+static pthread_once_t g_ctx_once = PTHREAD_ONCE_INIT;
+static ecg_ctx_t *g_ctx[DROPIN_MAXDEV];
+static int g_nctx;
+static int g_ctx_rc;
+static char g_ctx_err[256];
+static unsigned g_next;
+static __thread ecg_ctx_t *t_ctx;
+static int g_warned;
+
+static void once_init(void)
+{
+	const char *force = getenv("ECG_FORCE_CPU");
+	const char *x = getenv("ECG_DROPIN_CROSSOVER");
+
+	if (x && *x)
+		g_crossover = strtoull(x, NULL, 0);
+	g_gpu = !(force && force[0] == '1') && ecg_device_count() > 0;
+}
+
+static void ctx_init(void)
+{
+	const char *list = getenv("ECG_DEVICES");
+	const char *one = getenv("ECG_DEVICE");
+	int dev[DROPIN_MAXDEV], n, i;
+
+	if (list) {
+		n = ecg_parse_devices(list, dev, DROPIN_MAXDEV);
+	} else {
+		dev[0] = one ? atoi(one) : 0;
+		n = 1;
+	}
+	if (n <= 0) {
+		g_ctx_rc = n < 0 ? ecg_fail(-ECG_DER_INVAL, "bad ECG_DEVICES '%s'", list)
+				 : ecg_fail(-ECG_DER_NOSYS, "ECG_DEVICES names no device");
+	}
+	for (i = 0; i < n && g_ctx_rc == 0; i++)
+		g_ctx_rc = ecg_ctx_create(dev[i], &g_ctx[i]);
+	if (g_ctx_rc) {
+		snprintf(g_ctx_err, sizeof(g_ctx_err), "%s", ecg_strerror());
+		while (i-- > 0)
+			if (g_ctx[i]) {
+				ecg_ctx_destroy(g_ctx[i]);
+				g_ctx[i] = NULL;
+			}
+		n = 0;
+	}
+	g_nctx = n;
+}
+
+int ecg_dropin_gpu(void)
+{
+	pthread_once(&g_once, once_init);
+	return g_gpu;
+}
+
+int ecg_set_dropin_crossover(uint64_t bytes)
+{
+	pthread_once(&g_once, once_init);
+	__atomic_store_n(&g_crossover, bytes, __ATOMIC_RELAXED);
+	return 0;
+}
+
+uint64_t ecg_dropin_crossover(void)
+{
+	pthread_once(&g_once, once_init);
+	return __atomic_load_n(&g_crossover, __ATOMIC_RELAXED);
+}
+
+/* The calling thread's default context (NULL + error text when the devices
+ * of $ECG_DEVICES cannot be opened). */
+static ecg_ctx_t *thread_ctx(void)
+{
+	pthread_once(&g_ctx_once, ctx_init);
+	if (g_ctx_rc) {
+		ecg_fail(g_ctx_rc, "%s", g_ctx_err);
+		return NULL;
+	}
+	if (t_ctx == NULL)
+		t_ctx = g_ctx[__atomic_fetch_add(&g_next, 1u, __ATOMIC_RELAXED) % (unsigned)g_nctx];
+	return t_ctx;
+}
+
+/* The context of device `dev` among the default ones. */
+static ecg_ctx_t *device_ctx(const char *fn, int dev)
+{
+	ecg_ctx_t *c = thread_ctx();
+	int i;
+
+	if (c == NULL || ecg_ctx_device(c) == dev)
+		return c;
+	for (i = 0; i < g_nctx; i++)
+		if (ecg_ctx_device(g_ctx[i]) == dev)
+			return g_ctx[i];
+	ecg_fail(-ECG_DER_INVAL, "%s: cells are memory of device %d, which $ECG_DEVICES does not list "
+		 "(add it to ECG_DEVICES)", fn, dev);
+	return NULL;
+}
+
+ecg_ctx_t *ecg_dropin_ctx(void)
+{
+	return ecg_dropin_gpu() ? thread_ctx() : NULL;
+}
+
+int ecg_dropin_product(const char *fn, ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
+		       unsigned char *const *src, unsigned char *const *dst, unsigned flags)
+{
+	int dev, rc;
+
+	if (len <= 0 || src == NULL)
+		return ecg_cpu_matmul(len, k, rows, coef, src, dst, flags);
+	if (!ecg_dropin_gpu())
+		return ecg_cpu_matmul(len, k, rows, coef, src, dst, flags);
+	dev = ecg_ptr_device(src[0]);
+	if (dev >= 0) {
+		/* device cells: only the GPU can touch them */
+		if (ctx == NULL || ecg_ctx_device(ctx) != dev)
+			ctx = device_ctx(fn, dev);
+		if (ctx == NULL)
+			return g_ctx_rc ? g_ctx_rc : -ECG_DER_INVAL;
+		return ecg_matmul_host_mem(ctx, len, k, rows, coef, src, dst, flags, dev);
+	}
+	if ((uint64_t)len * (uint64_t)(k + rows) < ecg_dropin_crossover())
+		return ecg_cpu_matmul(len, k, rows, coef, src, dst, flags);
+	if (ctx == NULL)
+		ctx = thread_ctx();
+	if (ctx != NULL) {
+		rc = ecg_matmul_host_mem(ctx, len, k, rows, coef, src, dst, flags, -1);
+		if (rc == 0)
+			return 0;
+	}
+	/* host cells: the CPU computes the same bytes, so a GPU that cannot be
+	 * used (not openable, a HIP failure) costs speed, never parity */
+	if (!__atomic_exchange_n(&g_warned, 1, __ATOMIC_RELAXED))
+		fprintf(stderr, "ecg: %s: GPU path unavailable (%s); host cells run on the CPU\n", fn,
+			ecg_strerror());
+	return ecg_cpu_matmul(len, k, rows, coef, src, dst, flags);
+}

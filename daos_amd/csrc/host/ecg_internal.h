@@ -79,6 +79,9 @@ struct ecg_ctx {
 	} kh_cache[ECG_NKH_CACHE];
 	unsigned kh_next;
 	struct ecg_scratch scratch;
+#define ECG_DROPIN_STREAMS 4
+	hipStream_t dpool[ECG_DROPIN_STREAMS];	/* device-cell drop-in calls (ecg_stage.c) */
+	int ndpool;
 	struct ecg_tuner *tuner;	/* blocks-per-CU cap per shape (ecg_tune.c) */
 	ecg_stats_t stats;		/* telemetry (ecg_get_stats), updated with atomics */
 };
@@ -175,6 +178,20 @@ typedef int (*ecg_mm_launch_fn)(const ecg_mm_params_t *p, const ecg_launch_cfg_t
 #define ECG_TUNE_LAYOUT_PTRS 2u		/* per-stripe pointer table */
 int ecg_tune_launch_fn(ecg_ctx_t *ctx, const ecg_mm_params_t *p, uint32_t g, uint32_t layout,
 		       ecg_mm_launch_fn fn, const void *arg, hipStream_t st, uint32_t *kid);
+
+/* synchronous one-stripe product on ctx's GPU; src_dev = ecg_ptr_device(src[0])
+ * (ecg_stage.c) */
+int ecg_matmul_host_mem(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
+			unsigned char *const *src, unsigned char *const *dst, unsigned flags, int src_dev);
+/* drop-in routing (ecg_dropin.c): device cells -> GPU, host cells -> CPU
+ * below the crossover or without a usable device, else GPU.  ctx NULL = the
+ * calling thread's default context. */
+int ecg_dropin_product(const char *fn, ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
+		       unsigned char *const *src, unsigned char *const *dst, unsigned flags);
+/* 1 when the drop-in may use a GPU in this process */
+int ecg_dropin_gpu(void);
+/* the calling thread's default context; NULL without a usable device */
+ecg_ctx_t *ecg_dropin_ctx(void);
 
 /* context helpers (ecg_core.c) */
 int ecg_ctx_enter(ecg_ctx_t *ctx);

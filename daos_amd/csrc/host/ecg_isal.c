@@ -2,8 +2,13 @@
  * ecg_isal.c -- ISA-L-signature exports (see include/ecg_isal.h).
  *
  * Setup functions (matrices, tables) are host code, as in ISA-L.  The
- * data-plane functions run on the MI355X through ecg_matmul_host; there is
- * deliberately no CPU path.
+ * data-plane functions (ec_encode_data, ec_encode_data_update, xor_gen) go
+ * through ecg_dropin_product (ecg_dropin.c): device cells run the gfx950
+ * kernels in place, host cells run the product's CPU path below the measured
+ * crossover and in every process without a usable gfx950 device -- ISA-L's
+ * contract is a `void` call that succeeds on any CPU, and libdaos (the
+ * client library, ref:src/object/SConscript:19-23) calls ec_encode_data
+ * (ref:src/object/cli_ec.c:540) on nodes without a GPU.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -12,76 +17,17 @@
 #include "../../../include/ecg_isal.h"
 #include "ecg_internal.h"
 
-int ecg_matmul_host(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
-		    unsigned char *const *src, unsigned char *const *dst, unsigned flags);
-
-/* One context per device of $ECG_DEVICES ("0,1,2,3" / "all"; default
- * $ECG_DEVICE, else device 0).  Calling threads are spread over them
- * round-robin on their first call, so an engine's xstreams calling the
- * synchronous ISA-L API use every listed GPU. */
-#define ISAL_MAXDEV 64
-static ecg_ctx_t *g_ctx[ISAL_MAXDEV];
-static int g_nctx;
-static int g_ctx_rc;
-static unsigned g_next;
-static pthread_once_t g_ctx_once = PTHREAD_ONCE_INIT;
-static __thread ecg_ctx_t *t_ctx;
-
-static void default_ctx_init(void)
-{
-	const char *list = getenv("ECG_DEVICES");
-	const char *one = getenv("ECG_DEVICE");
-	int dev[ISAL_MAXDEV], n, i;
-
-	if (list) {
-		n = ecg_parse_devices(list, dev, ISAL_MAXDEV);
-	} else {
-		dev[0] = one ? atoi(one) : 0;
-		n = 1;
-	}
-	if (n <= 0) {
-		g_ctx_rc = n < 0 ? ecg_fail(-ECG_DER_INVAL, "bad ECG_DEVICES '%s'", list)
-				 : ecg_fail(-ECG_DER_NOSYS, "ECG_DEVICES: no device");
-		return;
-	}
-	for (i = 0; i < n && g_ctx_rc == 0; i++)
-		g_ctx_rc = ecg_ctx_create(dev[i], &g_ctx[i]);
-	g_nctx = i;
-}
-
 /* The ISA-L data-plane ABI is `void`: a failure cannot be returned, and
- * silently skipping the parity would corrupt stored objects.  Fail loudly. */
+ * silently skipping the parity would corrupt stored objects.  What is left to
+ * fail once host cells always have the CPU path is a call on device cells
+ * (the GPU is then the only thing that can reach them) or bad arguments:
+ * name the cause and the remedy, then abort. */
 static void die(const char *fn, int rc)
 {
-	fprintf(stderr, "ecg: %s failed (rc=%d): %s\n", fn, rc, ecg_strerror());
-	abort();
-}
-
-static ecg_ctx_t *default_ctx(const char *fn)
-{
-	pthread_once(&g_ctx_once, default_ctx_init);
-	if (g_ctx_rc)
-		die(fn, g_ctx_rc);
-	if (t_ctx == NULL)
-		t_ctx = g_ctx[__atomic_fetch_add(&g_next, 1u, __ATOMIC_RELAXED) % (unsigned)g_nctx];
-	return t_ctx;
-}
-
-/* The context for a call's cells: the thread's for host cells (staged), the
- * one on the cells' own device for device cells (used in place; a device not
- * in $ECG_DEVICES is an error, not a silent peer access). */
-static ecg_ctx_t *ctx_for(const char *fn, const void *cell)
-{
-	ecg_ctx_t *c = default_ctx(fn);
-	const int dev = ecg_ptr_device(cell);
-	int i;
-
-	if (dev < 0 || ecg_ctx_device(c) == dev)
-		return c;
-	for (i = 0; i < g_nctx; i++)
-		if (ecg_ctx_device(g_ctx[i]) == dev)
-			return g_ctx[i];
-	fprintf(stderr, "ecg: %s: cells in memory of device %d, which $ECG_DEVICES does not list\n", fn, dev);
+	fprintf(stderr, "ecg: %s failed (rc=%d): %s\n"
+		"ecg: host cells never fail this way (they run on the CPU when no GPU is usable); for "
+		"device cells list their device in $ECG_DEVICES and check the HIP runtime (rocminfo), "
+		"or pass host buffers\n", fn, rc, ecg_strerror());
 	abort();
 }
 
@@ -113,8 +59,10 @@ static unsigned char table_coef(const char *fn, const unsigned char *t)
 {
 	const unsigned char c = t[1];
 
-	if (t[0] != 0 || t[16] != 0 || t[2] != ecg_gf_mul(c, 2) || t[15] != ecg_gf_mul(c, 15) ||
-	    t[17] != ecg_gf_mul(c, 0x10) || t[31] != ecg_gf_mul(c, 0xF0)) {
+	const unsigned char *m = ecg_gf_mul_tbl[c];
+
+	if (t[0] != 0 || t[16] != 0 || t[2] != m[2] || t[15] != m[15] || t[17] != m[0x10] ||
+	    t[31] != m[0xF0]) {
 		fprintf(stderr, "ecg: %s: gftbls are not ec_init_tables' 32-byte layout "
 			"(tables from another ISA-L build?)\n", fn);
 		abort();
@@ -127,6 +75,7 @@ static void coef_from_tables(const char *fn, int k, int rows, const unsigned cha
 {
 	int i;
 
+	ecg_gf_init();
 	for (i = 0; i < k * rows; i++)
 		coef[i] = table_coef(fn, gftbls + 32 * i);
 }
@@ -134,15 +83,21 @@ static void coef_from_tables(const char *fn, int k, int rows, const unsigned cha
 void ec_encode_data(int len, int k, int rows, unsigned char *gftbls, unsigned char **data,
 		    unsigned char **coding)
 {
-	unsigned char coef[ECG_MAX_K * 256];
+	unsigned char small[ECG_MAX_K * 8];
+	unsigned char *coef = small;
 	int rc;
 
 	if (len <= 0 || rows <= 0 || k <= 0)
 		return;
 	if (k > ECG_MAX_K || rows > 256)
 		die("ec_encode_data (k/rows out of range)", -ECG_DER_INVAL);
+	/* a user-level thread's stack is small: only rows > 8 take the heap */
+	if ((size_t)k * rows > sizeof(small) && (coef = malloc((size_t)k * rows)) == NULL)
+		die("ec_encode_data (malloc)", -ECG_DER_NOMEM);
 	coef_from_tables("ec_encode_data", k, rows, gftbls, coef);
-	rc = ecg_matmul_host(ctx_for("ec_encode_data", data[0]), len, k, rows, coef, data, coding, 0);
+	rc = ecg_dropin_product("ec_encode_data", NULL, len, k, rows, coef, data, coding, 0);
+	if (coef != small)
+		free(coef);
 	if (rc)
 		die("ec_encode_data", rc);
 }
@@ -158,11 +113,12 @@ void ec_encode_data_update(int len, int k, int rows, int vec_i, unsigned char *g
 		return;
 	if (rows > 256 || vec_i < 0 || vec_i >= k)
 		die("ec_encode_data_update (bad arguments)", -ECG_DER_INVAL);
+	ecg_gf_init();
 	for (r = 0; r < rows; r++)
 		coef[r] = table_coef("ec_encode_data_update", gftbls + 32 * (r * k + vec_i));
 	src[0] = data;
-	rc = ecg_matmul_host(ctx_for("ec_encode_data_update", data), len, 1, rows, coef, src, coding,
-			     ECG_F_ACCUMULATE);
+	rc = ecg_dropin_product("ec_encode_data_update", NULL, len, 1, rows, coef, src, coding,
+				ECG_F_ACCUMULATE);
 	if (rc)
 		die("ec_encode_data_update", rc);
 }
@@ -222,7 +178,7 @@ int xor_gen(int vects, int len, void **array)
 	if (vects - 1 > ECG_MAX_K + 256)
 		return 1;
 	memset(ones, 1, sizeof(ones));
-	rc = ecg_matmul_host(ctx_for("xor_gen", v[0]), len, vects - 1, 1, ones, v, &v[vects - 1], 0);
+	rc = ecg_dropin_product("xor_gen", NULL, len, vects - 1, 1, ones, v, &v[vects - 1], 0);
 	if (rc)
 		die("xor_gen", rc);
 	return 0;

@@ -22,6 +22,8 @@ struct tstage {
 	void *dev;
 	size_t dev_bytes;
 	hipStream_t st;
+	hipEvent_t ev;		/* device-cell calls wait on this */
+	int ev_device;
 };
 
 static pthread_key_t g_key;
@@ -43,6 +45,10 @@ static void tstage_release(struct tstage *t)
 		(void)hipHostFree(t->host);
 	if (t->dev)
 		(void)hipFree(t->dev);
+	if (t->ev) {
+		(void)hipSetDevice(t->ev_device);
+		(void)hipEventDestroy(t->ev);
+	}
 	memset(t, 0, sizeof(*t));
 }
 
@@ -63,21 +69,63 @@ static void key_init(void)
 		g_zero_copy_max = (size_t)strtoull(env, NULL, 0);
 }
 
-static int tstage_get(ecg_ctx_t *ctx, size_t bytes, struct tstage **out)
+static struct tstage *tstage_self(void)
 {
 	struct tstage *t;
-	hipError_t e;
 
 	pthread_once(&g_key_once, key_init);
 	t = pthread_getspecific(g_key);
 	if (t == NULL) {
 		t = calloc(1, sizeof(*t));
-		if (t == NULL)
-			return ecg_fail(-ECG_DER_NOMEM, "stage: calloc");
-		pthread_setspecific(g_key, t);
+		if (t != NULL)
+			pthread_setspecific(g_key, t);
 	}
-	if (t->ctx != ctx || t->device != ctx->device)
+	return t;
+}
+
+/* The calling thread's completion event on ctx's device (device-cell calls);
+ * kept apart from the host staging so alternating host and device cells of
+ * different devices does not free either. */
+static int tstage_event(ecg_ctx_t *ctx, struct tstage **out)
+{
+	struct tstage *t = tstage_self();
+	hipError_t e;
+
+	if (t == NULL)
+		return ecg_fail(-ECG_DER_NOMEM, "stage: calloc");
+	if (t->ev && t->ev_device != ctx->device) {
+		(void)hipEventDestroy(t->ev);
+		t->ev = NULL;
+	}
+	if (t->ev == NULL) {
+		e = hipEventCreateWithFlags(&t->ev, hipEventDisableTiming);
+		if (e != hipSuccess) {
+			t->ev = NULL;
+			return ecg_hip_fail(e, "stage event");
+		}
+		t->ev_device = ctx->device;
+	}
+	*out = t;
+	return 0;
+}
+
+static int tstage_get(ecg_ctx_t *ctx, size_t bytes, struct tstage **out)
+{
+	struct tstage *t = tstage_self();
+	hipError_t e;
+
+	if (t == NULL)
+		return ecg_fail(-ECG_DER_NOMEM, "stage: calloc");
+	if (t->ctx != ctx || t->device != ctx->device) {
+		/* host staging of another context: free it, keep the event */
+		hipEvent_t ev = t->ev;
+		int ev_device = t->ev_device;
+
+		t->ev = NULL;
 		tstage_release(t);
+		t->ev = ev;
+		t->ev_device = ev_device;
+	}
 	t->ctx = ctx;
 	t->device = ctx->device;
 	if (t->st == NULL) {
@@ -124,46 +172,143 @@ int ecg_ptr_device(const void *p)
 	return a.type == hipMemoryTypeDevice ? a.device : -1;
 }
 
+/* Every cell [v[i], v[i] + len) lies inside one allocation of ctx's device:
+ * a pointer into host memory, another device or past an allocation's end
+ * would make the launch fault the GPU, so it is refused here.  Cells of one
+ * buffer (the usual stripe) cost one attribute and one range query in all. */
+static int cells_on_device(ecg_ctx_t *ctx, unsigned char *const *v, int n, int len, const char *what)
+{
+	struct {
+		uintptr_t lo, hi;
+	} seen[4];
+	int nseen = 0, i, x;
+
+	for (i = 0; i < n; i++) {
+		const uintptr_t a = (uintptr_t)v[i], e = a + (uintptr_t)len;
+		hipDeviceptr_t base = NULL;
+		size_t size = 0;
+
+		for (x = 0; x < nseen; x++)
+			if (a >= seen[x].lo && e <= seen[x].hi)
+				break;
+		if (x < nseen)
+			continue;
+		if (ecg_ptr_device(v[i]) != ctx->device)
+			return ecg_fail(-ECG_DER_INVAL, "matmul_host: %s %d is not memory of device %d "
+					"(every cell of a call must be)", what, i, ctx->device);
+		if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)v[i]) != hipSuccess) {
+			(void)hipGetLastError();
+			return ecg_fail(-ECG_DER_INVAL, "matmul_host: %s %d: no device allocation", what, i);
+		}
+		if (e > (uintptr_t)base + size)
+			return ecg_fail(-ECG_DER_INVAL, "matmul_host: %s %d: %d bytes run past the end of its "
+					"allocation", what, i, len);
+		x = nseen < 4 ? nseen++ : i % 4;
+		seen[x].lo = (uintptr_t)base;
+		seen[x].hi = (uintptr_t)base + size;
+	}
+	return 0;
+}
+
+/* The stream of the calling thread among the context's drop-in pool
+ * (created on first use): concurrent synchronous callers spread over up to
+ * ECG_DROPIN_STREAMS streams -- the box's hardware queues -- instead of
+ * queueing behind each other on one. */
+static int pool_stream(ecg_ctx_t *ctx, hipStream_t *out)
+{
+	static unsigned next_slot;
+	static __thread unsigned slot = ~0u;
+	hipError_t e = hipSuccess;
+	int n;
+
+	if (slot == ~0u)
+		slot = __atomic_fetch_add(&next_slot, 1u, __ATOMIC_RELAXED);
+	n = __atomic_load_n(&ctx->ndpool, __ATOMIC_ACQUIRE);
+	if (n == 0) {
+		const char *env = getenv("ECG_DROPIN_STREAMS");
+		int want = env ? atoi(env) : ECG_DROPIN_STREAMS, i;
+
+		if (want < 1 || want > ECG_DROPIN_STREAMS)
+			want = ECG_DROPIN_STREAMS;
+		pthread_mutex_lock(&ctx->lock);
+		n = ctx->ndpool;
+		for (i = n; i < want && e == hipSuccess; i++) {
+			e = hipStreamCreateWithFlags(&ctx->dpool[i], hipStreamNonBlocking);
+			if (e == hipSuccess)
+				n = i + 1;
+		}
+		__atomic_store_n(&ctx->ndpool, n, __ATOMIC_RELEASE);
+		pthread_mutex_unlock(&ctx->lock);
+		if (n == 0)
+			return ecg_hip_fail(e, "drop-in stream pool");
+	}
+	*out = ctx->dpool[slot % (unsigned)n];
+	return 0;
+}
+
 /* The ISA-L data-plane calls with DEVICE cells (an engine whose bio buffers
- * live in HBM keeps its ec_encode_data call sites): one strided launch, cell
- * offsets relative to the first source / output, then the stream is drained
- * (ISA-L's calls are synchronous). */
+ * live in HBM keeps its ec_encode_data call sites): strided launches on the
+ * cells in place (cell offsets relative to the first source / output; more
+ * than ECG_MAX_K sources -- xor_gen -- as accumulating groups), on the
+ * caller's pool stream, then a wait for an event recorded right after them:
+ * the call waits for its own launches and what precedes them on that stream,
+ * not for every other thread's work (ISA-L's calls are synchronous). */
 static int matmul_device(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
 			 unsigned char *const *src, unsigned char *const *dst, unsigned flags)
 {
-	int64_t soff[ECG_MAX_K], doff[256];
+	int64_t soff[ECG_MAX_K + 256], doff[256];
+	unsigned char cc[ECG_MAX_K * 8];
+	struct tstage *t = NULL;
+	hipStream_t st = NULL;
 	hipError_t e;
-	int j, r, rc;
+	int j0, j, r, rc;
 
-	if (k > ECG_MAX_K)
-		return ecg_fail(-ECG_DER_INVAL, "matmul_host: k=%d device cells (max %d)", k, ECG_MAX_K);
-	for (j = 0; j < k; j++) {
-		if (ecg_ptr_device(src[j]) != ctx->device)
-			return ecg_fail(-ECG_DER_INVAL, "matmul_host: source %d is not memory of device %d "
-					"(every cell of a call must be)", j, ctx->device);
-		soff[j] = (int64_t)((uintptr_t)src[j] - (uintptr_t)src[0]);
-	}
-	for (r = 0; r < rows; r++) {
-		if (ecg_ptr_device(dst[r]) != ctx->device)
-			return ecg_fail(-ECG_DER_INVAL, "matmul_host: output %d is not memory of device %d "
-					"(every cell of a call must be)", r, ctx->device);
-		doff[r] = (int64_t)((uintptr_t)dst[r] - (uintptr_t)dst[0]);
-	}
-	rc = ecg_matmul(ctx, k, rows, coef, (uint64_t)len, 1, src[0], soff, 0, dst[0], doff, 0, flags, NULL);
+	rc = cells_on_device(ctx, src, k, len, "source");
+	if (rc == 0)
+		rc = cells_on_device(ctx, dst, rows, len, "output");
+	if (rc == 0)
+		rc = pool_stream(ctx, &st);
+	if (rc == 0)
+		rc = tstage_event(ctx, &t);
 	if (rc)
 		return rc;
-	e = hipStreamSynchronize(ctx->stream);
+	for (j = 0; j < k; j++)
+		soff[j] = (int64_t)((uintptr_t)src[j] - (uintptr_t)src[0]);
+	for (r = 0; r < rows; r++)
+		doff[r] = (int64_t)((uintptr_t)dst[r] - (uintptr_t)dst[0]);
+	for (j0 = 0; rc == 0 && j0 < k; j0 += ECG_MAX_K) {
+		const int kk = k - j0 < ECG_MAX_K ? k - j0 : ECG_MAX_K;
+		const unsigned f = flags | (j0 ? ECG_F_ACCUMULATE : 0u);
+		int r0;
+
+		/* coefficient slices of at most 8 rows (cc's size); the kernel
+		 * splits rows the same way */
+		for (r0 = 0; rc == 0 && r0 < rows; r0 += 8) {
+			const int rr = rows - r0 < 8 ? rows - r0 : 8;
+
+			for (r = 0; r < rr; r++)
+				memcpy(&cc[r * kk], &coef[(size_t)(r0 + r) * k + j0], (size_t)kk);
+			rc = ecg_matmul(ctx, kk, rr, cc, (uint64_t)len, 1, src[0], soff + j0, 0, dst[0],
+					doff + r0, 0, f, st);
+		}
+	}
+	if (rc)
+		return rc;
+	e = hipEventRecord(t->ev, st);
+	if (e == hipSuccess)
+		e = hipEventSynchronize(t->ev);
 	return e == hipSuccess ? 0 : ecg_hip_fail(e, "matmul_host: device cells sync");
 }
 
 /*
- * dst[r][i] (^)= XOR_j coef[r*k + j] * src[j][i], i < len.  Host cells are
- * staged through pinned memory; device cells (every cell hipMalloc'd) run
- * in place.  With ECG_F_ACCUMULATE the current dst bytes travel to the
- * device first (ec_encode_data_update semantics).
+ * dst[r][i] (^)= XOR_j coef[r*k + j] * src[j][i], i < len, on ctx's GPU.
+ * Host cells are staged through pinned memory; device cells (every cell
+ * hipMalloc'd) run in place.  With ECG_F_ACCUMULATE the current dst bytes
+ * travel to the device first (ec_encode_data_update semantics).  src_dev is
+ * ecg_ptr_device(src[0]), looked up once by the caller.
  */
-int ecg_matmul_host(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
-		    unsigned char *const *src, unsigned char *const *dst, unsigned flags)
+int ecg_matmul_host_mem(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
+			unsigned char *const *src, unsigned char *const *dst, unsigned flags, int src_dev)
 {
 	int64_t soff[ECG_MAX_K + 256], doff[256];
 	struct tstage *t = NULL;
@@ -182,7 +327,7 @@ int ecg_matmul_host(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned cha
 	rc = ecg_ctx_enter(ctx);
 	if (rc)
 		return rc;
-	if (ecg_ptr_device(src[0]) >= 0)
+	if (src_dev >= 0)
 		return matmul_device(ctx, len, k, rows, coef, src, dst, flags);
 	pitch = ((size_t)len + 255) & ~(size_t)255;
 	bytes = pitch * (size_t)(k + rows);
@@ -252,4 +397,15 @@ int ecg_matmul_host(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned cha
 	for (r = 0; r < rows; r++)
 		memcpy(dst[r], h + (k + r) * pitch, (size_t)len);
 	return 0;
+}
+
+int ecg_matmul_host(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
+		    unsigned char *const *src, unsigned char *const *dst, unsigned flags)
+{
+	if (ctx == NULL)
+		return ecg_fail(-ECG_DER_INVAL, "NULL context");
+	if (len <= 0 || src == NULL)
+		return ecg_matmul_host_mem(ctx, len, k, rows, coef, src, dst, flags, -1);
+	return ecg_matmul_host_mem(ctx, len, k, rows, coef, src, dst, flags,
+				   ecg_ctx_enter(ctx) == 0 ? ecg_ptr_device(src[0]) : -1);
 }

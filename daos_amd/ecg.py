@@ -60,6 +60,11 @@ _SIGS = [
                              vp, C.c_int64, C.c_int64, vp]),
     ("ecg_matmul_ptrs", C.c_int, [vp, C.c_int, C.c_int, u8p, C.c_uint64, C.c_uint32, C.POINTER(vp), vp]),
     ("ecg_matmul_host", C.c_int, [vp, C.c_int, C.c_int, C.c_int, u8p, C.POINTER(u8p), C.POINTER(u8p), C.c_uint]),
+    ("ecg_cpu_matmul", C.c_int, [C.c_int, C.c_int, C.c_int, u8p, C.POINTER(u8p), C.POINTER(u8p), C.c_uint]),
+    ("ecg_cpu_isa", C.c_char_p, []),
+    ("ecg_cpu_set_isa", C.c_int, [C.c_char_p]),
+    ("ecg_set_dropin_crossover", C.c_int, [C.c_uint64]),
+    ("ecg_dropin_crossover", C.c_uint64, []),
     ("ecg_encode_host", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, vp, vp, C.c_uint32]),
     ("ecg_recover_host", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, vp, u32p, C.c_int, C.c_uint32]),
     ("ecg_queue_create", C.c_int, [vp, vp, C.POINTER(vp)]),
@@ -778,6 +783,31 @@ class Queue:
 
 
 # ---------------------------------------------------------------- ISA-L drop-in
+def cpu_matmul(coef: np.ndarray, src: Sequence[np.ndarray], dst: Sequence[np.ndarray], flags: int = 0):
+    """The product's CPU path (ecg_cpu_matmul) on host arrays."""
+    coef = np.ascontiguousarray(coef, dtype=np.uint8)
+    rows, k = coef.shape
+    sp = (u8p * k)(*[_u8(a) for a in src])
+    dp = (u8p * rows)(*[_u8(a) for a in dst])
+    _chk(lib().ecg_cpu_matmul(src[0].shape[0], k, rows, _u8(coef), sp, dp, flags), "cpu_matmul")
+
+
+def cpu_isa() -> str:
+    return lib().ecg_cpu_isa().decode()
+
+
+def cpu_set_isa(isa: str) -> int:
+    return lib().ecg_cpu_set_isa(isa.encode())
+
+
+def set_dropin_crossover(nbytes: int) -> None:
+    lib().ecg_set_dropin_crossover(nbytes)
+
+
+def dropin_crossover() -> int:
+    return lib().ecg_dropin_crossover()
+
+
 def isal_init_tables(coef: np.ndarray) -> np.ndarray:
     rows, k = coef.shape
     t = np.zeros(rows * k * 32, dtype=np.uint8)

@@ -155,12 +155,34 @@ int ecg_update(ecg_ctx_t *ctx, int k, int p, uint64_t cell_bytes, uint32_t nstri
 /* ---- host-resident pipeline (PCIe-inclusive) ---------------------------- */
 /* One stripe, ISA-L ec_encode_data calling convention: pointers src[k],
  * dst[rows] (any alignment), `len` bytes each;
- * dst[r] (^)= XOR_j coef[r*k+j] * src[j].  Host cells run on the GPU
+ * dst[r] (^)= XOR_j coef[r*k+j] * src[j], on ctx's GPU.  Host cells go
  * through per-thread pinned staging; device cells (src[0] hipMalloc'd: then
- * every cell must be) run in place as one strided launch.  Synchronous.  k
- * may exceed ECG_MAX_K for host cells (xor_gen). */
+ * every cell must lie inside a device allocation, else -ECG_DER_INVAL) run
+ * in place on one of the context's ECG_DROPIN_STREAMS (4) drop-in streams,
+ * and the call waits only for its own launch.  Synchronous.  k may exceed
+ * ECG_MAX_K (xor_gen: accumulating launches). */
 int ecg_matmul_host(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
 		    unsigned char *const *src, unsigned char *const *dst, unsigned flags);
+/* ---- CPU product and drop-in routing (host memory) ----------------------
+ * The same product on the calling CPU thread (host pointers only; no device
+ * needed): vgf2p8affineqb with AVX-512 or AVX2 GFNI, vpshufb nibble tables
+ * with AVX2, byte tables otherwise (widest the CPU has; ecg_cpu_set_isa /
+ * $ECG_CPU_ISA choose a narrower one: "avx512-gfni", "avx2-gfni", "avx2",
+ * "scalar", "auto").  k <= ECG_MAX_K + 256, rows <= 256.  Synchronous. */
+int ecg_cpu_matmul(int len, int k, int rows, const unsigned char *coef,
+		   unsigned char *const *src, unsigned char *const *dst, unsigned flags);
+const char *ecg_cpu_isa(void);
+int ecg_cpu_set_isa(const char *isa);
+/* Where the drop-in surfaces (ecg_isal.h data-plane calls, and the
+ * synchronous one-stripe calls of ecg_daos.h) run a call: device cells on
+ * the GPU; host cells on the CPU when len * (k + rows) is below this
+ * crossover (bytes), when the process has no usable gfx950 device, or with
+ * $ECG_FORCE_CPU=1; otherwise on the GPU through pinned staging.  Default:
+ * the measured crossover, $ECG_DROPIN_CROSSOVER overrides;
+ * 0 = host cells always on the GPU, UINT64_MAX = never. */
+int ecg_set_dropin_crossover(uint64_t bytes);
+uint64_t ecg_dropin_crossover(void);
+
 /* Encode host-resident stripes (data [S][k][C], parity [p][S][C] in host
  * memory; pinned memory from ecg_host_alloc is fastest) by streaming chunks
  * of `chunk_stripes` through device staging on 3 rotating streams

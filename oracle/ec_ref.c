@@ -213,6 +213,13 @@ int ref_xor_gen(int vects, int len, void **array)
  *  - data-error rows taken from inv for the first er_data_nerrs entries of
  *    err_list (:2226-2231) -- the reference assumes data errors come first;
  *    callers that pass parity errors first get what the reference gets.
+ *    The inverse lives in a buffer of roundup((k+p)*k, 8) bytes from a
+ *    zeroing D_ALLOC (obj_ec_recov_codec_alloc, :1963-1984; D_ALLOC ->
+ *    d_calloc, ref:src/include/gurt/common.h:143-146,308) of which
+ *    gf_invert_matrix writes only the k x k head (:2223), so a parity cell
+ *    listed among the first er_data_nerrs entries reads an all-zero row of
+ *    it and the reference writes an all-zero cell there.  Restated exactly:
+ *    the inverse here is the same zeroed (k+p) x k buffer.
  *  - parity-error rows = enc[e] * inv (:2233-2243) */
 int ref_obj_ec_recov_codec_init(int k, int p, const unsigned char *en_matrix,
 				const uint32_t *err_list, int nerrs,
@@ -242,7 +249,7 @@ int ref_obj_ec_recov_codec_init(int k, int p, const unsigned char *en_matrix,
 	}
 
 	b = malloc((size_t)k * k);
-	inv = malloc((size_t)k * k);
+	inv = calloc((size_t)(k + p), (size_t)k);	/* rows k.. stay zero, as in the reference */
 	if (b == NULL || inv == NULL) {
 		free(b);
 		free(inv);

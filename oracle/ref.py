@@ -14,7 +14,9 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "build", "libecg_oracle.so")
+# ECG_ORACLE_LIB: another build of the same sources (the ASan one,
+# tests/test_oracle_asan.py)
+LIB_PATH = os.environ.get("ECG_ORACLE_LIB") or os.path.join(_HERE, "build", "libecg_oracle.so")
 _lib = None
 
 u8p = C.POINTER(C.c_ubyte)

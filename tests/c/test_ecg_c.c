@@ -285,15 +285,17 @@ static void qcb(void *arg, int rc)
 	pthread_mutex_unlock(&d->lock);
 }
 
-static void device_checks(void)
+/* concurrent ISA-L-convention calls on host cells, mixed shapes and odd
+ * lengths: the CPU path (ecg_cpu.c) with or without a device -- under
+ * ThreadSanitizer in the host-only run -- and, with a device, once more with
+ * the crossover at 0 so the same calls take the GPU staging path */
+static void isal_threads(const char *what)
 {
 	enum { NT = 12 };
 	pthread_t th[NT];
 	struct tjob jobs[NT];
-	ecg_ctx_t *ctx = NULL;
 	int t;
 
-	/* concurrent ISA-L-convention calls, mixed shapes and odd lengths */
 	for (t = 0; t < NT; t++) {
 		static const int shapes[][3] = {{4, 2, 4096}, {8, 2, 933}, {16, 3, 8569}, {2, 1, 37}};
 
@@ -302,8 +304,19 @@ static void device_checks(void)
 	}
 	for (t = 0; t < NT; t++) {
 		pthread_join(th[t], NULL);
-		CHECK(jobs[t].fails == 0, "thread %d: %d mismatches", t, jobs[t].fails);
+		CHECK(jobs[t].fails == 0, "%s thread %d: %d mismatches", what, t, jobs[t].fails);
 	}
+}
+
+static void device_checks(void)
+{
+	const uint64_t crossover = ecg_dropin_crossover();
+	ecg_ctx_t *ctx = NULL;
+	int t;
+
+	CHECK(ecg_set_dropin_crossover(0) == 0, "crossover");
+	isal_threads("gpu-staged");
+	ecg_set_dropin_crossover(crossover);
 
 	/* batched device encode + recovery through ecg.h */
 	CHECK(ecg_ctx_create(0, &ctx) == 0, "ctx_create: %s", ecg_strerror());
@@ -415,6 +428,7 @@ static void device_checks(void)
 int main(void)
 {
 	host_checks();
+	isal_threads("cpu-path");
 	if (ecg_device_count() > 0)
 		device_checks();
 	else

@@ -231,7 +231,8 @@ def test_queue_updates_overlapping_parity_ranges(ecglib, ctx, oracle):
 
 def test_isal_dropin_over_device_list(oracle):
     """ECG_DEVICES=0,0,0 gives the synchronous ISA-L drop-in three contexts;
-    threads are spread over them and every call stays bit-exact."""
+    threads are spread over them and every call stays bit-exact (host cells
+    forced onto the GPU with ECG_DROPIN_CROSSOVER=0)."""
     code = r'''
 import sys, threading, numpy as np
 sys.path.insert(0, %r)
@@ -246,6 +247,8 @@ def work(t):
         d = np.random.default_rng(t * 10 + i).integers(0, 256, (k, C), dtype=np.uint8)
         out = [np.zeros(C, np.uint8) for _ in range(p)]
         ecg.isal_encode_data(tb, k, p, [d[j] for j in range(k)], out)
+        if not ecg.last_kernel().startswith("ecg_mm"):
+            bad.append(ecg.last_kernel())
         if not np.array_equal(np.stack(out), ref.encode_data(en[k:], d)):
             bad.append((t, i))
 th = [threading.Thread(target=work, args=(t,)) for t in range(6)]
@@ -253,7 +256,7 @@ th = [threading.Thread(target=work, args=(t,)) for t in range(6)]
 print("bad", bad)
 sys.exit(1 if bad else 0)
 ''' % ROOT
-    env = dict(os.environ, ECG_DEVICES="0,0,0")
+    env = dict(os.environ, ECG_DEVICES="0,0,0", ECG_DROPIN_CROSSOVER="0")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
 

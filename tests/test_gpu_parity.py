@@ -42,6 +42,22 @@ def oracle_parity(oracle, k, p, data):
     return np.stack([oracle.encode_data(en[k:], data[s]) for s in range(data.shape[0])], axis=1)
 
 
+@pytest.fixture(params=["cpu", "gpu"])
+def route(request, ecglib):
+    """Host-cell drop-in calls on the product CPU path (the default: below
+    the measured crossover) or forced onto the GPU staging path (crossover
+    0); device cells always take the GPU."""
+    old = ecglib.dropin_crossover()
+    ecglib.set_dropin_crossover((1 << 64) - 1 if request.param == "cpu" else 0)
+    yield request.param
+    ecglib.set_dropin_crossover(old)
+
+
+def check_route(ecglib, route):
+    k = ecglib.last_kernel()
+    assert k.startswith("cpu:") if route == "cpu" else k.startswith("ecg_mm"), (route, k)
+
+
 # --------------------------------------------------------------- field level
 def test_every_gf_product(ctx, oracle):
     """All 256 x 256 products: coefficient c applied to bytes 0..255."""
@@ -191,9 +207,25 @@ def test_recover_sampled_erasure_sets(ctx, oracle, k, p):
 
 def test_recover_parity_first_order(ctx, oracle):
     """err_list in failure-insertion order with parity before data
-    (ref:src/object/cli_ec.c:1388-1391): data cells match the reference,
-    parity cells are regenerated correctly (the reference's would not be)."""
+    (ref:src/object/cli_ec.c:1388-1391): the reference indexes its zero-filled
+    (k+p) x k inverse buffer past the k x k head for a parity cell listed
+    among the first er_data_nerrs entries, so it writes that parity cell as
+    ALL ZEROS (oracle restatement, tests/test_oracle.py); data cells match it.
+    The product builds its rows data-first and regenerates the true parity
+    there -- the one deliberate byte divergence, in a cell degraded reads
+    never return."""
     _recovery_check(ctx, oracle, 4, 2, 4096, 2, [(5, 0), (4, 3), (5, 1)], 3)
+    k, p, C_ = 4, 2, 4096
+    data = rand((1, k, C_), 4)
+    stripes = np.concatenate([data, oracle_parity(oracle, k, p, data).transpose(1, 0, 2)], axis=1)
+    rc, de, dec, el, gt, reused = oracle.recov_codec(k, p, [5, 0])
+    ref_out = oracle.encode_data(de, stripes[0][dec])
+    assert not ref_out[0].any() and np.array_equal(ref_out[1], stripes[0, 0])
+    d = ctx.to_device(np.where(np.isin(np.arange(k + p), [5, 0])[None, :, None], 0xA5, stripes).astype(np.uint8))
+    ctx.recover(k, p, C_, 1, d.ptr, (k + p) * C_, [5, 0])
+    got = d.download().reshape(1, k + p, C_)
+    d.free()
+    assert np.array_equal(got, stripes) and got[0, 5].any()
 
 
 def test_recover_data_loss(ctx, ecglib):
@@ -237,7 +269,7 @@ def test_update_matches_oracle(ctx, oracle, ecglib, k, p, cells):
 
 
 # --------------------------------------------------------------- ISA-L drop-in
-def test_isal_drop_in(ecglib, oracle, ctx):
+def test_isal_drop_in(ecglib, oracle, ctx, route):
     k, p, n = 8, 3, 32768 + 5
     en = np.zeros((k + p) * k, dtype=np.uint8)
     ecglib.lib().gf_gen_cauchy1_matrix(en.ctypes.data_as(ecglib.u8p), k + p, k)
@@ -246,6 +278,7 @@ def test_isal_drop_in(ecglib, oracle, ctx):
     data = [rand(n, 40 + j) for j in range(k)]
     coding = [np.zeros(n, dtype=np.uint8) for _ in range(p)]
     ecglib.isal_encode_data(tbls, k, p, data, coding)
+    check_route(ecglib, route)
     want = oracle.encode_data(en[k:], np.stack(data))
     assert all(np.array_equal(coding[r], want[r]) for r in range(p))
     # ec_encode_data_update on one cell
@@ -305,7 +338,127 @@ def test_isal_drop_in_device_cells(ecglib, oracle, ctx):
         pbuf.free()
 
 
-def test_isal_reference_aggregate_pattern(ecglib, oracle, ctx):
+def test_dropin_routes_by_placement_and_size(ecglib, oracle, ctx):
+    """SURVEY §8b's rule, observed through ecg_last_kernel: a 4 KiB host-cell
+    ec_encode_data runs the CPU path at the default (measured) crossover,
+    device cells run the HIP kernel, and a host call above the crossover
+    runs the HIP kernel through staging -- same bytes every time."""
+    L = ecglib.lib()
+    k, p = 8, 2
+    en = oracle.cauchy1(k, p)
+    tbls = ecglib.isal_init_tables(en[k:])
+    small = [rand(4096, 300 + j) for j in range(k)]
+    out = [np.zeros(4096, dtype=np.uint8) for _ in range(p)]
+    ecglib.isal_encode_data(tbls, k, p, small, out)
+    assert ecglib.last_kernel().startswith("cpu:"), ecglib.last_kernel()
+    assert np.array_equal(np.stack(out), oracle.encode_data(en[k:], np.stack(small)))
+    # device cells of the same call
+    dbuf = ctx.to_device(np.stack(small + out))
+    try:
+        dp = (ecglib.u8p * k)(*[C.cast(C.c_void_p(dbuf.ptr + j * 4096), ecglib.u8p) for j in range(k)])
+        cp = (ecglib.u8p * p)(*[C.cast(C.c_void_p(dbuf.ptr + (k + r) * 4096), ecglib.u8p) for r in range(p)])
+        L.ec_encode_data(4096, k, p, tbls.ctypes.data_as(ecglib.u8p), dp, cp)
+        assert ecglib.last_kernel().startswith("ecg_mm_kernel<8,2"), ecglib.last_kernel()
+        got = dbuf.download().reshape(k + p, 4096)
+        assert np.array_equal(got[k:], np.stack(out))
+    finally:
+        dbuf.free()
+    # host cells above a crossover of 64 KiB * (k + p)
+    old = ecglib.dropin_crossover()
+    ecglib.set_dropin_crossover(65536 * (k + p))
+    try:
+        for n, gpu in ((65536 - 1, False), (65536, True), (1 << 20, True)):
+            data = [rand(n, 400 + j) for j in range(k)]
+            coding = [np.zeros(n, dtype=np.uint8) for _ in range(p)]
+            ecglib.isal_encode_data(tbls, k, p, data, coding)
+            assert ecglib.last_kernel().startswith("ecg_mm" if gpu else "cpu:"), (n, ecglib.last_kernel())
+            assert np.array_equal(np.stack(coding), oracle.encode_data(en[k:], np.stack(data)))
+    finally:
+        ecglib.set_dropin_crossover(old)
+
+
+def test_isal_device_cells_16_threads(ecglib, oracle, ctx):
+    """16 threads at once calling ec_encode_data on device cells at odd
+    offsets (the engine's xstreams, ref:src/engine/ult.c:394-470): calls
+    spread over the context's drop-in stream pool and each waits for its own
+    launch; every output equals the oracle's."""
+    import threading
+
+    L = ecglib.lib()
+    T, iters = 16, 6
+    errs = []
+
+    def worker(t):
+        try:
+            k, p = ((4, 2), (8, 2), (16, 3), (8, 3))[t % 4]
+            n = 32768 + 7 * t + 1
+            en = oracle.cauchy1(k, p)
+            tbls = ecglib.isal_init_tables(en[k:])
+            slot = n + 64
+            buf = ctx.alloc((k + p) * slot)
+            try:
+                for it in range(iters):
+                    data = rand((k, n), 1000 * t + it)
+                    offs = [j * slot + 1 + (t + j) % 13 for j in range(k)]
+                    pofs = [(k + r) * slot + 3 + r for r in range(p)]
+                    for j in range(k):
+                        buf.upload(data[j], offset=offs[j])
+                    dp = (ecglib.u8p * k)(*[C.cast(C.c_void_p(buf.ptr + o), ecglib.u8p) for o in offs])
+                    cp = (ecglib.u8p * p)(*[C.cast(C.c_void_p(buf.ptr + o), ecglib.u8p) for o in pofs])
+                    L.ec_encode_data(n, k, p, tbls.ctypes.data_as(ecglib.u8p), dp, cp)
+                    raw = buf.download()
+                    want = oracle.encode_data(en[k:], data)
+                    for r in range(p):
+                        if not np.array_equal(raw[pofs[r]: pofs[r] + n], want[r]):
+                            errs.append((t, it, r))
+            finally:
+                buf.free()
+        except Exception as e:          # noqa: BLE001 -- reported below
+            errs.append((t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs[:5]
+
+
+def test_xor_gen_many_device_cells(ecglib, ctx):
+    """xor_gen with more sources than one launch takes (ECG_MAX_K = 64) on
+    device cells: accumulating launches, not an error."""
+    L = ecglib.lib()
+    nv, n = 70, 4096 + 3
+    srcs = rand((nv - 1, n), 77)
+    buf = ctx.alloc(nv * (n + 16))
+    try:
+        for i in range(nv - 1):
+            buf.upload(srcs[i], offset=i * (n + 16) + 1)
+        v = (C.c_void_p * nv)(*[buf.ptr + i * (n + 16) + 1 for i in range(nv)])
+        assert L.xor_gen(nv, n, v) == 0
+        got = buf.download(n, offset=(nv - 1) * (n + 16) + 1)
+        assert np.array_equal(got, np.bitwise_xor.reduce(srcs, axis=0))
+    finally:
+        buf.free()
+
+
+def test_device_cell_past_allocation_refused(ecglib, ctx):
+    """A device cell that runs past the end of its allocation is refused on
+    the host (-DER_INVAL) instead of faulting the GPU."""
+    L = ecglib.lib()
+    buf = ctx.alloc(4 * 4096)
+    try:
+        coef = np.ones((1, 2), dtype=np.uint8)
+        sp = (ecglib.u8p * 2)(C.cast(C.c_void_p(buf.ptr), ecglib.u8p),
+                              C.cast(C.c_void_p(buf.ptr + 3 * 4096 + 100), ecglib.u8p))
+        dp = (ecglib.u8p * 1)(C.cast(C.c_void_p(buf.ptr + 4096), ecglib.u8p))
+        rc = L.ecg_matmul_host(ctx.h, 4096, 2, 1, coef.ctypes.data_as(ecglib.u8p), sp, dp, 0)
+        assert rc == -ecglib.DER_INVAL and "past the end" in ecglib.lib().ecg_strerror().decode()
+    finally:
+        buf.free()
+
+
+def test_isal_reference_aggregate_pattern(ecglib, oracle, ctx, route):
     """The reference's only byte-level parity test
     (ref:src/tests/suite/daos_aggregate_ec.c:371-395): cell j filled with j
     (or 0x80), TEST_EC_CELL_SZ = 32 KiB, ec_encode_data with the codec tables."""
@@ -321,12 +474,13 @@ def test_isal_reference_aggregate_pattern(ecglib, oracle, ctx):
         data = [np.full(ln, 0x80 if overwrite else j, dtype=np.uint8) for j in range(k)]
         parity = [np.zeros(ln, dtype=np.uint8) for _ in range(p)]
         ecglib.isal_encode_data(tbls, k, p, data, parity)
+        check_route(ecglib, route)
         want = oracle.encode_data(oracle.cauchy1(k, p)[k:], np.stack(data))
         assert all(np.array_equal(parity[r], want[r]) for r in range(p))
 
 
 # --------------------------------------------------------------- DAOS surface
-def test_daos_encode_buf_and_recovery(ecglib, oracle, ctx):
+def test_daos_encode_buf_and_recovery(ecglib, oracle, ctx, route):
     L = ecglib.lib()
     assert L.ecg_obj_ec_codec_init() == 0
     oc = (37 << 24) | 1                 # OC_EC_8P2G1
@@ -334,6 +488,7 @@ def test_daos_encode_buf_and_recovery(ecglib, oracle, ctx):
     buf = rand(k * cell, 70)
     pbufs = (ecglib.u8p * p)()         # NULL -> allocated by the callee
     assert L.ecg_obj_ec_encode_buf(oc, cell, buf.ctypes.data_as(ecglib.u8p), pbufs) == 0
+    check_route(ecglib, route)
     par = np.stack([np.ctypeslib.as_array(pbufs[r], shape=(cell,)).copy() for r in range(p)])
     libc = C.CDLL(None)
     for r in range(p):
@@ -357,7 +512,7 @@ def test_daos_encode_buf_and_recovery(ecglib, oracle, ctx):
     L.ecg_obj_ec_recov_codec_free(rv)
 
 
-def test_daos_encode_stripes_and_agg_update(ecglib, oracle, ctx):
+def test_daos_encode_stripes_and_agg_update(ecglib, oracle, ctx, route):
     L = ecglib.lib()
     oc = (35 << 24) | 1                 # OC_EC_4P2G1
     k, p, cell, S = 4, 2, 32768, 6
@@ -374,6 +529,7 @@ def test_daos_encode_stripes_and_agg_update(ecglib, oracle, ctx):
     assert L.ecg_agg_update_parity(None, oc, cell, 1, bitmap.ctypes.data_as(ecglib.u8p), 2,
                                    old.ctypes.data_as(ecglib.u8p), new.ctypes.data_as(ecglib.u8p),
                                    None, None, 0, parity.ctypes.data_as(ecglib.u8p)) == 0
+    check_route(ecglib, route)
     d2 = data[0].copy()
     d2[[1, 3]] = new
     assert np.array_equal(parity, oracle.encode_data(oracle.cauchy1(k, p)[k:], d2))
@@ -524,7 +680,7 @@ def _u64(seq):
     [(3 * 64 + 60, 40)],                  # overruns cell 3's end: no tail zeroing
     [(7 * 64, 8)],                        # touches no updated cell -> whole diffs kept
 ])
-def test_agg_update_parity_holes(ctx, oracle, ecglib, exts):
+def test_agg_update_parity_holes(ctx, oracle, ecglib, exts, route):
     """agg_update_parity + agg_diff_preprocess semantics, including the
     reference's rules for cells no extent touches (ref:src/object/
     srv_ec_aggregate.c:1006-1105), vs the oracle restatement."""
@@ -545,10 +701,11 @@ def test_agg_update_parity_holes(ctx, oracle, ecglib, exts):
                                  _u64([e[1] for e in exts]) if exts else None, len(exts),
                                  got.ctypes.data_as(ecglib.u8p))
     assert rc == 0
+    check_route(ecglib, route)
     assert np.array_equal(got, want)
 
 
-def test_agg_recalc_parity(ctx, oracle, ecglib):
+def test_agg_recalc_parity(ctx, oracle, ecglib, route):
     L = ecglib.lib()
     oc = (41 << 24) | 1                      # EC_8P3
     k, p, cb = 8, 3, 4096 + 8
@@ -559,6 +716,7 @@ def test_agg_recalc_parity(ctx, oracle, ecglib):
     assert L.ecg_agg_recalc_parity(None, oc, cb, bitmap.ctypes.data_as(ecglib.u8p), 4,
                                    rbuf.ctypes.data_as(ecglib.u8p), lbuf.ctypes.data_as(ecglib.u8p),
                                    parity.ctypes.data_as(ecglib.u8p)) == 0
+    check_route(ecglib, route)
     data = np.stack([rbuf[[1, 2, 4, 7].index(j)] if j in (1, 2, 4, 7) else lbuf[[0, 3, 5, 6].index(j)]
                      for j in range(k)])
     assert np.array_equal(parity, oracle.encode_data(oracle.cauchy1(k, p)[k:], data))
@@ -567,7 +725,7 @@ def test_agg_recalc_parity(ctx, oracle, ecglib):
 @pytest.mark.parametrize("oc,size", [((32 << 24) | 1, 8569), ((35 << 24) | 1, 8569), ((37 << 24) | 1, 8569),
                                      ((42 << 24) | 1, 8569), ((35 << 24) | 1, 4 * 1048576 + 347),
                                      ((39 << 24) | 1, 65536 + 3)])
-def test_singv_encode(ctx, oracle, ecglib, oc, size):
+def test_singv_encode(ctx, oracle, ecglib, oc, size, route):
     """Single values of the reference's test sizes (LARGE_SINGLE_VALUE_SIZE
     8569, DATA_SIZE 4 MiB + 347; ref:src/tests/suite/daos_rebuild_common.c:
     654-658): zero-padded last cell, parity vs the oracle restatement."""
@@ -580,6 +738,7 @@ def test_singv_encode(ctx, oracle, ecglib, oc, size):
     value = rand(size, size)
     pbufs = (ecglib.u8p * p)()
     assert L.ecg_obj_ec_singv_encode(oc, size, value.ctypes.data_as(ecglib.u8p), pbufs) == 0
+    check_route(ecglib, route)
     got = np.stack([np.ctypeslib.as_array(pbufs[r], shape=(cb,)).copy() for r in range(p)])
     libc = C.CDLL(None)
     for r in range(p):

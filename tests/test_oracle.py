@@ -144,10 +144,13 @@ def test_recovery_too_many(oracle):
 
 
 def test_reference_quirk_parity_first(oracle):
-    """ref:src/object/cli_ec.c:2226-2243 indexes inv with the first
+    """ref:src/object/cli_ec.c:2226-2243 indexes the inverse with the first
     er_data_nerrs entries of the insertion-ordered err_list.  With a parity
-    error listed first, the data row is still right (enc[e]*inv == inv[e] for
-    e < k) but the parity row is not: document that behaviour."""
+    cell listed first, that row index is >= k: the reference reads a row of
+    its zero-filled (k+p) x k inverse buffer beyond the k x k that
+    gf_invert_matrix wrote (:1963-1984, :2223), so the parity cell it writes
+    is ALL ZERO BYTES, while the data cells listed later are still right
+    (their rows come from enc[e] * inv == inv[e] for e < k)."""
     k, p = 4, 2
     rng = np.random.default_rng(1)
     en = oracle.cauchy1(k, p)
@@ -155,9 +158,24 @@ def test_reference_quirk_parity_first(oracle):
     stripe = np.concatenate([data, oracle.encode_data(en[k:], data)])
     rc, de, dec, el, gt, reused = oracle.recov_codec(k, p, [5, 0])
     assert rc == 0 and not reused
+    assert not de[0].any()                          # the misindexed decode row is zeros
     out = oracle.encode_data(de, stripe[dec])
     assert np.array_equal(out[1], stripe[0])        # data cell recovered
-    assert not np.array_equal(out[0], stripe[5])    # parity cell garbage
+    assert not out[0].any()                         # the reference's parity cell: zeros
+    assert stripe[5].any()                          # ... which is not the true parity
+    # k=4, p=3: {4, 5, 0} and {4, 0, 1}: exactly the parity cells among the first
+    # er_data_nerrs entries come out zero, every other cell is right
+    en3 = oracle.cauchy1(4, 3)
+    stripe3 = np.concatenate([data, oracle.encode_data(en3[4:], data)])
+    for errs, zero in (([4, 5, 0], {0}), ([4, 0, 1], {0}), ([5, 6, 1], {0}), ([0, 4, 1], {1}), ([0, 1, 4], set())):
+        rc, de, dec, el, gt, reused = oracle.recov_codec(4, 3, errs)
+        assert rc == 0 and not reused
+        out = oracle.encode_data(de, stripe3[dec])
+        for i, e in enumerate(el):
+            if i in zero:
+                assert not out[i].any(), (errs, e)
+            else:
+                assert np.array_equal(out[i], stripe3[e]), (errs, e)
 
 
 def test_fixtures_reproduce(oracle):

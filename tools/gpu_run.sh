@@ -138,6 +138,22 @@ for what in "$@"; do
 	fillback)
 		step bench_fillback 300 python tools/bench_fillback.py || exit $?
 		;;
+	sel)              # SEL="tests/x.py tests/y.py::t": a selection of the GPU suite
+		step pytest_sel 900 $PYTEST -x -m gpu ${SEL:-tests/test_gpu_parity.py}
+		rc=$?; [ $rc -le 1 ] || exit $rc
+		;;
+	dropinx)          # the drop-in crossover: CPU path vs GPU staging vs device cells (tools/dropin_bench.c)
+		make -s -C tests/c dropin_bench > /dev/null || exit 2
+		step dropin_bench 600 ./build/ctest/dropin_bench || exit $?
+		;;
+	qdev)             # device-cell drop-in calls from T threads (tools/queue_bench.c device)
+		make -s -C tests/c queue_bench > /dev/null || exit 2
+		for C in 131072 1048576; do
+			for T in 1 2 4 8 16; do
+				step qdev_${C}_$T 120 ./build/ctest/queue_bench $C $T device || exit $?
+			done
+		done
+		;;
 	ctest)
 		make -C tests/c > /dev/null || exit 2
 		step ctest 300 ./build/ctest/test_ecg_c || exit $?
