@@ -722,6 +722,53 @@ def update_rows(ctx, iters=11):
     return rows
 
 
+def layout_rows(ctx, iters=11):
+    """The caller's parity layout, not the bench's: EC_4P2 1 MiB
+    x 1024 (the headline's encode) and EC_8P2 1 MiB x 512, client-layout
+    encode with the p parity rows
+      padded   -- one buffer, rows S*C + 4 KiB apart (the headline's layout);
+      unpadded -- one buffer, rows exactly S*C apart;
+      separate -- p separate hipMalloc allocations of S*C bytes, as
+                  obj_ec_pbufs_init allocates oer_pbufs (ref:src/object/
+                  cli_ec.c:75-97), written through per-row cell offsets.
+    Launches interleaved (one of each per round, so clock drift cannot bias
+    the ratio); `of_padded` = the padded row's ms / this row's ms."""
+    import numpy as np
+    from daos_amd import ecg
+
+    rows = {}
+    for name, k, p, C, S in (("EC_4P2_1MiB_x1024", 4, 2, 1 << 20, 1024), ("EC_8P2_1MiB_x512", 8, 2, 1 << 20, 512)):
+        data = ctx.alloc(S * k * C)
+        fill_device(ctx, data, S * k * C, 10)
+        padded = ctx.alloc(p * (S * C + PARITY_ROW_PAD))
+        unpadded = ctx.alloc(p * S * C)
+        sep = [ctx.alloc(S * C) for _ in range(p)]
+        base = min(b.ptr for b in sep)
+        soff = [j * C for j in range(k)]
+        doff = [b.ptr - base for b in sep]
+        coef = ecg.cauchy1(k, p)[k:]
+        fns = {"padded": lambda: ctx.encode(k, p, C, S, data.ptr, k * C, padded.ptr, S * C + PARITY_ROW_PAD, C),
+               "unpadded": lambda: ctx.encode(k, p, C, S, data.ptr, k * C, unpadded.ptr, S * C, C),
+               "separate": lambda: ctx.matmul(coef, C, S, data.ptr, soff, k * C, base, doff, C)}
+        ms = dict(zip(fns, time_interleaved(ctx, list(fns.values()), iters, warm=40)))
+        kern = ecg.last_kernel()
+        # the separate rows' bytes equal the padded rows' (same product, other addresses)
+        ok = all(np.array_equal(sep[r].download(C, offset=s * C), padded.download(C, offset=r * (S * C + PARITY_ROW_PAD)
+                                                                                 + s * C))
+                 for r in range(p) for s in (0, S - 1))
+        alg = (k + p) * C * S
+        for lay, t in ms.items():
+            rows[f"{name}_encode_parity_{lay}"] = {
+                "layout": lay, "ms": round(t, 4), "GiBps_user": round(k * C * S / (t / 1e3) / GIB, 1),
+                "alg_GBps": round(alg / t / 1e6, 1), "roofline_frac": round(alg / t / 1e6 / HBM_PEAK_GBS, 4),
+                "of_padded": round(ms["padded"] / t, 4), "kernel": kern,
+                **({"parity_row_addresses": [hex(b.ptr) for b in sep], "matches_padded": ok}
+                   if lay == "separate" else {})}
+        for b in [data, padded, unpadded] + sep:
+            b.free()
+    return rows
+
+
 def detail_rows(ctx, ceil, iters=11, shapes=DETAIL_SHAPES, csum=True):
     """Extra device-resident rows (per GPU): the north-star EC_8P2 encode,
     EC_8P2 2-erasure decode, EC_16P2 128 KiB encode, EC_2P1 128 KiB encode.
@@ -777,6 +824,7 @@ def detail_rows(ctx, ceil, iters=11, shapes=DETAIL_SHAPES, csum=True):
     rows.update(offset_rows(ctx, rows.get("EC_8P2_1MiB_encode"), iters))
     rows.update(sgl_rows(ctx, rows.get("EC_8P2_1MiB_encode"), iters))
     rows.update(update_rows(ctx, iters))
+    rows.update(layout_rows(ctx, iters))
     if not csum:
         return rows
     # checksums of regenerated cells (include/ecg_csum.h): EC_8P2 encode with

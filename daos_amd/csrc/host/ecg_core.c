@@ -121,12 +121,18 @@ int ecg_ctx_create(int device, ecg_ctx_t **out)
 		 * columns of unaligned sources); ECG_UNALIGNED=0 forces the byte
 		 * kernels for those operands, as a device without them would get */
 		const char *env = getenv("ECG_UNALIGNED");
-		int ok = 0;
+		int ok = 0, rc;
 
-		if (env && env[0] == '0')
+		if (env && env[0] == '0') {
 			ok = 0;
-		else if (ecg_k_unaligned_check((void *)ctx->stream, &ok) != 0)
+		} else if ((rc = ecg_k_unaligned_check((void *)ctx->stream, &ok)) != 0) {
+			/* the probe itself failed: byte kernels for misaligned
+			 * operands (same bytes, ~8x slower) -- say so */
+			(void)hipGetLastError();
+			fprintf(stderr, "ecg: device %d: misaligned-access probe failed (%s); misaligned "
+				"operands run the byte kernels\n", device, hipGetErrorString((hipError_t)rc));
 			ok = 0;
+		}
 		ctx->cfg.no_unaligned = ok ? 0u : 1u;
 	}
 	*out = ctx;

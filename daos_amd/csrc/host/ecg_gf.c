@@ -146,10 +146,13 @@ int ecg_invert_matrix(unsigned char *in, unsigned char *out, int n)
  *   all p parity cells lost (and no data) -> plain re-encode (:2205-2210).
  * Rows are produced data-errors-first (out_idx says which cell each row
  * regenerates).  The reference indexes inv with the first er_data_nerrs
- * entries of its insertion-ordered list, so it only gets parity cells right
- * when data errors come first; data cells it always gets right.  Producing
- * rows data-first gives the reference's bytes whenever the reference is
- * correct, and correct parity where it is not.
+ * entries of its insertion-ordered list: a parity cell among them reads a
+ * row past the k x k inverse inside its zero-filled (k+p) x k buffer
+ * (:1963-1984), so the reference writes that parity cell as all zeros; data
+ * cells it always gets right.  Producing rows data-first gives the
+ * reference's bytes wherever the reference is right, and the true parity in
+ * that one cell -- a deliberate divergence in a cell degraded reads never
+ * return (tests/test_oracle.py pins the reference's zeros).
  */
 int ecg_recov_rows(int k, int p, const unsigned char *en, const uint32_t *err_list,
 		   int nerrs, unsigned char *rows, uint32_t *out_idx, uint32_t *dec_idx,

@@ -56,6 +56,11 @@
 #define ECG_TUNE_MARGIN 0.015	/* the cap must win by more than 1.5 % */
 #define ECG_TUNE_MAX_CYCLES 64	/* probe cycles per context */
 #define ECG_TUNE_RESTARTS 2	/* probes restarted after invalid timings */
+/* launches of a probing shape from other streams, with the probe's own stream
+ * silent meanwhile, after which the probe moves to the stream asking: the
+ * stream that started it went idle (its thread exited, its stream was
+ * destroyed -- whose handle may even be reused by an unrelated stream) */
+#define ECG_TUNE_STALL 64
 
 struct ecg_tune_ent {
 	int valid, decided, events, restarts;
@@ -65,6 +70,8 @@ struct ecg_tune_ent {
 	uint32_t cand;		/* candidate cap */
 	uint32_t choice;	/* decided: the cap, or ECG_WG_UNCAPPED */
 	uint32_t n;		/* probing launches so far */
+	uint32_t stall;		/* foreign launches since the probe last advanced */
+	uint32_t handovers;	/* times the probe moved to another stream */
 	uint64_t stamp;
 	hipEvent_t ev[2][ECG_TUNE_T][2];
 	uint64_t blocks[2][ECG_TUNE_T];	/* blocks of each timed launch */
@@ -333,6 +340,14 @@ int ecg_tune_launch_fn(ecg_ctx_t *ctx, const ecg_mm_params_t *p, uint32_t g, uin
 		pthread_mutex_unlock(&t->lock);
 		return fn(p, &cfg, (void *)st, kid, arg);
 	}
+	if (e->n < ECG_TUNE_PROBE && st != e->stream && ++e->stall >= ECG_TUNE_STALL) {
+		/* the probe's stream went quiet: start over on this one (events of
+		 * the old stream are re-recorded before they are read again) */
+		e->stream = st;
+		e->n = 0;
+		e->stall = 0;
+		e->handovers++;
+	}
 	if (e->n >= ECG_TUNE_PROBE || st != e->stream) {
 		/* timings still in flight, or another stream: run uncapped */
 		cfg.wg_per_cu = ECG_WG_UNCAPPED;
@@ -349,6 +364,7 @@ int ecg_tune_launch_fn(ecg_ctx_t *ctx, const ecg_mm_params_t *p, uint32_t g, uin
 	/* probing: arm 0 uncapped, arm 1 capped, each W untimed + T timed, back
 	 * to back; the lock is held across the timed launch so concurrent callers
 	 * of the shape cannot interleave inside an event pair */
+	e->stall = 0;
 	arm = e->n < ECG_TUNE_ARM0 ? 0 : 1;
 	idx = arm ? (int)(e->n - ECG_TUNE_ARM0) - ECG_TUNE_W1 : (int)e->n - ECG_TUNE_W0;
 	e->n++;

@@ -15,11 +15,6 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #define CHUNK_BYTES 4096u	// 256 lanes x 16 B
 #define BLOCK 256
-#ifndef ECG_MM_WG_DEFAULT
-// per-shape default blocks per CU (mm_wg_cap) by the cell streams a block
-// keeps in flight (k + rows): none -- see mm_wg_cap
-#define ECG_MM_WG_DEFAULT(streams) 0u
-#endif
 
 template <bool B>
 struct ecg_bool {
@@ -626,17 +621,17 @@ __device__ __forceinline__ void item_map(uint32_t order, uint32_t it, uint32_t t
 // (any cap <= 4 loses).  Timed back to back as bench.py does, the gain does
 // not hold: k = 16 at 2 blocks per CU +2 % on one box and -4..-6 % on
 // another, k = 8 at 3 -2..-4 % (bench_wg*.log), so no shape is capped by
-// default; the knob stays for A/B runs.  A default cap would apply only to
-// launches of more than 2048 blocks (a smaller grid is latency-bound).
+// default: without a cap from the context (ecg_set_wg_per_cu) or the launch
+// tuner (ecg_tune.c, which measures one per shape) a launch is uncapped.
 __host__ static inline uint32_t mm_wg_cap(const ecg_mm_params_t *p, const ecg_launch_cfg_t *cfg, uint64_t blocks)
 {
 	const uint32_t c = cfg ? cfg->wg_per_cu : 0;
 
-	if (c == ECG_WG_UNCAPPED)
+	(void)p;
+	(void)blocks;
+	if (c == ECG_WG_UNCAPPED || c == 0)
 		return 0;
-	if (c)
-		return c < 2 ? 2 : c;
-	return blocks > 2048 ? ECG_MM_WG_DEFAULT(p->k + p->rows) : 0u;
+	return c < 2 ? 2 : c;
 }
 
 // Unused dynamic LDS that leaves room for exactly `cap` blocks per CU (160 KiB

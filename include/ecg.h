@@ -59,7 +59,9 @@ int ecg_ctx_device(const ecg_ctx_t *ctx);
  * creation (the unaligned access mode ROCm enables on gfx9+): destinations
  * off a dword boundary then run on the vector lanes; 0 when it did not (or
  * ECG_UNALIGNED=0 was set): such launches run the byte kernels, same
- * results, ~8x slower. */
+ * results, ~8x slower.  The probe assumes a misaligned access is served (or
+ * rounded), not trapped: on a device configured to FAULT on misaligned
+ * accesses, set ECG_UNALIGNED=0 before creating a context. */
 int ecg_ctx_unaligned_ok(ecg_ctx_t *ctx);
 /* PCI bus id ("0000:c1:00.0") of a visible device: tells ranks or shards
  * that landed on the same physical GPU apart. */

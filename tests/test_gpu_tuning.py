@@ -215,6 +215,43 @@ def test_autotune_probe_other_stream_not_timed(ctx, ecglib, oracle):
         ctx.set_autotune(1)
 
 
+def test_autotune_probe_moves_off_idle_stream(ctx, ecglib, oracle):
+    """A probe whose starting stream goes idle (its thread exits, its stream is
+    destroyed) moves to the stream that keeps launching the shape after
+    ECG_TUNE_STALL (64) such launches, and decides there: the
+    shape is not left probing -- and uncapped -- for good."""
+    k, p, S, C_ = 16, 2, 300, 32768
+    data = rand((S, k, C_), 1603)
+    en = oracle.cauchy1(k, p)
+    want = np.stack([oracle.encode_data(en[k:], data[s]) for s in range(S)], axis=1)
+    ctx.set_autotune(2)
+    st2 = ctx.stream()
+    try:
+        d = ctx.to_device(data)
+        par = ctx.alloc(p * S * C_)
+        ctx.encode(k, p, C_, S, d.ptr, k * C_, par.ptr, S * C_, C_, stream=st2)     # starts the probe on st2
+        ctx.sync(st2)
+        ctx.destroy_stream(st2)
+        st2 = None
+        for _ in range(63):             # foreign launches: uncapped, probe untouched
+            ctx.encode(k, p, C_, S, d.ptr, k * C_, par.ptr, S * C_, C_)
+        ctx.sync()
+        assert ctx.tune_counters()[1] == 1
+        assert ctx.tune_state(k, p, C_, S, k * C_, C_) is None
+        for _ in range(PROBE):          # the 64th hands the probe over; it completes here
+            ctx.encode(k, p, C_, S, d.ptr, k * C_, par.ptr, S * C_, C_)
+        ctx.sync()
+        assert ctx.tune_counters()[1] == 1 + PROBE
+        assert ctx.tune_state(k, p, C_, S, k * C_, C_) is not None
+        assert np.array_equal(par.download().reshape(p, S, C_), want)
+        d.free()
+        par.free()
+    finally:
+        if st2 is not None:
+            ctx.destroy_stream(st2)
+        ctx.set_autotune(1)
+
+
 def test_autotune_pointer_tables(ctx, oracle, ecglib):
     """Pointer-table launches (ecg_matmul_ptrs with a table that is not affine:
     the stripes listed in shuffled order) go through the launch tuner as
