@@ -118,7 +118,7 @@ def test_bench_gpus_n_spawns_ranks():
     # node ceiling = their sum (solo denominators gave fractions > 1 at N = 8)
     for r in stream["ranks"]:
         assert set(r["concurrent_pinned_GBps"]) == {"h2d", "d2h"} and r["concurrent_pinned_GBps"]["h2d"] > 0
-        assert r["frac_of_h2d"] == round(r["h2d_GBps"] / r["concurrent_pinned_GBps"]["h2d"], 4)
+        assert abs(r["frac_of_h2d"] / (r["h2d_GBps"] / r["concurrent_pinned_GBps"]["h2d"]) - 1) < 1e-3
     node = stream["node_concurrent_copy_ceiling"]
     assert abs(node["h2d_GBps"] - sum(r["concurrent_pinned_GBps"]["h2d"] for r in stream["ranks"])) < 0.02
 
