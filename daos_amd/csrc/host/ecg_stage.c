@@ -23,6 +23,7 @@ struct tstage {
 	size_t dev_bytes;
 	hipStream_t st;
 	hipEvent_t ev;		/* device-cell calls wait on this */
+	hipEvent_t ev_in;	/* ... after ordering behind the context stream with this */
 	int ev_device;
 };
 
@@ -48,6 +49,7 @@ static void tstage_release(struct tstage *t)
 	if (t->ev) {
 		(void)hipSetDevice(t->ev_device);
 		(void)hipEventDestroy(t->ev);
+		(void)hipEventDestroy(t->ev_in);
 	}
 	memset(t, 0, sizeof(*t));
 }
@@ -95,12 +97,18 @@ static int tstage_event(ecg_ctx_t *ctx, struct tstage **out)
 		return ecg_fail(-ECG_DER_NOMEM, "stage: calloc");
 	if (t->ev && t->ev_device != ctx->device) {
 		(void)hipEventDestroy(t->ev);
-		t->ev = NULL;
+		(void)hipEventDestroy(t->ev_in);
+		t->ev = t->ev_in = NULL;
 	}
 	if (t->ev == NULL) {
 		e = hipEventCreateWithFlags(&t->ev, hipEventDisableTiming);
+		if (e == hipSuccess) {
+			e = hipEventCreateWithFlags(&t->ev_in, hipEventDisableTiming);
+			if (e != hipSuccess)
+				(void)hipEventDestroy(t->ev);
+		}
 		if (e != hipSuccess) {
-			t->ev = NULL;
+			t->ev = t->ev_in = NULL;
 			return ecg_hip_fail(e, "stage event");
 		}
 		t->ev_device = ctx->device;
@@ -117,13 +125,14 @@ static int tstage_get(ecg_ctx_t *ctx, size_t bytes, struct tstage **out)
 	if (t == NULL)
 		return ecg_fail(-ECG_DER_NOMEM, "stage: calloc");
 	if (t->ctx != ctx || t->device != ctx->device) {
-		/* host staging of another context: free it, keep the event */
-		hipEvent_t ev = t->ev;
+		/* host staging of another context: free it, keep the events */
+		hipEvent_t ev = t->ev, ev_in = t->ev_in;
 		int ev_device = t->ev_device;
 
-		t->ev = NULL;
+		t->ev = t->ev_in = NULL;
 		tstage_release(t);
 		t->ev = ev;
+		t->ev_in = ev_in;
 		t->ev_device = ev_device;
 	}
 	t->ctx = ctx;
@@ -250,9 +259,10 @@ static int pool_stream(ecg_ctx_t *ctx, hipStream_t *out)
  * live in HBM keeps its ec_encode_data call sites): strided launches on the
  * cells in place (cell offsets relative to the first source / output; more
  * than ECG_MAX_K sources -- xor_gen -- as accumulating groups), on the
- * caller's pool stream, then a wait for an event recorded right after them:
- * the call waits for its own launches and what precedes them on that stream,
- * not for every other thread's work (ISA-L's calls are synchronous). */
+ * caller's pool stream (ordered behind the work queued on the context's own
+ * stream), then a wait for an event recorded right after them: the call
+ * waits for its own launches and what precedes them on that stream, not for
+ * every other thread's drop-in work (ISA-L's calls are synchronous). */
 static int matmul_device(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
 			 unsigned char *const *src, unsigned char *const *dst, unsigned flags)
 {
@@ -276,6 +286,14 @@ static int matmul_device(ecg_ctx_t *ctx, int len, int k, int rows, const unsigne
 		soff[j] = (int64_t)((uintptr_t)src[j] - (uintptr_t)src[0]);
 	for (r = 0; r < rows; r++)
 		doff[r] = (int64_t)((uintptr_t)dst[r] - (uintptr_t)dst[0]);
+	/* keep the order a caller of the context's own stream relies on (an
+	 * ecg_memcpy / ecg_memset there before this call, as when device cells
+	 * used that stream): the pool stream waits for what is queued on it now */
+	e = hipEventRecord(t->ev_in, ctx->stream);
+	if (e == hipSuccess)
+		e = hipStreamWaitEvent(st, t->ev_in, 0);
+	if (e != hipSuccess)
+		return ecg_hip_fail(e, "matmul_host: order behind the context stream");
 	for (j0 = 0; rc == 0 && j0 < k; j0 += ECG_MAX_K) {
 		const int kk = k - j0 < ECG_MAX_K ? k - j0 : ECG_MAX_K;
 		const unsigned f = flags | (j0 ? ECG_F_ACCUMULATE : 0u);

@@ -1,8 +1,10 @@
-"""Latency of the synchronous ISA-L drop-in (ec_encode_data, one EC_8P2
-stripe per call, host buffers) by cell size -- what an unbatched DAOS caller
-linked against libecg sees.  Run once per staging mode (env
-ECG_ZERO_COPY_MAX: 0 = always DMA copies, large = kernel on the pinned
-staging in place); appends one JSON line to gpurun_out/bench_dropin.jsonl.
+"""Latency of the synchronous ISA-L drop-in's GPU staging path
+(ec_encode_data, one EC_8P2 stripe per call, host buffers, run with
+ECG_DROPIN_CROSSOVER=0 so host cells take the GPU) by cell size.  Run once per
+staging mode (env ECG_ZERO_COPY_MAX: 0 = always DMA copies, large = kernel on
+the pinned staging in place); appends one JSON line to
+gpurun_out/bench_dropin.jsonl.  The CPU path and the crossover between the
+two: tools/dropin_bench.c.
 DROPIN_DEVICE=1: the cells live in device memory instead (the drop-in then
 launches on them in place).  Bench infrastructure (no oracle)."""
 import json

@@ -129,7 +129,7 @@ for what in "$@"; do
 		;;
 	dropin)
 		for zc in 0 1048576; do
-			ECG_ZERO_COPY_MAX=$zc step dropin_$zc 300 python tools/bench_dropin.py || exit $?
+			ECG_DROPIN_CROSSOVER=0 ECG_ZERO_COPY_MAX=$zc step dropin_$zc 300 python tools/bench_dropin.py || exit $?
 		done
 		;;
 	rebuild)
@@ -151,6 +151,14 @@ for what in "$@"; do
 		for C in 131072 1048576; do
 			for T in 1 2 4 8 16; do
 				step qdev_${C}_$T 120 ./build/ctest/queue_bench $C $T device || exit $?
+			done
+		done
+		;;
+	qhost)            # host-cell one-stripe callers from T threads: drop-in (CPU path) / queue / oracle GFNI
+		make -s -C tests/c queue_bench > /dev/null || exit 2
+		for C in 32768 131072 1048576; do
+			for T in 1 8 16; do
+				step qhost_${C}_$T 120 ./build/ctest/queue_bench $C $T || exit $?
 			done
 		done
 		;;

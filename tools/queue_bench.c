@@ -2,7 +2,9 @@
  * queue_bench.c -- one-stripe callers, the reference's calling pattern
  * (SURVEY §0.6): T pthreads each encode N stripes of EC_k+p with C-byte
  * cells, one stripe per call, via
- *   isal : ec_encode_data()        (synchronous ISA-L drop-in, GPU per call)
+ *   isal : ec_encode_data()        (synchronous ISA-L drop-in: host cells run the
+ *                                   product CPU path at the default crossover,
+ *                                   the GPU with ECG_DROPIN_CROSSOVER=0)
  *   queue: ecg_queue_encode()      (batching facade, async completion)
  *   cpu  : ref_simd_encode_data()  (ISA-L-equivalent CPU restatement, the
  *                                   baseline DAOS runs today)
@@ -15,7 +17,8 @@
  *          into the parity (ISA-L-equivalent CPU restatement)
  * and GiB/s counts the updated cell bytes.  With "device" the cells live in
  * device memory and only the drop-in runs (ec_encode_data on device cells,
- * in place, each thread on its own stream).  Bench infrastructure.
+ * in place, the calling threads spread over the context's drop-in stream
+ * pool, each call waiting for its own launch).  Bench infrastructure.
  */
 #include <pthread.h>
 #include <stdio.h>
