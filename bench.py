@@ -52,7 +52,7 @@ sys.path.insert(0, ROOT)
 GIB = float(1 << 30)
 PARITY_ROW_PAD = 4096
 HBM_PEAK_GBS = 8000.0          # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
-ROUND = "r04"
+ROUND = "r05"
 
 # name -> (k, p, cell bytes, stripes, ops, strong scaling?)
 WORKLOADS = {
@@ -1024,7 +1024,7 @@ def cpu_baseline(k, p, C, budget_s, ops=("enc", "dec"), per_config=True):
 
 def pmc_traffic():
     path = os.path.join(ROOT, "profiles", ROUND, "pmc_traffic.json")
-    for older in ("r03", "r02", "r01"):          # the newest committed pass
+    for older in ("r04", "r03", "r02", "r01"):    # the newest committed pass
         if not os.path.exists(path):
             path = os.path.join(ROOT, "profiles", older, "pmc_traffic.json")
     if os.path.exists(path):
@@ -1117,11 +1117,13 @@ def leg_strong(args, ctx, world, rank, steps, weak=False):
 
 
 def concurrent_copy_rates(world, ctx, host, nbytes, reps=3):
-    """This rank's pinned H2D / D2H GB/s while EVERY rank copies at once
-    (barrier-aligned start of each copy), over `host` -- the leg's own pinned
-    buffer -- and one device buffer of its size: the per-rank PCIe / host
-    memory ceiling at this N.  Without a context (CPU rehearsal) the "copy" is
-    a host memcpy of the buffer, so the plumbing and keys are the same."""
+    """Pinned H2D / D2H copies with EVERY rank copying at once (barrier-aligned
+    start of each copy), over `host` -- the leg's own pinned buffer -- and one
+    device buffer of its size.  Returns this rank's own rate ("h2d"/"d2h") and
+    the node aggregate: world x nbytes over the slowest rank's time
+    ("node_h2d"/"node_d2h"), whose 1/world share is a rank's fair share of the
+    host memory / PCIe the ranks contend for.  Without a context (CPU
+    rehearsal) the "copy" is a host memcpy of the buffer."""
     import numpy as np
 
     dev = ctx.alloc(nbytes) if ctx is not None else None
@@ -1129,7 +1131,7 @@ def concurrent_copy_rates(world, ctx, host, nbytes, reps=3):
     out = {}
     try:
         for name in ("h2d", "d2h"):
-            ts = []
+            ts, tmaxs = [], []
             for _ in range(reps):
                 barrier(world)
                 t0 = time.perf_counter()
@@ -1142,8 +1144,11 @@ def concurrent_copy_rates(world, ctx, host, nbytes, reps=3):
                     ecg._chk(ecg.lib().ecg_memcpy(ctx.h, dst, src, nbytes, 0 if name == "h2d" else 1, None),
                              name)
                     ctx.sync()
-                ts.append(time.perf_counter() - t0)
+                t = time.perf_counter() - t0
+                ts.append(t)
+                tmaxs.append(max_over_ranks(world, t))
             out[name] = round(nbytes / sorted(ts)[len(ts) // 2] / 1e9, 2)
+            out["node_" + name] = round(world * nbytes / sorted(tmaxs)[len(tmaxs) // 2] / 1e9, 2)
     finally:
         if dev is not None:
             dev.free()
@@ -1189,9 +1194,12 @@ def leg_stream(args, ctx, world, rank, steps, numa_info):
     host = wl.data.array if wl is not None else np.ones(64 << 20, dtype=np.uint8)
     conc = concurrent_copy_rates(world, ctx if wl is not None else None, host, host.size)
     solo = solo_copy_rates(world, rank, ctx if wl is not None else None, 256 << 20)
-    row.update({"h2d_GBps": round(h2d, 2), "concurrent_pinned_GBps": conc,
-                "frac_of_h2d": round(h2d / conc["h2d"], 4),
-                "denominator": "pinned H2D rate of this rank with all ranks copying at once"})
+    share = conc["node_h2d"] / world
+    row.update({"h2d_GBps": round(h2d, 2),
+                "concurrent_pinned_GBps": {"h2d": conc["h2d"], "d2h": conc["d2h"]},
+                "fair_share_h2d_GBps": round(share, 2), "frac_of_h2d": round(h2d / share, 4),
+                "frac_of_own_concurrent_h2d": round(h2d / conc["h2d"], 4),
+                "denominator": "1/N of the node's concurrent pinned H2D rate (all ranks copying at once)"})
     if solo is not None:
         row.update({"measured_pinned_GBps": solo, "frac_of_solo_h2d": round(h2d / solo["h2d"], 4)})
     if wl is not None:
@@ -1199,9 +1207,9 @@ def leg_stream(args, ctx, world, rank, steps, numa_info):
                     "verified": all(wl.verify().values())})
         wl.free()
     rows = gather(world, row)
-    node = {"h2d_GBps": round(sum(r["concurrent_pinned_GBps"]["h2d"] for r in rows), 2),
-            "d2h_GBps": round(sum(r["concurrent_pinned_GBps"]["d2h"] for r in rows), 2),
-            "what": "concurrent pinned copies summed over ranks: the node's host-memory / PCIe ceiling at this N"}
+    node = {"h2d_GBps": conc["node_h2d"], "d2h_GBps": conc["node_d2h"],
+            "what": "N x the pinned copy bytes of one rank over the slowest rank's time, every rank copying at "
+                    "once: the node's host-memory / PCIe ceiling at this N"}
     return {"config": f"EC_{k}P{p} {C >> 20} MiB cells: per rank one encode batch + one {{d0,d1}} recovery "
                       f"batch of {S} stripes per step, stripes in NUMA-local pinned host memory, "
                       f"host<->device copies included ({args.host_chunk or HOST_CHUNK}-stripe staging chunks)",

@@ -849,11 +849,13 @@ int ecg_encode_host_rows(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S, c
 		chunk = S;
 	pthread_mutex_lock(&ctx->lock);
 	ecg_trace_push("ecg:encode_host");
-	rc = stage_reserve(ctx, (size_t)chunk * (k + p) * C);
+	/* staged parity rows at a pitch of cs*C + ECG_PARITY_ROW_PAD (include/ecg.h) */
+	rc = stage_reserve(ctx, (size_t)chunk * (k + p) * C + (size_t)p * ECG_PARITY_ROW_PAD);
 	for (s0 = 0; rc == 0 && s0 < S; s0 += chunk, slot = (slot + 1) % ECG_NSLOT) {
 		uint32_t cs = S - s0 < chunk ? S - s0 : chunk;
 		unsigned char *dd = ctx->stage.dev[slot];
 		unsigned char *dp = dd + (size_t)cs * k * C;
+		const size_t dprow = (size_t)cs * C + ECG_PARITY_ROW_PAD;
 		hipStream_t st = ctx->stage.st[slot];
 		hipError_t e;
 
@@ -876,10 +878,9 @@ int ecg_encode_host_rows(ecg_ctx_t *ctx, int k, int p, uint64_t C, uint32_t S, c
 			rc = ecg_hip_fail(e, "encode_host H2D");
 			break;
 		}
-		rc = ecg_encode(ctx, k, p, C, cs, dd, (int64_t)k * C, dp, (int64_t)cs * C,
-				(int64_t)C, st);
+		rc = ecg_encode(ctx, k, p, C, cs, dd, (int64_t)k * C, dp, (int64_t)dprow, (int64_t)C, st);
 		for (r = 0; rc == 0 && r < p; r++) {
-			e = ecg_stage_copy(hp + (size_t)r * prow + (size_t)s0 * C, dp + (size_t)r * cs * C,
+			e = ecg_stage_copy(hp + (size_t)r * prow + (size_t)s0 * C, dp + (size_t)r * dprow,
 					   (size_t)cs * C, C, hipMemcpyDeviceToHost, st);
 			if (e != hipSuccess)
 				rc = ecg_hip_fail(e, "encode_host D2H");

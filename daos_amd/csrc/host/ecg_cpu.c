@@ -135,20 +135,27 @@ struct pass {
 	unsigned char *const *dst;
 };
 
+/* Bytes [i0, len) through the field's product table, one source at a time
+ * (the scalar variant, and the AVX2 variants' tails).  Sources and outputs
+ * are distinct cells, as in ISA-L. */
 static void tail_bytes(const struct pass *q, size_t i0)
 {
 	int r, j;
 
+	if (i0 >= q->len)
+		return;
 	for (r = 0; r < q->nr; r++) {
 		unsigned char *d = q->dst[r];
 		size_t i;
 
-		for (i = i0; i < q->len; i++) {
-			unsigned char v = q->acc ? d[i] : 0;
+		if (!q->acc)
+			memset(d + i0, 0, q->len - i0);
+		for (j = 0; j < q->ns; j++) {
+			const unsigned char *tb = ecg_gf_mul_tbl[q->cf[r * q->ns + j]];
+			const unsigned char *sj = q->src[j];
 
-			for (j = 0; j < q->ns; j++)
-				v ^= ecg_gf_mul_tbl[q->cf[r * q->ns + j]][q->src[j][i]];
-			d[i] = v;
+			for (i = i0; i < q->len; i++)
+				d[i] ^= tb[sj[i]];
 		}
 	}
 }
@@ -211,27 +218,34 @@ void pass_avx512_gfni_body(const struct pass *q, const int nr)
 static inline __attribute__((always_inline, target("avx2,gfni")))
 void pass_avx2_gfni_body(const struct pass *q, const int nr)
 {
-	uint64_t m[RG * SG];
+	uint64_t m[SG * RG];			/* [source][row] */
+	const unsigned char *s[SG];
+	unsigned char *d[RG];
 	__m256i a[RG];
-	const int ns = q->ns;
+	const int ns = q->ns, acc = q->acc, all_one = q->all_one;
+	const size_t len = q->len;
 	size_t i;
 	int r, j;
 
-	for (r = 0; r < nr * ns; r++)
-		m[r] = g_aff[q->cf[r]];
-	for (i = 0; i + 32 <= q->len; i += 32) {
+	for (j = 0; j < ns; j++) {
+		s[j] = q->src[j];
+		for (r = 0; r < nr; r++)
+			m[j * RG + r] = g_aff[q->cf[r * ns + j]];
+	}
+	for (r = 0; r < nr; r++)
+		d[r] = q->dst[r];
+	for (i = 0; i + 32 <= len; i += 32) {
 		_Pragma("GCC unroll 8") for (r = 0; r < nr; r++)
-			a[r] = q->acc ? _mm256_loadu_si256((const __m256i *)(q->dst[r] + i))
-				      : _mm256_setzero_si256();
+			a[r] = acc ? _mm256_loadu_si256((const __m256i *)(d[r] + i)) : _mm256_setzero_si256();
 		for (j = 0; j < ns; j++) {
-			const __m256i x = _mm256_loadu_si256((const __m256i *)(q->src[j] + i));
+			const __m256i x = _mm256_loadu_si256((const __m256i *)(s[j] + i));
 
 			_Pragma("GCC unroll 8") for (r = 0; r < nr; r++)
-				a[r] = _mm256_xor_si256(a[r], q->all_one ? x : _mm256_gf2p8affine_epi64_epi8(
-						x, _mm256_set1_epi64x((long long)m[r * ns + j]), 0));
+				a[r] = _mm256_xor_si256(a[r], all_one ? x : _mm256_gf2p8affine_epi64_epi8(
+						x, _mm256_set1_epi64x((long long)m[j * RG + r]), 0));
 		}
 		_Pragma("GCC unroll 8") for (r = 0; r < nr; r++)
-			_mm256_storeu_si256((__m256i *)(q->dst[r] + i), a[r]);
+			_mm256_storeu_si256((__m256i *)(d[r] + i), a[r]);
 	}
 	tail_bytes(q, i);
 }
@@ -240,32 +254,46 @@ static inline __attribute__((always_inline, target("avx2")))
 void pass_avx2_body(const struct pass *q, const int nr)
 {
 	const __m256i low4 = _mm256_set1_epi8(0x0f);
+	const unsigned char *t[SG * RG];	/* [source][row] nibble tables */
+	const unsigned char *s[SG];
+	unsigned char *d[RG];
 	__m256i a[RG];
-	const int ns = q->ns;
+	const int ns = q->ns, acc = q->acc, all_one = q->all_one;
+	const size_t len = q->len;
 	size_t i;
 	int r, j;
 
-	for (i = 0; i + 32 <= q->len; i += 32) {
+	for (j = 0; j < ns; j++) {
+		s[j] = q->src[j];
+		for (r = 0; r < nr; r++)
+			t[j * RG + r] = g_nib[q->cf[r * ns + j]];
+	}
+	for (r = 0; r < nr; r++)
+		d[r] = q->dst[r];
+	for (i = 0; i + 32 <= len; i += 32) {
 		_Pragma("GCC unroll 8") for (r = 0; r < nr; r++)
-			a[r] = q->acc ? _mm256_loadu_si256((const __m256i *)(q->dst[r] + i))
-				      : _mm256_setzero_si256();
+			a[r] = acc ? _mm256_loadu_si256((const __m256i *)(d[r] + i)) : _mm256_setzero_si256();
 		for (j = 0; j < ns; j++) {
-			const __m256i x = _mm256_loadu_si256((const __m256i *)(q->src[j] + i));
+			const __m256i x = _mm256_loadu_si256((const __m256i *)(s[j] + i));
 			const __m256i lo = _mm256_and_si256(x, low4);
 			const __m256i hi = _mm256_and_si256(_mm256_srli_epi16(x, 4), low4);
 
-			for (r = 0; r < nr; r++) {
-				const unsigned char *t = g_nib[q->cf[r * ns + j]];
-				const __m256i tl = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)t));
-				const __m256i th = _mm256_broadcastsi128_si256(
-					_mm_loadu_si128((const __m128i *)(t + 16)));
+			if (all_one) {
+				_Pragma("GCC unroll 8") for (r = 0; r < nr; r++)
+					a[r] = _mm256_xor_si256(a[r], x);
+				continue;
+			}
+			_Pragma("GCC unroll 8") for (r = 0; r < nr; r++) {
+				const unsigned char *tb = t[j * RG + r];
+				const __m256i tl = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)tb));
+				const __m256i th = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)(tb + 16)));
 
-				a[r] = _mm256_xor_si256(a[r], q->all_one ? x :
-					_mm256_xor_si256(_mm256_shuffle_epi8(tl, lo), _mm256_shuffle_epi8(th, hi)));
+				a[r] = _mm256_xor_si256(a[r], _mm256_xor_si256(_mm256_shuffle_epi8(tl, lo),
+										_mm256_shuffle_epi8(th, hi)));
 			}
 		}
 		_Pragma("GCC unroll 8") for (r = 0; r < nr; r++)
-			_mm256_storeu_si256((__m256i *)(q->dst[r] + i), a[r]);
+			_mm256_storeu_si256((__m256i *)(d[r] + i), a[r]);
 	}
 	tail_bytes(q, i);
 }

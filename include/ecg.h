@@ -41,6 +41,15 @@ extern "C" {
 #define ECG_MAX_K		64
 #define ECG_MAX_P		8
 
+/* Parity row pitch.  Client-layout parity [p][S][C] runs fastest with its p
+ * rows one buffer at a pitch of S*C + ECG_PARITY_ROW_PAD: rows a large power
+ * of two apart, or separately allocated rows the allocator happens to place
+ * at such distances, alias in HBM (measured, profiles/r05/: EC_4P2 1 MiB x
+ * 1024 encode with the rows as two hipMalloc allocations 0.91 of the padded
+ * rate, EC_8P2 x 512 with the unpadded pitch 0.96).  The library's own
+ * staging pads its parity rows this way; callers choose their own layout. */
+#define ECG_PARITY_ROW_PAD	4096
+
 /* Flags for ecg_matmul */
 #define ECG_F_ACCUMULATE	0x1u	/* dst ^= product (else dst = product) */
 

@@ -114,14 +114,15 @@ def test_bench_gpus_n_spawns_ranks():
     assert weak["scaling"] == "weak" and sorted(r["stripes"] for r in weak["ranks"]) == [1024, 1024]
     stream = d["detail"]["config4_EC_8P2_1MiB_rebuild_stream"]
     assert stream["scaling"] == "weak" and sorted(r["rank"] for r in stream["ranks"]) == [0, 1]
-    # its denominator: each rank's pinned copy rate with both ranks copying at once, and the
-    # node ceiling = their sum (solo denominators gave fractions > 1 at N = 8)
+    # its denominator: the node's pinned copy rate with both ranks copying at once (N x bytes over the
+    # slowest rank's time), a rank's fair share of it, and each rank's own concurrent rate beside
+    # (solo denominators gave fractions > 1 at N = 8)
+    node = stream["node_concurrent_copy_ceiling"]
+    assert node["h2d_GBps"] > 0 and node["d2h_GBps"] > 0
     for r in stream["ranks"]:
         assert set(r["concurrent_pinned_GBps"]) == {"h2d", "d2h"} and r["concurrent_pinned_GBps"]["h2d"] > 0
-        assert abs(r["frac_of_h2d"] / (r["h2d_GBps"] / r["concurrent_pinned_GBps"]["h2d"]) - 1) < 1e-3
-    node = stream["node_concurrent_copy_ceiling"]
-    assert abs(node["h2d_GBps"] - sum(r["concurrent_pinned_GBps"]["h2d"] for r in stream["ranks"])) < 0.02
-
+        assert abs(r["fair_share_h2d_GBps"] - node["h2d_GBps"] / 2) < 0.02
+        assert abs(r["frac_of_h2d"] / (r["h2d_GBps"] / r["fair_share_h2d_GBps"]) - 1) < 1e-3
 
 def test_strong_split_ranges():
     """configs[3]'s 8192 stripes cut into contiguous ranges that cover the

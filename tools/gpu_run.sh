@@ -154,6 +154,9 @@ for what in "$@"; do
 			done
 		done
 		;;
+	layoutab)         # parity-row placement x block order (tools/layout_ab.py)
+		step layout_ab 600 python tools/layout_ab.py || exit $?
+		;;
 	qhost)            # host-cell one-stripe callers from T threads: drop-in (CPU path) / queue / oracle GFNI
 		make -s -C tests/c queue_bench > /dev/null || exit 2
 		for C in 32768 131072 1048576; do
