@@ -154,6 +154,9 @@ for what in "$@"; do
 			done
 		done
 		;;
+	hsoverlap)        # configs[4]: serial vs overlapped host batches (tools/hoststream_overlap.py)
+		step hoststream_overlap 300 python tools/hoststream_overlap.py || exit $?
+		;;
 	layoutab)         # parity-row placement x block order (tools/layout_ab.py)
 		step layout_ab 600 python tools/layout_ab.py || exit $?
 		;;
