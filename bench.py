@@ -1169,18 +1169,31 @@ def solo_copy_rates(world, rank, ctx, nbytes):
 
 
 def leg_stream(args, ctx, world, rank, steps, numa_info):
-    """configs[4] per rank from node-local pinned buffers.  Its denominator at
-    N > 1 is the pinned copy rate each rank reaches while all ranks copy at
-    once (`concurrent_pinned_GBps`, the same pinned buffers the leg streams
-    from); the solo rate (ranks in turn) is reported beside it, and the node's
-    host-memory / PCIe ceiling is the concurrent rates summed over ranks."""
+    """configs[4] per rank from node-local pinned buffers.  Its denominator is
+    the rank's fair share of the node's concurrent pinned copy rate (every
+    rank copying its leg buffer at once: N x bytes over the slowest rank's
+    time, `node_concurrent_copy_ceiling`); each rank's own concurrent rate and
+    its solo rate (ranks in turn) are reported beside it."""
     import numpy as np
 
     k, p, C, S = 8, 2, 1 << 20, 64
+    saved = None
     if args.rehearse:
         wl = None
         step, sync = (lambda timed: time.sleep(2e-4)), (lambda: None)
     else:
+        if not (numa_info or {}).get("pinned_cpus"):
+            # N = 1 (or pinning off): the process was not pinned at start, so run the leg's
+            # thread on its GPU's node while it allocates and first-touches the pinned stripes
+            # and streams them -- "NUMA-local" must hold at every N, not only N > 1
+            from daos_amd import ecg, numa
+
+            node = ecg.lib().ecg_device_numa_node(ecg.lib().ecg_ctx_device(ctx.h))
+            cpus = numa.node_cpus(node) & set(os.sched_getaffinity(0)) if node >= 0 else set()
+            if cpus and os.environ.get("ECG_NUMA") != "0":
+                saved = os.sched_getaffinity(0)
+                os.sched_setaffinity(0, cpus)
+                numa_info = dict(numa_info or {}, numa_node=node, pinned_cpus=len(cpus), pinned_for="leg")
         wl = HostWorkload(ctx, k, p, C, S, chunk=args.host_chunk)
         step, sync = wl.step, ctx.sync
     # 8 warm-up steps: the first batches of a process's host pipeline ran 42 instead of 50 GiB/s
@@ -1206,6 +1219,8 @@ def leg_stream(args, ctx, world, rank, steps, numa_info):
         row.update({"d2h_GBps": round(wl.d2h_bytes_per_step() * steps / mine / 1e9, 2),
                     "verified": all(wl.verify().values())})
         wl.free()
+    if saved is not None:
+        os.sched_setaffinity(0, saved)
     rows = gather(world, row)
     node = {"h2d_GBps": conc["node_h2d"], "d2h_GBps": conc["node_d2h"],
             "what": "N x the pinned copy bytes of one rank over the slowest rank's time, every rank copying at "

@@ -35,7 +35,8 @@
 #define DROPIN_CROSSOVER_DEFAULT UINT64_MAX
 
 static pthread_once_t g_once = PTHREAD_ONCE_INIT;
-static int g_gpu;		/* a gfx950 device is visible and usable */
+static int g_gpu;		/* a gfx950 device is visible */
+static int g_force_cpu;		/* ECG_FORCE_CPU=1: host cells never take the GPU */
 static uint64_t g_crossover = DROPIN_CROSSOVER_DEFAULT;
 
 static pthread_once_t g_ctx_once = PTHREAD_ONCE_INIT;
@@ -54,7 +55,8 @@ static void once_init(void)
 
 	if (x && *x)
 		g_crossover = strtoull(x, NULL, 0);
-	g_gpu = !(force && force[0] == '1') && ecg_device_count() > 0;
+	g_force_cpu = force && force[0] == '1';
+	g_gpu = ecg_device_count() > 0;
 }
 
 static void ctx_init(void)
@@ -138,7 +140,7 @@ static ecg_ctx_t *device_ctx(const char *fn, int dev)
 
 ecg_ctx_t *ecg_dropin_ctx(void)
 {
-	return ecg_dropin_gpu() ? thread_ctx() : NULL;
+	return ecg_dropin_gpu() && !g_force_cpu ? thread_ctx() : NULL;
 }
 
 int ecg_dropin_product(const char *fn, ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
@@ -159,7 +161,7 @@ int ecg_dropin_product(const char *fn, ecg_ctx_t *ctx, int len, int k, int rows,
 			return g_ctx_rc ? g_ctx_rc : -ECG_DER_INVAL;
 		return ecg_matmul_host_mem(ctx, len, k, rows, coef, src, dst, flags, dev);
 	}
-	if ((uint64_t)len * (uint64_t)(k + rows) < ecg_dropin_crossover())
+	if (g_force_cpu || (uint64_t)len * (uint64_t)(k + rows) < ecg_dropin_crossover())
 		return ecg_cpu_matmul(len, k, rows, coef, src, dst, flags);
 	if (ctx == NULL)
 		ctx = thread_ctx();

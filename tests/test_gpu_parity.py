@@ -377,6 +377,45 @@ def test_dropin_routes_by_placement_and_size(ecglib, oracle, ctx):
         ecglib.set_dropin_crossover(old)
 
 
+def test_force_cpu_keeps_device_cells_on_gpu():
+    """ECG_FORCE_CPU=1 sends host cells to the CPU path even above the
+    crossover, but device cells -- which no CPU can read -- still run the HIP
+    kernel."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = r"""
+import ctypes as C, sys, numpy as np
+sys.path.insert(0, %r)
+from daos_amd import ecg
+from oracle import ref
+ecg.set_dropin_crossover(0)
+k, p, n = 4, 2, 8192
+en = ref.cauchy1(k, p)
+tb = ecg.isal_init_tables(en[k:])
+d = np.random.default_rng(3).integers(0, 256, (k, n), dtype=np.uint8)
+o = [np.zeros(n, np.uint8) for _ in range(p)]
+ecg.isal_encode_data(tb, k, p, list(d), o)
+host = ecg.last_kernel()
+assert np.array_equal(np.stack(o), ref.encode_data(en[k:], d))
+ctx = ecg.Context(0)
+buf = ctx.to_device(np.concatenate([d, np.zeros((p, n), np.uint8)]))
+dp = (ecg.u8p * k)(*[C.cast(C.c_void_p(buf.ptr + j * n), ecg.u8p) for j in range(k)])
+cp = (ecg.u8p * p)(*[C.cast(C.c_void_p(buf.ptr + (k + r) * n), ecg.u8p) for r in range(p)])
+ecg.lib().ec_encode_data(n, k, p, tb.ctypes.data_as(ecg.u8p), dp, cp)
+dev = ecg.last_kernel()
+assert np.array_equal(buf.download().reshape(k + p, n)[k:], np.stack(o))
+buf.free(); ctx.close()
+print(host, dev)
+""" % root
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, ECG_FORCE_CPU="1"),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    host, dev = r.stdout.split()
+    assert host.startswith("cpu:") and dev.startswith("ecg_mm_kernel<4,2"), (host, dev)
+
+
 def test_isal_device_cells_16_threads(ecglib, oracle, ctx):
     """16 threads at once calling ec_encode_data on device cells at odd
     offsets (the engine's xstreams, ref:src/engine/ult.c:394-470): calls
