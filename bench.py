@@ -1066,11 +1066,15 @@ def split_range(total, world, rank):
     return rank * base + min(rank, extra), n
 
 
-def timed_leg(world, steps, warm, step, sync):
-    """warm untimed steps, then `steps` timed from a common barrier; returns
-    (this rank's seconds, the max over ranks)."""
-    for _ in range(warm):
+def timed_leg(world, steps, warm, step, sync, warm_s=0.0):
+    """warm untimed steps (and at least warm_s seconds of them), then `steps`
+    timed from a common barrier; returns (this rank's seconds, the max over
+    ranks)."""
+    t0 = time.perf_counter()
+    n = 0
+    while n < warm or time.perf_counter() - t0 < warm_s:
         step(False)
+        n += 1
     sync()
     barrier(world)
     t0 = time.perf_counter()
@@ -1196,9 +1200,12 @@ def leg_stream(args, ctx, world, rank, steps, numa_info):
                 numa_info = dict(numa_info or {}, numa_node=node, pinned_cpus=len(cpus), pinned_for="leg")
         wl = HostWorkload(ctx, k, p, C, S, chunk=args.host_chunk)
         step, sync = wl.step, ctx.sync
-    # 8 warm-up steps: the first batches of a process's host pipeline ran 42 instead of 50 GiB/s
-    # after 2 warm-up steps, steady from 4 on (tools/hoststream_probe.py, profiles/r04/hoststream_probe/)
-    mine, tmax = timed_leg(world, steps, 0 if args.rehearse else 8, step, sync)
+    # >= 8 warm-up steps and >= 1 s of them: the first batches of a process's host pipeline ran 42
+    # instead of 50 GiB/s after 2 warm-up steps (tools/hoststream_probe.py, profiles/r04/hoststream_probe/),
+    # and right after the configs[3] legs' HBM-bound launches the first ~0.3 s of host streaming
+    # ran 44-45 instead of 50.8 GiB/s whatever the context (tools/leg_probe.py, profiles/r05/leg_probe/)
+    mine, tmax = timed_leg(world, steps, 0 if args.rehearse else 8, step, sync,
+                           0.0 if args.rehearse else 1.0)
     row = {"rank": rank, "ms_per_step": round(mine / steps * 1e3, 4),
            "numa_node": (numa_info or {}).get("numa_node"), "pinned_cpus": (numa_info or {}).get("pinned_cpus")}
     user = 2 * k * C * S

@@ -160,8 +160,6 @@ for what in "$@"; do
 		;;
 	legprobe)         # configs[4] leg in phases (tools/leg_probe.py)
 		step leg_probe 300 python tools/leg_probe.py || exit $?
-		LP_TORCH=1 step leg_probe_torch 300 python tools/leg_probe.py || exit $?
-		step bench_short 600 python bench.py --steps 5 --warmup 2 --no-cpu || exit $?
 		;;
 	layoutab)         # parity-row placement x block order (tools/layout_ab.py)
 		step layout_ab 600 python tools/layout_ab.py || exit $?
