@@ -85,7 +85,12 @@ int ecg_obj_ec_class_kp(uint32_t oc_id, int *k, int *p);
 /* Encode one contiguous stripe buffer[k*cell_bytes] into p_bufs[p].  As in
  * the reference, leading NULL entries of p_bufs are allocated here
  * (cell_bytes each, caller frees with free()).  0 / -ECG_DER_NOMEM /
- * -ECG_DER_INVAL (not an EC class).  Runs on the GPU (synchronous). */
+ * -ECG_DER_INVAL (not an EC class).  Synchronous; placed like an ISA-L
+ * drop-in call (ecg.h ecg_set_dropin_crossover: host cells on the CPU path
+ * below the crossover or without a usable device, else the GPU; device cells
+ * on their GPU).  The same holds for ecg_agg_update_parity,
+ * ecg_agg_recalc_parity and ecg_obj_ec_singv_encode below, whose ctx (may be
+ * NULL) only picks the GPU when the GPU is used. */
 int ecg_obj_ec_encode_buf(uint32_t oc_id, uint64_t cell_bytes, unsigned char *buffer,
 			  unsigned char *p_bufs[]);
 
@@ -102,12 +107,15 @@ int ecg_obj_ec_recov_codec_init(uint32_t oc_id, const uint32_t *err_list, uint32
 
 /* Regenerate the erased cells of `nstripes` host stripes laid out
  * [nstripes][k+p][cell_sz] (the recovery buffer of ref:src/object/cli_ec.c:
- * 2449-2464), in place, on device ctx (NULL = process default device). */
+ * 2449-2464), in place, through device ctx's staging pipeline (NULL = the
+ * calling thread's default device; in a process without a usable device, or
+ * with ECG_FORCE_CPU=1, the product CPU path, stripe by stripe). */
 int ecg_obj_ec_recov_data(ecg_ctx_t *ctx, const struct ecg_obj_ec_recov_codec *recov,
 			  uint64_t cell_sz, unsigned char *buf_stripes, uint32_t nstripes);
 
 /* Full-stripe encode of host stripes: data [S][k][C] (user sgl order),
- * parity [p][S][C] (oer_pbufs layout, ref:src/object/cli_ec.c:75-97). */
+ * parity [p][S][C] (oer_pbufs layout, ref:src/object/cli_ec.c:75-97); ctx as
+ * for ecg_obj_ec_recov_data (NULL without a device: the CPU path). */
 int ecg_obj_ec_encode_stripes(ecg_ctx_t *ctx, uint32_t oc_id, uint64_t cell_bytes,
 			      uint32_t nstripes, const unsigned char *data,
 			      unsigned char *parity);
