@@ -59,8 +59,9 @@ typedef struct ecg_ctx ecg_ctx_t;
 /* Number of usable (gfx950) HIP devices; 0 when none.  Never fails. */
 int ecg_device_count(void);
 /* Binds a context to `device` (index into the visible HIP devices).
- * -ECG_DER_NOSYS when the device is absent or not gfx950: there is no CPU
- * fallback in the product path. */
+ * -ECG_DER_NOSYS when the device is absent or not gfx950: the batched device
+ * API has no CPU fallback (the drop-in surfaces route host cells to the CPU
+ * path themselves, ecg_set_dropin_crossover). */
 int ecg_ctx_create(int device, ecg_ctx_t **ctx);
 void ecg_ctx_destroy(ecg_ctx_t *ctx);
 int ecg_ctx_device(const ecg_ctx_t *ctx);

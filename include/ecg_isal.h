@@ -25,12 +25,21 @@
  * (it only allocates k*p*32 bytes and memcpy's them, ref:src/object/cli_ec.c:
  * 2205-2210).  ec_encode_data recovers each coefficient as byte 1 (= c*1).
  *
- * Data-plane calls (ec_encode_data, ec_encode_data_update, xor_gen) run on
- * the GPU: a process-wide context on device $ECG_DEVICE (default 0), with
- * per-thread pinned staging for host cells; cells in device memory (every
- * pointer of the call hipMalloc'd -- an engine whose buffers live in HBM)
- * are used in place, no staging.  There is no CPU fallback: if no gfx950 device
- * is usable these `void` functions print the reason and abort().
+ * Data-plane calls (ec_encode_data, ec_encode_data_update, xor_gen) run
+ * where their cells are (ecg.h ecg_set_dropin_crossover):
+ *   - cells in device memory (every pointer of the call inside a hipMalloc'd
+ *     allocation -- an engine whose buffers live in HBM): the gfx950 kernels
+ *     in place, on the cells' device (listed in $ECG_DEVICES), synchronous;
+ *   - host cells: the product CPU path (GFNI / AVX2 / scalar by cpuid) below
+ *     the measured crossover (by default: always -- one core beats a staged
+ *     PCIe round trip at every size measured), in any process without a usable
+ *     gfx950 device (a libdaos client node), and with $ECG_FORCE_CPU=1; above
+ *     the crossover, the GPU through per-thread pinned staging ($ECG_DEVICES /
+ *     $ECG_DEVICE pick the devices), with the CPU as fallback.
+ * Like ISA-L's, these calls succeed on any CPU.  A call on device cells that
+ * cannot run (device not listed, a cell past its allocation, a HIP failure)
+ * prints the cause and aborts: the ABI is `void`, and skipping the parity
+ * silently would corrupt stored objects.
  */
 #ifndef ECG_ISAL_H
 #define ECG_ISAL_H
