@@ -135,27 +135,43 @@ struct pass {
 	unsigned char *const *dst;
 };
 
-/* Bytes [i0, len) through the field's product table, one source at a time
- * (the scalar variant, and the AVX2 variants' tails).  Sources and outputs
- * are distinct cells, as in ISA-L. */
+/* Bytes [i0, len) through the field's product table (the scalar variant,
+ * and the AVX2 variants' tails): eight bytes of every source at a time,
+ * their eight lookups packed into one 64-bit word per row, so a row's bytes
+ * are loaded and stored once per word.  Sources and outputs are distinct
+ * cells, as in ISA-L. */
 static void tail_bytes(const struct pass *q, size_t i0)
 {
+	const size_t len = q->len;
 	int r, j;
 
-	if (i0 >= q->len)
-		return;
 	for (r = 0; r < q->nr; r++) {
 		unsigned char *d = q->dst[r];
-		size_t i;
+		size_t i = i0;
 
-		if (!q->acc)
-			memset(d + i0, 0, q->len - i0);
-		for (j = 0; j < q->ns; j++) {
-			const unsigned char *tb = ecg_gf_mul_tbl[q->cf[r * q->ns + j]];
-			const unsigned char *sj = q->src[j];
+		for (; i + 8 <= len; i += 8) {
+			uint64_t a = 0;
 
-			for (i = i0; i < q->len; i++)
-				d[i] ^= tb[sj[i]];
+			if (q->acc)
+				memcpy(&a, d + i, 8);
+			for (j = 0; j < q->ns; j++) {
+				const unsigned char *tb = ecg_gf_mul_tbl[q->cf[r * q->ns + j]];
+				uint64_t x;
+
+				memcpy(&x, q->src[j] + i, 8);
+				a ^= (uint64_t)tb[x & 0xff] | (uint64_t)tb[(x >> 8) & 0xff] << 8 |
+				     (uint64_t)tb[(x >> 16) & 0xff] << 16 | (uint64_t)tb[(x >> 24) & 0xff] << 24 |
+				     (uint64_t)tb[(x >> 32) & 0xff] << 32 | (uint64_t)tb[(x >> 40) & 0xff] << 40 |
+				     (uint64_t)tb[(x >> 48) & 0xff] << 48 | (uint64_t)tb[x >> 56] << 56;
+			}
+			memcpy(d + i, &a, 8);
+		}
+		for (; i < len; i++) {
+			unsigned char v = q->acc ? d[i] : 0;
+
+			for (j = 0; j < q->ns; j++)
+				v ^= ecg_gf_mul_tbl[q->cf[r * q->ns + j]][q->src[j][i]];
+			d[i] = v;
 		}
 	}
 }
