@@ -235,3 +235,85 @@ def test_random_pointer_tables(ctx, oracle, ecglib):
         seen[got] = seen.get(got, 0) + 1
     print("kernels:", seen)
     assert {"g1", "g4", "g16"} <= set(seen), seen
+
+
+@pytest.mark.gpu
+def test_random_dropin_calls(ctx, oracle, ecglib):
+    """Seeded random ISA-L-convention calls through the drop-in's router
+    (ecg_dropin.c): ec_encode_data / ec_encode_data_update / xor_gen with k up
+    to 70 sources and up to 10 output rows, lengths from 1 byte to 70 KiB,
+    cells at random byte offsets -- on host cells at a random crossover (so the
+    CPU path and the GPU staging both run) and on device cells (the HIP
+    kernels in place).  Every output equals the oracle's; the route taken is
+    the one the placement and the crossover name."""
+    import ctypes as C
+
+    L = ecglib.lib()
+    rng = np.random.default_rng(0xD80)
+    old = ecglib.dropin_crossover()
+    routes = set()
+    try:
+        for case in range(96):
+            op = ("encode", "update", "xor")[case % 3]
+            k = int(rng.choice([1, 2, 3, 4, 8, 16, 17, 33, 64, 70])) if op != "update" else 1
+            if op == "encode":
+                k = min(k, 64)
+            rows = 1 if op == "xor" else int(rng.integers(1, 11))
+            n = int(rng.choice([1, 15, 64, 100, 4096, 4097, 33333, 70000]))
+            device = bool(rng.integers(0, 2))
+            cross = [0, n * (k + rows), (1 << 64) - 1][int(rng.integers(0, 3))]
+            ecglib.set_dropin_crossover(cross)
+            coef = rng.integers(0, 256, (rows, k), dtype=np.uint8) if op != "xor" else np.ones((1, k), np.uint8)
+            src = rng.integers(0, 256, (k, n), dtype=np.uint8)
+            dst0 = rng.integers(0, 256, (rows, n), dtype=np.uint8)
+            want = oracle.encode_data(coef, src)
+            if op == "update":
+                want = want ^ dst0
+            soff = [int(rng.integers(0, 16)) + j * (n + 32) for j in range(k)]
+            doff = [int(rng.integers(0, 16)) + r * (n + 32) for r in range(rows)]
+            if device:
+                sb, db = ctx.alloc(k * (n + 32)), ctx.alloc(rows * (n + 32))
+                for j in range(k):
+                    sb.upload(src[j], offset=soff[j])
+                for r in range(rows):
+                    db.upload(dst0[r], offset=doff[r])
+                sp = [sb.ptr + o for o in soff]
+                dp = [db.ptr + o for o in doff]
+            else:
+                hs = np.zeros(k * (n + 32), np.uint8)
+                hd = np.zeros(rows * (n + 32), np.uint8)
+                for j in range(k):
+                    hs[soff[j]: soff[j] + n] = src[j]
+                for r in range(rows):
+                    hd[doff[r]: doff[r] + n] = dst0[r]
+                sp = [hs.ctypes.data + o for o in soff]
+                dp = [hd.ctypes.data + o for o in doff]
+            if op == "xor":
+                v = (C.c_void_p * (k + 1))(*(sp + dp))
+                assert L.xor_gen(k + 1, n, v) == (0 if k >= 2 else 1)
+                if k < 2:
+                    want = dst0
+            else:
+                tb = ecglib.isal_init_tables(coef)
+                spp = (ecglib.u8p * k)(*[C.cast(C.c_void_p(x), ecglib.u8p) for x in sp])
+                dpp = (ecglib.u8p * rows)(*[C.cast(C.c_void_p(x), ecglib.u8p) for x in dp])
+                if op == "encode":
+                    L.ec_encode_data(n, k, rows, tb.ctypes.data_as(ecglib.u8p), spp, dpp)
+                else:
+                    L.ec_encode_data_update(n, k, rows, 0, tb.ctypes.data_as(ecglib.u8p), spp[0], dpp)
+            if op != "xor" or k >= 2:
+                kern = ecglib.last_kernel()
+                gpu = device or n * (k + rows) >= cross
+                assert kern.startswith("ecg_mm") if gpu else kern.startswith("cpu:"), (case, op, device, cross, kern)
+                routes.add((device, gpu))
+            if device:
+                raw = db.download()
+                got = np.stack([raw[o: o + n] for o in doff])
+                sb.free()
+                db.free()
+            else:
+                got = np.stack([hd[o: o + n] for o in doff])
+            assert np.array_equal(got, want), (case, op, k, rows, n, device, cross)
+    finally:
+        ecglib.set_dropin_crossover(old)
+    assert routes >= {(True, True), (False, True), (False, False)}, routes
