@@ -99,3 +99,28 @@ def test_force_cpu_env():
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert r.stdout.strip().startswith("cpu:")
+
+
+def test_cpu_random_shapes(ecglib, oracle, isa):
+    """Seeded random calls of every variant: k 1..80, rows 1..12, lengths
+    1 byte..20 KiB, every cell at its own byte offset, overwrite or
+    accumulate -- bytes equal to the scalar oracle's."""
+    rng = np.random.default_rng(0xC9)
+    for name in ISAS:
+        if ecglib.cpu_set_isa(name) != 0:
+            continue
+        for _ in range(40):
+            k, rows = int(rng.integers(1, 81)), int(rng.integers(1, 13))
+            n = int(rng.choice([1, 2, 7, 31, 32, 33, 63, 64, 65, 200, 4096, 20000 + int(rng.integers(0, 64))]))
+            coef = rng.integers(0, 256, (rows, k), dtype=np.uint8)
+            buf = rng.integers(0, 256, (k + rows) * (n + 64), dtype=np.uint8)
+            offs = [i * (n + 64) + int(rng.integers(0, 64)) for i in range(k + rows)]
+            src = [buf[o: o + n] for o in offs[:k]]
+            dst = [buf[o: o + n] for o in offs[k:]]
+            acc = bool(rng.integers(0, 2))
+            before = np.stack([d.copy() for d in dst])
+            ecglib.cpu_matmul(coef, src, dst, ecglib.F_ACCUMULATE if acc else 0)
+            want = oracle.encode_data(coef, np.stack(src))
+            if acc:
+                want = want ^ before
+            assert np.array_equal(np.stack(dst), want), (name, k, rows, n, acc)

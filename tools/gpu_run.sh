@@ -161,6 +161,9 @@ for what in "$@"; do
 	legprobe)         # configs[4] leg in phases (tools/leg_probe.py)
 		step leg_probe 300 python tools/leg_probe.py || exit $?
 		;;
+	dsoak)            # concurrent drop-in soak vs the oracle (tools/dropin_soak.py)
+		step dropin_soak 600 python tools/dropin_soak.py || exit $?
+		;;
 	layoutab)         # parity-row placement x block order (tools/layout_ab.py)
 		step layout_ab 600 python tools/layout_ab.py || exit $?
 		;;
