@@ -77,7 +77,7 @@ def worker(ctx, tid, calls, out):
     out[tid] = (bad, routes)
 
 
-def phase(ctx, crossover, threads=16, calls=150):
+def phase(ctx, crossover, threads=16, calls=1000):
     if crossover is not None:
         ecg.set_dropin_crossover(crossover)
     out = {}
