@@ -255,6 +255,34 @@ static int pool_stream(ecg_ctx_t *ctx, hipStream_t *out)
 	return 0;
 }
 
+/* One-stripe product of any k (<= ECG_MAX_K + 256) and rows (<= 256) as
+ * launches of at most ECG_MAX_K sources (later source groups accumulate) and
+ * 8 rows, so the sliced coefficients stay a 512-byte stack array (a caller
+ * may be a user-level thread with a small stack). */
+static int launch_split(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef, const void *sbase,
+			const int64_t *soff, void *dbase, const int64_t *doff, unsigned flags, hipStream_t st)
+{
+	unsigned char cc[ECG_MAX_K * 8];
+	int j0, r0, r, rc = 0;
+
+	if (k <= ECG_MAX_K)
+		return ecg_matmul(ctx, k, rows, coef, (uint64_t)len, 1, sbase, soff, 0, dbase, doff, 0, flags, st);
+	for (j0 = 0; rc == 0 && j0 < k; j0 += ECG_MAX_K) {
+		const int kk = k - j0 < ECG_MAX_K ? k - j0 : ECG_MAX_K;
+		const unsigned f = flags | (j0 ? ECG_F_ACCUMULATE : 0u);
+
+		for (r0 = 0; rc == 0 && r0 < rows; r0 += 8) {
+			const int rr = rows - r0 < 8 ? rows - r0 : 8;
+
+			for (r = 0; r < rr; r++)
+				memcpy(&cc[r * kk], &coef[(size_t)(r0 + r) * k + j0], (size_t)kk);
+			rc = ecg_matmul(ctx, kk, rr, cc, (uint64_t)len, 1, sbase, soff + j0, 0, dbase, doff + r0, 0,
+					f, st);
+		}
+	}
+	return rc;
+}
+
 /* The ISA-L data-plane calls with DEVICE cells (an engine whose bio buffers
  * live in HBM keeps its ec_encode_data call sites): strided launches on the
  * cells in place (cell offsets relative to the first source / output; more
@@ -267,11 +295,10 @@ static int matmul_device(ecg_ctx_t *ctx, int len, int k, int rows, const unsigne
 			 unsigned char *const *src, unsigned char *const *dst, unsigned flags)
 {
 	int64_t soff[ECG_MAX_K + 256], doff[256];
-	unsigned char cc[ECG_MAX_K * 8];
 	struct tstage *t = NULL;
 	hipStream_t st = NULL;
 	hipError_t e;
-	int j0, j, r, rc;
+	int j, r, rc;
 
 	rc = cells_on_device(ctx, src, k, len, "source");
 	if (rc == 0)
@@ -299,22 +326,7 @@ static int matmul_device(ecg_ctx_t *ctx, int len, int k, int rows, const unsigne
 	}
 	if (e != hipSuccess)
 		return ecg_hip_fail(e, "matmul_host: order behind the context stream");
-	for (j0 = 0; rc == 0 && j0 < k; j0 += ECG_MAX_K) {
-		const int kk = k - j0 < ECG_MAX_K ? k - j0 : ECG_MAX_K;
-		const unsigned f = flags | (j0 ? ECG_F_ACCUMULATE : 0u);
-		int r0;
-
-		/* coefficient slices of at most 8 rows (cc's size); the kernel
-		 * splits rows the same way */
-		for (r0 = 0; rc == 0 && r0 < rows; r0 += 8) {
-			const int rr = rows - r0 < 8 ? rows - r0 : 8;
-
-			for (r = 0; r < rr; r++)
-				memcpy(&cc[r * kk], &coef[(size_t)(r0 + r) * k + j0], (size_t)kk);
-			rc = ecg_matmul(ctx, kk, rr, cc, (uint64_t)len, 1, src[0], soff + j0, 0, dst[0],
-					doff + r0, 0, f, st);
-		}
-	}
+	rc = launch_split(ctx, len, k, rows, coef, src[0], soff, dst[0], doff, flags, st);
 	if (rc)
 		return rc;
 	e = hipEventRecord(t->ev, st);
@@ -386,24 +398,7 @@ int ecg_matmul_host_mem(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned
 		if (e != hipSuccess)
 			return ecg_hip_fail(e, "matmul_host H2D");
 	}
-	if (k <= ECG_MAX_K) {
-		rc = ecg_matmul(ctx, k, rows, coef, (uint64_t)len, 1, d, soff, 0, d, doff, 0,
-				flags, t->st);
-	} else {
-		/* xor_gen may pass more sources than ECG_MAX_K: chain launches */
-		int j0;
-
-		rc = 0;
-		for (j0 = 0; rc == 0 && j0 < k; j0 += ECG_MAX_K) {
-			int kk = k - j0 < ECG_MAX_K ? k - j0 : ECG_MAX_K;
-			unsigned char cc[ECG_MAX_K * 256];
-
-			for (r = 0; r < rows; r++)
-				memcpy(&cc[r * kk], &coef[r * k + j0], kk);
-			rc = ecg_matmul(ctx, kk, rows, cc, (uint64_t)len, 1, d, soff + j0, 0, d,
-					doff, 0, (j0 ? ECG_F_ACCUMULATE : 0) | flags, t->st);
-		}
-	}
+	rc = launch_split(ctx, len, k, rows, coef, d, soff, d, doff, flags, t->st);
 	if (rc)
 		return rc;
 	e = hipSuccess;
