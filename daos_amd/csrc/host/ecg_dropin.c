@@ -25,6 +25,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "ecg_internal.h"
 
@@ -138,6 +139,61 @@ static ecg_ctx_t *device_ctx(const char *fn, int dev)
 	return NULL;
 }
 
+/*
+ * Where does a call's src[0] live?  The HIP runtime's pointer queries take a
+ * process-wide lock: 0.08 us alone, 7.4 us per query with 16 threads asking
+ * at once (tools/hipcall_cost.hip, profiles/r05/dropin/), which capped 16
+ * threads of 32 KiB host-cell calls at 212 GiB/s against 1417 GiB/s with no
+ * query at all (tools/dropin_threads.c).  So each thread remembers, for
+ * HOSTC_TTL_NS, the 2 MiB regions in which it found memory the runtime does
+ * not know at all (plain malloc / mmap -- DAOS's sgl and bio buffers).  Such
+ * a region cannot hold a device allocation: ROCm carves those out of GPU
+ * apertures it reserves at initialisation, apart from ordinary mappings; the
+ * expiry is a second guard.  Runtime-known host memory (pinned, registered,
+ * managed -- which may share an aperture with device allocations) and device
+ * answers are never cached.  ECG_DROPIN_HOSTCACHE=0 queries every call.
+ */
+#define HOSTC_N 8
+#define HOSTC_TTL_NS 10000000ull	/* 10 ms */
+static __thread struct {
+	uintptr_t region;	/* (address >> 21) + 1; 0 = empty */
+	uint64_t until;
+} t_hostc[HOSTC_N];
+static int g_hostc = -1;
+
+static uint64_t coarse_ns(void)
+{
+	struct timespec t;
+
+	clock_gettime(CLOCK_MONOTONIC_COARSE, &t);
+	return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
+
+static int cell_device(const void *p)
+{
+	const uintptr_t region = ((uintptr_t)p >> 21) + 1;
+	const unsigned slot = (unsigned)(region * 0x9E3779B1u) >> 29;	/* top 3 bits: 0..7 */
+	uint64_t now;
+	int dev;
+
+	if (__atomic_load_n(&g_hostc, __ATOMIC_RELAXED) < 0) {
+		const char *env = getenv("ECG_DROPIN_HOSTCACHE");
+
+		__atomic_store_n(&g_hostc, !(env && env[0] == '0'), __ATOMIC_RELAXED);
+	}
+	if (!g_hostc)
+		return ecg_ptr_device(p);
+	now = coarse_ns();
+	if (t_hostc[slot].region == region && now < t_hostc[slot].until)
+		return ECG_PTR_UNKNOWN;
+	dev = ecg_ptr_device(p);
+	if (dev == ECG_PTR_UNKNOWN) {
+		t_hostc[slot].region = region;
+		t_hostc[slot].until = now + HOSTC_TTL_NS;
+	}
+	return dev;
+}
+
 ecg_ctx_t *ecg_dropin_ctx(void)
 {
 	return ecg_dropin_gpu() && !g_force_cpu ? thread_ctx() : NULL;
@@ -152,7 +208,7 @@ int ecg_dropin_product(const char *fn, ecg_ctx_t *ctx, int len, int k, int rows,
 		return ecg_cpu_matmul(len, k, rows, coef, src, dst, flags);
 	if (!ecg_dropin_gpu())
 		return ecg_cpu_matmul(len, k, rows, coef, src, dst, flags);
-	dev = ecg_ptr_device(src[0]);
+	dev = cell_device(src[0]);
 	if (dev >= 0) {
 		/* device cells: only the GPU can touch them */
 		if (ctx == NULL || ecg_ctx_device(ctx) != dev)

@@ -166,7 +166,11 @@ struct ecg_tuner;
 int ecg_tune_init(ecg_ctx_t *ctx);
 void ecg_tune_fini(ecg_ctx_t *ctx);
 int ecg_tune_launch(ecg_ctx_t *ctx, const ecg_mm_params_t *p, hipStream_t st, uint32_t *kid);
-/* The device whose memory p is, -1 for host memory (ecg_stage.c). */
+/* The device whose memory p is; < 0 for host memory: ECG_PTR_HOST (known to
+ * the HIP runtime: pinned, registered, managed) or ECG_PTR_UNKNOWN (plain
+ * malloc / mmap) (ecg_stage.c). */
+#define ECG_PTR_HOST (-1)
+#define ECG_PTR_UNKNOWN (-2)
 int ecg_ptr_device(const void *p);
 /* The same for any launcher of the product (the pointer-table kernel): `g`
  * its lane granule, `layout` its layout class (ECG_TUNE_LAYOUT_*), `fn(p,

@@ -166,9 +166,10 @@ static int tstage_get(ecg_ctx_t *ctx, size_t bytes, struct tstage **out)
 	return 0;
 }
 
-/* The device whose memory p is (hipMalloc'd), -1 for host memory.  A query
- * of unregistered host memory may fail: its error is cleared here so a later
- * launch check does not report it. */
+/* The device whose memory p is (hipMalloc'd), ECG_PTR_HOST for host memory
+ * the HIP runtime knows (pinned, registered, managed), ECG_PTR_UNKNOWN for
+ * memory it does not (plain malloc / mmap: host memory).  The failed query's
+ * error is cleared so a later launch check does not report it. */
 int ecg_ptr_device(const void *p)
 {
 	hipPointerAttribute_t a;
@@ -176,9 +177,9 @@ int ecg_ptr_device(const void *p)
 	memset(&a, 0, sizeof(a));
 	if (hipPointerGetAttributes(&a, p) != hipSuccess) {
 		(void)hipGetLastError();
-		return -1;
+		return ECG_PTR_UNKNOWN;
 	}
-	return a.type == hipMemoryTypeDevice ? a.device : -1;
+	return a.type == hipMemoryTypeDevice ? a.device : ECG_PTR_HOST;
 }
 
 /* Every cell [v[i], v[i] + len) lies inside one allocation of ctx's device:

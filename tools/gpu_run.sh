@@ -161,6 +161,15 @@ for what in "$@"; do
 	legprobe)         # configs[4] leg in phases (tools/leg_probe.py)
 		step leg_probe 300 python tools/leg_probe.py || exit $?
 		;;
+	dthreads)         # host-cell drop-in calls from T threads, with and without a visible GPU
+		make -s -C tests/c dropin_threads > /dev/null || exit 2
+		for T in 1 8 16; do
+			step dthreads_gpu_$T 120 ./build/ctest/dropin_threads 32768 $T || exit $?
+			HIP_VISIBLE_DEVICES= step dthreads_nogpu_$T 120 ./build/ctest/dropin_threads 32768 $T || exit $?
+			step dthreads_tiny_gpu_$T 120 ./build/ctest/dropin_threads 32768 $T 20000 8 tiny || exit $?
+			HIP_VISIBLE_DEVICES= step dthreads_tiny_nogpu_$T 120 ./build/ctest/dropin_threads 32768 $T 20000 8 tiny || exit $?
+		done
+		;;
 	dsoak)            # concurrent drop-in soak vs the oracle (tools/dropin_soak.py)
 		step dropin_soak 600 python tools/dropin_soak.py || exit $?
 		;;

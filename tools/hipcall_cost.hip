@@ -4,9 +4,13 @@
  * attribute and address-range queries, event record / stream wait / event
  * synchronize, stream query and synchronize, an empty-kernel launch.  Sizes
  * the per-call overheads of ecg_stage.c's matmul_device.  Bench
- * infrastructure.  Build: hipcc -O2 --offload-arch=gfx950 -o build/tools/hipcall_cost tools/hipcall_cost.hip
+ * infrastructure; the placement queries are also timed from 1 / 4 / 16
+ * threads at once.  Build: hipcc -O2 --offload-arch=gfx950 -lhsa-runtime64
+ * -o build/tools/hipcall_cost tools/hipcall_cost.hip
  */
 #include <hip/hip_runtime.h>
+#include <hsa/hsa_ext_amd.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <time.h>
@@ -46,6 +50,61 @@ static double now(void)
 		printf("{\"call\": \"%s\", \"us\": %.3f}\n", name, best[2]);     \
 	} while (0)
 
+/* a placement query from T threads at once, each on its own host buffer */
+static int g_which;
+static pthread_barrier_t g_bar;
+
+static void *qthread(void *arg)
+{
+	char *h = (char *)malloc(65536);
+	hipPointerAttribute_t a;
+	hsa_amd_pointer_info_t info;
+	unsigned int mt;
+
+	(void)arg;
+	pthread_barrier_wait(&g_bar);
+	for (int i = 0; i < 20000; i++) {
+		if (g_which == 0) {
+			(void)hipPointerGetAttributes(&a, h + 64);
+			(void)hipGetLastError();
+		} else if (g_which == 1) {
+			(void)hipPointerGetAttribute(&mt, HIP_POINTER_ATTRIBUTE_MEMORY_TYPE, (hipDeviceptr_t)(h + 64));
+			(void)hipGetLastError();
+		} else {
+			info.size = sizeof(info);
+			(void)hsa_amd_pointer_info(h + 64, &info, NULL, NULL, NULL);
+		}
+	}
+	pthread_barrier_wait(&g_bar);
+	free(h);
+	return NULL;
+}
+
+static void threaded(void)
+{
+	static const char *names[] = {"hipPointerGetAttributes", "hipPointerGetAttribute(MEMORY_TYPE)",
+				      "hsa_amd_pointer_info"};
+	for (int w = 0; w < 3; w++)
+		for (int T = 1; T <= 16; T *= 4) {
+			pthread_t th[16];
+			double t0, t1;
+
+			g_which = w;
+			pthread_barrier_init(&g_bar, NULL, T + 1);
+			for (int t = 0; t < T; t++)
+				pthread_create(&th[t], NULL, qthread, NULL);
+			pthread_barrier_wait(&g_bar);
+			t0 = now();
+			pthread_barrier_wait(&g_bar);
+			t1 = now();
+			for (int t = 0; t < T; t++)
+				pthread_join(th[t], NULL);
+			pthread_barrier_destroy(&g_bar);
+			printf("{\"call\": \"%s (host ptr)\", \"threads\": %d, \"us\": %.3f}\n", names[w], T,
+			       (t1 - t0) / 20000 * 1e6);
+		}
+}
+
 int main(void)
 {
 	hipStream_t st, st2;
@@ -78,6 +137,7 @@ int main(void)
 	TIME("launch+poll hipStreamQuery", hipLaunchKernelGGL(nop_kernel, dim3(1), dim3(64), 0, st, (int *)0);
 	     while (hipStreamQuery(st) == hipErrorNotReady););
 	TIME("hipSetDevice", hipSetDevice(0));
+	threaded();
 	hipFree(d);
 	return 0;
 }
