@@ -179,6 +179,8 @@ int ecg_ptr_device(const void *p)
 		(void)hipGetLastError();
 		return ECG_PTR_UNKNOWN;
 	}
+	if (a.type == hipMemoryTypeUnregistered)	/* pageable memory the runtime never saw */
+		return ECG_PTR_UNKNOWN;
 	return a.type == hipMemoryTypeDevice ? a.device : ECG_PTR_HOST;
 }
 
