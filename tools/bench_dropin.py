@@ -1,12 +1,11 @@
-"""Latency of the synchronous ISA-L drop-in's GPU staging path
-(ec_encode_data, one EC_8P2 stripe per call, host buffers, run with
-ECG_DROPIN_CROSSOVER=0 so host cells take the GPU) by cell size.  Run once per
+"""Latency of the synchronous ISA-L drop-in (ec_encode_data, one EC_8P2
+stripe per call, through ctypes with the pointer arrays built once, as
+the C tool does) by cell size.  At the default crossover host cells run the product
+CPU path; with ECG_DROPIN_CROSSOVER=0 they take the GPU staging, once per
 staging mode (env ECG_ZERO_COPY_MAX: 0 = always DMA copies, large = kernel on
-the pinned staging in place); appends one JSON line to
-gpurun_out/bench_dropin.jsonl.  The CPU path and the crossover between the
-two: tools/dropin_bench.c.
-DROPIN_DEVICE=1: the cells live in device memory instead (the drop-in then
-launches on them in place).  Bench infrastructure (no oracle)."""
+the pinned staging in place); DROPIN_DEVICE=1: device cells.  Appends one JSON
+line (with the kernel each size ran) to gpurun_out/bench_dropin.jsonl.  The
+same without ctypes, and the crossover: tools/dropin_bench.c.  Bench infrastructure (no oracle)."""
 import json
 import os
 import sys
@@ -23,7 +22,8 @@ def main():
     tbls = ecg.isal_init_tables(ecg.cauchy1(k, p)[k:])
     rng = np.random.default_rng(5)
     device = os.environ.get("DROPIN_DEVICE") == "1"
-    res = {"zero_copy_max": os.environ.get("ECG_ZERO_COPY_MAX", "default"), "cells": "device" if device else "host"}
+    res = {"zero_copy_max": os.environ.get("ECG_ZERO_COPY_MAX", "default"), "cells": "device" if device else "host",
+           "crossover": os.environ.get("ECG_DROPIN_CROSSOVER", "default")}
     ctx = ecg.Context(0) if device else None
     L = ecg.lib()
     for C in (4096, 16384, 32768, 65536, 131072, 262144, 1 << 20):
@@ -39,9 +39,12 @@ def main():
         else:
             cells = [rng.integers(0, 256, C, dtype=np.uint8) for _ in range(k)]
             coding = [np.zeros(C, dtype=np.uint8) for _ in range(p)]
+            dp = (ecg.u8p * k)(*[c.ctypes.data_as(ecg.u8p) for c in cells])
+            cp = (ecg.u8p * p)(*[c.ctypes.data_as(ecg.u8p) for c in coding])
+            tp = tbls.ctypes.data_as(ecg.u8p)
 
             def call():
-                ecg.isal_encode_data(tbls, k, p, cells, coding)
+                L.ec_encode_data(C, k, p, tp, dp, cp)
         for _ in range(5):
             call()
         it = 200 if C <= 65536 else 40
@@ -50,6 +53,7 @@ def main():
             call()
         us = (time.perf_counter() - t0) / it * 1e6
         res[f"{C >> 10}KiB_us"] = round(us, 1)
+        res[f"{C >> 10}KiB_kernel"] = ecg.last_kernel()
         res[f"{C >> 10}KiB_GiBps"] = round(k * C / (us / 1e6) / (1 << 30), 2)
         if device:
             buf.free()

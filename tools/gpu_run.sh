@@ -128,6 +128,8 @@ for what in "$@"; do
 		step pcie 600 python tools/bench_pcie.py || exit $?
 		;;
 	dropin)
+		step dropin_default 300 python tools/bench_dropin.py || exit $?
+		DROPIN_DEVICE=1 step dropin_device 300 python tools/bench_dropin.py || exit $?
 		for zc in 0 1048576; do
 			ECG_DROPIN_CROSSOVER=0 ECG_ZERO_COPY_MAX=$zc step dropin_$zc 300 python tools/bench_dropin.py || exit $?
 		done
