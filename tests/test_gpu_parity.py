@@ -377,6 +377,54 @@ def test_dropin_routes_by_placement_and_size(ecglib, oracle, ctx):
         ecglib.set_dropin_crossover(old)
 
 
+def test_dropin_routes_after_placement_cache(ecglib, oracle, ctx):
+    """The per-thread placement cache remembers only memory HIP does not know
+    (plain malloc): interleaving calls on cached malloc cells with pinned host
+    cells (ecg_host_alloc) and device cells keeps every call on its own
+    route -- pinned host cells take the CPU path at the default crossover and
+    the staging above a set one, device cells the kernel -- with oracle
+    bytes every time."""
+    L = ecglib.lib()
+    k, p, n = 4, 2, 8192
+    en = oracle.cauchy1(k, p)
+    tbls = ecglib.isal_init_tables(en[k:])
+    tp = tbls.ctypes.data_as(ecglib.u8p)
+    src = np.stack([rand(n, 500 + j) for j in range(k)])
+    want = oracle.encode_data(en[k:], src)
+    plain = [np.ascontiguousarray(s) for s in src]
+    pinned = ctx.host_alloc((k + p) * n)
+    dev = ctx.to_device(np.concatenate([src, np.zeros((p, n), np.uint8)]))
+    old = ecglib.dropin_crossover()
+
+    def ptrs(base):
+        return ((ecglib.u8p * k)(*[C.cast(C.c_void_p(base + j * n), ecglib.u8p) for j in range(k)]),
+                (ecglib.u8p * p)(*[C.cast(C.c_void_p(base + (k + r) * n), ecglib.u8p) for r in range(p)]))
+
+    try:
+        pinned.array[:] = np.concatenate([src, np.zeros((p, n), np.uint8)]).ravel()
+        pd, pc = ptrs(pinned.ptr)
+        vd, vc = ptrs(dev.ptr)
+        for crossover, pinned_route in ((old, "cpu:"), (0, "ecg_mm")):
+            ecglib.set_dropin_crossover(crossover)
+            for rnd in range(3):
+                out = [np.zeros(n, np.uint8) for _ in range(p)]
+                ecglib.isal_encode_data(tbls, k, p, plain, out)
+                route = ecglib.last_kernel()
+                assert route.startswith("cpu:" if crossover else "ecg_mm"), (crossover, route)
+                assert np.array_equal(np.stack(out), want)
+                pinned.array[k * n:] = 0
+                L.ec_encode_data(n, k, p, tp, pd, pc)
+                assert ecglib.last_kernel().startswith(pinned_route), (crossover, ecglib.last_kernel())
+                assert np.array_equal(pinned.array[k * n:].reshape(p, n), want)
+                L.ec_encode_data(n, k, p, tp, vd, vc)
+                assert ecglib.last_kernel().startswith("ecg_mm_kernel<4,2"), ecglib.last_kernel()
+                assert np.array_equal(dev.download().reshape(k + p, n)[k:], want)
+    finally:
+        ecglib.set_dropin_crossover(old)
+        dev.free()
+        pinned.free()
+
+
 def test_force_cpu_keeps_device_cells_on_gpu():
     """ECG_FORCE_CPU=1 sends host cells to the CPU path even above the
     crossover, but device cells -- which no CPU can read -- still run the HIP
