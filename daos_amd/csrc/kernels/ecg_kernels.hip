@@ -284,6 +284,10 @@ static const kentry g_kernels[] = {
 	KE(4, 1, 1, 1), KE(4, 2, 1, 1), KE(4, 3, 1, 1),
 	KE(0, 0, 0, 0), KE(0, 0, 1, 0), KE(0, 0, 0, 1), KE(0, 0, 1, 1),
 	KEG_SET(4), KEG_SET(1),
+	// k = 8 sources off a 16-byte boundary: 16-byte lanes, funnel-shifted
+	// (ld_src16); measured neutral at k = 2 / 4 and slower at k = 16
+	// (tools/unaligned_ab.py, profiles/r05/unaligned_ab/), so only k = 8 has them
+	KEG(8, 1, 0, 0, 2), KEG(8, 2, 0, 0, 2), KEG(8, 3, 0, 0, 2),
 };
 #define N_KERNELS ((uint32_t)(sizeof(g_kernels) / sizeof(g_kernels[0])))
 
@@ -358,6 +362,31 @@ static bool dst_misaligned(const ecg_mm_params_t *p)
 	return (db & 3u) != 0;
 }
 
+// Sources (not only destinations) off a 16-byte boundary.
+static bool src_off16(const ecg_mm_params_t *p)
+{
+	uint64_t sb = (uint64_t)(uintptr_t)p->src | (uint64_t)p->src_stripe_stride;
+
+	for (uint32_t j = 0; j < p->k; j++)
+		sb |= (uint64_t)p->src_cell_off[j];
+	if (p->diff) {
+		sb |= (uint64_t)(uintptr_t)p->src2 | (uint64_t)p->src2_stripe_stride;
+		for (uint32_t j = 0; j < p->k; j++)
+			sb |= (uint64_t)p->src2_cell_off[j];
+	}
+	return (sb & 15u) != 0;
+}
+
+// A G = 2 instantiation exists for this shape.
+static bool has_g2(const ecg_mm_params_t *p)
+{
+	for (uint32_t i = 0; i < N_KERNELS; i++)
+		if (g_kernels[i].g == 2 && g_kernels[i].k == (int)p->k && g_kernels[i].r == (int)p->rows &&
+		    g_kernels[i].acc == (int)(p->accumulate != 0) && g_kernels[i].diff == (int)(p->diff != 0))
+			return true;
+	return false;
+}
+
 extern "C" uint32_t ecg_k_align_granule(const ecg_mm_params_t *p)
 {
 	return align_granule(p);
@@ -411,6 +440,13 @@ extern "C" int ecg_k_launch_matmul(const ecg_mm_params_t *p, const ecg_launch_cf
 		g = 0;		// the device serves no misaligned dwords: bytewise
 	else if (variant == 3 && g < 4)
 		g = 4;		// A/B: misaligned source dwords loaded as they are
+	else if (variant == 4 && g < 16)
+		g = 16;		// A/B: misaligned operands as dwordx4 accesses as they are
+	else if ((variant == 0 || variant == 5) && g < 16 && !(cfg && cfg->no_unaligned) && src_off16(p) &&
+		 has_g2(p))
+		g = 2;		// k = 8, sources off a 16-byte boundary: funnel-shifted 16-byte lanes
+	else if (variant == 5 && g == 4 && has_g2(p))
+		g = 2;		// A/B: the same when only destinations are off
 	if (variant == 2 || g == 0) {
 		uint64_t total = p->cell_bytes * p->nstripes;
 		uint64_t blocks = (total + BLOCK - 1) / BLOCK;

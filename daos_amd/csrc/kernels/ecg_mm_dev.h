@@ -31,11 +31,14 @@ __device__ __forceinline__ void st_nt(uint8_t *p, u32x4 v)
 	__builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
 }
 
-// Lane access granule G (16, 4 or 1; align_granule below picks it per
+// Lane access granule G (16, 4, 2 or 1; align_granule below picks it per
 // launch).  A wave always covers 1 KiB of each cell per column and a lane
 // always owns 4 dwords of it; only how the dwords are fetched changes:
 //   G = 16: one dwordx4 at wave*1024 + lane*16
 //   G = 4 : four dwords at wave*1024 + {0, 256, 512, 768} + lane*4
+//   G = 2 : the G = 16 layout, source pieces funnel-shifted out of
+//           dword-aligned dwordx4 loads (ld_src16 below); destinations as
+//           dwordx4 at their own (possibly misaligned) addresses
 //   G = 1 : the G = 4 layout, source dwords funnel-shifted (ld_src below)
 // so every wave-wide access is one contiguous 1024- or 256-byte run.  GF
 // arithmetic is per byte, so which bytes a lane owns does not matter, only
@@ -44,7 +47,7 @@ __device__ __forceinline__ void st_nt(uint8_t *p, u32x4 v)
 template <int G>
 __device__ __forceinline__ uint32_t lane_off()
 {
-	constexpr uint32_t GL = G == 1 ? 4u : (uint32_t)G;	// G = 1: the dword layout
+	constexpr uint32_t GL = G == 1 ? 4u : G == 2 ? 16u : (uint32_t)G;
 	return (threadIdx.x >> 6) * 1024u + (threadIdx.x & 63u) * GL;
 }
 
@@ -52,7 +55,7 @@ __device__ __forceinline__ uint32_t lane_off()
 template <int G>
 __device__ __forceinline__ uint32_t elem_off(int i)
 {
-	return G == 16 ? 4u * i : (uint32_t)i * 256u;
+	return G == 16 || G == 2 ? 4u * i : (uint32_t)i * 256u;
 }
 
 // G = 1 (sources at any byte alignment): the dword layout of G = 4 for the
@@ -67,7 +70,7 @@ __device__ __forceinline__ u32x4 ld_g(const uint8_t *p)
 {
 	if constexpr (G == 1) {
 		return ld_g<4>(p);	// destinations (ACC reads)
-	} else if constexpr (G == 16) {
+	} else if constexpr (G == 16 || G == 2) {
 		return ld_nt(p);
 	} else {
 		static_assert(G == 4, "granule");
@@ -82,7 +85,7 @@ __device__ __forceinline__ void st_g(uint8_t *p, u32x4 v)
 {
 	if constexpr (G == 1) {
 		st_g<4>(p, v);
-	} else if constexpr (G == 16) {
+	} else if constexpr (G == 16 || G == 2) {
 		st_nt(p, v);
 	} else {
 		uint32_t *q = reinterpret_cast<uint32_t *>(p);
@@ -91,6 +94,37 @@ __device__ __forceinline__ void st_g(uint8_t *p, u32x4 v)
 		__builtin_nontemporal_store(v[2], q + 128);
 		__builtin_nontemporal_store(v[3], q + 192);
 	}
+}
+
+// G = 2: the lane's 16 bytes at cell + lo (the G = 16 layout) for a cell at
+// any byte.  With m = cell & 3 (wave-uniform) they are bytes [m, m + 16) of
+// the 20 bytes {a, b}: a = the lane's dwordx4 at cell - m + lo (dword-aligned,
+// served by the hardware's unaligned access mode), b = the dword after it,
+// which is lane l+1's a0 (a DPP wave rotate, no second load) except for lane
+// 63, whose b is the dword right after the wave's 1 KiB (one wave-uniform
+// load; when m = 0 it reads the wave's own last dword instead, so nothing
+// past the column is read).  Dword w = v_alignbyte_b32(next, a_w, m).  No
+// branch: with m = 0 the shift is 0, so the k loads of a column still issue
+// back to back.
+__device__ __forceinline__ u32x4 ld_src16(const uint8_t *cell, uint32_t lo)
+{
+	const uint32_t m = (uint32_t)(uintptr_t)cell & 3u;
+	const uint8_t *base = cell - m;
+	const u32x4 a = ld_nt(base + lo);
+	const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const uint32_t e = __builtin_nontemporal_load(
+		reinterpret_cast<const uint32_t *>(base + wv * 1024u + (m ? 1024u : 1020u)));
+	// lane 63's b is written into the rotate with v_writelane, not chosen by
+	// a per-lane select: the compiler turns such a select of a load into a
+	// branch, sinks the rotate under it, and lane 62 then reads a disabled
+	// lane
+	const uint32_t es = __builtin_amdgcn_readfirstlane(e);
+	uint32_t b = (uint32_t)__builtin_amdgcn_mov_dpp((int)a[0], 0x134, 0xf, 0xf, false);
+
+	asm("v_writelane_b32 %0, %1, 63" : "+v"(b) : "s"(es));
+
+	return (u32x4){__builtin_amdgcn_alignbyte(a[1], a[0], m), __builtin_amdgcn_alignbyte(a[2], a[1], m),
+		       __builtin_amdgcn_alignbyte(a[3], a[2], m), __builtin_amdgcn_alignbyte(b, a[3], m)};
 }
 
 // The lane's 4 dwords of a source cell at (wave-uniform) address `cell`.
@@ -125,6 +159,8 @@ __device__ __forceinline__ u32x4 ld_src(const uint8_t *cell, uint32_t lo)
 			x[w] = __builtin_amdgcn_alignbyte(b, a[w], m);
 		}
 		return x;
+	} else if constexpr (G == 2) {
+		return ld_src16(cell, lo);
 	} else {
 		return ld_g<G>(cell + lo);
 	}
@@ -206,11 +242,14 @@ __device__ __forceinline__ void mm_load_any(const ecg_mm_params_t &P, int k, uin
 // 0.859), encode 0.844 -> 0.831, the dword-lane (G = 4) variant 0.895 ->
 // 0.887.  The funnel-shift kernels (G = 1) spill when phased.  k = 16 in
 // phases of 4 lost 5-20 % at 4 or 5 waves (phases of 8 spill).
+#ifndef ECG_G2_PHASE
+#define ECG_G2_PHASE 0
+#endif
 #ifndef ECG_MM_PHASE
-#define ECG_MM_PHASE(K, G) ((K) == 8 && ((G) == 16 || (G) == 4) ? 4 : 0)
+#define ECG_MM_PHASE(K, G) ((K) == 8 && ((G) == 16 || (G) == 4) ? 4 : (K) == 8 && (G) == 2 ? ECG_G2_PHASE : 0)
 #endif
 #ifndef ECG_MM_WPE
-#define ECG_MM_WPE(K, R, G) ((K) == 8 && ((G) == 16 || (G) == 4) ? 4 : 0)
+#define ECG_MM_WPE(K, R, G) ((K) == 8 && ((G) == 16 || (G) == 4 || ((G) == 2 && ECG_G2_PHASE)) ? 4 : 0)
 #endif
 
 // The product of one column: x[j] = the lane's 16 bytes of cell j.  STORE =
@@ -554,7 +593,11 @@ __device__ __forceinline__ void mm_partial(const ecg_mm_params_t &P, const u32x4
 {
 	const uint64_t C = P.cell_bytes;
 
-	if constexpr (G == 16) {
+	if constexpr (G == 2) {
+		// the funnel needs every lane of the wave: the partial column runs
+		// the G = 1 dword layout instead (misaligned dword loads)
+		mm_partial<KM, RM, ACC, DIFF, 1>(P, tb, k, rows, s, cbase, lane_off<1>());
+	} else if constexpr (G == 16) {
 		if (cbase + lo + 16 <= C)
 			mm_item<KM, RM, ACC, DIFF>(P, tb, k, rows, s, cbase, lo);
 		else if (cbase + lo < C)
@@ -662,7 +705,9 @@ static inline uint32_t granule_of(uint64_t bits)
 // dword boundary take the dword lanes' stores as they are: misaligned dword
 // stores (and ACC loads), served by the hardware's unaligned access mode,
 // ran 0.93-0.96 of the aligned kernel where the byte kernel ran 0.10 of the
-// HBM spec (tools/unaligned_ab.py, profiles/r04/unaligned_ab/).
+// HBM spec (tools/unaligned_ab.py, profiles/r04/unaligned_ab/).  The launcher
+// (ecg_k_launch_matmul) then runs k = 8 launches whose sources are off a
+// 16-byte boundary on G = 2 (profiles/r05/unaligned_ab/).
 static inline uint32_t align_granule(const ecg_mm_params_t *p)
 {
 	uint64_t sb = (uint64_t)(uintptr_t)p->src | (uint64_t)p->src_stripe_stride;

@@ -6,9 +6,10 @@ when all are 16-byte aligned; dword lanes (g4) for 8- and 4-byte alignment
 (DAOS rounds its parity rows to 8 bytes, ref:src/object/cli_ec.c:86); dword
 lanes whose source dwords are funnel-shifted out of aligned loads (g1: user
 sgl cells carry no alignment, ref:src/object/cli_ec.c:510-536, while DAOS
-allocates the parity aligned); destinations at any byte take the
-same lanes' stores as misaligned dwords (the hardware's unaligned access
-mode).  Every case is compared byte for byte with the oracle, and
+allocates the parity aligned); for k = 8, sources off a 16-byte boundary
+run 16-byte lanes funnel-shifted out of dword-aligned loads (g2);
+destinations at any byte take the same lanes' stores as misaligned dwords
+(the hardware's unaligned access mode).  Every case is compared byte for byte with the oracle, and
 the test asserts which kernel ran.  Offsets 1, 4, 8 and 12 of the data and/or parity bases, cells whose last
 4 KiB column is partial, and cell sizes that are not multiples of 4 / 16.
 """
@@ -29,13 +30,17 @@ def granule(*vals):
     return 16 if bits % 16 == 0 else 8 if bits % 8 == 0 else 4 if bits % 4 == 0 else 1
 
 
-def launch_granule(src_vals, dst_vals):
-    """ecg_mm_dev.h align_granule: the lanes a launch runs, from its source /
-    destination base offsets, cell offsets and strides.  16 / 4: dwordx4 /
-    dword lanes (8-byte alignment runs the dword lanes); 1: a source at any
-    byte (funnel-shifted loads).  Destinations at any byte take the lanes'
-    stores as misaligned dwords; the byte kernel (0) is never chosen."""
+def launch_granule(src_vals, dst_vals, k=0, rows=0, acc=False):
+    """ecg_mm_dev.h align_granule + ecg_k_launch_matmul: the lanes a launch
+    runs, from its source / destination base offsets, cell offsets and
+    strides.  16 / 4: dwordx4 / dword lanes (8-byte alignment runs the dword
+    lanes); 1: a source at any byte (funnel-shifted loads); 2: k = 8 (rows
+    1-3, no accumulate) with a source off a 16-byte boundary (16-byte lanes,
+    funnel-shifted).  Destinations at any byte take the lanes' stores as
+    misaligned dwords; the byte kernel (0) is never chosen."""
     gs, gd = granule(*src_vals), granule(*dst_vals)
+    if gs < 16 and k == 8 and 1 <= rows <= 3 and not acc:
+        return 2
     return 1 if gs < 4 else 16 if gs == gd == 16 else 4
 
 
@@ -73,7 +78,7 @@ def test_encode_offsets(ctx, oracle, ecglib, C_, doff, poff):
     try:
         ctx.encode(k, p, C_, S, d.ptr + doff, k * C_, par.ptr + poff, pitch, C_)
         ctx.sync()
-        expect_kernel(ecglib.last_kernel(), launch_granule((doff, k * C_, C_), (poff, pitch, C_)), k, p)
+        expect_kernel(ecglib.last_kernel(), launch_granule((doff, k * C_, C_), (poff, pitch, C_), k, p), k, p)
         raw = par.download()
         got = np.stack([raw[poff + r * pitch: poff + r * pitch + S * C_].reshape(S, C_) for r in range(p)])
         assert np.array_equal(got, oracle_parity(oracle, k, p, data))
@@ -91,7 +96,7 @@ def test_encode_offsets(ctx, oracle, ecglib, C_, doff, poff):
 def test_encode_classes_at_offset(ctx, oracle, ecglib, k, p, off):
     """Every specialised (k, p) has g4 (4- or 8-byte aligned operands) and g1
     instantiations (g1: the data cells at a byte offset, the parity
-    dword-aligned)."""
+    dword-aligned); k = 8 runs g2 for both."""
     S, C_ = 4, 8192 + 4096
     data = rand((S, k, C_), k * 10 + p + off)
     d = ctx.alloc(data.nbytes + 64)
@@ -102,7 +107,8 @@ def test_encode_classes_at_offset(ctx, oracle, ecglib, k, p, off):
         ctx.encode(k, p, C_, S, d.ptr + off, k * C_, par.ptr + poff, S * C_, C_)
         ctx.sync()
         name = ecglib.last_kernel()
-        assert name.startswith(f"ecg_mm_kernel<{k},{p},") and name.endswith(f",g{min(off, 4)}>"), name
+        g = 2 if k == 8 else min(off, 4)
+        assert name.startswith(f"ecg_mm_kernel<{k},{p},") and name.endswith(f",g{g}>"), name
         got = par.download(p * S * C_, offset=poff).reshape(p, S, C_)
         assert np.array_equal(got, oracle_parity(oracle, k, p, data))
     finally:
@@ -126,7 +132,7 @@ def test_recover_in_place_at_offset(ctx, oracle, ecglib, off, C_, errs):
         ctx.recover(k, p, C_, S, d.ptr + off, (k + p) * C_, errs)
         ctx.sync()
         vals = (off, (k + p) * C_, C_)             # in place: sources and destinations alike
-        expect_kernel(ecglib.last_kernel(), launch_granule(vals, vals), k, len(errs))
+        expect_kernel(ecglib.last_kernel(), launch_granule(vals, vals, k, len(errs)), k, len(errs))
         got = d.download(stripes.nbytes, offset=off).reshape(S, k + p, C_)
         assert np.array_equal(got, stripes)
     finally:

@@ -24,10 +24,12 @@ def gran(bits):
     return 16 if bits % 16 == 0 else 8 if bits % 8 == 0 else 4 if bits % 4 == 0 else 1
 
 
-def predict(sbase, soff, sstride, dbase, doff, dstride):
-    """The lanes one launch runs (ecg_mm_dev.h align_granule); bases are byte
-    offsets from a 256-byte-aligned allocation.  Destinations at any byte take
-    the lanes' stores as misaligned dwords."""
+def predict(sbase, soff, sstride, dbase, doff, dstride, acc=False):
+    """The lanes one launch runs (ecg_mm_dev.h align_granule, and
+    ecg_k_launch_matmul's g2 for k = 8 with rows 1-3 and no accumulate whose
+    sources are off a 16-byte boundary); bases are byte offsets from a
+    256-byte-aligned allocation, soff / doff the launch's cells.
+    Destinations at any byte take the lanes' stores as misaligned dwords."""
     sb = sbase | sstride
     for o in soff:
         sb |= o
@@ -35,6 +37,8 @@ def predict(sbase, soff, sstride, dbase, doff, dstride):
     for o in doff:
         db |= o
     gs, gd = gran(sb), gran(db)
+    if gs < 16 and len(soff) == 8 and 1 <= len(doff) <= 3 and not acc:
+        return "g2"
     return "g1" if gs < 4 else "g16" if gs == gd == 16 else "g4"
 
 
@@ -91,7 +95,7 @@ def run_case(ctx, oracle, ecglib, seed):
         before = rng.integers(0, 256, dbase + rows * drow + 64, dtype=np.uint8)
         bufs = (ctx.to_device(img), ctx.to_device(before))
     last = src_off[(k - 1) // 16 * 16:]           # k > 16: the last launch takes the last <= 16 cells
-    want = predict(sbase, last, src_stride, dbase, dst_off, dst_stride)
+    want = predict(sbase, last, src_stride, dbase, dst_off, dst_stride, acc or k > 16)
     try:
         ctx.matmul(coef, C, S, bufs[0].ptr + sbase, src_off, src_stride, bufs[-1].ptr + dbase, dst_off,
                    dst_stride, 1 if acc else 0)
@@ -128,14 +132,14 @@ def test_predict_covers_every_class():
             order = rng.permutation(k + rows)
             stride = (k + rows) * pitch + pad
             cls = predict(sbase, [int(c) * pitch for c in order[:k]][(k - 1) // 16 * 16:], stride, sbase,
-                          [int(c) * pitch for c in order[k:]], stride)
+                          [int(c) * pitch for c in order[k:]], stride, acc or k > 16)
         else:
             rng.integers(0, 256, sbase + S * (k * pitch + pad) + 64, dtype=np.uint8)
             soff = [int(c) * pitch for c in rng.permutation(k)]
             cls = predict(sbase, soff[(k - 1) // 16 * 16:], k * pitch + pad, dbase,
-                          [int(r) * (S * C + pad) for r in rng.permutation(rows)], C)
+                          [int(r) * (S * C + pad) for r in rng.permutation(rows)], C, acc or k > 16)
         seen[cls] = seen.get(cls, 0) + 1
-    assert {"g1", "g4", "g16"} <= set(seen), seen
+    assert {"g1", "g2", "g4", "g16"} <= set(seen), seen
     # and outputs off a dword boundary (the byte kernel's case before round 4)
     assert sum(1 for s in range(N_CASES) if s % 5 == 2) >= 10
     assert predict(0, [0], 4096, 1, [0, 8193], 4096) == "g4"
@@ -149,7 +153,7 @@ def test_random_layouts(ctx, oracle, ecglib):
         got = run_case(ctx, oracle, ecglib, seed)
         kernels[got] = kernels.get(got, 0) + 1
     print("kernels:", kernels)
-    assert {"g1", "g4", "g16"} <= set(kernels), kernels
+    assert {"g1", "g2", "g4", "g16"} <= set(kernels), kernels
 
 
 def table_affine(offs, S, k, rows):

@@ -2,7 +2,12 @@
 source dwords for sources at any byte, misaligned dword stores for
 destinations at any byte; before round 4's change, a bytewise head + shifted
 body or the byte kernel) against dword lanes issued at the misaligned
-addresses themselves for the sources too (variant 3).  EC_8P2 1 MiB client-layout encode;
+addresses themselves for the sources too (variant 3), and 16-byte lanes
+issued at the misaligned addresses (variant 4, misaligned dwordx4), and
+16-byte lanes funnel-shifted out of dword-aligned dwordx4 loads (variant 5,
+G = 2).  Client-layout encode, EC_8P2 1 MiB x 512 and EC_4P2 / EC_16P2 /
+EC_2P1 rows; ECG_TEST_LIB = an experimental build, UNALIGNED_CASES = a
+comma list of case names, UNALIGNED_TAG = output file suffix;
 median of 20 back-to-back launches after 10; both variants' parity compared
 byte for byte.  usage: python tools/unaligned_ab.py -> gpurun_out/unaligned_ab.json.
 Bench infrastructure."""
@@ -17,7 +22,11 @@ sys.path.insert(0, ROOT)
 os.environ.setdefault("ECG_AUTOTUNE", "0")
 from daos_amd import ecg  # noqa: E402
 
+if os.environ.get("ECG_TEST_LIB"):	# an experimental build (tools/build_exp.sh)
+    ecg.LIB_PATH = os.path.abspath(os.environ["ECG_TEST_LIB"])
+
 MiB = 1 << 20
+VARIANTS = tuple(int(v) for v in os.environ.get("UNALIGNED_VARIANTS", "0,3,4,5").split(","))
 
 
 def timed(ctx, fn, iters=20, warm=10):
@@ -37,24 +46,35 @@ def timed(ctx, fn, iters=20, warm=10):
 
 def main():
     ctx = ecg.Context(0)
-    k, p, C = 8, 2, MiB
+    C = MiB
     res = {}
-    # name, stripes, data offset, parity offset, extra parity row pitch, cell bytes
+    # name, (k, p), stripes, data offset, parity offset, extra parity row pitch, cell bytes
     # (cells short of 1 MiB: every cell ends in a partial 4 KiB column)
-    cases = (("aligned", 512, 0, 0, 0, C), ("data_off1", 512, 1, 0, 0, C), ("parity_off1", 512, 0, 1, 0, C),
-             ("parity_off2_data_off1", 512, 1, 2, 0, C), ("parity_off1_unequal", 64, 0, 1, 1, C),
-             ("data_off3_parity_off1_unequal", 64, 3, 1, 1, C),
-             ("aligned_C-16", 512, 0, 0, 0, C - 16), ("aligned_C-4", 512, 0, 0, 0, C - 4),
-             ("data_off1_C-4", 512, 1, 0, 0, C - 4), ("C-3", 512, 0, 0, 0, C - 3))
-    for name, S, doff, poff, extra, C in cases:
+    cases = (("aligned", (8, 2), 512, 0, 0, 0, C), ("data_off1", (8, 2), 512, 1, 0, 0, C),
+             ("data_off4", (8, 2), 512, 4, 0, 0, C), ("data_off8", (8, 2), 512, 8, 0, 0, C),
+             ("parity_off1", (8, 2), 512, 0, 1, 0, C), ("parity_off8", (8, 2), 512, 0, 8, 0, C),
+             ("parity_off2_data_off1", (8, 2), 512, 1, 2, 0, C), ("parity_off1_unequal", (8, 2), 64, 0, 1, 1, C),
+             ("data_off3_parity_off1_unequal", (8, 2), 64, 3, 1, 1, C),
+             ("aligned_C-16", (8, 2), 512, 0, 0, 0, C - 16), ("aligned_C-4", (8, 2), 512, 0, 0, 0, C - 4),
+             ("data_off1_C-4", (8, 2), 512, 1, 0, 0, C - 4), ("C-3", (8, 2), 512, 0, 0, 0, C - 3),
+             ("4p2_aligned", (4, 2), 1024, 0, 0, 0, C), ("4p2_data_off1", (4, 2), 1024, 1, 0, 0, C),
+             ("4p2_data_off4", (4, 2), 1024, 4, 0, 0, C),
+             ("16p2_128K_aligned", (16, 2), 1024, 0, 0, 0, 128 << 10),
+             ("16p2_128K_data_off1", (16, 2), 1024, 1, 0, 0, 128 << 10),
+             ("16p2_128K_data_off4", (16, 2), 1024, 4, 0, 0, 128 << 10),
+             ("2p1_128K_data_off1", (2, 1), 1024, 1, 0, 0, 128 << 10))
+    only = os.environ.get("UNALIGNED_CASES")
+    for name, (k, p), S, doff, poff, extra, C in cases:
+        if only and name not in only.split(","):
+            continue
         data = ctx.alloc(S * k * C + 64)
         data.fill(0x3C)
         data.upload(np.random.default_rng(S + doff).integers(0, 256, 64 * MiB, dtype=np.uint8))
         pitch = S * C + 4096 + extra
         par = ctx.alloc(p * pitch + 64)
-        row = {"stripes": S}
+        row = {"k": k, "p": p, "cell_bytes": C, "stripes": S}
         outs = {}
-        for variant in (0, 3):
+        for variant in VARIANTS:
             ctx.set_launch(0, 0, variant)
             fn = lambda: ctx.encode(k, p, C, S, data.ptr + doff, k * C, par.ptr + poff, pitch, C)
             par.fill(0)
@@ -64,16 +84,18 @@ def main():
                                   "kernel": ecg.last_kernel()}
             outs[variant] = par.download()
         ctx.set_launch(0, 0, 0)
-        row["v3_over_v0"] = round(row["v0"]["ms"] / row["v3"]["ms"], 4)
-        row["equal"] = bool(np.array_equal(outs[0], outs[3]))
+        for v in VARIANTS[1:]:
+            row[f"v{v}_over_v0"] = round(row["v0"]["ms"] / row[f"v{v}"]["ms"], 4)
+        row["equal"] = all(bool(np.array_equal(outs[VARIANTS[0]], outs[v])) for v in VARIANTS[1:])
         res[name] = row
         print(name, json.dumps(row), flush=True)
         data.free()
         par.free()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(ROOT, "gpurun_out", "unaligned_ab.json"), "w") as f:
+    tag = os.environ.get("UNALIGNED_TAG", "")
+    with open(os.path.join(ROOT, "gpurun_out", f"unaligned_ab{tag}.json"), "w") as f:
         json.dump(res, f, indent=1)
-    assert all(r["equal"] for r in res.values()), "variant 3 parity differs"
+    assert all(r["equal"] for r in res.values()), "a variant's parity differs"
 
 
 if __name__ == "__main__":
