@@ -289,10 +289,11 @@ const char *ecg_k_fused_kernel_name(uint32_t kernel_id);
 uint32_t ecg_k_align_granule(const ecg_mm_params_t *p);
 /* Pointer-table product (kernels/ecg_ptr_kernels.hip): cells_dev[s*(k+rows)+j]
  * = device address of input cell j / output cell j-k of stripe s.  granule:
- * 16 = every address 16-byte aligned; 4 = inputs dword-aligned; 1 = an input
- * at any byte -- with outputs at any byte in both of the last two (stored as
- * misaligned dwords, so both need the device's unaligned access mode); 0 =
- * the byte-granular kernel (ecg_ptrs.c ptr_granule). */
+ * 16 = every address 16-byte aligned; 4 = inputs dword-aligned; 2 = k = 8
+ * with an input off a 16-byte boundary (16-byte lanes, funnel-shifted); 1 =
+ * an input at any byte -- with outputs at any byte in the last three (stored
+ * misaligned, so they need the device's unaligned access mode); 0 = the
+ * byte-granular kernel (ecg_ptrs.c ptr_granule). */
 int ecg_k_launch_matmul_ptrs(const ecg_mm_params_t *p, const uint64_t *cells_dev, int granule,
 			     const ecg_launch_cfg_t *cfg, void *stream, uint32_t *kernel_id);
 #define ECG_KID_PTR 600u	/* pointer-table kernel ids start here */

@@ -98,6 +98,10 @@ static int ptr_granule(const uint64_t *tab, uint32_t S, int k, int rows, int no_
 	}
 	if (no_unaligned && ((in | out) & 3u))
 		return 0;
+	/* k = 8 inputs off a 16-byte boundary: 16-byte lanes funnel-shifted out
+	 * of dword-aligned loads, as the offset kernel (ecg_kernels.hip) */
+	if ((in & 15u) && !no_unaligned && k == 8 && rows >= 1 && rows <= 3)
+		return 2;
 	if (in & 3u)
 		return 1;	/* outputs at any byte: misaligned dword stores */
 	return ((in | out) & 15u) == 0 ? 16 : 4;

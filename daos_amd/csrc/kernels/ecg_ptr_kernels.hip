@@ -11,8 +11,10 @@
 // The lane access G follows the cells' alignment exactly as the offset kernel:
 // 16 (every address and the cell size 16-byte aligned), 4 (every input
 // dword-aligned), 1 (an input at any byte: each input dword funnel-shifted out
-// of aligned loads, ld_src<1>); outputs at any byte take misaligned dword
-// stores (the hardware's unaligned access mode, ecg_mm_dev.h mm_dword).
+// of aligned loads, ld_src<1>), 2 (k = 8 with an input off a 16-byte boundary:
+// 16-byte lanes funnel-shifted, ld_src16); outputs at any byte take
+// misaligned stores (the hardware's unaligned access mode, ecg_mm_dev.h
+// mm_dword).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -216,6 +218,7 @@ static const pentry g_pkernels[] = {
 	PE(2, 1), PE(2, 2), PE(2, 3), PE(4, 1), PE(4, 2), PE(4, 3),
 	PE(8, 1), PE(8, 2), PE(8, 3), PE(16, 1), PE(16, 2), PE(16, 3), PE(0, 0),
 	PEG_SET(4), PEG_SET(1),
+	PEG(8, 1, 2), PEG(8, 2, 2), PEG(8, 3, 2),	/* k = 8 inputs off 16 B (ecg_ptrs.c ptr_granule) */
 };
 #define N_PKERNELS ((uint32_t)(sizeof(g_pkernels) / sizeof(g_pkernels[0])))
 #define KID_PTR ECG_KID_PTR		/* pointer-table kernel ids: KID_PTR + index */
@@ -253,7 +256,7 @@ extern "C" int ecg_k_launch_matmul_ptrs(const ecg_mm_params_t *p, const uint64_t
 			*kernel_id = KID_PTR_BYTE;
 		return (int)hipGetLastError();
 	}
-	if (g != 16 && g != 4 && g != 1)
+	if (g != 16 && g != 4 && g != 2 && g != 1)
 		return (int)hipErrorInvalidValue;
 	for (uint32_t i = 0; i < N_PKERNELS && (!cfg || cfg->variant != 1); i++)
 		if (g_pkernels[i].g == g && g_pkernels[i].k == (int)p->k && g_pkernels[i].r == (int)p->rows) {

@@ -10,16 +10,19 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _ptr_granule(in_skews, out_skews, C):
+def _ptr_granule(in_skews, out_skews, C, k=0, rows=0):
     """ecg_ptrs.c ptr_granule + ecg_k_launch_matmul_ptrs: 1 funnel-shifted
-    inputs, 4 dword lanes, 16 dwordx4 lanes (outputs at any byte: misaligned
-    dword stores)."""
+    inputs, 4 dword lanes, 16 dwordx4 lanes, 2 (k = 8, rows 1-3, an input off
+    16 bytes) funnel-shifted 16-byte lanes (outputs at any byte: misaligned
+    stores)."""
     ib = 0
     for x in in_skews:
         ib |= x
     ob = 0
     for x in out_skews:
         ob |= x
+    if ib & 15 and k == 8 and 1 <= rows <= 3:
+        return 2
     if ib & 3:
         return 1
     return 16 if ((ib | ob) & 15) == 0 and C % 16 == 0 else 4
@@ -60,7 +63,7 @@ def test_matmul_ptrs(oracle, ecglib, ctx, k, rows, C, S, iskew, oskew):
         ctx.sync()
         kern = ecglib.last_kernel()
         g = _ptr_granule([a for i, a in enumerate(addrs) if i % (k + rows) < k],
-                         [a for i, a in enumerate(addrs) if i % (k + rows) >= k], C)
+                         [a for i, a in enumerate(addrs) if i % (k + rows) >= k], C, k, rows)
         if g == 16:
             assert kern.startswith("ecg_mm_ptr_kernel<") and ",g" not in kern, kern
         else:
@@ -140,8 +143,8 @@ def test_recx_encode_sgl(oracle, ecglib, ctx, k, p, C, recx_plan, n_iov, zeros, 
         else:
             assert kern.startswith("ecg_mm_ptr_kernel<"), kern
         if shift % 4:       # in-place cells at odd addresses, parity aligned: funnel-shifted inputs
-            # (the offset kernel runs k = 8 on 16-byte lanes, g2; the pointer tables dword lanes, g1)
-            g = 2 if k == 8 and n_iov == 1 and len(recx_plan) == 1 else 1
+            # (k = 8 on 16-byte lanes, g2, in both the offset and the pointer-table kernel)
+            g = 2 if k == 8 else 1
             assert kern.endswith(f",g{g}>"), kern
         en = oracle.cauchy1(k, p)
         n = 0

@@ -3,7 +3,8 @@ over stripes, the client's in-place sgl encode) against the offset kernel
 (ecg_encode) on the same client layout -- data [S][k][C], parity rows
 [p][S][C] -- uncapped and at the candidate blocks-per-CU cap.  The pointer
 table is built once; each timed call uploads it (part of the path) and
-launches.  Median of 30 back-to-back calls after 40; tuner off.
+launches.  Median of 30 back-to-back calls after 40; tuner off.  Env:
+PTR_SHUFFLE, PTR_GX_DIVS, PTR_DATA_OFF, PTR_TAG, ECG_TEST_LIB (below).
 -> gpurun_out/ptr_ab.json.  Bench infrastructure."""
 import ctypes as C
 import json
@@ -24,6 +25,10 @@ GX_DIVS = [int(d) for d in os.environ.get("PTR_GX_DIVS", "1").split(",")]
 # PTR_SHUFFLE=1: the table lists the stripes in a shuffled order -- the same
 # cells, no longer an affine table, so the pointer-table kernel runs
 SHUFFLE = os.environ.get("PTR_SHUFFLE") == "1"
+# PTR_DATA_OFF: the data cells start this many bytes into their buffer (user
+# sgl cells in place at any byte); PTR_TAG: output file suffix
+DATA_OFF = int(os.environ.get("PTR_DATA_OFF", "0"))
+TAG = os.environ.get("PTR_TAG", "")
 if os.environ.get("ECG_TEST_LIB"):
     ecg.LIB_PATH = os.path.abspath(os.environ["ECG_TEST_LIB"])
 
@@ -50,14 +55,14 @@ def main():
     for k, p, Cb, S in ((4, 2, MiB, 1024), (8, 2, MiB, 512), (16, 2, 128 << 10, 1024), (2, 1, 128 << 10, 1024)):
         coef = np.ascontiguousarray(ecg.cauchy1(k, p)[k:])
         cptr = coef.ctypes.data_as(C.POINTER(C.c_ubyte))
-        data = ctx.alloc(S * k * Cb)
+        data = ctx.alloc(S * k * Cb + 64)
         data.fill(0x3C)
         pitch = S * Cb + 4096
         par = ctx.alloc(p * pitch)
         cells = []
         order = np.random.default_rng(S).permutation(S) if SHUFFLE else range(S)
         for s in order:
-            cells += [data.ptr + (int(s) * k + j) * Cb for j in range(k)]
+            cells += [data.ptr + DATA_OFF + (int(s) * k + j) * Cb for j in range(k)]
             cells += [par.ptr + r * pitch + int(s) * Cb for r in range(p)]
         arr = (C.c_void_p * len(cells))(*cells)
         h = ctx.h
@@ -66,7 +71,7 @@ def main():
             ecg._chk(lib.ecg_matmul_ptrs(h, k, p, cptr, Cb, S, arr, None), "matmul_ptrs")
 
         def off_call():
-            ctx.encode(k, p, Cb, S, data.ptr, k * Cb, par.ptr, pitch, Cb)
+            ctx.encode(k, p, Cb, S, data.ptr + DATA_OFF, k * Cb, par.ptr, pitch, Cb)
 
         alg = (k + p) * Cb * S
         nchunk = Cb // 4096
@@ -85,7 +90,7 @@ def main():
         data.free()
         par.free()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(ROOT, "gpurun_out", "ptr_ab.json"), "w") as f:
+    with open(os.path.join(ROOT, "gpurun_out", f"ptr_ab{TAG}.json"), "w") as f:
         json.dump(res, f, indent=1)
 
 
