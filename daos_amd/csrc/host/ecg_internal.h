@@ -187,6 +187,9 @@ int ecg_tune_launch_fn(ecg_ctx_t *ctx, const ecg_mm_params_t *p, uint32_t g, uin
  * (ecg_stage.c) */
 int ecg_matmul_host_mem(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
 			unsigned char *const *src, unsigned char *const *dst, unsigned flags, int src_dev);
+/* every cell [v[i], v[i] + len) inside one allocation of ctx's device, else
+ * -DER_INVAL naming `what` (ecg_stage.c) */
+int ecg_cells_on_device(ecg_ctx_t *ctx, unsigned char *const *v, int n, uint64_t len, const char *what);
 /* drop-in routing (ecg_dropin.c): device cells -> GPU, host cells -> CPU
  * below the crossover or without a usable device, else GPU.  ctx NULL = the
  * calling thread's default context. */

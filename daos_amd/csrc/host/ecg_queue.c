@@ -35,10 +35,20 @@
  * Slots are spread round-robin over the contexts of an ecg_multi_t
  * (ecg_queue_create_multi): each slot's staging, stream and launches live on
  * its own device.
+ *
+ * Device cells (an engine whose bio buffers live in HBM): encode and recover
+ * requests whose cells are memory of one of the queue's devices go to slots of
+ * that device that hold no data at all -- only the stripes' cell pointers,
+ * ISA-L's data[] / coding[] laid end to end -- and a batch is one
+ * pointer-table launch on the cells in place (ecg_matmul_ptrs), no PCIe.  Such
+ * a slot closes as soon as its device has no batch of this queue in flight, so
+ * a lone request launches at once and requests arriving while a batch runs
+ * form the next one.
  */
 #define _GNU_SOURCE
 #include <stdlib.h>
 #include <string.h>
+#include <sys/prctl.h>
 #include <time.h>
 
 #include "../../../include/ecg_multi.h"
@@ -67,6 +77,7 @@ struct qslot {
 	enum slot_state state;
 	/* class */
 	int op, k, p, nerrs, rows;
+	int devcells;			/* cells in device memory of ctx's device: tab, no staging */
 	uint64_t C, pitch;
 	uint32_t err[ECG_MAX_P];
 	unsigned char coef[ECG_MAX_P * ECG_MAX_K];
@@ -77,6 +88,7 @@ struct qslot {
 	uint32_t fin_next, fin_done;	/* completion progress (S_DONE) */
 	uint64_t t_open_ns;
 	struct qreq *reqs;		/* cap entries */
+	uint64_t *tab;			/* devcells: cap x (k + rows) cell addresses */
 	/* staging */
 	unsigned char *host;		/* pinned: inputs [cap][k][pitch], (updates: vec_i [cap]),
 					 * outputs [cap][rows][pitch] at out_off */
@@ -138,18 +150,20 @@ static uint64_t pitch_of(uint64_t C)
 	return (C + 63) & ~63ull;
 }
 
+/* dev: the cells' device (device-cell requests), -1 for host cells */
 static int slot_matches(const struct qslot *s, int op, int k, int p, uint64_t C,
-			const uint32_t *err, int nerrs)
+			const uint32_t *err, int nerrs, int dev)
 {
 	return s->state == S_FILLING && s->reserved < s->cap && s->op == op && s->k == k &&
-	       s->p == p && s->C == C && s->nerrs == nerrs &&
+	       s->p == p && s->C == C && s->nerrs == nerrs && s->devcells == (dev >= 0) &&
+	       (dev < 0 || s->ctx->device == dev) &&
 	       (op != OP_RECOVER || memcmp(s->err, err, sizeof(uint32_t) * nerrs) == 0);
 }
 
 /* Assign a FREE slot to a class: decode rows for recovery, capacity from the
  * slot's staging bytes. */
 static int slot_open(struct ecg_queue *q, struct qslot *s, int op, int k, int p, uint64_t C,
-		     const uint32_t *err, int nerrs)
+		     const uint32_t *err, int nerrs, int dev)
 {
 	unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
 	uint64_t per;
@@ -177,9 +191,11 @@ static int slot_open(struct ecg_queue *q, struct qslot *s, int op, int k, int p,
 		s->rows = nerrs;
 	}
 	s->nin = op == OP_UPDATE ? 1 : k;	/* staged input cells per request */
+	s->devcells = dev >= 0;
 	/* an update request also stages its vec_i byte (+64 B of alignment slack) */
 	per = s->pitch * (uint64_t)(s->nin + s->rows) + (op == OP_UPDATE ? 1 : 0);
-	s->cap = (uint32_t)((q->slot_bytes - 64) / per);
+	/* device cells stage nothing: only the pointer table bounds a batch */
+	s->cap = s->devcells ? q->attr.max_batch : (uint32_t)((q->slot_bytes - 64) / per);
 	if (s->cap > q->attr.max_batch)
 		s->cap = q->attr.max_batch;
 	if (s->cap == 0)
@@ -196,6 +212,24 @@ static int slot_open(struct ecg_queue *q, struct qslot *s, int op, int k, int p,
 	return 0;
 }
 
+/* Device-cell batches of this queue queued or running on one device at once:
+ * a second one hides the first's completion poll and the next launch
+ * (profiles/r05/queue_dev/). */
+#ifndef ECG_QUEUE_DEV_DEPTH
+#define ECG_QUEUE_DEV_DEPTH 2
+#endif
+
+/* ctx's device has ECG_QUEUE_DEV_DEPTH batches of this queue queued or running. */
+static int device_busy(const struct ecg_queue *q, const ecg_ctx_t *ctx)
+{
+	int n = 0;
+
+	for (int i = 0; i < q->nslot; i++)
+		if (q->slot[i].ctx == ctx && (q->slot[i].state == S_INFLIGHT || q->slot[i].state == S_READY))
+			n++;
+	return n >= ECG_QUEUE_DEV_DEPTH;
+}
+
 static void close_due_slots(struct ecg_queue *q, uint64_t t, int force)
 {
 	for (int i = 0; i < q->nslot; i++) {
@@ -203,7 +237,8 @@ static void close_due_slots(struct ecg_queue *q, uint64_t t, int force)
 
 		if (s->state == S_FILLING && s->reserved > 0 &&
 		    (force || s->reserved == s->cap ||
-		     t >= s->t_open_ns + (uint64_t)q->attr.max_wait_us * 1000ull))
+		     t >= s->t_open_ns + (uint64_t)q->attr.max_wait_us * 1000ull ||
+		     (s->devcells && !device_busy(q, s->ctx))))
 			s->state = S_READY;
 	}
 }
@@ -224,6 +259,30 @@ static void launch_slot(struct ecg_queue *q, struct qslot *s)
 	(void)q;
 	ecg_trace_push("ecg:queue_batch");
 	e = hipSetDevice(s->ctx->device);
+	if (s->devcells) {
+		/* the cells in place: one pointer-table launch (its table upload
+		 * and kernel on the slot's stream), nothing crosses back */
+		rc = e == hipSuccess ? 0 : ecg_hip_fail(e, "queue set device");
+		if (rc == 0)
+			rc = ecg_matmul_ptrs(s->ctx, s->k, s->rows, s->coef, s->C, n, (void *const *)s->tab, s->st);
+		if (rc == 0) {
+			e = hipEventRecord(s->done, s->st);
+			if (e != hipSuccess)
+				rc = ecg_hip_fail(e, "queue batch event");
+		}
+		if (rc == 0 && s->op == OP_ENCODE) {
+			ECG_STAT_ADD(s->ctx, encode_stripes, n);
+			ECG_STAT_ADD(s->ctx, encode_bytes, (uint64_t)s->k * s->C * n);
+		} else if (rc == 0) {
+			ECG_STAT_ADD(s->ctx, recover_stripes, n);
+			ECG_STAT_ADD(s->ctx, recover_bytes, (uint64_t)s->rows * s->C * n);
+		}
+		s->rc = rc;
+		s->state = S_INFLIGHT;
+		q->batches++;
+		ecg_trace_pop();
+		return;
+	}
 	for (j = 0; j < s->k; j++)
 		soff[j] = (int64_t)(j * s->pitch);
 	for (j = 0; j < s->rows; j++)
@@ -332,7 +391,9 @@ static void finish_req(struct ecg_queue *q, struct qslot *s, uint32_t i)
 	struct qreq *r = &s->reqs[i];
 
 	ecg_trace_push("ecg:queue_complete");
-	if (s->rc == 0 && s->op == OP_UPDATE)	/* parity ^= coef[r][vec_i] * diff */
+	if (s->devcells)
+		;				/* written in place by the launch */
+	else if (s->rc == 0 && s->op == OP_UPDATE)	/* parity ^= coef[r][vec_i] * diff */
 		for (int j = 0; j < s->rows; j++)
 			xor_into_locked(q, r->dst[j], out + j * s->pitch, s->C);
 	else if (s->rc == 0)
@@ -343,9 +404,10 @@ static void finish_req(struct ecg_queue *q, struct qslot *s, uint32_t i)
 		r->cb(r->arg, s->rc);
 }
 
-/* Completion threads: claim requests of S_DONE slots one at a time, so the
- * host-side scatter of a batch runs on NFIN threads; the last one frees the
- * slot. */
+/* Completion threads: claim requests of S_DONE slots -- one at a time for
+ * host cells, so the host-side scatter of a batch runs on NFIN threads; a
+ * whole batch at once for device cells, which have only callbacks to run --
+ * and the last one frees the slot. */
 static void *fin_main(void *argp)
 {
 	struct ecg_queue *q = argp;
@@ -353,7 +415,7 @@ static void *fin_main(void *argp)
 	pthread_mutex_lock(&q->lock);
 	for (;;) {
 		struct qslot *s = NULL;
-		uint32_t i;
+		uint32_t i, n;
 
 		for (int j = 0; j < q->nslot && s == NULL; j++)
 			if (q->slot[j].state == S_DONE && q->slot[j].fin_next < q->slot[j].reserved)
@@ -364,11 +426,14 @@ static void *fin_main(void *argp)
 			pthread_cond_wait(&q->cv_fin, &q->lock);
 			continue;
 		}
-		i = s->fin_next++;
+		i = s->fin_next;
+		n = s->devcells ? s->reserved - i : 1;
+		s->fin_next += n;
 		pthread_mutex_unlock(&q->lock);
-		finish_req(q, s, i);
+		for (uint32_t x = 0; x < n; x++)
+			finish_req(q, s, i + x);
 		pthread_mutex_lock(&q->lock);
-		if (++s->fin_done == s->reserved) {
+		if ((s->fin_done += n) == s->reserved) {
 			q->completed += s->reserved;
 			s->state = S_FREE;
 			pthread_cond_broadcast(&q->cv_slot);
@@ -384,6 +449,9 @@ static void *worker_main(void *argp)
 {
 	struct ecg_queue *q = argp;
 
+	/* the in-flight polls below wait 20 us: without this the kernel's
+	 * default 50 us timer slack would stretch every one of them */
+	(void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
 	pthread_mutex_lock(&q->lock);
 	for (;;) {
 		int busy = 0, idle = 1;
@@ -465,6 +533,7 @@ static void slot_free(struct qslot *s)
 	if (s->done)
 		(void)hipEventDestroy(s->done);
 	free(s->reqs);
+	free(s->tab);
 }
 
 /* Slots round-robin over ctxs[nctx] (one context = one device). */
@@ -511,7 +580,8 @@ static int queue_create(ecg_ctx_t *const *ctxs, int nctx, const ecg_queue_attr_t
 
 		s->ctx = ctxs[i % nctx];
 		s->reqs = calloc(q->attr.max_batch, sizeof(*s->reqs));
-		if (s->reqs == NULL) {
+		s->tab = calloc((size_t)q->attr.max_batch * (ECG_KMAX_K + ECG_KMAX_R), sizeof(*s->tab));
+		if (s->reqs == NULL || s->tab == NULL) {
 			e = hipErrorOutOfMemory;
 			break;
 		}
@@ -612,6 +682,75 @@ void ecg_queue_destroy(ecg_queue_t *q)
 
 /* Reserve a stripe index in a slot of this class (opening one if needed),
  * copy the inputs in without the lock, then publish. */
+/* Every cell of a device-cell request inside one allocation of ctx's device
+ * (a launch on anything else would fault the GPU).  The HIP runtime's
+ * pointer queries serialise across threads, so the usual stripe -- every cell
+ * in one allocation -- costs one range query beyond the placement query; only
+ * cells outside that allocation are looked up one by one. */
+static int cells_checked(ecg_ctx_t *ctx, int op, int k, int p, uint64_t C, unsigned char *const *src,
+			 unsigned char *stripe, unsigned char *const *dst)
+{
+	const unsigned char *first = op == OP_RECOVER ? stripe : src[0];
+	hipDeviceptr_t base = NULL;
+	size_t size = 0;
+	uintptr_t lo, hi;
+	int i, rc = 0;
+
+	if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)first) != hipSuccess) {
+		(void)hipGetLastError();
+		return ecg_fail(-ECG_DER_INVAL, "queue: device cell %p: no device allocation", (const void *)first);
+	}
+	lo = (uintptr_t)base;
+	hi = lo + size;
+	if (op == OP_RECOVER) {
+		const uintptr_t a = (uintptr_t)stripe;
+
+		if (a + C * (uint64_t)(k + p) > hi)
+			return ecg_fail(-ECG_DER_INVAL, "queue: the [k+p][cell] stripe runs past the end of its "
+					"allocation");
+		return 0;
+	}
+	for (i = 0; i < k + p && rc == 0; i++) {
+		unsigned char *c = i < k ? src[i] : dst[i - k];
+		const uintptr_t a = (uintptr_t)c;
+
+		if (a < lo || a + C > hi)	/* another allocation: look it up */
+			rc = ecg_cells_on_device(ctx, &c, 1, C, i < k ? "source" : "parity");
+	}
+	return rc;
+}
+
+/* Device-cell requests: the cells' device must be one of the queue's, every
+ * cell inside one of its allocations, and the shape one pointer-table launch
+ * takes.  Returns the device, -1 for host cells, or a negative DER code
+ * through *rc. */
+static int request_device(struct ecg_queue *q, int op, int k, int p, uint64_t C, int rows,
+			  unsigned char *const *src, unsigned char *stripe, unsigned char *const *dst, int *rc)
+{
+	const unsigned char *first = op == OP_RECOVER ? stripe : src[0];
+	const int dev = ecg_ptr_device(first);
+	ecg_ctx_t *ctx = NULL;
+
+	*rc = 0;
+	if (dev < 0)
+		return -1;
+	for (int i = 0; i < q->nslot && ctx == NULL; i++)
+		if (q->slot[i].ctx->device == dev)
+			ctx = q->slot[i].ctx;
+	if (ctx == NULL)
+		*rc = ecg_fail(-ECG_DER_INVAL, "queue: cells are memory of device %d, which has no slot in "
+			       "this queue", dev);
+	else if (op == OP_UPDATE)
+		*rc = ecg_fail(-ECG_DER_NOSYS, "queue_update: device cells (use ecg_update / "
+			       "ecg_agg_update_parity on the device)");
+	else if (k > ECG_KMAX_K || rows > ECG_KMAX_R)
+		*rc = ecg_fail(-ECG_DER_INVAL, "queue: device cells need k <= %d and rows <= %d (k=%d rows=%d)",
+			       ECG_KMAX_K, ECG_KMAX_R, k, rows);
+	else
+		*rc = cells_checked(ctx, op, k, p, C, src, stripe, dst);
+	return dev;
+}
+
 static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const uint32_t *err,
 		  int nerrs, unsigned char *const *src, unsigned char *stripe,
 		  unsigned char *const *dst, int vec_i, ecg_done_cb_t cb, void *arg)
@@ -619,7 +758,10 @@ static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const u
 	struct qslot *s = NULL;
 	uint32_t idx;
 	int i, rc = 0;
+	const int dev = request_device(q, op, k, p, C, op == OP_RECOVER ? nerrs : p, src, stripe, dst, &rc);
 
+	if (rc)
+		return rc;
 	pthread_mutex_lock(&q->lock);
 	while (s == NULL) {
 		if (q->stop) {
@@ -627,15 +769,15 @@ static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const u
 			return ecg_fail(-ECG_DER_INVAL, "queue is being destroyed");
 		}
 		for (i = 0; i < q->nslot && s == NULL; i++)
-			if (slot_matches(&q->slot[i], op, k, p, C, err, nerrs))
+			if (slot_matches(&q->slot[i], op, k, p, C, err, nerrs, dev))
 				s = &q->slot[i];
 		/* open FREE slots from a rotating start: batches spread over the
 		 * devices of a multi-device queue */
 		for (i = 0; i < q->nslot && s == NULL; i++) {
 			struct qslot *f = &q->slot[(q->open_next + (uint32_t)i) % (uint32_t)q->nslot];
 
-			if (f->state == S_FREE) {
-				rc = slot_open(q, f, op, k, p, C, err, nerrs);
+			if (f->state == S_FREE && (dev < 0 || f->ctx->device == dev)) {
+				rc = slot_open(q, f, op, k, p, C, err, nerrs, dev);
 				if (rc) {
 					f->state = S_FREE;
 					pthread_mutex_unlock(&q->lock);
@@ -667,11 +809,20 @@ static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const u
 		r->nerrs = nerrs;
 		r->cb = cb;
 		r->arg = arg;
-		if (op == OP_UPDATE) {		/* the xor_gen: diff = old ^ new */
+		if (s->devcells) {		/* the stripe's ISA-L pointers, nothing copied */
+			uint64_t *t = s->tab + (size_t)idx * (uint64_t)(k + s->rows);
+
+			for (i = 0; i < k; i++)
+				t[i] = (uint64_t)(uintptr_t)(op == OP_ENCODE ? src[i]
+							     : stripe + (uint64_t)s->dec_idx[i] * C);
+			for (i = 0; i < s->rows; i++)
+				t[k + i] = (uint64_t)(uintptr_t)(op == OP_ENCODE ? dst[i]
+								 : stripe + (uint64_t)s->out_idx[i] * C);
+		} else if (op == OP_UPDATE) {	/* the xor_gen: diff = old ^ new */
 			xor_into(in, src[0], src[1], C);
 			s->host[(size_t)s->pitch * s->nin * s->cap + idx] = (unsigned char)vec_i;
 		}
-		for (i = 0; op != OP_UPDATE && i < k; i++) {
+		for (i = 0; !s->devcells && op != OP_UPDATE && i < k; i++) {
 			const unsigned char *from = op == OP_ENCODE ? src[i]
 					: stripe + (uint64_t)s->dec_idx[i] * C;
 
@@ -683,7 +834,11 @@ static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const u
 
 	pthread_mutex_lock(&q->lock);
 	s->filled++;
-	pthread_cond_signal(&q->cv_work);
+	/* wake the worker only for what it acts on: a closed slot whose copies
+	 * have all landed, a slot's first request (a new deadline to wait for;
+	 * for device cells, a batch that may launch at once) */
+	if ((s->state == S_READY && s->filled == s->reserved) || s->filled == 1)
+		pthread_cond_signal(&q->cv_work);
 	pthread_mutex_unlock(&q->lock);
 	return 0;
 }

@@ -188,7 +188,7 @@ int ecg_ptr_device(const void *p)
  * a pointer into host memory, another device or past an allocation's end
  * would make the launch fault the GPU, so it is refused here.  Cells of one
  * buffer (the usual stripe) cost one attribute and one range query in all. */
-static int cells_on_device(ecg_ctx_t *ctx, unsigned char *const *v, int n, int len, const char *what)
+int ecg_cells_on_device(ecg_ctx_t *ctx, unsigned char *const *v, int n, uint64_t len, const char *what)
 {
 	struct {
 		uintptr_t lo, hi;
@@ -213,8 +213,8 @@ static int cells_on_device(ecg_ctx_t *ctx, unsigned char *const *v, int n, int l
 			return ecg_fail(-ECG_DER_INVAL, "matmul_host: %s %d: no device allocation", what, i);
 		}
 		if (e > (uintptr_t)base + size)
-			return ecg_fail(-ECG_DER_INVAL, "matmul_host: %s %d: %d bytes run past the end of its "
-					"allocation", what, i, len);
+			return ecg_fail(-ECG_DER_INVAL, "matmul_host: %s %d: %llu bytes run past the end of its "
+					"allocation", what, i, (unsigned long long)len);
 		x = nseen < 4 ? nseen++ : i % 4;
 		seen[x].lo = (uintptr_t)base;
 		seen[x].hi = (uintptr_t)base + size;
@@ -303,9 +303,9 @@ static int matmul_device(ecg_ctx_t *ctx, int len, int k, int rows, const unsigne
 	hipError_t e;
 	int j, r, rc;
 
-	rc = cells_on_device(ctx, src, k, len, "source");
+	rc = ecg_cells_on_device(ctx, src, k, (uint64_t)len, "source");
 	if (rc == 0)
-		rc = cells_on_device(ctx, dst, rows, len, "output");
+		rc = ecg_cells_on_device(ctx, dst, rows, (uint64_t)len, "output");
 	if (rc == 0)
 		rc = pool_stream(ctx, &st);
 	if (rc == 0)

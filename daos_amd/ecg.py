@@ -725,7 +725,7 @@ DONE_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_int)
 class Queue:
     """ecg_queue_t: one-stripe requests from many threads -> batched launches.
     Completion is reported through a C callback; this wrapper records rc per
-    request id (callbacks run on the queue's worker thread)."""
+    request id (callbacks run on the queue's completion threads)."""
 
     def __init__(self, ctx, max_batch: int = 0, max_wait_us: int = 0, max_cell_bytes: int = 0):
         """ctx: a Context, or a Multi (slots spread over its devices)."""
@@ -751,6 +751,18 @@ class Queue:
         dp = (u8p * p)(*[_u8(d) for d in parity])
         self._keep[rid] = (data, parity)
         _chk(lib().ecg_queue_encode(self.h, k, p, C_, sp, dp, self._cb, rid + 1), "queue_encode")
+
+    def encode_ptrs(self, rid: int, k: int, p: int, cell_bytes: int, data_ptrs, parity_ptrs):
+        """ecg_queue_encode on cells given by address (device cells: batched
+        into pointer-table launches in place)."""
+        sp = (u8p * k)(*[C.cast(C.c_void_p(a), u8p) for a in data_ptrs])
+        dp = (u8p * p)(*[C.cast(C.c_void_p(a), u8p) for a in parity_ptrs])
+        _chk(lib().ecg_queue_encode(self.h, k, p, cell_bytes, sp, dp, self._cb, rid + 1), "queue_encode")
+
+    def recover_ptr(self, rid: int, k: int, p: int, cell_bytes: int, stripe_ptr: int, err_list):
+        """ecg_queue_recover on a [k+p][cell] stripe given by address."""
+        _chk(lib().ecg_queue_recover(self.h, k, p, cell_bytes, C.cast(C.c_void_p(stripe_ptr), u8p),
+                                     _u32(err_list), len(err_list), self._cb, rid + 1), "queue_recover")
 
     def recover(self, rid: int, k: int, p: int, stripe: np.ndarray, err_list):
         C_ = stripe.shape[-1]

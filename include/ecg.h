@@ -217,7 +217,12 @@ int ecg_recover_host(ecg_ctx_t *ctx, int k, int p, uint64_t cell_bytes, uint32_t
  * erasure set) into one device batch, and completes each request through its
  * callback -- the place DAOS sets its ABT_eventual (srv_ec_aggregate.c:696).
  * Host buffers must stay valid until the callback runs.  Callbacks run on the
- * queue's worker thread and must not block on the queue. */
+ * queue's completion threads and must not block on the queue.
+ * Cells may be host memory (staged through the queue's pinned slots, PCIe
+ * both ways) or, for encode and recover, device memory of one of the queue's
+ * devices (k <= 16): such requests batch into one pointer-table launch on the
+ * cells in place, and a batch launches as soon as the device has none of the
+ * queue's in flight -- a lone request does not wait max_wait_us. */
 typedef struct ecg_queue ecg_queue_t;
 typedef void (*ecg_done_cb_t)(void *arg, int rc);
 
@@ -231,12 +236,14 @@ typedef struct ecg_queue_attr {
 int ecg_queue_create(ecg_ctx_t *ctx, const ecg_queue_attr_t *attr, ecg_queue_t **q);
 /* Drains outstanding requests (their callbacks run) then frees the queue. */
 void ecg_queue_destroy(ecg_queue_t *q);
-/* Encode one stripe: data[k] -> parity[p] (host pointers, cell_bytes each). */
+/* Encode one stripe: data[k] -> parity[p] (cell_bytes each; host, or device
+ * memory of one of the queue's devices). */
 int ecg_queue_encode(ecg_queue_t *q, int k, int p, uint64_t cell_bytes,
 		     unsigned char *const *data, unsigned char *const *parity,
 		     ecg_done_cb_t cb, void *arg);
-/* Recover one stripe in place: `stripe` is [k+p][cell_bytes] host memory in
- * logical cell order; err_list holds the erased logical cells. */
+/* Recover one stripe in place: `stripe` is [k+p][cell_bytes] in logical cell
+ * order (host, or device memory of one of the queue's devices); err_list
+ * holds the erased logical cells. */
 int ecg_queue_recover(ecg_queue_t *q, int k, int p, uint64_t cell_bytes, unsigned char *stripe,
 		      const uint32_t *err_list, int nerrs, ecg_done_cb_t cb, void *arg);
 /* Aggregation delta update of one stripe's parity (agg_update_parity:
@@ -244,7 +251,8 @@ int ecg_queue_recover(ecg_queue_t *q, int k, int p, uint64_t cell_bytes, unsigne
  * srv_ec_aggregate.c:1086-1102):  parity[r] ^= coef[r][vec_i] * (old ^ new)
  * for the p parity cells (host memory, updated in place when the callback
  * runs).  Requests of one (k, p, cell size) batch together whatever their
- * vec_i.  k <= 16. */
+ * vec_i.  k <= 16; host cells only (-DER_NOSYS for device cells: ecg_update
+ * / ecg_agg_update_parity run them on the device). */
 int ecg_queue_update(ecg_queue_t *q, int k, int p, uint64_t cell_bytes, int vec_i,
 		     const unsigned char *old_cell, const unsigned char *new_cell,
 		     unsigned char *const *parity, ecg_done_cb_t cb, void *arg);

@@ -742,6 +742,133 @@ def test_queue_mixed_classes_and_recovery(ctx, oracle, ecglib):
     q.close()
 
 
+def test_queue_device_cells_batched_in_place(ctx, oracle, ecglib):
+    """Device-cell requests (an engine whose buffers live in HBM): 8 threads x
+    24 one-stripe EC_8P2 encodes and {d0, d9} recoveries on device stripes --
+    some at odd byte offsets -- interleaved with host-cell encodes in the
+    same queue.  Device batches are pointer-table launches on the cells in
+    place; every byte equals the oracle's."""
+    import threading
+
+    k, p, C_, per = 8, 2, 32768 + 40, 24
+    en = oracle.cauchy1(k, p)
+    T = 8
+    S = T * per
+    slot = (k + p) * C_ + 64
+    data = rand((S, k, C_), 8100)
+    par = np.stack([oracle.encode_data(en[k:], data[s]) for s in range(S)])          # [S][p][C]
+    skew = [(s * 7) % 16 for s in range(S)]
+    img = np.zeros(S * slot, dtype=np.uint8)
+    for s in range(S):
+        base = s * slot + skew[s]
+        img[base: base + k * C_] = data[s].reshape(-1)
+        if s % 2:                      # recovery stripes: parity present, d0 and d9 erased below
+            img[base + k * C_: base + (k + p) * C_] = par[s].reshape(-1)
+            img[base: base + C_] = 0
+            img[base + (k + 1) * C_: base + (k + 2) * C_] = 0
+    dbuf = ctx.to_device(img)
+    q = ecglib.Queue(ctx, max_batch=64, max_wait_us=100000)
+    host_jobs = {}
+    try:
+        def worker(t):
+            for i in range(per):
+                s = t * per + i
+                base = dbuf.ptr + s * slot + skew[s]
+                if s % 2:
+                    q.recover_ptr(s, k, p, C_, base, [0, 9])
+                else:
+                    q.encode_ptrs(s, k, p, C_, [base + j * C_ for j in range(k)],
+                                  [base + (k + r) * C_ for r in range(p)])
+                if i % 6 == 0:         # a host-cell request of the same class in between
+                    rid = 100000 + s
+                    hd = [rand(C_, rid + j) for j in range(k)]
+                    ho = [np.zeros(C_, dtype=np.uint8) for _ in range(p)]
+                    host_jobs[rid] = (hd, ho)
+                    q.encode(rid, k, p, hd, ho)
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        q.flush()
+        nreq, nbatch = q.stats()
+        assert nreq == S + len(host_jobs) and all(rc == 0 for rc in q.done.values()), q.done
+        # device batches launch whenever the device is idle (latency first),
+        # so only requests that arrive while a batch runs coalesce
+        assert nbatch < nreq, (nreq, nbatch)
+        got = dbuf.download()
+        for s in range(S):
+            base = s * slot + skew[s]
+            stripe = got[base: base + (k + p) * C_].reshape(k + p, C_)
+            assert np.array_equal(stripe[:k], data[s]), s
+            assert np.array_equal(stripe[k:], par[s]), s
+        for rid, (hd, ho) in host_jobs.items():
+            assert np.array_equal(np.stack(ho), oracle.encode_data(en[k:], np.stack(hd))), rid
+    finally:
+        q.close()
+        dbuf.free()
+
+
+def test_queue_device_cell_alone_launches_at_once(ctx, oracle, ecglib):
+    """A lone device-cell request does not wait max_wait_us for company: its
+    slot closes as soon as the device has no batch of the queue in flight."""
+    import time
+
+    k, p, C_ = 4, 2, 65536
+    data = rand((k, C_), 8200)
+    dbuf = ctx.to_device(np.concatenate([data, np.zeros((p, C_), np.uint8)]))
+    q = ecglib.Queue(ctx, max_batch=256, max_wait_us=5000000)      # host classes would wait 5 s
+    try:
+        t0 = time.perf_counter()
+        q.encode_ptrs(1, k, p, C_, [dbuf.ptr + j * C_ for j in range(k)],
+                      [dbuf.ptr + (k + r) * C_ for r in range(p)])
+        while 1 not in q.done and time.perf_counter() - t0 < 2.0:
+            time.sleep(0.0005)
+        assert q.done.get(1) == 0, "not completed within 2 s"
+        assert time.perf_counter() - t0 < 1.0
+        got = dbuf.download().reshape(k + p, C_)
+        assert np.array_equal(got[k:], oracle.encode_data(oracle.cauchy1(k, p)[k:], data))
+    finally:
+        q.close()
+        dbuf.free()
+
+
+def test_queue_device_cell_errors(ctx, ecglib):
+    """Device cells: updates are not queued (-DER_NOSYS), a cell running past
+    its allocation and more than 16 data cells are refused (-DER_INVAL) --
+    before anything reaches the GPU."""
+    L = ecglib.lib()
+    k, p, C_ = 8, 2, 4096
+    dbuf = ctx.alloc((k + p) * C_)
+    q = ecglib.Queue(ctx)
+    try:
+        dp = (ecglib.u8p * p)(*[C.cast(C.c_void_p(dbuf.ptr + (k + r) * C_), ecglib.u8p) for r in range(p)])
+        old = C.cast(C.c_void_p(dbuf.ptr), ecglib.u8p)
+        new = C.cast(C.c_void_p(dbuf.ptr + C_), ecglib.u8p)
+        rc = L.ecg_queue_update(q.h, k, p, C_, 0, old, new, dp, None, None)
+        assert rc == -ecglib.DER_NOSYS, rc
+        sp = (ecglib.u8p * k)(*[C.cast(C.c_void_p(dbuf.ptr + j * C_ + (C_ // 2 if j == k - 1 else 0)),
+                                       ecglib.u8p) for j in range(k)])
+        dp_bad = (ecglib.u8p * p)(*[C.cast(C.c_void_p(dbuf.ptr + (k + p) * C_ - C_ // 2 if r == p - 1 else
+                                                      dbuf.ptr + (k + r) * C_), ecglib.u8p) for r in range(p)])
+        rc = L.ecg_queue_encode(q.h, k, p, C_, sp, dp_bad, None, None)
+        assert rc == -ecglib.DER_INVAL, rc
+        big = ctx.alloc(20 * C_)
+        try:
+            sp20 = (ecglib.u8p * 18)(*[C.cast(C.c_void_p(big.ptr + j * C_), ecglib.u8p) for j in range(18)])
+            dp20 = (ecglib.u8p * 2)(*[C.cast(C.c_void_p(big.ptr + (18 + r) * C_), ecglib.u8p) for r in range(2)])
+            rc = L.ecg_queue_encode(q.h, 18, 2, C_, sp20, dp20, None, None)
+            assert rc == -ecglib.DER_INVAL, rc
+        finally:
+            big.free()
+        q.flush()
+        assert q.stats()[0] == 0
+    finally:
+        q.close()
+        dbuf.free()
+
+
 def test_queue_destroy_drains(ctx, oracle, ecglib):
     k, p, C_ = 2, 1, 4096
     q = ecglib.Queue(ctx, max_batch=1000, max_wait_us=1000000)   # would wait 1 s for company

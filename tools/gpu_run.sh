@@ -148,11 +148,11 @@ for what in "$@"; do
 		make -s -C tests/c dropin_bench > /dev/null || exit 2
 		step dropin_bench 600 ./build/ctest/dropin_bench || exit $?
 		;;
-	qdev)             # device-cell drop-in calls from T threads (tools/queue_bench.c device)
+	qdev)             # device-cell drop-in calls and queue requests from T threads (tools/queue_bench.c device)
 		make -s -C tests/c queue_bench > /dev/null || exit 2
-		for C in 131072 1048576; do
+		for C in 32768 131072 1048576; do
 			for T in 1 2 4 8 16; do
-				step qdev_${C}_$T 120 ./build/ctest/queue_bench $C $T device || exit $?
+				step qdev_${C}_$T 120 ./build/ctest/queue_bench $C $T device $((C > 131072 ? 128 : 1024)) || exit $?
 			done
 		done
 		;;

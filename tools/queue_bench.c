@@ -16,9 +16,12 @@
  *   cpu  : diff loop + ref_simd_encode_data(k = 1, the vec_i column) XORed
  *          into the parity (ISA-L-equivalent CPU restatement)
  * and GiB/s counts the updated cell bytes.  With "device" the cells live in
- * device memory and only the drop-in runs (ec_encode_data on device cells,
- * in place, the calling threads spread over the context's drop-in stream
- * pool, each call waiting for its own launch).  Bench infrastructure.
+ * device memory: the drop-in (ec_encode_data on device cells, in place, the
+ * calling threads spread over the context's drop-in stream pool, each call
+ * waiting for its own launch) and the queue (device-cell requests batched
+ * into pointer-table launches in place).
+ * usage: queue_bench C T [update|device] [stripes per thread, default 64].
+ * Bench infrastructure.
  */
 #include <pthread.h>
 #include <stdio.h>
@@ -176,11 +179,15 @@ int main(int argc, char **argv)
 		T = atoi(argv[2]);
 	g_update = argc > 3 && strcmp(argv[3], "update") == 0;
 	const int device = argc > 3 && strcmp(argv[3], "device") == 0;
-	g_cells = malloc((size_t)T * N * (K + P) * CB);
-	g_new = malloc((size_t)T * N * CB);
-	for (size_t i = 0; i < (size_t)T * N * (K + P) * CB; i++)
+	if (argc > 4)
+		N = atoi(argv[4]);	/* stripes per thread (device cells: HBM holds many) */
+	if (N < 1 || T < 1 || T > 64)
+		return 2;
+	g_cells = malloc(device ? 1 : (size_t)T * N * (K + P) * CB);
+	g_new = malloc(device ? 1 : (size_t)T * N * CB);
+	for (size_t i = 0; !device && i < (size_t)T * N * (K + P) * CB; i++)
 		g_cells[i] = (unsigned char)(i * 2654435761u >> 13);
-	for (size_t i = 0; i < (size_t)T * N * CB; i++)
+	for (size_t i = 0; !device && i < (size_t)T * N * CB; i++)
 		g_new[i] = (unsigned char)(i * 40503u >> 7);
 	gf_gen_cauchy1_matrix(en, K + P, K);
 	ec_init_tables(K, P, &en[K * K], g_tbls);
@@ -195,7 +202,7 @@ int main(int argc, char **argv)
 		void *d = NULL;
 		const size_t nb = (size_t)T * N * (K + P) * CB;
 
-		if (ecg_dev_alloc(ctx, nb, &d) || ecg_memcpy(ctx, d, g_cells, nb, 0, NULL) ||
+		if (ecg_dev_alloc(ctx, nb, &d) || ecg_memset(ctx, d, 0x5A, nb, NULL) ||
 		    ecg_stream_sync(ctx, NULL)) {
 			fprintf(stderr, "device cells: %s\n", ecg_strerror());
 			return 1;
@@ -203,9 +210,24 @@ int main(int argc, char **argv)
 		g_dcells = d;
 		run(0);
 		isal = run(0);
+		run(1);
+		queue = run(1);
+		ecg_queue_stats(g_q, &reqs, &batches);
+		if (getenv("QB_REPS")) {	/* spread of repeated queue runs */
+			for (int r = atoi(getenv("QB_REPS")); r > 0; r--) {
+				uint64_t r0 = reqs, b0 = batches;
+				const double v = run(1);
+
+				ecg_queue_stats(g_q, &reqs, &batches);
+				fprintf(stderr, "queue run: %.2f GiB/s, %llu requests in %llu batches\n", v,
+					(unsigned long long)(reqs - r0), (unsigned long long)(batches - b0));
+			}
+		}
 		printf("{\"op\": \"encode\", \"cells\": \"device\", \"k\": %d, \"p\": %d, \"cell_bytes\": %llu, "
-		       "\"threads\": %d, \"stripes_per_thread\": %d, \"isal_one_stripe_GiBps\": %.2f}\n", K, P,
-		       (unsigned long long)CB, T, N, isal);
+		       "\"threads\": %d, \"stripes_per_thread\": %d, \"isal_one_stripe_GiBps\": %.2f, "
+		       "\"queue_GiBps\": %.2f, \"queue_requests\": %llu, \"queue_batches\": %llu}\n", K, P,
+		       (unsigned long long)CB, T, N, isal, queue, (unsigned long long)reqs,
+		       (unsigned long long)batches);
 		ecg_dev_free(ctx, d);
 		ecg_queue_destroy(g_q);
 		ecg_ctx_destroy(ctx);
