@@ -323,3 +323,96 @@ def test_random_dropin_calls(ctx, oracle, ecglib):
     finally:
         ecglib.set_dropin_crossover(old)
     assert routes >= {(True, True), (False, True), (False, False)}, routes
+
+
+@pytest.mark.gpu
+def test_random_queue_requests(ctx, oracle, ecglib):
+    """Seeded random one-stripe requests posted to one ecg_queue from 6
+    threads at once: encodes and recoveries on host or device cells (device
+    stripes at random byte offsets in one shared allocation, so the queue's
+    device slots batch them into pointer-table launches) and host-cell delta
+    updates, EC classes 2+1 .. 16+3, cell sizes 1 byte .. 40 KiB.  After one
+    flush every request's callback reported 0 and every output equals the
+    oracle's."""
+    import threading
+
+    rng = np.random.default_rng(0xB47)
+    classes = [(2, 1), (4, 2), (8, 2), (8, 3), (16, 2), (16, 3)]
+    sizes = [1, 31, 4096, 4100, 12288, 40000]
+    jobs = []
+    for case in range(144):
+        k, p = classes[int(rng.integers(0, len(classes)))]
+        Cb = int(rng.choice(sizes))
+        op = ("encode", "recover", "update")[case % 3]
+        device = op != "update" and bool(rng.integers(0, 2))
+        data = rng.integers(0, 256, (k, Cb), dtype=np.uint8)
+        par = oracle.encode_data(oracle.cauchy1(k, p)[k:], data)
+        job = {"op": op, "k": k, "p": p, "C": Cb, "device": device, "data": data, "par": par}
+        if op == "recover":
+            nerr = int(rng.integers(1, p + 1))
+            job["err"] = sorted(int(x) for x in rng.choice(k + p, nerr, replace=False))
+        if op == "update":
+            job["vec_i"] = int(rng.integers(0, k))
+            job["new"] = rng.integers(0, 256, Cb, dtype=np.uint8)
+        jobs.append(job)
+    # device stripes: each [k+p][C] image at a random byte offset of its own slot in one allocation
+    slots = [(k + p) * Cb + 64 for j in jobs for k, p, Cb in [(j["k"], j["p"], j["C"])]]
+    base = np.cumsum([0] + slots[:-1])
+    img = np.zeros(int(sum(slots)), dtype=np.uint8)
+    for j, b in zip(jobs, base):
+        j["off"] = int(b) + int(rng.integers(0, 16))
+        stripe = np.concatenate([j["data"], j["par"]])
+        if j["op"] == "recover":
+            stripe = stripe.copy()
+            stripe[j["err"]] = 0xA5
+        elif j["op"] == "encode":
+            stripe = np.concatenate([j["data"], np.zeros_like(j["par"])])
+        j["host"] = stripe.copy()            # host-cell requests work on their own arrays
+        img[j["off"]: j["off"] + stripe.size] = stripe.reshape(-1)
+    dev = ctx.to_device(img)
+    q = ecglib.Queue(ctx, max_batch=32, max_wait_us=200)
+    try:
+        def worker(t):
+            for i in range(t, len(jobs), 6):
+                j = jobs[i]
+                k, p, Cb = j["k"], j["p"], j["C"]
+                if j["op"] == "update":
+                    h = j["host"]
+                    q.update(i, k, p, j["vec_i"], h[j["vec_i"]], j["new"], [h[k + r] for r in range(p)])
+                elif j["device"]:
+                    a = dev.ptr + j["off"]
+                    if j["op"] == "encode":
+                        q.encode_ptrs(i, k, p, Cb, [a + c * Cb for c in range(k)],
+                                      [a + (k + r) * Cb for r in range(p)])
+                    else:
+                        q.recover_ptr(i, k, p, Cb, a, j["err"])
+                elif j["op"] == "encode":
+                    h = j["host"]
+                    q.encode(i, k, p, [h[c] for c in range(k)], [h[k + r] for r in range(p)])
+                else:
+                    q.recover(i, k, p, j["host"], j["err"])
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(6)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        q.flush()
+        assert len(q.done) == len(jobs) and all(rc == 0 for rc in q.done.values()), q.done
+        got = dev.download()
+        for i, j in enumerate(jobs):
+            k, p, Cb = j["k"], j["p"], j["C"]
+            if j["op"] == "update":
+                d2 = j["data"].copy()
+                d2[j["vec_i"]] = j["new"]
+                want = oracle.encode_data(oracle.cauchy1(k, p)[k:], d2)
+                assert np.array_equal(j["host"][k:], want), (i, j["op"])
+                continue
+            out = got[j["off"]: j["off"] + (k + p) * Cb].reshape(k + p, Cb) if j["device"] else j["host"]
+            assert np.array_equal(out[:k], j["data"]), (i, j["op"], j["device"])
+            assert np.array_equal(out[k:], j["par"]), (i, j["op"], j["device"], k, p, Cb)
+        nreq, nbatch = q.stats()
+        assert nreq == len(jobs) and nbatch < nreq
+    finally:
+        q.close()
+        dev.free()
