@@ -308,6 +308,46 @@ static void isal_threads(const char *what)
 	}
 }
 
+/* device-cell requests to one queue from several pthreads: thread t posts
+ * stripes t, t + NQT, ... -- encodes of even stripes, {d1, p0} recoveries of
+ * odd ones -- with device pointers (the queue batches them into pointer-
+ * table launches in place) */
+enum { NQT = 4 };
+struct qdev_job {
+	ecg_queue_t *q;
+	unsigned char *d;		/* device image: stripe s at s * sst + off(s) */
+	int k, p, S, t;
+	uint64_t C;
+	size_t sst;
+	struct qdone *qd;
+	int fails;
+};
+
+static size_t qdev_off(int s)
+{
+	return (size_t)(s * 5) % 16;
+}
+
+static void *qdev_thread(void *arg)
+{
+	struct qdev_job *j = arg;
+	static const uint32_t err[2] = {1, 8};
+
+	for (int s = j->t; s < j->S; s += NQT) {
+		unsigned char *base = j->d + (size_t)s * j->sst + qdev_off(s), *data[16], *par[8];
+
+		for (int c = 0; c < j->k; c++)
+			data[c] = base + c * j->C;
+		for (int r = 0; r < j->p; r++)
+			par[r] = base + (j->k + r) * j->C;
+		if ((s & 1) == 0)
+			j->fails += ecg_queue_encode(j->q, j->k, j->p, j->C, data, par, qcb, j->qd) != 0;
+		else
+			j->fails += ecg_queue_recover(j->q, j->k, j->p, j->C, base, err, 2, qcb, j->qd) != 0;
+	}
+	return NULL;
+}
+
 static void device_checks(void)
 {
 	const uint64_t crossover = ecg_dropin_crossover();
@@ -421,6 +461,72 @@ static void device_checks(void)
 		}
 		ecg_queue_destroy(q);
 		free(cells);
+	}
+	/* the same queue API on device cells, from NQT pthreads */
+	{
+		ecg_queue_t *q = NULL;
+		struct qdone qd = {PTHREAD_MUTEX_INITIALIZER, 0, 0};
+		const int k = 8, p = 2, S = 48;
+		const uint64_t C = 8192 + 4;
+		const size_t sst = (size_t)(k + p) * C + 16;
+		unsigned char *h = malloc(S * sst), *g = malloc(S * sst), en[10 * 8], tb[8 * 2 * 32];
+		pthread_t qth[NQT];
+		struct qdev_job jobs[NQT];
+		void *d = NULL;
+
+		fill(h, S * sst);
+		ref_gf_gen_cauchy1_matrix(en, k + p, k);
+		ref_ec_init_tables(k, p, &en[k * k], tb);
+		for (int s = 0; s < S; s++) {		/* odd stripes: true parity, then d1 / p0 erased */
+			unsigned char *b = h + (size_t)s * sst + qdev_off(s), *src[8], *dst[2];
+
+			if ((s & 1) == 0)
+				continue;
+			for (int c = 0; c < k; c++)
+				src[c] = b + c * C;
+			dst[0] = b + k * C;
+			dst[1] = b + (k + 1) * C;
+			ref_ec_encode_data((int)C, k, p, tb, src, dst);
+		}
+		memcpy(g, h, S * sst);			/* g: the expected image */
+		for (int s = 0; s < S; s++) {
+			unsigned char *b = h + (size_t)s * sst + qdev_off(s), *src[8], *dst[2];
+
+			if (s & 1) {
+				memset(b + 1 * C, 0, C);
+				memset(b + 8 * C, 0, C);
+				continue;
+			}
+			b = g + (size_t)s * sst + qdev_off(s);
+			for (int c = 0; c < k; c++)
+				src[c] = b + c * C;
+			dst[0] = b + k * C;
+			dst[1] = b + (k + 1) * C;
+			ref_ec_encode_data((int)C, k, p, tb, src, dst);
+		}
+		CHECK(ecg_dev_alloc(ctx, S * sst, &d) == 0 && ecg_memcpy(ctx, d, h, S * sst, 0, NULL) == 0 &&
+		      ecg_stream_sync(ctx, NULL) == 0, "device image");
+		CHECK(ecg_queue_create(ctx, NULL, &q) == 0, "queue_create (device cells)");
+		for (int t = 0; t < NQT && q && d; t++) {
+			jobs[t] = (struct qdev_job){q, d, k, p, S, t, C, sst, &qd, 0};
+			pthread_create(&qth[t], NULL, qdev_thread, &jobs[t]);
+		}
+		for (int t = 0; t < NQT && q && d; t++) {
+			pthread_join(qth[t], NULL);
+			CHECK(jobs[t].fails == 0, "device-cell queue thread %d: %d refused", t, jobs[t].fails);
+		}
+		if (q) {
+			CHECK(ecg_queue_flush(q) == 0 && qd.done == S && qd.bad == 0, "device-cell queue done %d bad %d",
+			      qd.done, qd.bad);
+			ecg_queue_destroy(q);
+		}
+		CHECK(ecg_memcpy(ctx, h, d, S * sst, 1, NULL) == 0 && ecg_stream_sync(ctx, NULL) == 0, "d2h 3");
+		for (int s = 0; s < S; s++)
+			CHECK(memcmp(h + (size_t)s * sst + qdev_off(s), g + (size_t)s * sst + qdev_off(s),
+				     (size_t)(k + p) * C) == 0, "device-cell queue stripe %d", s);
+		ecg_dev_free(ctx, d);
+		free(h);
+		free(g);
 	}
 	ecg_ctx_destroy(ctx);
 }

@@ -2,7 +2,7 @@
 C, plain, with ASan/UBSan and with ThreadSanitizer on the host code, checked
 against the oracle.  Without a GPU only its host-side checks run; under -m
 gpu the device paths (concurrent ISA-L calls from 12 pthreads, batched
-encode/recover, queue).  The TSan build runs host-side only: on the GPU boxes
+encode/recover, queue on host cells and on device cells from 4 pthreads).  The TSan build runs host-side only: on the GPU boxes
 its runtime (gcc 11) aborts at start-up on the kernel's high-entropy mmap
 layout ("unexpected memory mapping"), with or without PIE."""
 import os
