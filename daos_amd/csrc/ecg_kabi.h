@@ -62,8 +62,7 @@ typedef struct ecg_launch_cfg {
 	uint32_t grid_x;	/* chunks per stripe handled in parallel */
 	uint32_t grid_y;	/* stripes handled in parallel */
 	uint32_t variant;	/* 0 auto, 1 force generic, 2 force byte kernel, 3 dword
-				 * lanes at any alignment (hardware unaligned access),
-				 * 4 16-byte lanes at any alignment (the same) */
+				 * lanes at any alignment (hardware unaligned access) */
 	uint32_t order;		/* 0 = 2D grid x columns / y stripes; 1-3 1D orders (ecg_kernels.hip) */
 	uint32_t wg_per_cu;	/* product kernel blocks per CU: 0 = per-shape default, 1..16 = cap,
 				 * ECG_WG_UNCAPPED = none (ecg_kernels.hip mm_wg_cap) */

@@ -440,13 +440,8 @@ extern "C" int ecg_k_launch_matmul(const ecg_mm_params_t *p, const ecg_launch_cf
 		g = 0;		// the device serves no misaligned dwords: bytewise
 	else if (variant == 3 && g < 4)
 		g = 4;		// A/B: misaligned source dwords loaded as they are
-	else if (variant == 4 && g < 16)
-		g = 16;		// A/B: misaligned operands as dwordx4 accesses as they are
-	else if ((variant == 0 || variant == 5) && g < 16 && !(cfg && cfg->no_unaligned) && src_off16(p) &&
-		 has_g2(p))
+	else if (variant == 0 && g < 16 && !(cfg && cfg->no_unaligned) && src_off16(p) && has_g2(p))
 		g = 2;		// k = 8, sources off a 16-byte boundary: funnel-shifted 16-byte lanes
-	else if (variant == 5 && g == 4 && has_g2(p))
-		g = 2;		// A/B: the same when only destinations are off
 	if (variant == 2 || g == 0) {
 		uint64_t total = p->cell_bytes * p->nstripes;
 		uint64_t blocks = (total + BLOCK - 1) / BLOCK;

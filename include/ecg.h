@@ -312,8 +312,7 @@ int ecg_get_stats(ecg_ctx_t *ctx, ecg_stats_t *out, int reset);
 /* ---- launch tuning (benchmarks; 0 = default) ----------------------------
  * variant: 0 auto, 1 runtime-shaped kernel, 2 byte kernel, 3 dword lanes
  * whatever the operands' alignment (misaligned dword accesses served by the
- * hardware's unaligned access mode; A/B only), 4 the same with 16-byte lanes
- * (misaligned dwordx4 accesses; A/B only). */
+ * hardware's unaligned access mode; A/B only). */
 int ecg_set_launch(ecg_ctx_t *ctx, uint32_t grid_x, uint32_t grid_y, uint32_t variant);
 /* Block -> (stripe, 4 KiB column) mapping of the product kernel: 0 = 2D
  * grid (columns x stripes, default); 1 = 1D stripe-fastest; 2 = 1D with each
