@@ -242,14 +242,13 @@ __device__ __forceinline__ void mm_load_any(const ecg_mm_params_t &P, int k, uin
 // 0.859), encode 0.844 -> 0.831, the dword-lane (G = 4) variant 0.895 ->
 // 0.887.  The funnel-shift kernels (G = 1) spill when phased.  k = 16 in
 // phases of 4 lost 5-20 % at 4 or 5 waves (phases of 8 spill).
-#ifndef ECG_G2_PHASE
-#define ECG_G2_PHASE 0
-#endif
+// (The g2 lanes run one phase: two phases of 4 measured the same,
+// profiles/r05/unaligned_ab/g2_phased.log.)
 #ifndef ECG_MM_PHASE
-#define ECG_MM_PHASE(K, G) ((K) == 8 && ((G) == 16 || (G) == 4) ? 4 : (K) == 8 && (G) == 2 ? ECG_G2_PHASE : 0)
+#define ECG_MM_PHASE(K, G) ((K) == 8 && ((G) == 16 || (G) == 4) ? 4 : 0)
 #endif
 #ifndef ECG_MM_WPE
-#define ECG_MM_WPE(K, R, G) ((K) == 8 && ((G) == 16 || (G) == 4 || ((G) == 2 && ECG_G2_PHASE)) ? 4 : 0)
+#define ECG_MM_WPE(K, R, G) ((K) == 8 && ((G) == 16 || (G) == 4) ? 4 : 0)
 #endif
 
 // The product of one column: x[j] = the lane's 16 bytes of cell j.  STORE =
