@@ -61,6 +61,8 @@
 #define NSLOT_MAX 32
 #define NFIN 4		/* completion threads: output scatter + callbacks */
 #define NDSTLOCK 64	/* striped locks serialising update deltas into one parity cell */
+#define RES_OPEN (1ull << 31)
+#define RES_CNT (RES_OPEN - 1)
 
 enum slot_state { S_FREE, S_FILLING, S_READY, S_INFLIGHT, S_DONE };
 
@@ -84,7 +86,16 @@ struct qslot {
 	uint32_t dec_idx[ECG_MAX_K], out_idx[ECG_MAX_P];
 	int nin;			/* input cells staged per request (k, or 1 for updates) */
 	/* fill state */
-	uint32_t cap, reserved, filled;
+	uint32_t cap;
+	/* Reservations without the queue lock: res = generation << 32 | RES_OPEN
+	 * | requests reserved, CAS-incremented by submitters while the slot is
+	 * open (FILLING), its open bit cleared by the worker when it closes the
+	 * slot -- which fixes `reserved`.  The generation changes at every
+	 * slot_open, so a submitter that checked the class of an earlier
+	 * opening cannot reserve in a reopened slot.  `filled` counts requests
+	 * whose inputs are in (atomic). */
+	uint64_t res;
+	uint32_t reserved, filled;
 	uint32_t fin_next, fin_done;	/* completion progress (S_DONE) */
 	uint64_t t_open_ns;
 	struct qreq *reqs;		/* cap entries */
@@ -150,14 +161,49 @@ static uint64_t pitch_of(uint64_t C)
 	return (C + 63) & ~63ull;
 }
 
-/* dev: the cells' device (device-cell requests), -1 for host cells */
-static int slot_matches(const struct qslot *s, int op, int k, int p, uint64_t C,
-			const uint32_t *err, int nerrs, int dev)
+/* The slot's class is the request's.  dev: the cells' device (device-cell
+ * requests), -1 for host cells.  Read without the lock by the reservation
+ * fast path: a slot reopened meanwhile fails that path's CAS (generation). */
+static int class_matches(const struct qslot *s, int op, int k, int p, uint64_t C,
+			 const uint32_t *err, int nerrs, int dev)
 {
-	return s->state == S_FILLING && s->reserved < s->cap && s->op == op && s->k == k &&
-	       s->p == p && s->C == C && s->nerrs == nerrs && s->devcells == (dev >= 0) &&
-	       (dev < 0 || s->ctx->device == dev) &&
+	return s->op == op && s->k == k && s->p == p && s->C == C && s->nerrs == nerrs &&
+	       s->devcells == (dev >= 0) && (dev < 0 || s->ctx->device == dev) &&
 	       (op != OP_RECOVER || memcmp(s->err, err, sizeof(uint32_t) * nerrs) == 0);
+}
+
+/* Reserve a request index in an open slot of this class; 0 if it is not
+ * open, not this class or full. */
+static int slot_try_reserve(struct qslot *s, int op, int k, int p, uint64_t C, const uint32_t *err,
+			    int nerrs, int dev, uint32_t *idx)
+{
+	uint64_t w = __atomic_load_n(&s->res, __ATOMIC_ACQUIRE);
+	const uint64_t gen = w >> 32;
+
+	if (!(w & RES_OPEN) || !class_matches(s, op, k, p, C, err, nerrs, dev))
+		return 0;
+	/* the class was checked for this opening (generation) only */
+	while ((w >> 32) == gen && (w & RES_OPEN) && (uint32_t)(w & RES_CNT) < s->cap) {
+		if (__atomic_compare_exchange_n(&s->res, &w, w + 1, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
+			*idx = (uint32_t)(w & RES_CNT);
+			return 1;
+		}
+	}
+	return 0;
+}
+
+static uint32_t res_count(const struct qslot *s)
+{
+	return (uint32_t)(__atomic_load_n(&s->res, __ATOMIC_ACQUIRE) & RES_CNT);
+}
+
+/* FILLING -> READY (lock held): no reservation after this one. */
+static void slot_close(struct qslot *s)
+{
+	const uint64_t w = __atomic_fetch_and(&s->res, ~RES_OPEN, __ATOMIC_ACQ_REL);
+
+	s->reserved = (uint32_t)(w & RES_CNT);
+	s->state = S_READY;
 }
 
 /* Assign a FREE slot to a class: decode rows for recovery, capacity from the
@@ -205,10 +251,12 @@ static int slot_open(struct ecg_queue *q, struct qslot *s, int op, int k, int p,
 	if (op == OP_UPDATE)
 		s->out_off += ((size_t)s->cap + 63) & ~(size_t)63;
 	s->reserved = 0;
-	s->filled = 0;
+	__atomic_store_n(&s->filled, 0u, __ATOMIC_RELAXED);
 	s->rc = 0;
 	s->t_open_ns = now_ns();
 	s->state = S_FILLING;
+	/* the class above is published with the open bit */
+	__atomic_store_n(&s->res, ((s->res >> 32) + 1) << 32 | RES_OPEN, __ATOMIC_RELEASE);
 	return 0;
 }
 
@@ -235,11 +283,13 @@ static void close_due_slots(struct ecg_queue *q, uint64_t t, int force)
 	for (int i = 0; i < q->nslot; i++) {
 		struct qslot *s = &q->slot[i];
 
-		if (s->state == S_FILLING && s->reserved > 0 &&
-		    (force || s->reserved == s->cap ||
+		uint32_t n;
+
+		if (s->state == S_FILLING && (n = res_count(s)) > 0 &&
+		    (force || n >= s->cap ||
 		     t >= s->t_open_ns + (uint64_t)q->attr.max_wait_us * 1000ull ||
 		     (s->devcells && !device_busy(q, s->ctx))))
-			s->state = S_READY;
+			slot_close(s);
 	}
 }
 
@@ -461,7 +511,7 @@ static void *worker_main(void *argp)
 		for (int i = 0; i < q->nslot; i++) {
 			struct qslot *s = &q->slot[i];
 
-			if (s->state == S_READY && s->filled == s->reserved) {
+			if (s->state == S_READY && __atomic_load_n(&s->filled, __ATOMIC_ACQUIRE) == s->reserved) {
 				launch_slot(q, s);
 				idle = 0;
 			}
@@ -483,7 +533,7 @@ static void *worker_main(void *argp)
 				s->state = S_DONE;
 				pthread_cond_broadcast(&q->cv_fin);
 				idle = 0;
-			} else if (s->state == S_FILLING && s->reserved > 0) {
+			} else if (s->state == S_FILLING && res_count(s) > 0) {
 				uint64_t dl = s->t_open_ns + (uint64_t)q->attr.max_wait_us * 1000ull;
 
 				if (dl < next)
@@ -762,41 +812,46 @@ static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const u
 
 	if (rc)
 		return rc;
-	pthread_mutex_lock(&q->lock);
-	while (s == NULL) {
-		if (q->stop) {
-			pthread_mutex_unlock(&q->lock);
-			return ecg_fail(-ECG_DER_INVAL, "queue is being destroyed");
-		}
-		for (i = 0; i < q->nslot && s == NULL; i++)
-			if (slot_matches(&q->slot[i], op, k, p, C, err, nerrs, dev))
-				s = &q->slot[i];
-		/* open FREE slots from a rotating start: batches spread over the
-		 * devices of a multi-device queue */
-		for (i = 0; i < q->nslot && s == NULL; i++) {
-			struct qslot *f = &q->slot[(q->open_next + (uint32_t)i) % (uint32_t)q->nslot];
+	/* fast path, no lock: an open slot of this class with room */
+	for (i = 0; i < q->nslot && s == NULL; i++)
+		if (slot_try_reserve(&q->slot[i], op, k, p, C, err, nerrs, dev, &idx))
+			s = &q->slot[i];
+	if (s == NULL) {
+		pthread_mutex_lock(&q->lock);
+		while (s == NULL) {
+			if (q->stop) {
+				pthread_mutex_unlock(&q->lock);
+				return ecg_fail(-ECG_DER_INVAL, "queue is being destroyed");
+			}
+			for (i = 0; i < q->nslot && s == NULL; i++)
+				if (q->slot[i].state == S_FILLING &&
+				    slot_try_reserve(&q->slot[i], op, k, p, C, err, nerrs, dev, &idx))
+					s = &q->slot[i];
+			/* open FREE slots from a rotating start: batches spread over
+			 * the devices of a multi-device queue */
+			for (i = 0; i < q->nslot && s == NULL; i++) {
+				struct qslot *f = &q->slot[(q->open_next + (uint32_t)i) % (uint32_t)q->nslot];
 
-			if (f->state == S_FREE && (dev < 0 || f->ctx->device == dev)) {
-				rc = slot_open(q, f, op, k, p, C, err, nerrs, dev);
-				if (rc) {
-					f->state = S_FREE;
-					pthread_mutex_unlock(&q->lock);
-					return rc;
+				if (f->state == S_FREE && (dev < 0 || f->ctx->device == dev)) {
+					rc = slot_open(q, f, op, k, p, C, err, nerrs, dev);
+					if (rc) {
+						f->state = S_FREE;
+						pthread_mutex_unlock(&q->lock);
+						return rc;
+					}
+					q->open_next = (uint32_t)(f - q->slot) + 1;
+					if (slot_try_reserve(f, op, k, p, C, err, nerrs, dev, &idx))
+						s = f;
 				}
-				s = f;
-				q->open_next = (uint32_t)(s - q->slot) + 1;
+			}
+			if (s == NULL) {
+				pthread_cond_broadcast(&q->cv_work);	/* make the worker drain */
+				pthread_cond_wait(&q->cv_slot, &q->lock);
 			}
 		}
-		if (s == NULL) {
-			pthread_cond_broadcast(&q->cv_work);	/* make the worker drain */
-			pthread_cond_wait(&q->cv_slot, &q->lock);
-		}
+		pthread_mutex_unlock(&q->lock);
 	}
-	idx = s->reserved++;
-	q->submitted++;
-	if (s->reserved == s->cap)
-		s->state = S_READY;
-	pthread_mutex_unlock(&q->lock);
+	__atomic_add_fetch(&q->submitted, 1, __ATOMIC_RELAXED);
 
 	{
 		struct qreq *r = &s->reqs[idx];
@@ -832,14 +887,19 @@ static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const u
 			r->dst[i] = op != OP_RECOVER ? dst[i] : stripe + (uint64_t)s->out_idx[i] * C;
 	}
 
-	pthread_mutex_lock(&q->lock);
-	s->filled++;
-	/* wake the worker only for what it acts on: a closed slot whose copies
-	 * have all landed, a slot's first request (a new deadline to wait for;
-	 * for device cells, a batch that may launch at once) */
-	if ((s->state == S_READY && s->filled == s->reserved) || s->filled == 1)
-		pthread_cond_signal(&q->cv_work);
-	pthread_mutex_unlock(&q->lock);
+	/* wake the worker only for what it acts on: a slot's first request (a new
+	 * deadline to wait for; for device cells, a batch that may launch at
+	 * once), a slot this request filled up, and a closed slot -- whose last
+	 * inputs may be the ones landing now */
+	{
+		const uint32_t n = __atomic_add_fetch(&s->filled, 1u, __ATOMIC_ACQ_REL);
+
+		if (n == 1 || idx + 1 == s->cap || !(__atomic_load_n(&s->res, __ATOMIC_ACQUIRE) & RES_OPEN)) {
+			pthread_mutex_lock(&q->lock);
+			pthread_cond_signal(&q->cv_work);
+			pthread_mutex_unlock(&q->lock);
+		}
+	}
 	return 0;
 }
 
@@ -895,7 +955,7 @@ int ecg_queue_flush(ecg_queue_t *q)
 	if (q == NULL)
 		return ecg_fail(-ECG_DER_INVAL, "queue_flush: NULL queue");
 	pthread_mutex_lock(&q->lock);
-	target = q->submitted;
+	target = __atomic_load_n(&q->submitted, __ATOMIC_RELAXED);
 	if (q->flush_target < target)
 		q->flush_target = target;
 	pthread_cond_broadcast(&q->cv_work);
