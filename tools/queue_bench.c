@@ -19,7 +19,9 @@
  * device memory: the drop-in (ec_encode_data on device cells, in place, the
  * calling threads spread over the context's drop-in stream pool, each call
  * waiting for its own launch) and the queue (device-cell requests batched
- * into pointer-table launches in place).
+ * into pointer-table launches in place; QB_VERIFY=1: one queue run over a
+ * patterned image, every stripe's parity checked against the CPU
+ * restatement).
  * usage: queue_bench C T [update|device] [stripes per thread, default 64].
  * Bench infrastructure.
  */
@@ -208,6 +210,39 @@ int main(int argc, char **argv)
 			return 1;
 		}
 		g_dcells = d;
+		if (getenv("QB_VERIFY")) {
+			/* every stripe distinct: one queue run over a patterned image,
+			 * then every stripe's parity against the CPU restatement */
+			unsigned char *h = malloc(nb), *want = malloc(P * CB);
+			long bad = 0;
+
+			for (size_t i = 0; i < nb / 8; i++) {
+				const uint64_t v = (i + 1) * 0x9E3779B97F4A7C15ull;
+
+				memcpy(h + i * 8, &v, 8);
+			}
+			if (ecg_memcpy(ctx, d, h, nb, 0, NULL) || ecg_stream_sync(ctx, NULL))
+				return 1;
+			run(1);
+			if (ecg_memcpy(ctx, h, d, nb, 1, NULL) || ecg_stream_sync(ctx, NULL))
+				return 1;
+			for (size_t st = 0; st < (size_t)T * N; st++) {
+				unsigned char *s = h + st * (K + P) * CB, *src[64], *dst[8];
+
+				for (int c = 0; c < K; c++)
+					src[c] = s + c * CB;
+				for (int r = 0; r < P; r++)
+					dst[r] = want + r * CB;
+				ref_simd_encode_data((int)CB, K, P, g_tbls, src, dst);
+				bad += memcmp(want, s + (size_t)K * CB, (size_t)P * CB) != 0;
+			}
+			printf("{\"op\": \"encode\", \"cells\": \"device\", \"verify\": true, \"k\": %d, \"p\": %d, "
+			       "\"cell_bytes\": %llu, \"threads\": %d, \"stripes\": %d, \"bad_stripes\": %ld}\n", K, P,
+			       (unsigned long long)CB, T, T * N, bad);
+			free(h);
+			free(want);
+			return bad ? 1 : 0;
+		}
 		run(0);
 		isal = run(0);
 		run(1);
