@@ -21,7 +21,7 @@
  * waiting for its own launch) and the queue (device-cell requests batched
  * into pointer-table launches in place; QB_VERIFY=1: one queue run over a
  * patterned image, every stripe's parity checked against the CPU
- * restatement).
+ * restatement -- in host mode likewise, parity zeroed first).
  * usage: queue_bench C T [update|device] [stripes per thread, default 64].
  * Bench infrastructure.
  */
@@ -269,6 +269,30 @@ int main(int argc, char **argv)
 		free(g_cells);
 		free(g_new);
 		return 0;
+	}
+	if (getenv("QB_VERIFY") && !g_update) {
+		/* host cells: parity zeroed, one queue run, every stripe checked */
+		unsigned char *want = malloc(P * CB);
+		long bad = 0;
+
+		for (size_t st = 0; st < (size_t)T * N; st++)
+			memset(g_cells + (st * (K + P) + K) * CB, 0, (size_t)P * CB);
+		run(1);
+		for (size_t st = 0; st < (size_t)T * N; st++) {
+			unsigned char *s = g_cells + st * (K + P) * CB, *src[64], *dst[8];
+
+			for (int c = 0; c < K; c++)
+				src[c] = s + c * CB;
+			for (int r = 0; r < P; r++)
+				dst[r] = want + r * CB;
+			ref_simd_encode_data((int)CB, K, P, g_tbls, src, dst);
+			bad += memcmp(want, s + (size_t)K * CB, (size_t)P * CB) != 0;
+		}
+		printf("{\"op\": \"encode\", \"cells\": \"host\", \"verify\": true, \"k\": %d, \"p\": %d, "
+		       "\"cell_bytes\": %llu, \"threads\": %d, \"stripes\": %d, \"bad_stripes\": %ld}\n", K, P,
+		       (unsigned long long)CB, T, T * N, bad);
+		free(want);
+		return bad ? 1 : 0;
 	}
 	run(0);			/* warm up staging / code objects */
 	isal = run(0);
