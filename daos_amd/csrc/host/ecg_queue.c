@@ -267,14 +267,18 @@ static int slot_open(struct ecg_queue *q, struct qslot *s, int op, int k, int p,
 #define ECG_QUEUE_DEV_DEPTH 2
 #endif
 
-/* ctx's device has ECG_QUEUE_DEV_DEPTH batches of this queue queued or running. */
+/* ctx's device has ECG_QUEUE_DEV_DEPTH device-cell batches of this queue
+ * queued or running (host-cell batches, PCIe-bound, do not count). */
 static int device_busy(const struct ecg_queue *q, const ecg_ctx_t *ctx)
 {
 	int n = 0;
 
-	for (int i = 0; i < q->nslot; i++)
-		if (q->slot[i].ctx == ctx && (q->slot[i].state == S_INFLIGHT || q->slot[i].state == S_READY))
+	for (int i = 0; i < q->nslot; i++) {
+		const struct qslot *s = &q->slot[i];
+
+		if (s->ctx == ctx && s->devcells && (s->state == S_INFLIGHT || s->state == S_READY))
 			n++;
+	}
 	return n >= ECG_QUEUE_DEV_DEPTH;
 }
 
@@ -730,8 +734,6 @@ void ecg_queue_destroy(ecg_queue_t *q)
 	free(q);
 }
 
-/* Reserve a stripe index in a slot of this class (opening one if needed),
- * copy the inputs in without the lock, then publish. */
 /* Every cell of a device-cell request inside one allocation of ctx's device
  * (a launch on anything else would fault the GPU).  The HIP runtime's
  * pointer queries serialise across threads, so the usual stripe -- every cell
@@ -801,6 +803,9 @@ static int request_device(struct ecg_queue *q, int op, int k, int p, uint64_t C,
 	return dev;
 }
 
+/* Reserve a stripe index in a slot of this class (opening one if needed),
+ * copy the inputs in (device cells: their addresses) without the lock, then
+ * publish. */
 static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const uint32_t *err,
 		  int nerrs, unsigned char *const *src, unsigned char *stripe,
 		  unsigned char *const *dst, int vec_i, ecg_done_cb_t cb, void *arg)
