@@ -511,6 +511,55 @@ def test_isal_device_cells_16_threads(ecglib, oracle, ctx):
     assert not errs, errs[:5]
 
 
+def test_isal_device_cells_one_shape_16_threads(ecglib, oracle, ctx):
+    """16 threads released together calling ec_encode_data on device cells of
+    ONE shape (EC_8P2, same tables and length -- the engine's xstreams
+    encoding one class), 12 calls each: every output equals the oracle's and
+    every caller's last_kernel names a product kernel."""
+    import threading
+
+    L = ecglib.lib()
+    T, iters, k, p, n = 16, 12, 8, 2, 65536 + 20
+    en = oracle.cauchy1(k, p)
+    tbls = ecglib.isal_init_tables(en[k:])
+    errs, kernels = [], set()
+    bufs = [ctx.alloc((k + p) * (n + 64)) for _ in range(T)]
+    start = threading.Barrier(T)
+
+    def worker(t):
+        try:
+            buf = bufs[t]
+            offs = [j * (n + 64) + (t % 5) for j in range(k + p)]
+            dp = (ecglib.u8p * k)(*[C.cast(C.c_void_p(buf.ptr + o), ecglib.u8p) for o in offs[:k]])
+            cp = (ecglib.u8p * p)(*[C.cast(C.c_void_p(buf.ptr + o), ecglib.u8p) for o in offs[k:]])
+            datas = [rand((k, n), 5000 + 100 * t + it) for it in range(iters)]
+            start.wait()
+            for it in range(iters):
+                for j in range(k):
+                    buf.upload(datas[it][j], offset=offs[j])
+                L.ec_encode_data(n, k, p, tbls.ctypes.data_as(ecglib.u8p), dp, cp)
+                kernels.add(ecglib.last_kernel().split("<")[0])
+                raw = buf.download()
+                want = oracle.encode_data(en[k:], datas[it])
+                for r in range(p):
+                    if not np.array_equal(raw[offs[k + r]: offs[k + r] + n], want[r]):
+                        errs.append((t, it, r))
+        except Exception as e:          # noqa: BLE001 -- reported below
+            errs.append((t, repr(e)))
+
+    try:
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+    finally:
+        for b in bufs:
+            b.free()
+    assert not errs, errs[:5]
+    assert kernels <= {"ecg_mm_kernel", "ecg_mm_ptr_kernel"} and kernels, kernels
+
+
 def test_xor_gen_many_device_cells(ecglib, ctx):
     """xor_gen with more sources than one launch takes (ECG_MAX_K = 64) on
     device cells: accumulating launches, not an error."""
