@@ -164,12 +164,19 @@ static uint64_t pitch_of(uint64_t C)
 /* The slot's class is the request's.  dev: the cells' device (device-cell
  * requests), -1 for host cells.  Read without the lock by the reservation
  * fast path: a slot reopened meanwhile fails that path's CAS (generation). */
+#define LD(x) __atomic_load_n(&(x), __ATOMIC_RELAXED)
+#define ST(x, v) __atomic_store_n(&(x), (v), __ATOMIC_RELAXED)
+
 static int class_matches(const struct qslot *s, int op, int k, int p, uint64_t C,
 			 const uint32_t *err, int nerrs, int dev)
 {
-	return s->op == op && s->k == k && s->p == p && s->C == C && s->nerrs == nerrs &&
-	       s->devcells == (dev >= 0) && (dev < 0 || s->ctx->device == dev) &&
-	       (op != OP_RECOVER || memcmp(s->err, err, sizeof(uint32_t) * nerrs) == 0);
+	if (LD(s->op) != op || LD(s->k) != k || LD(s->p) != p || LD(s->C) != C || LD(s->nerrs) != nerrs ||
+	    LD(s->devcells) != (dev >= 0) || (dev >= 0 && s->ctx->device != dev))
+		return 0;
+	for (int i = 0; op == OP_RECOVER && i < nerrs; i++)
+		if (LD(s->err[i]) != err[i])
+			return 0;
+	return 1;
 }
 
 /* Reserve a request index in an open slot of this class; 0 if it is not
@@ -183,7 +190,7 @@ static int slot_try_reserve(struct qslot *s, int op, int k, int p, uint64_t C, c
 	if (!(w & RES_OPEN) || !class_matches(s, op, k, p, C, err, nerrs, dev))
 		return 0;
 	/* the class was checked for this opening (generation) only */
-	while ((w >> 32) == gen && (w & RES_OPEN) && (uint32_t)(w & RES_CNT) < s->cap) {
+	while ((w >> 32) == gen && (w & RES_OPEN) && (uint32_t)(w & RES_CNT) < LD(s->cap)) {
 		if (__atomic_compare_exchange_n(&s->res, &w, w + 1, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
 			*idx = (uint32_t)(w & RES_CNT);
 			return 1;
@@ -215,12 +222,14 @@ static int slot_open(struct ecg_queue *q, struct qslot *s, int op, int k, int p,
 	uint64_t per;
 	int j, reused, rc;
 
-	s->op = op;
-	s->k = k;
-	s->p = p;
-	s->C = C;
+	/* the class fields are read without the lock by slot_try_reserve
+	 * (relaxed atomics; the generation in `res` decides) */
+	ST(s->op, op);
+	ST(s->k, k);
+	ST(s->p, p);
+	ST(s->C, C);
 	s->pitch = pitch_of(C);
-	s->nerrs = nerrs;
+	ST(s->nerrs, nerrs);
 	ecg_gen_cauchy1(k, p, en);
 	if (op == OP_ENCODE || op == OP_UPDATE) {
 		s->rows = p;
@@ -230,20 +239,23 @@ static int slot_open(struct ecg_queue *q, struct qslot *s, int op, int k, int p,
 		for (j = 0; j < p; j++)
 			s->out_idx[j] = (uint32_t)(k + j);
 	} else {
-		memcpy(s->err, err, sizeof(uint32_t) * nerrs);
+		for (j = 0; j < nerrs; j++)
+			ST(s->err[j], err[j]);
 		rc = ecg_recov_rows(k, p, en, err, nerrs, s->coef, s->out_idx, s->dec_idx, &reused);
 		if (rc)
 			return rc;
 		s->rows = nerrs;
 	}
 	s->nin = op == OP_UPDATE ? 1 : k;	/* staged input cells per request */
-	s->devcells = dev >= 0;
+	ST(s->devcells, dev >= 0);
 	/* an update request also stages its vec_i byte (+64 B of alignment slack) */
 	per = s->pitch * (uint64_t)(s->nin + s->rows) + (op == OP_UPDATE ? 1 : 0);
 	/* device cells stage nothing: only the pointer table bounds a batch */
-	s->cap = s->devcells ? q->attr.max_batch : (uint32_t)((q->slot_bytes - 64) / per);
-	if (s->cap > q->attr.max_batch)
-		s->cap = q->attr.max_batch;
+	{
+		uint32_t cap = dev >= 0 ? q->attr.max_batch : (uint32_t)((q->slot_bytes - 64) / per);
+
+		ST(s->cap, cap > q->attr.max_batch ? q->attr.max_batch : cap);
+	}
 	if (s->cap == 0)
 		return ecg_fail(-ECG_DER_REC2BIG, "queue: one stripe (%llu B) exceeds a slot",
 				(unsigned long long)per);
