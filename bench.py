@@ -798,12 +798,12 @@ def detail_rows(ctx, ceil, iters=11, shapes=DETAIL_SHAPES, csum=True):
             fn = (lambda buf=buf, k=k, p=p, C=C, S=S, st=st:
                   ctx.recover(k, p, C, S, buf.ptr, st, [0, 1]))
             rd, wr = k, 2
-        # 40 warm-up launches: the launch tuner (include/ecg.h ecg_set_autotune) times its
+        # 80 warm-up launches: the launch tuner (include/ecg.h ecg_set_autotune) times its
         # two arms over the first 23 launches of a wide shape (its capped arm last, so a kept
         # cap needs no switch; the first ~10-20 launches after a switch to a cap run up to
         # 12 % slow: EC_16P2 cap 2 0.434 ms, then 0.38, tools/state_check3.py,
-        # profiles/r03/tuner_check/); the timed launches run its choice
-        ms = time_kernel(ctx, fn, iters, warm=40)
+        # profiles/r03/tuner_check/); the timed launches run its choice in steady state
+        ms = time_kernel(ctx, fn, iters, warm=80)
         tuned = (ctx.tune_state(k, p, C, S, k * C, C) if mode == "enc"
                  else ctx.tune_state(k, 2, C, S, st, st))
         alg = (rd + wr) * C * S
