@@ -297,6 +297,23 @@ int ecg_k_launch_matmul_ptrs(const ecg_mm_params_t *p, const uint64_t *cells_dev
 			     const ecg_launch_cfg_t *cfg, void *stream, uint32_t *kernel_id);
 #define ECG_KID_PTR 600u	/* pointer-table kernel ids start here */
 const char *ecg_k_ptr_kernel_name(uint32_t kernel_id);
+/* Per-request delta updates through a pointer table (the batching queue's
+ * device-cell aggregation updates, ecg_update_ptrs):  item s of the launch,
+ * a record of ECG_UPD_REC(rows) uint64_t at items_dev + s * ECG_UPD_REC(rows):
+ *   [0, rows)            parity cell r (device address; updated in place)
+ *   rows + 2m, + 2m + 1  old / new cell of pair m (m < ECG_UPD_MU)
+ *   rows + 2 MU          byte m = coefficient column of pair m (< ncols)
+ *   rows + 2 MU + 1      n, the pairs in use (1 .. ECG_UPD_MU)
+ *   parity[r] ^= XOR_{m<n} tbl[r][col_m] * (old_m ^ new_m)
+ * p->nstripes = items, p->rows, p->cell_bytes and p->tbl[r][0 .. ncols) are
+ * used.  No two items of one launch may share a parity byte (the host splits
+ * such requests into ordered launches).  granule: 16 (every address and C
+ * 16-byte aligned), 4 (C % 4 == 0; addresses dword-aligned, or any address on
+ * a device that serves misaligned dwords), 0 = one byte per lane. */
+#define ECG_UPD_MU 8
+#define ECG_UPD_REC(rows) ((rows) + 2 * ECG_UPD_MU + 2)
+int ecg_k_launch_update_ptrs(const ecg_mm_params_t *p, const uint64_t *items_dev, uint32_t ncols, int granule,
+			     void *stream, uint32_t *kernel_id);
 /* Chunked checksums (kernels/ecg_csum_kernels.hip). max_blocks 0 = default. */
 int ecg_k_launch_csum(const ecg_csum_params_t *p, void *stream, uint32_t max_blocks,
 		      uint32_t *kernel_id);

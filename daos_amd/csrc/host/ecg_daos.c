@@ -143,11 +143,26 @@ int ecg_obj_ec_recov_codec_init(uint32_t oc_id, const uint32_t *err_list, uint32
 		return rc;
 	if (nerrs > (uint32_t)p)
 		return ecg_fail(-ECG_DER_DATA_LOSS, "recov_codec_init: nerrs %u > p %d", nerrs, p);
-	memset(rv, 0, sizeof(*rv));
+	/* the codec already holds these erasures' rows: nothing to build
+	 * (obj_ec_err_match, ref:src/object/cli_ec.c:2176-2185; the class is
+	 * compared too, the reference's codec belongs to one object) */
+	if (rv->er_builds && rv->k == k && rv->p == p && rv->er_nerrs == nerrs) {
+		for (i = 0; i < nerrs && rv->er_err_list[i] == err_list[i]; i++)
+			;
+		if (i == nerrs)
+			return 0;
+	}
+	{
+		const uint32_t builds = rv->er_builds;
+
+		memset(rv, 0, sizeof(*rv));
+		rv->er_builds = builds;
+	}
 	rv->k = k;
 	rv->p = p;
-	rv->er_nerrs = nerrs;
 	for (i = 0; i < nerrs; i++) {
+		if (err_list[i] >= (uint32_t)(k + p))
+			return ecg_fail(-ECG_DER_INVAL, "recov_codec_init: cell %u of a %d+%d stripe", err_list[i], k, p);
 		rv->er_err_list[i] = err_list[i];
 		if (err_list[i] < (uint32_t)k)
 			rv->er_data_nerrs++;
@@ -159,6 +174,9 @@ int ecg_obj_ec_recov_codec_init(uint32_t oc_id, const uint32_t *err_list, uint32
 		return rc;
 	rv->reused_encode = reused;
 	ec_init_tables(k, (int)nerrs, rv->er_de_matrix, rv->er_gftbls);
+	/* published last: a failed build leaves er_nerrs 0, which never matches */
+	rv->er_nerrs = nerrs;
+	rv->er_builds++;
 	return 0;
 }
 

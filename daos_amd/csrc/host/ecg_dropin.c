@@ -5,12 +5,19 @@
  *
  * The rule ("CPU for small len, GPU via staging above a
  * threshold"):
- *   - device cells (src[0] is hipMalloc'd memory)   -> HIP kernels, in place;
+ *   - every cell device memory (hipMalloc'd)        -> HIP kernels, in place;
+ *   - host and device cells mixed (host bio buffers,
+ *     parity in HBM)                                  -> HIP kernels, the host
+ *                                                       cells through pinned
+ *                                                       staging;
  *   - host cells, len * (k + rows) >= crossover       -> HIP kernels through
  *                                                       pinned staging;
  *   - host cells below the crossover, every call in a process without a
  *     usable gfx950 device, and ECG_FORCE_CPU=1       -> the CPU path
  *                                                       (ecg_cpu.c).
+ * Placement is decided from EVERY cell (ecg_cells_place), so a device address
+ * never reaches the CPU path; cells of two devices in one call, or a device
+ * cell past its allocation, fail with the cell named.
  * The default crossover is the measured one (on the MI355X box
  * one EPYC core with GFNI beats the PCIe round trip of a synchronous call at
  * every size up to the largest measured, so host cells stay on the CPU);
@@ -181,7 +188,7 @@ static int cell_device(const void *p)
 
 		__atomic_store_n(&g_hostc, !(env && env[0] == '0'), __ATOMIC_RELAXED);
 	}
-	if (!g_hostc)
+	if (!__atomic_load_n(&g_hostc, __ATOMIC_RELAXED))
 		return ecg_ptr_device(p);
 	now = coarse_ns();
 	if (t_hostc[slot].region == region && now < t_hostc[slot].until)
@@ -194,6 +201,11 @@ static int cell_device(const void *p)
 	return dev;
 }
 
+int ecg_ptr_device_cached(const void *p)
+{
+	return cell_device(p);
+}
+
 ecg_ctx_t *ecg_dropin_ctx(void)
 {
 	return ecg_dropin_gpu() && !g_force_cpu ? thread_ctx() : NULL;
@@ -202,27 +214,34 @@ ecg_ctx_t *ecg_dropin_ctx(void)
 int ecg_dropin_product(const char *fn, ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
 		       unsigned char *const *src, unsigned char *const *dst, unsigned flags)
 {
-	int dev, rc;
+	signed char place[ECG_MAX_K + 256 + 256];
+	int dev, ndev, rc;
 
-	if (len <= 0 || src == NULL)
+	if (len <= 0 || src == NULL || dst == NULL || k < 1 || k > ECG_MAX_K + 256 || rows < 1 || rows > 256)
 		return ecg_cpu_matmul(len, k, rows, coef, src, dst, flags);
 	if (!ecg_dropin_gpu())
 		return ecg_cpu_matmul(len, k, rows, coef, src, dst, flags);
-	dev = cell_device(src[0]);
-	if (dev >= 0) {
+	/* where every cell is, not only src[0]: a device address must never
+	 * reach the CPU path (it would fault there), and a call mixing host and
+	 * device cells -- host bio buffers, parity kept in HBM -- runs on that
+	 * device with its host cells staged */
+	ndev = ecg_cells_place(src, k, dst, rows, (uint64_t)len, cell_device, place, &dev);
+	if (ndev < 0)
+		return ndev;	/* ecg_strerror() names the cell; the caller names fn */
+	if (ndev > 0) {
 		/* device cells: only the GPU can touch them */
 		if (ctx == NULL || ecg_ctx_device(ctx) != dev)
 			ctx = device_ctx(fn, dev);
 		if (ctx == NULL)
 			return g_ctx_rc ? g_ctx_rc : -ECG_DER_INVAL;
-		return ecg_matmul_host_mem(ctx, len, k, rows, coef, src, dst, flags, dev);
+		return ecg_matmul_host_mem(ctx, len, k, rows, coef, src, dst, flags, place);
 	}
 	if (g_force_cpu || (uint64_t)len * (uint64_t)(k + rows) < ecg_dropin_crossover())
 		return ecg_cpu_matmul(len, k, rows, coef, src, dst, flags);
 	if (ctx == NULL)
 		ctx = thread_ctx();
 	if (ctx != NULL) {
-		rc = ecg_matmul_host_mem(ctx, len, k, rows, coef, src, dst, flags, -1);
+		rc = ecg_matmul_host_mem(ctx, len, k, rows, coef, src, dst, flags, NULL);
 		if (rc == 0)
 			return 0;
 	}

@@ -113,6 +113,10 @@ int ecg_recov_rows(int k, int p, const unsigned char *en_matrix,
 
 /* pointer tables (ecg_ptrs.c) */
 void ecg_scratch_free(ecg_ctx_t *ctx);
+/* ecg_update_ptrs with explicit parity rows coef[rows][k]; *nlaunch (may be
+ * NULL) = the ordered launches the batch took */
+int ecg_update_ptrs_coef(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, uint64_t C, uint32_t nreq,
+			 void *const *cells, const uint8_t *vec_i, void *stream, uint32_t *nlaunch);
 /* next scratch slot with at least these sizes, free of readers (ctx->lock held) */
 int ecg_scratch_reserve(ecg_ctx_t *ctx, size_t pin_bytes, size_t dev_bytes,
 			struct ecg_scratch_slot **out);
@@ -172,6 +176,10 @@ int ecg_tune_launch(ecg_ctx_t *ctx, const ecg_mm_params_t *p, hipStream_t st, ui
 #define ECG_PTR_HOST (-1)
 #define ECG_PTR_UNKNOWN (-2)
 int ecg_ptr_device(const void *p);
+/* ecg_ptr_device through the calling thread's short-lived cache of 2 MiB
+ * regions of plain host memory (ecg_dropin.c): near-free for a caller's
+ * reused malloc'd buffers */
+int ecg_ptr_device_cached(const void *p);
 /* The same for any launcher of the product (the pointer-table kernel): `g`
  * its lane granule, `layout` its layout class (ECG_TUNE_LAYOUT_*), `fn(p,
  * cfg, stream, kid, arg)` the launch under a given geometry. */
@@ -183,10 +191,15 @@ typedef int (*ecg_mm_launch_fn)(const ecg_mm_params_t *p, const ecg_launch_cfg_t
 int ecg_tune_launch_fn(ecg_ctx_t *ctx, const ecg_mm_params_t *p, uint32_t g, uint32_t layout,
 		       ecg_mm_launch_fn fn, const void *arg, hipStream_t st, uint32_t *kid);
 
-/* synchronous one-stripe product on ctx's GPU; src_dev = ecg_ptr_device(src[0])
- * (ecg_stage.c) */
+/* synchronous one-stripe product on ctx's GPU; place = ecg_cells_place's
+ * placement of the k + rows cells (NULL: all host memory) (ecg_stage.c) */
 int ecg_matmul_host_mem(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
-			unsigned char *const *src, unsigned char *const *dst, unsigned flags, int src_dev);
+			unsigned char *const *src, unsigned char *const *dst, unsigned flags, const signed char *place);
+/* placement of every cell of a one-stripe call: place[i] = device or -1
+ * (host); returns the device cells' count (*dev their device) or a negative
+ * DER code (cells on two devices, a device cell past its allocation) */
+int ecg_cells_place(unsigned char *const *src, int k, unsigned char *const *dst, int rows, uint64_t len,
+		    int (*query)(const void *), signed char *place, int *dev);
 /* every cell [v[i], v[i] + len) inside one allocation of ctx's device, else
  * -DER_INVAL naming `what` (ecg_stage.c) */
 int ecg_cells_on_device(ecg_ctx_t *ctx, unsigned char *const *v, int n, uint64_t len, const char *what);

@@ -261,6 +261,297 @@ int ecg_matmul_ptrs(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, 
 	return rc;
 }
 
+/* ---- per-request delta updates on device cells -------------------------- */
+
+/*
+ * agg_update_parity runs, per updated data cell of a stripe, xor_gen(old, new)
+ * then ec_encode_data_update(vec_i) into the stripe's parity cells
+ * (ref:src/object/srv_ec_aggregate.c:1086-1102).  A batch of such requests
+ * becomes launches of ecg_upd_ptr_kernel (kernels/ecg_ptr_kernels.hip):
+ *   1. requests naming the same parity cells (the cells of one stripe updated
+ *      one by one) fold into one item of up to ECG_UPD_MU pairs, so that
+ *      stripe's parity is read and written once;
+ *   2. the parity read-modify-writes of one launch must not touch a byte
+ *      twice: items of one parity set beyond the first MU pairs go to later
+ *      launches, and so does any item whose parity cells overlap another's
+ *      (different pointers into one buffer) -- launches on one stream run in
+ *      order, XOR commutes, so the result is the requests applied one by one.
+ */
+struct upd_req {
+	uint64_t par[ECG_KMAX_R];	/* the sort key: the parity cells, then the request's index */
+	uint32_t idx;
+};
+
+static int upd_req_cmp(const void *a, const void *b)
+{
+	const struct upd_req *x = a, *y = b;
+
+	for (int r = 0; r < ECG_KMAX_R; r++)
+		if (x->par[r] != y->par[r])
+			return x->par[r] < y->par[r] ? -1 : 1;
+	return x->idx < y->idx ? -1 : x->idx > y->idx;
+}
+
+struct upd_ival {
+	uint64_t lo, hi;
+	uint32_t item;
+};
+
+static int upd_ival_cmp(const void *a, const void *b)
+{
+	const struct upd_ival *x = a, *y = b;
+
+	return x->lo < y->lo ? -1 : x->lo > y->lo;
+}
+
+struct upd_item {
+	uint32_t first, n;	/* sorted requests [first, first + n) */
+	uint32_t wave;
+	uint32_t set;		/* parity set (group of identical parity pointers) */
+};
+
+/* Any two items of different parity sets whose parity bytes overlap?  A
+ * request whose own parity cells overlap one another is refused (its rows
+ * would race inside one work item). */
+static int upd_sets_overlap(const struct upd_req *rq, const struct upd_item *it, uint32_t nit, int rows,
+			    uint64_t C, int *overlap)
+{
+	struct upd_ival *v;
+	uint64_t hi = 0;
+	size_t n = 0;
+
+	*overlap = 0;
+	for (uint32_t i = 0; i < nit; i++) {
+		const uint64_t *par = rq[it[i].first].par;
+
+		for (int r = 0; r < rows; r++)
+			for (int q = 0; q < r; q++)
+				if (par[r] < par[q] + C && par[q] < par[r] + C)
+					return ecg_fail(-ECG_DER_INVAL,
+							"update_ptrs: parity cells %d and %d of one request overlap", q, r);
+	}
+	v = malloc(sizeof(*v) * (size_t)nit * (size_t)rows);
+	if (v == NULL)
+		return ecg_fail(-ECG_DER_NOMEM, "update_ptrs: malloc");
+	for (uint32_t i = 0; i < nit; i++) {
+		if (i && it[i].set == it[i - 1].set)
+			continue;		/* one interval list per parity set */
+		for (int r = 0; r < rows; r++)
+			v[n++] = (struct upd_ival){rq[it[i].first].par[r], rq[it[i].first].par[r] + C, it[i].set};
+	}
+	qsort(v, n, sizeof(*v), upd_ival_cmp);
+	/* a set's own intervals are disjoint (checked above), so an interval
+	 * starting below the highest end so far overlaps another set's */
+	for (size_t i = 0; i < n; i++) {
+		if (i && v[i].lo < hi)
+			*overlap = 1;
+		if (v[i].hi > hi)
+			hi = v[i].hi;
+	}
+	free(v);
+	return 0;
+}
+
+static int upd_items_conflict(const struct upd_req *rq, const struct upd_item *a, const struct upd_item *b,
+			      int rows, uint64_t C)
+{
+	if (a->set == b->set)
+		return 1;
+	for (int r = 0; r < rows; r++)
+		for (int q = 0; q < rows; q++) {
+			const uint64_t x = rq[a->first].par[r], y = rq[b->first].par[q];
+
+			if (x < y + C && y < x + C)
+				return 1;
+		}
+	return 0;
+}
+
+int ecg_update_ptrs_coef(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, uint64_t C, uint32_t nreq,
+			 void *const *cells, const uint8_t *vec_i, void *stream, uint32_t *nlaunch)
+{
+	const uint32_t per = (uint32_t)(rows + 2), rec = (uint32_t)ECG_UPD_REC(rows);
+	struct upd_req *rq = NULL;
+	struct upd_item *it = NULL;
+	struct ecg_scratch_slot *sc = NULL;
+	ecg_mm_params_t *prm = NULL;
+	uint64_t bits = C;
+	uint32_t nit = 0, nset = 0, nwave = 0, kid = 0;
+	hipStream_t st;
+	int rc = 0, overlap = 0, granule;
+
+	if (nlaunch)
+		*nlaunch = 0;
+	if (ctx == NULL || coef == NULL || (nreq && (cells == NULL || vec_i == NULL)))
+		return ecg_fail(-ECG_DER_INVAL, "update_ptrs: NULL argument");
+	if (k < 1 || k > ECG_KMAX_K || rows < 1 || rows > ECG_KMAX_R)
+		return ecg_fail(-ECG_DER_INVAL, "update_ptrs: k=%d rows=%d (max %d x %d)", k, rows, ECG_KMAX_K,
+				ECG_KMAX_R);
+	if (C == 0 || nreq == 0)
+		return 0;
+	for (uint32_t i = 0; i < nreq; i++) {
+		if (vec_i[i] >= (uint8_t)k)
+			return ecg_fail(-ECG_DER_INVAL, "update_ptrs: request %u: vec_i %u >= k=%d", i, vec_i[i], k);
+		for (uint32_t j = 0; j < per; j++) {
+			if (cells[(size_t)i * per + j] == NULL)
+				return ecg_fail(-ECG_DER_INVAL, "update_ptrs: request %u: NULL cell %u", i, j);
+			bits |= (uint64_t)(uintptr_t)cells[(size_t)i * per + j];
+		}
+	}
+	rc = ecg_ctx_enter(ctx);
+	if (rc)
+		return rc;
+	rq = calloc(nreq, sizeof(*rq));
+	it = calloc(nreq, sizeof(*it));
+	prm = calloc(1, sizeof(*prm));
+	if (rq == NULL || it == NULL || prm == NULL) {
+		rc = ecg_fail(-ECG_DER_NOMEM, "update_ptrs: calloc");
+		goto out;
+	}
+	for (uint32_t i = 0; i < nreq; i++) {
+		for (int r = 0; r < rows; r++)
+			rq[i].par[r] = (uint64_t)(uintptr_t)cells[(size_t)i * per + 2 + r];
+		rq[i].idx = i;
+	}
+	qsort(rq, nreq, sizeof(*rq), upd_req_cmp);
+	/* items: runs of one parity set, at most MU pairs each; the j-th item of
+	 * a set goes to launch j */
+	for (uint32_t i = 0; i < nreq;) {
+		uint32_t e = i + 1, lvl = 0;
+
+		while (e < nreq && memcmp(rq[e].par, rq[i].par, sizeof(rq[i].par)) == 0)
+			e++;
+		for (uint32_t f = i; f < e; f += ECG_UPD_MU, lvl++) {
+			it[nit] = (struct upd_item){f, e - f < ECG_UPD_MU ? e - f : ECG_UPD_MU, lvl, nset};
+			if (lvl + 1 > nwave)
+				nwave = lvl + 1;
+			nit++;
+		}
+		nset++;
+		i = e;
+	}
+	rc = upd_sets_overlap(rq, it, nit, rows, C, &overlap);
+	if (rc)
+		goto out;
+	if (overlap) {
+		/* parity sets that share bytes: greedy, each item in the first
+		 * launch none of its conflicting items is in */
+		nwave = 0;
+		for (uint32_t i = 0; i < nit; i++) {
+			uint32_t w = 0;
+
+			for (;;) {
+				uint32_t j;
+
+				for (j = 0; j < i; j++)
+					if (it[j].wave == w && upd_items_conflict(rq, &it[i], &it[j], rows, C))
+						break;
+				if (j == i)
+					break;
+				w++;
+			}
+			it[i].wave = w;
+			if (w + 1 > nwave)
+				nwave = w + 1;
+		}
+	}
+	/* lane access: 16-byte lanes when everything is 16-byte aligned; dword
+	 * lanes when C % 4 == 0 and the addresses are dword-aligned or the device
+	 * serves misaligned dwords; else one byte per lane */
+	if ((bits & 15u) == 0)
+		granule = 16;
+	else if ((C & 3u) == 0 && ((bits & 3u) == 0 || !ctx->cfg.no_unaligned))
+		granule = 4;
+	else
+		granule = 0;
+	ecg_gf_init();
+	prm->cell_bytes = C;
+	prm->rows = (uint32_t)rows;
+	prm->k = 1;
+	for (int r = 0; r < rows; r++)
+		for (int j = 0; j < k; j++)
+			ecg_build_ptbl(coef[(size_t)r * k + j], &prm->tbl[r][j]);
+	st = ecg_pick_stream(ctx, stream);
+	pthread_mutex_lock(&ctx->lock);
+	rc = ecg_scratch_reserve(ctx, (size_t)nit * rec * sizeof(uint64_t), (size_t)nit * rec * sizeof(uint64_t),
+				 &sc);
+	if (rc == 0) {
+		uint64_t *t = sc->pin;
+		uint32_t at = 0, w, i;
+		hipError_t e;
+
+		/* records launch by launch: launch w is the records [start_w, at) */
+		for (w = 0; w < nwave; w++) {
+			for (i = 0; i < nit; i++) {
+				uint64_t *o = t + (size_t)at * rec, cols = 0;
+
+				if (it[i].wave != w)
+					continue;
+				memset(o, 0, rec * sizeof(uint64_t));
+				for (int r = 0; r < rows; r++)
+					o[r] = rq[it[i].first].par[r];
+				for (uint32_t m = 0; m < it[i].n; m++) {
+					const uint32_t q = rq[it[i].first + m].idx;
+
+					o[rows + 2 * m] = (uint64_t)(uintptr_t)cells[(size_t)q * per];
+					o[rows + 2 * m + 1] = (uint64_t)(uintptr_t)cells[(size_t)q * per + 1];
+					cols |= (uint64_t)vec_i[q] << (8 * m);
+				}
+				o[rows + 2 * ECG_UPD_MU] = cols;
+				o[rows + 2 * ECG_UPD_MU + 1] = it[i].n;
+				at++;
+			}
+		}
+		e = hipMemcpyAsync(sc->dev, sc->pin, (size_t)nit * rec * sizeof(uint64_t), hipMemcpyHostToDevice, st);
+		if (e != hipSuccess)
+			rc = ecg_hip_fail(e, "update table H2D");
+		for (w = 0, at = 0; w < nwave && rc == 0; w++) {
+			uint32_t cnt = 0;
+			int ke;
+
+			for (i = 0; i < nit; i++)
+				cnt += it[i].wave == w;
+			prm->nstripes = cnt;
+			ke = ecg_k_launch_update_ptrs(prm, (const uint64_t *)sc->dev + (size_t)at * rec, (uint32_t)k,
+						      granule, (void *)st, &kid);
+			if (ke != 0)
+				rc = ecg_hip_fail((hipError_t)ke, "update_ptrs kernel launch");
+			at += cnt;
+		}
+		if (rc == 0) {
+			e = hipEventRecord(sc->done, st);
+			if (e != hipSuccess)
+				rc = ecg_hip_fail(e, "scratch event record");
+			sc->pending = rc == 0;
+		}
+	}
+	pthread_mutex_unlock(&ctx->lock);
+	if (rc == 0) {
+		ECG_STAT_ADD(ctx, launches, nwave);
+		ECG_STAT_ADD(ctx, update_cells, nreq);
+		ECG_STAT_ADD(ctx, update_bytes, (uint64_t)nreq * C);
+		ecg_set_last_kernel(ecg_k_kernel_name(kid));
+		if (nlaunch)
+			*nlaunch = nwave;
+	}
+out:
+	free(rq);
+	free(it);
+	free(prm);
+	return rc;
+}
+
+int ecg_update_ptrs(ecg_ctx_t *ctx, int k, int p, uint64_t cell_bytes, uint32_t nreq, void *const *cells,
+		    const uint8_t *vec_i, void *stream)
+{
+	unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
+
+	if (k < 1 || k > ECG_KMAX_K || p < 1 || p > ECG_KMAX_R)
+		return ecg_fail(-ECG_DER_INVAL, "update_ptrs: k=%d p=%d (max %d + %d)", k, p, ECG_KMAX_K, ECG_KMAX_R);
+	ecg_gen_cauchy1(k, p, en);	/* parity rows: the codec's, ref:src/object/obj_class.c:614 */
+	return ecg_update_ptrs_coef(ctx, k, p, &en[k * k], cell_bytes, nreq, cells, vec_i, stream, NULL);
+}
+
 /* ---- obj_ec_recx_encode over a device-resident sgl ---------------------- */
 
 struct sgl_cur {

@@ -36,14 +36,27 @@
  * (ecg_queue_create_multi): each slot's staging, stream and launches live on
  * its own device.
  *
- * Device cells (an engine whose bio buffers live in HBM): encode and recover
- * requests whose cells are memory of one of the queue's devices go to slots of
- * that device that hold no data at all -- only the stripes' cell pointers,
- * ISA-L's data[] / coding[] laid end to end -- and a batch is one
- * pointer-table launch on the cells in place (ecg_matmul_ptrs), no PCIe.  Such
- * a slot closes as soon as its device has no batch of this queue in flight, so
- * a lone request launches at once and requests arriving while a batch runs
- * form the next one.
+ * Device cells (an engine whose bio buffers live in HBM): requests whose cells
+ * are memory of one of the queue's devices go to slots of that device that
+ * hold no data at all -- only the stripes' cell pointers, ISA-L's data[] /
+ * coding[] laid end to end -- and a batch is one pointer-table launch on the
+ * cells in place (ecg_matmul_ptrs), no PCIe.  Updates batch the same way into
+ * ecg_update_ptrs launches: requests naming the same parity cells (one
+ * stripe's cells updated one by one) fold into one pass over that parity, and
+ * requests whose parity bytes would meet inside one launch go to ordered
+ * launches; the update batches of one device are ordered behind each other
+ * (q->uev), so two batches never read-modify-write one parity byte at once.
+ * Such a slot closes as soon as its device has no batch of this queue in
+ * flight, so a lone request launches at once and requests arriving while a
+ * batch runs form the next one.
+ *
+ * CPU executor (ecg_queue_create(NULL, ...), or $ECG_FORCE_CPU=1): the same
+ * slots, reservations and state machine with no device -- the engine's
+ * DSS_XS_OFFLOAD ULT + ABT_eventual pattern this facade replaces
+ * (ref:src/object/srv_ec_aggregate.c:701-734, ref:src/engine/ult.c:394-470).
+ * A closed slot goes straight to DONE and the completion threads compute each
+ * request's product from its staged inputs with ecg_cpu_matmul.  Host cells
+ * only.
  */
 #define _GNU_SOURCE
 #include <stdlib.h>
@@ -75,7 +88,8 @@ struct qreq {
 };
 
 struct qslot {
-	ecg_ctx_t *ctx;			/* device this slot's staging and launches live on */
+	ecg_ctx_t *ctx;			/* device this slot's staging and launches live on (NULL: CPU) */
+	int ci;				/* index of ctx in the queue's ctxs[] */
 	enum slot_state state;
 	/* class */
 	int op, k, p, nerrs, rows;
@@ -99,7 +113,9 @@ struct qslot {
 	uint32_t fin_next, fin_done;	/* completion progress (S_DONE) */
 	uint64_t t_open_ns;
 	struct qreq *reqs;		/* cap entries */
-	uint64_t *tab;			/* devcells: cap x (k + rows) cell addresses */
+	uint64_t *tab;			/* devcells: cap x (k + rows) cell addresses; updates
+					 * cap x (2 + rows): old, new, parity cells */
+	uint8_t *uvec;			/* devcells updates: vec_i per request */
 	/* staging */
 	unsigned char *host;		/* pinned: inputs [cap][k][pitch], (updates: vec_i [cap]),
 					 * outputs [cap][rows][pitch] at out_off */
@@ -113,6 +129,13 @@ struct qslot {
 
 struct ecg_queue {
 	ecg_ctx_t *ctx;
+	int cpu;			/* CPU executor: no device, host cells only */
+	int nctx;
+	ecg_ctx_t *ctxs[NSLOT_MAX];
+	/* device-cell update batches of device ctxs[i] run in order: each waits
+	 * for uev[i], recorded after the previous one (uev_set[i]) */
+	hipEvent_t uev[NSLOT_MAX];
+	int uev_set[NSLOT_MAX];
 	ecg_queue_attr_t attr;
 	size_t slot_bytes;
 	pthread_mutex_t lock;
@@ -207,7 +230,7 @@ static uint32_t res_count(const struct qslot *s)
 /* FILLING -> READY (lock held): no reservation after this one. */
 static void slot_close(struct qslot *s)
 {
-	const uint64_t w = __atomic_fetch_and(&s->res, ~RES_OPEN, __ATOMIC_ACQ_REL);
+	const uint64_t w = __atomic_fetch_and(&s->res, ~RES_OPEN, __ATOMIC_SEQ_CST);
 
 	s->reserved = (uint32_t)(w & RES_CNT);
 	s->state = S_READY;
@@ -322,21 +345,51 @@ static void launch_slot(struct ecg_queue *q, struct qslot *s)
 	hipError_t e;
 	int j, rc;
 
-	(void)q;
+	if (q->cpu) {
+		/* no device: the completion threads compute each request from
+		 * its staged inputs (finish_req) */
+		s->rc = 0;
+		s->fin_next = 0;
+		s->fin_done = 0;
+		s->state = S_DONE;
+		q->batches++;
+		pthread_cond_broadcast(&q->cv_fin);
+		return;
+	}
 	ecg_trace_push("ecg:queue_batch");
 	e = hipSetDevice(s->ctx->device);
 	if (s->devcells) {
 		/* the cells in place: one pointer-table launch (its table upload
 		 * and kernel on the slot's stream), nothing crosses back */
 		rc = e == hipSuccess ? 0 : ecg_hip_fail(e, "queue set device");
-		if (rc == 0)
+		if (rc == 0 && s->op == OP_UPDATE) {
+			/* after the device's previous update batch: one parity cell's
+			 * read-modify-writes never overlap across batches */
+			if (q->uev_set[s->ci]) {
+				e = hipStreamWaitEvent(s->st, q->uev[s->ci], 0);
+				if (e != hipSuccess)
+					rc = ecg_hip_fail(e, "queue update order");
+			}
+			if (rc == 0)
+				rc = ecg_update_ptrs_coef(s->ctx, s->k, s->rows, s->coef, s->C, n, (void *const *)s->tab,
+							  s->uvec, s->st, NULL);
+			if (rc == 0) {
+				e = hipEventRecord(q->uev[s->ci], s->st);
+				if (e != hipSuccess)
+					rc = ecg_hip_fail(e, "queue update event");
+				q->uev_set[s->ci] = rc == 0;
+			}
+		} else if (rc == 0) {
 			rc = ecg_matmul_ptrs(s->ctx, s->k, s->rows, s->coef, s->C, n, (void *const *)s->tab, s->st);
+		}
 		if (rc == 0) {
 			e = hipEventRecord(s->done, s->st);
 			if (e != hipSuccess)
 				rc = ecg_hip_fail(e, "queue batch event");
 		}
-		if (rc == 0 && s->op == OP_ENCODE) {
+		if (rc == 0 && s->op == OP_UPDATE) {
+			;	/* counted by ecg_update_ptrs_coef */
+		} else if (rc == 0 && s->op == OP_ENCODE) {
 			ECG_STAT_ADD(s->ctx, encode_stripes, n);
 			ECG_STAT_ADD(s->ctx, encode_bytes, (uint64_t)s->k * s->C * n);
 		} else if (rc == 0) {
@@ -450,14 +503,43 @@ static void xor_into_locked(struct ecg_queue *q, unsigned char *dst, const unsig
 	}
 }
 
+/* CPU executor: request i's product from its staged inputs -- encode and
+ * recovery straight into the request's cells, an update's parity deltas into
+ * the slot's output staging (XORed in below like the device's) */
+static int cpu_product(struct qslot *s, uint32_t i)
+{
+	const uint64_t in_stride = s->pitch * (uint64_t)s->nin, out_stride = s->pitch * (uint64_t)s->rows;
+	unsigned char *in = s->host + (size_t)i * in_stride;
+	unsigned char *src[ECG_MAX_K], *dst[ECG_MAX_P];
+	unsigned char col[ECG_MAX_P];
+
+	for (int j = 0; j < s->nin; j++)
+		src[j] = in + (uint64_t)j * s->pitch;
+	if (s->op == OP_UPDATE) {
+		const unsigned vec = s->host[(size_t)s->pitch * s->nin * s->cap + i];
+
+		for (int r = 0; r < s->rows; r++) {
+			dst[r] = s->host + s->out_off + i * out_stride + (uint64_t)r * s->pitch;
+			col[r] = s->coef[(size_t)r * s->k + vec];
+		}
+		return ecg_cpu_matmul((int)s->C, 1, s->rows, col, src, dst, 0);
+	}
+	return ecg_cpu_matmul((int)s->C, s->k, s->rows, s->coef, src, s->reqs[i].dst, 0);
+}
+
 static void finish_req(struct ecg_queue *q, struct qslot *s, uint32_t i)
 {
 	const uint64_t out_stride = s->pitch * (uint64_t)s->rows;
 	const unsigned char *out = s->host + s->out_off + i * out_stride;
 	struct qreq *r = &s->reqs[i];
+	int rc = s->rc;
 
 	ecg_trace_push("ecg:queue_complete");
-	if (s->devcells)
+	if (q->cpu) {
+		rc = cpu_product(s, i);
+		for (int j = 0; rc == 0 && s->op == OP_UPDATE && j < s->rows; j++)
+			xor_into_locked(q, r->dst[j], out + j * s->pitch, s->C);
+	} else if (s->devcells)
 		;				/* written in place by the launch */
 	else if (s->rc == 0 && s->op == OP_UPDATE)	/* parity ^= coef[r][vec_i] * diff */
 		for (int j = 0; j < s->rows; j++)
@@ -467,7 +549,7 @@ static void finish_req(struct ecg_queue *q, struct qslot *s, uint32_t i)
 			memcpy(r->dst[j], out + j * s->pitch, s->C);
 	ecg_trace_pop();
 	if (r->cb)
-		r->cb(r->arg, s->rc);
+		r->cb(r->arg, rc);
 }
 
 /* Completion threads: claim requests of S_DONE slots -- one at a time for
@@ -527,7 +609,7 @@ static void *worker_main(void *argp)
 		for (int i = 0; i < q->nslot; i++) {
 			struct qslot *s = &q->slot[i];
 
-			if (s->state == S_READY && __atomic_load_n(&s->filled, __ATOMIC_ACQUIRE) == s->reserved) {
+			if (s->state == S_READY && __atomic_load_n(&s->filled, __ATOMIC_SEQ_CST) == s->reserved) {
 				launch_slot(q, s);
 				idle = 0;
 			}
@@ -588,8 +670,14 @@ static void *worker_main(void *argp)
 
 static void slot_free(struct qslot *s)
 {
-	if (s->ctx)
-		(void)hipSetDevice(s->ctx->device);
+	if (s->ctx == NULL) {		/* CPU executor: plain memory, nothing on a device */
+		free(s->host);
+		free(s->reqs);
+		free(s->tab);
+		free(s->uvec);
+		return;
+	}
+	(void)hipSetDevice(s->ctx->device);
 	if (s->host)
 		(void)hipHostFree(s->host);
 	if (s->dev)
@@ -600,9 +688,11 @@ static void slot_free(struct qslot *s)
 		(void)hipEventDestroy(s->done);
 	free(s->reqs);
 	free(s->tab);
+	free(s->uvec);
 }
 
-/* Slots round-robin over ctxs[nctx] (one context = one device). */
+/* Slots round-robin over ctxs[nctx] (one context = one device); nctx = 0:
+ * the CPU executor. */
 static int queue_create(ecg_ctx_t *const *ctxs, int nctx, const ecg_queue_attr_t *attr,
 			ecg_queue_t **out)
 {
@@ -613,8 +703,12 @@ static int queue_create(ecg_ctx_t *const *ctxs, int nctx, const ecg_queue_attr_t
 	q = calloc(1, sizeof(*q));
 	if (q == NULL)
 		return ecg_fail(-ECG_DER_NOMEM, "queue_create: calloc");
-	q->ctx = ctxs[0];
-	q->nslot = nctx == 1 ? NSLOT_MIN : 2 * nctx;
+	q->cpu = nctx == 0;
+	q->ctx = nctx ? ctxs[0] : NULL;
+	q->nctx = nctx < NSLOT_MAX ? nctx : NSLOT_MAX;
+	for (i = 0; i < q->nctx; i++)
+		q->ctxs[i] = ctxs[i];
+	q->nslot = nctx <= 1 ? NSLOT_MIN : 2 * nctx;
 	if (q->nslot < NSLOT_MIN)
 		q->nslot = NSLOT_MIN;
 	if (q->nslot > NSLOT_MAX)
@@ -644,14 +738,22 @@ static int queue_create(ecg_ctx_t *const *ctxs, int nctx, const ecg_queue_attr_t
 	for (i = 0; i < q->nslot && e == hipSuccess; i++) {
 		struct qslot *s = &q->slot[i];
 
-		s->ctx = ctxs[i % nctx];
 		s->reqs = calloc(q->attr.max_batch, sizeof(*s->reqs));
 		s->tab = calloc((size_t)q->attr.max_batch * (ECG_KMAX_K + ECG_KMAX_R), sizeof(*s->tab));
-		if (s->reqs == NULL || s->tab == NULL) {
+		s->uvec = calloc(q->attr.max_batch, 1);
+		if (s->reqs == NULL || s->tab == NULL || s->uvec == NULL) {
 			e = hipErrorOutOfMemory;
 			break;
 		}
 		s->bytes = q->slot_bytes;
+		if (q->cpu) {
+			s->host = aligned_alloc(64, (s->bytes + 63) & ~(size_t)63);
+			if (s->host == NULL)
+				e = hipErrorOutOfMemory;
+			continue;
+		}
+		s->ci = i % nctx;
+		s->ctx = ctxs[s->ci];
 		e = hipSetDevice(s->ctx->device);
 		if (e == hipSuccess) {
 			/* the slot's pinned staging on its device's NUMA node: the
@@ -672,6 +774,11 @@ static int queue_create(ecg_ctx_t *const *ctxs, int nctx, const ecg_queue_attr_t
 		if (e == hipSuccess)
 			e = hipEventCreateWithFlags(&s->done, hipEventDisableTiming);
 	}
+	for (i = 0; i < q->nctx && e == hipSuccess; i++) {
+		e = hipSetDevice(q->ctxs[i]->device);
+		if (e == hipSuccess)
+			e = hipEventCreateWithFlags(&q->uev[i], hipEventDisableTiming);
+	}
 	for (i = 0; i < NFIN && e == hipSuccess; i++) {
 		if (pthread_create(&q->fin[i], NULL, fin_main, q) != 0)
 			e = hipErrorOutOfMemory;
@@ -691,8 +798,14 @@ static int queue_create(ecg_ctx_t *const *ctxs, int nctx, const ecg_queue_attr_t
 	if (e != hipSuccess) {
 		for (i = 0; i < q->nslot; i++)
 			slot_free(&q->slot[i]);
+		const int cpu = q->cpu;
+
+		for (i = 0; i < q->nctx; i++)
+			if (q->uev[i])
+				(void)hipEventDestroy(q->uev[i]);
 		free(q);
-		return ecg_hip_fail(e, "queue_create");
+		return cpu ? ecg_fail(-ECG_DER_NOMEM, "queue_create: out of memory or threads")
+			   : ecg_hip_fail(e, "queue_create");
 	}
 	*out = q;
 	return 0;
@@ -700,10 +813,14 @@ static int queue_create(ecg_ctx_t *const *ctxs, int nctx, const ecg_queue_attr_t
 
 int ecg_queue_create(ecg_ctx_t *ctx, const ecg_queue_attr_t *attr, ecg_queue_t **out)
 {
+	const char *force = getenv("ECG_FORCE_CPU");
 	int rc;
 
-	if (ctx == NULL || out == NULL)
+	if (out == NULL)
 		return ecg_fail(-ECG_DER_INVAL, "queue_create: NULL argument");
+	/* no context, or $ECG_FORCE_CPU=1: the CPU executor, no device touched */
+	if (ctx == NULL || (force && force[0] == '1'))
+		return queue_create(NULL, 0, attr, out);
 	rc = ecg_ctx_enter(ctx);
 	if (rc)
 		return rc;
@@ -736,6 +853,10 @@ void ecg_queue_destroy(ecg_queue_t *q)
 		pthread_join(q->fin[i], NULL);
 	for (int i = 0; i < q->nslot; i++)
 		slot_free(&q->slot[i]);
+	for (int i = 0; i < q->nctx; i++) {
+		(void)hipSetDevice(q->ctxs[i]->device);
+		(void)hipEventDestroy(q->uev[i]);
+	}
 	pthread_cond_destroy(&q->cv_work);
 	pthread_cond_destroy(&q->cv_slot);
 	pthread_cond_destroy(&q->cv_done);
@@ -746,72 +867,56 @@ void ecg_queue_destroy(ecg_queue_t *q)
 	free(q);
 }
 
-/* Every cell of a device-cell request inside one allocation of ctx's device
- * (a launch on anything else would fault the GPU).  The HIP runtime's
- * pointer queries serialise across threads, so the usual stripe -- every cell
- * in one allocation -- costs one range query beyond the placement query; only
- * cells outside that allocation are looked up one by one. */
-static int cells_checked(ecg_ctx_t *ctx, int op, int k, int p, uint64_t C, unsigned char *const *src,
-			 unsigned char *stripe, unsigned char *const *dst)
-{
-	const unsigned char *first = op == OP_RECOVER ? stripe : src[0];
-	hipDeviceptr_t base = NULL;
-	size_t size = 0;
-	uintptr_t lo, hi;
-	int i, rc = 0;
-
-	if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)first) != hipSuccess) {
-		(void)hipGetLastError();
-		return ecg_fail(-ECG_DER_INVAL, "queue: device cell %p: no device allocation", (const void *)first);
-	}
-	lo = (uintptr_t)base;
-	hi = lo + size;
-	if (op == OP_RECOVER) {
-		const uintptr_t a = (uintptr_t)stripe;
-
-		if (a + C * (uint64_t)(k + p) > hi)
-			return ecg_fail(-ECG_DER_INVAL, "queue: the [k+p][cell] stripe runs past the end of its "
-					"allocation");
-		return 0;
-	}
-	for (i = 0; i < k + p && rc == 0; i++) {
-		unsigned char *c = i < k ? src[i] : dst[i - k];
-		const uintptr_t a = (uintptr_t)c;
-
-		if (a < lo || a + C > hi)	/* another allocation: look it up */
-			rc = ecg_cells_on_device(ctx, &c, 1, C, i < k ? "source" : "parity");
-	}
-	return rc;
-}
-
-/* Device-cell requests: the cells' device must be one of the queue's, every
- * cell inside one of its allocations, and the shape one pointer-table launch
- * takes.  Returns the device, -1 for host cells, or a negative DER code
- * through *rc. */
+/* Where a request's cells are (ecg_cells_place, through the drop-in's
+ * per-thread cache of plain host memory): all host memory -> -1; all memory
+ * of one of the queue's devices -> that device (every cell inside one of its
+ * allocations, and the shape one pointer-table launch takes); anything else
+ * -> -1 with a negative DER code in *rc naming the cell.  A recovery's stripe
+ * is one [k+p][cell] range.  The CPU executor takes host memory only (and
+ * looks nothing up when the process sees no device at all). */
 static int request_device(struct ecg_queue *q, int op, int k, int p, uint64_t C, int rows,
 			  unsigned char *const *src, unsigned char *stripe, unsigned char *const *dst, int *rc)
 {
-	const unsigned char *first = op == OP_RECOVER ? stripe : src[0];
-	const int dev = ecg_ptr_device(first);
+	signed char place[ECG_MAX_K + ECG_MAX_P];
+	unsigned char *one[1] = {stripe};
+	const int nin = op == OP_RECOVER ? 1 : op == OP_UPDATE ? 2 : k;
+	const int nout = op == OP_RECOVER ? 0 : p;
 	ecg_ctx_t *ctx = NULL;
+	int dev = -1, ndev;
 
 	*rc = 0;
-	if (dev < 0)
+	if (q->cpu && !ecg_dropin_gpu())
 		return -1;
-	for (int i = 0; i < q->nslot && ctx == NULL; i++)
-		if (q->slot[i].ctx->device == dev)
-			ctx = q->slot[i].ctx;
+	ndev = ecg_cells_place(op == OP_RECOVER ? one : src, nin, dst, nout,
+			       op == OP_RECOVER ? C * (uint64_t)(k + p) : C, ecg_ptr_device_cached, place, &dev);
+	if (ndev <= 0) {
+		*rc = ndev < 0 ? ndev : 0;
+		return -1;
+	}
+	if (ndev != nin + nout) {
+		for (int i = 0; i < nin + nout; i++)
+			if (place[i] < 0) {
+				*rc = ecg_fail(-ECG_DER_INVAL, "queue: %s %d is host memory, other cells of the request "
+					       "memory of device %d (a request's cells are all host or all device "
+					       "memory)", i < nin ? "input" : "parity", i < nin ? i : i - nin, dev);
+				break;
+			}
+		return -1;
+	}
+	if (q->cpu) {
+		*rc = ecg_fail(-ECG_DER_INVAL, "queue: cells are memory of device %d, and this queue runs on the CPU "
+			       "(created without a context, or $ECG_FORCE_CPU=1)", dev);
+		return -1;
+	}
+	for (int i = 0; i < q->nctx && ctx == NULL; i++)
+		if (q->ctxs[i]->device == dev)
+			ctx = q->ctxs[i];
 	if (ctx == NULL)
 		*rc = ecg_fail(-ECG_DER_INVAL, "queue: cells are memory of device %d, which has no slot in "
 			       "this queue", dev);
-	else if (op == OP_UPDATE)
-		*rc = ecg_fail(-ECG_DER_NOSYS, "queue_update: device cells (use ecg_update / "
-			       "ecg_agg_update_parity on the device)");
 	else if (k > ECG_KMAX_K || rows > ECG_KMAX_R)
 		*rc = ecg_fail(-ECG_DER_INVAL, "queue: device cells need k <= %d and rows <= %d (k=%d rows=%d)",
 			       ECG_KMAX_K, ECG_KMAX_R, k, rows);
-	else
-		*rc = cells_checked(ctx, op, k, p, C, src, stripe, dst);
 	return dev;
 }
 
@@ -881,7 +986,15 @@ static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const u
 		r->nerrs = nerrs;
 		r->cb = cb;
 		r->arg = arg;
-		if (s->devcells) {		/* the stripe's ISA-L pointers, nothing copied */
+		if (s->devcells && op == OP_UPDATE) {	/* old, new, parity: ecg_update_ptrs' row */
+			uint64_t *t = s->tab + (size_t)idx * (uint64_t)(2 + s->rows);
+
+			t[0] = (uint64_t)(uintptr_t)src[0];
+			t[1] = (uint64_t)(uintptr_t)src[1];
+			for (i = 0; i < s->rows; i++)
+				t[2 + i] = (uint64_t)(uintptr_t)dst[i];
+			s->uvec[idx] = (uint8_t)vec_i;
+		} else if (s->devcells) {	/* the stripe's ISA-L pointers, nothing copied */
 			uint64_t *t = s->tab + (size_t)idx * (uint64_t)(k + s->rows);
 
 			for (i = 0; i < k; i++)
@@ -907,11 +1020,22 @@ static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const u
 	/* wake the worker only for what it acts on: a slot's first request (a new
 	 * deadline to wait for; for device cells, a batch that may launch at
 	 * once), a slot this request filled up, and a closed slot -- whose last
-	 * inputs may be the ones landing now */
+	 * inputs may be the ones landing now.  Store-then-load of two different
+	 * words on each side (here `filled` then `res`; slot_close clears `res`'s
+	 * open bit, the worker then loads `filled`): only sequentially consistent
+	 * operations rule out both sides reading the old values, which would skip
+	 * this wake-up (the worker's 20 us poll of READY slots would still catch
+	 * it, late).  The slot's fields are read BEFORE `filled` counts this
+	 * request: from then on the worker may launch it, the completion threads
+	 * free it and another submitter reopen it with a new class (the
+	 * ThreadSanitizer run of tests/c queue_cpu_stress caught a read of `cap`
+	 * racing with slot_open here).  `res` itself carries the generation: a
+	 * reopened slot's open bit means this one's batch has already launched. */
 	{
-		const uint32_t n = __atomic_add_fetch(&s->filled, 1u, __ATOMIC_ACQ_REL);
+		const uint32_t cap = LD(s->cap);
+		const uint32_t n = __atomic_add_fetch(&s->filled, 1u, __ATOMIC_SEQ_CST);
 
-		if (n == 1 || idx + 1 == s->cap || !(__atomic_load_n(&s->res, __ATOMIC_ACQUIRE) & RES_OPEN)) {
+		if (n == 1 || idx + 1 == cap || !(__atomic_load_n(&s->res, __ATOMIC_SEQ_CST) & RES_OPEN)) {
 			pthread_mutex_lock(&q->lock);
 			pthread_cond_signal(&q->cv_work);
 			pthread_mutex_unlock(&q->lock);

@@ -222,6 +222,75 @@ int ecg_cells_on_device(ecg_ctx_t *ctx, unsigned char *const *v, int n, uint64_t
 	return 0;
 }
 
+/* Placement of every cell of a one-stripe call (src[0..k) then dst[0..rows)):
+ * place[i] = the device whose allocation holds cell i whole, or -1 for host
+ * memory (plain malloc / mmap, pinned, registered, managed: the CPU can
+ * address it).  `query` is the placement lookup (ecg_ptr_device, or the
+ * drop-in's cached one).  Cells inside a range already seen in this call
+ * (one allocation: the usual stripe) cost no query.  Returns the number of
+ * device cells (*dev = their device), or -DER_INVAL naming the cell for cells
+ * on two devices or a device cell running past its allocation. */
+int ecg_cells_place(unsigned char *const *src, int k, unsigned char *const *dst, int rows, uint64_t len,
+		    int (*query)(const void *), signed char *place, int *dev)
+{
+	struct {
+		uintptr_t lo, hi;
+		int dev;
+	} seen[4];
+	int nseen = 0, ndev = 0, i, x;
+
+	*dev = -1;
+	for (i = 0; i < k + rows; i++) {
+		const unsigned char *c = i < k ? src[i] : dst[i - k];
+		const uintptr_t a = (uintptr_t)c, e = a + (uintptr_t)len;
+		const char *what = i < k ? "source" : "output";
+		const int idx = i < k ? i : i - k;
+		hipDeviceptr_t base = NULL;
+		size_t size = 0;
+		int d;
+
+		if (c == NULL)
+			return ecg_fail(-ECG_DER_INVAL, "%s %d is NULL", what, idx);
+		for (x = 0; x < nseen; x++)
+			if (a >= seen[x].lo && e <= seen[x].hi)
+				break;
+		if (x < nseen) {
+			d = seen[x].dev;
+		} else {
+			d = query(c);
+			if (d != ECG_PTR_UNKNOWN) {
+				/* runtime-known memory: its allocation's range, so the
+				 * stripe's other cells in it need no query */
+				if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)c) == hipSuccess) {
+					if (d >= 0 && e > (uintptr_t)base + size)
+						return ecg_fail(-ECG_DER_INVAL, "%s %d: %llu bytes run past the end of its "
+								"device allocation", what, idx, (unsigned long long)len);
+					x = nseen < 4 ? nseen++ : i % 4;
+					seen[x].lo = (uintptr_t)base;
+					seen[x].hi = (uintptr_t)base + size;
+					seen[x].dev = d >= 0 ? d : -1;
+				} else {
+					(void)hipGetLastError();
+					if (d >= 0)
+						return ecg_fail(-ECG_DER_INVAL, "%s %d: no device allocation", what, idx);
+				}
+			}
+			if (d < 0)
+				d = -1;
+		}
+		place[i] = (signed char)(d < 0 ? -1 : d);
+		if (d >= 0) {
+			if (*dev >= 0 && *dev != d)
+				return ecg_fail(-ECG_DER_INVAL, "%s %d is memory of device %d, an earlier cell of device %d "
+						"(one call's cells may span one device and host memory)", what, idx, d,
+						*dev);
+			*dev = d;
+			ndev++;
+		}
+	}
+	return ndev;
+}
+
 /* The stream of the calling thread among the context's drop-in pool
  * (created on first use): concurrent synchronous callers spread over up to
  * ECG_DROPIN_STREAMS streams -- the box's hardware queues -- instead of
@@ -303,11 +372,7 @@ static int matmul_device(ecg_ctx_t *ctx, int len, int k, int rows, const unsigne
 	hipError_t e;
 	int j, r, rc;
 
-	rc = ecg_cells_on_device(ctx, src, k, (uint64_t)len, "source");
-	if (rc == 0)
-		rc = ecg_cells_on_device(ctx, dst, rows, (uint64_t)len, "output");
-	if (rc == 0)
-		rc = pool_stream(ctx, &st);
+	rc = pool_stream(ctx, &st);
 	if (rc == 0)
 		rc = tstage_event(ctx, &t);
 	if (rc)
@@ -340,13 +405,15 @@ static int matmul_device(ecg_ctx_t *ctx, int len, int k, int rows, const unsigne
 
 /*
  * dst[r][i] (^)= XOR_j coef[r*k + j] * src[j][i], i < len, on ctx's GPU.
- * Host cells are staged through pinned memory; device cells (every cell
- * hipMalloc'd) run in place.  With ECG_F_ACCUMULATE the current dst bytes
- * travel to the device first (ec_encode_data_update semantics).  src_dev is
- * ecg_ptr_device(src[0]), looked up once by the caller.
+ * place[] (ecg_cells_place, k + rows entries; NULL = every cell host memory)
+ * says where each cell is: host cells are staged through pinned memory,
+ * device cells (memory of ctx's device, checked by the caller) are used in
+ * place -- all of them device cells: launches on the cells alone, no staging.
+ * With ECG_F_ACCUMULATE the current bytes of host dst cells travel to the
+ * device first (ec_encode_data_update semantics).
  */
 int ecg_matmul_host_mem(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
-			unsigned char *const *src, unsigned char *const *dst, unsigned flags, int src_dev)
+			unsigned char *const *src, unsigned char *const *dst, unsigned flags, const signed char *place)
 {
 	int64_t soff[ECG_MAX_K + 256], doff[256];
 	struct tstage *t = NULL;
@@ -365,8 +432,21 @@ int ecg_matmul_host_mem(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned
 	rc = ecg_ctx_enter(ctx);
 	if (rc)
 		return rc;
-	if (src_dev >= 0)
-		return matmul_device(ctx, len, k, rows, coef, src, dst, flags);
+	if (place) {
+		int ndev = 0;
+
+		for (j = 0; j < k + rows; j++) {
+			if (place[j] >= 0 && place[j] != ctx->device)
+				return ecg_fail(-ECG_DER_INVAL, "matmul_host: %s %d is memory of device %d, not of the "
+						"context's device %d", j < k ? "source" : "output", j < k ? j : j - k,
+						place[j], ctx->device);
+			ndev += place[j] >= 0;
+		}
+		if (ndev == k + rows)
+			return matmul_device(ctx, len, k, rows, coef, src, dst, flags);
+		if (ndev == 0)
+			place = NULL;
+	}
 	pitch = ((size_t)len + 255) & ~(size_t)255;
 	bytes = pitch * (size_t)(k + rows);
 	rc = tstage_get(ctx, bytes, &t);
@@ -374,15 +454,13 @@ int ecg_matmul_host_mem(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned
 		return rc;
 	h = t->host;
 	d = t->dev;
-	for (j = 0; j < k; j++) {
-		memcpy(h + j * pitch, src[j], (size_t)len);
-		soff[j] = (int64_t)(j * pitch);
-	}
-	for (r = 0; r < rows; r++) {
-		if (flags & ECG_F_ACCUMULATE)
+	/* host cells into the staging; device cells (mixed placement) stay put */
+	for (j = 0; j < k; j++)
+		if (!(place && place[j] >= 0))
+			memcpy(h + j * pitch, src[j], (size_t)len);
+	for (r = 0; r < rows; r++)
+		if ((flags & ECG_F_ACCUMULATE) && !(place && place[k + r] >= 0))
 			memcpy(h + (k + r) * pitch, dst[r], (size_t)len);
-		doff[r] = (int64_t)((k + r) * pitch);
-	}
 	if (bytes <= g_zero_copy_max) {
 		/* small call: the kernel reads and writes the pinned staging over
 		 * PCIe directly -- one launch instead of H2D + launch + D2H */
@@ -401,6 +479,13 @@ int ecg_matmul_host_mem(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned
 		if (e != hipSuccess)
 			return ecg_hip_fail(e, "matmul_host H2D");
 	}
+	/* cell offsets from the staging base d: a device cell's is its distance
+	 * from d (one address space) */
+	for (j = 0; j < k; j++)
+		soff[j] = place && place[j] >= 0 ? (int64_t)((uintptr_t)src[j] - (uintptr_t)d) : (int64_t)(j * pitch);
+	for (r = 0; r < rows; r++)
+		doff[r] = place && place[k + r] >= 0 ? (int64_t)((uintptr_t)dst[r] - (uintptr_t)d)
+						     : (int64_t)((k + r) * pitch);
 	rc = launch_split(ctx, len, k, rows, coef, d, soff, d, doff, flags, t->st);
 	if (rc)
 		return rc;
@@ -416,7 +501,8 @@ int ecg_matmul_host_mem(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned
 	if (e != hipSuccess)
 		return ecg_hip_fail(e, "matmul_host D2H");
 	for (r = 0; r < rows; r++)
-		memcpy(dst[r], h + (k + r) * pitch, (size_t)len);
+		if (!(place && place[k + r] >= 0))
+			memcpy(dst[r], h + (k + r) * pitch, (size_t)len);
 	return 0;
 }
 
@@ -425,8 +511,16 @@ int ecg_matmul_host(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned cha
 {
 	if (ctx == NULL)
 		return ecg_fail(-ECG_DER_INVAL, "NULL context");
-	if (len <= 0 || src == NULL)
-		return ecg_matmul_host_mem(ctx, len, k, rows, coef, src, dst, flags, -1);
-	return ecg_matmul_host_mem(ctx, len, k, rows, coef, src, dst, flags,
-				   ecg_ctx_enter(ctx) == 0 ? ecg_ptr_device(src[0]) : -1);
+	if (len <= 0 || src == NULL || dst == NULL || k < 1 || k > ECG_MAX_K + 256 || rows < 1 || rows > 256)
+		return ecg_matmul_host_mem(ctx, len, k, rows, coef, src, dst, flags, NULL);
+	{
+		signed char place[ECG_MAX_K + 256 + 256];
+		int dev, rc = ecg_ctx_enter(ctx);
+
+		if (rc == 0)
+			rc = ecg_cells_place(src, k, dst, rows, (uint64_t)len, ecg_ptr_device, place, &dev);
+		if (rc < 0)
+			return rc;
+		return ecg_matmul_host_mem(ctx, len, k, rows, coef, src, dst, flags, rc ? place : NULL);
+	}
 }

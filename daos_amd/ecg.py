@@ -59,6 +59,7 @@ _SIGS = [
     ("ecg_update", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, C.c_int, u32p, vp, vp, C.c_int64,
                              vp, C.c_int64, C.c_int64, vp]),
     ("ecg_matmul_ptrs", C.c_int, [vp, C.c_int, C.c_int, u8p, C.c_uint64, C.c_uint32, C.POINTER(vp), vp]),
+    ("ecg_update_ptrs", C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, C.c_uint32, C.POINTER(vp), u8p, vp]),
     ("ecg_matmul_host", C.c_int, [vp, C.c_int, C.c_int, C.c_int, u8p, C.POINTER(u8p), C.POINTER(u8p), C.c_uint]),
     ("ecg_cpu_matmul", C.c_int, [C.c_int, C.c_int, C.c_int, u8p, C.POINTER(u8p), C.POINTER(u8p), C.c_uint]),
     ("ecg_cpu_isa", C.c_char_p, []),
@@ -228,6 +229,17 @@ class MigratePiece(C.Structure):
     """ecg_migrate_piece_t: one piece of migrate_update_parity's walk."""
     _fields_ = [("recx", Recx), ("buf_off", C.c_uint64), ("buf_len", C.c_uint64), ("csum_off", C.c_uint64),
                 ("nr_csums", C.c_uint32), ("parity", C.c_uint32)]
+
+
+MAX_K, MAX_P = 64, 8
+
+
+class RecovCodec(C.Structure):
+    """struct ecg_obj_ec_recov_codec (include/ecg_daos.h), field for field."""
+    _fields_ = [("er_gftbls", C.c_ubyte * (MAX_K * MAX_P * 32)), ("er_de_matrix", C.c_ubyte * (MAX_P * MAX_K)),
+                ("er_dec_idx", C.c_uint32 * MAX_K), ("er_err_list", C.c_uint32 * MAX_P), ("er_nerrs", C.c_uint32),
+                ("er_data_nerrs", C.c_uint32), ("k", C.c_int), ("p", C.c_int), ("reused_encode", C.c_int),
+                ("er_builds", C.c_uint32)]
 
 
 DRT_SHADOW = 2
@@ -573,6 +585,20 @@ class Context:
         arr = (vp * len(cells))(*cells)
         _chk(lib().ecg_matmul_ptrs(self.h, k, rows, _u8(co), cell_bytes, nstripes, arr, stream), "matmul_ptrs")
 
+    def update_ptrs(self, k: int, p: int, cell_bytes: int, reqs: Sequence, stream=None):
+        """ecg_update_ptrs: reqs = [(vec_i, old_addr, new_addr, [parity_addr] * p)], device addresses;
+        parity ^= coef[r][vec_i] * (old ^ new) for every request."""
+        n = len(reqs)
+        cells = (vp * max(1, n * (2 + p)))()
+        vec = np.zeros(max(1, n), dtype=np.uint8)
+        for i, (v, o, nw, par) in enumerate(reqs):
+            vec[i] = v
+            cells[i * (2 + p)] = o
+            cells[i * (2 + p) + 1] = nw
+            for r in range(p):
+                cells[i * (2 + p) + 2 + r] = par[r]
+        _chk(lib().ecg_update_ptrs(self.h, k, p, cell_bytes, n, cells, _u8(vec), stream), "update_ptrs")
+
     def encode_host(self, k: int, p: int, cell_bytes: int, nstripes: int, data: np.ndarray, parity: np.ndarray,
                     chunk: int = 0):
         dp = _host_array(data, nstripes * k * cell_bytes, "encode_host data", write=False)
@@ -728,11 +754,14 @@ class Queue:
     request id (callbacks run on the queue's completion threads)."""
 
     def __init__(self, ctx, max_batch: int = 0, max_wait_us: int = 0, max_cell_bytes: int = 0):
-        """ctx: a Context, or a Multi (slots spread over its devices)."""
+        """ctx: a Context, a Multi (slots spread over its devices), or None
+        (the CPU executor: host cells, no device)."""
         self.ctx = ctx
         h = vp()
         attr = QueueAttr(max_batch, max_wait_us, max_cell_bytes)
-        if isinstance(ctx, Multi):
+        if ctx is None:
+            _chk(lib().ecg_queue_create(None, C.byref(attr), C.byref(h)), "queue_create(NULL)")
+        elif isinstance(ctx, Multi):
             _chk(lib().ecg_queue_create_multi(ctx.h, C.byref(attr), C.byref(h)), "queue_create_multi")
         else:
             _chk(lib().ecg_queue_create(ctx.h, C.byref(attr), C.byref(h)), "queue_create")
@@ -778,6 +807,13 @@ class Queue:
         self._keep[rid] = (old, new, parity)
         _chk(lib().ecg_queue_update(self.h, k, p, C_, vec_i, _u8(old), _u8(new), dp, self._cb, rid + 1),
              "queue_update")
+
+    def update_ptrs(self, rid: int, k: int, p: int, cell_bytes: int, vec_i: int, old: int, new: int, parity):
+        """ecg_queue_update on cells given by address (device cells: batched
+        into ecg_update_ptrs launches in place)."""
+        dp = (u8p * p)(*[C.cast(C.c_void_p(a), u8p) for a in parity])
+        _chk(lib().ecg_queue_update(self.h, k, p, cell_bytes, vec_i, C.cast(C.c_void_p(old), u8p),
+                                    C.cast(C.c_void_p(new), u8p), dp, self._cb, rid + 1), "queue_update")
 
     def flush(self):
         _chk(lib().ecg_queue_flush(self.h), "queue_flush")

@@ -363,6 +363,23 @@ int ecg_tune_counters(ecg_ctx_t *ctx, uint64_t *probe_cycles, uint64_t *probe_la
 int ecg_matmul_ptrs(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef,
 		    uint64_t cell_bytes, uint32_t nstripes, void *const *cells, void *stream);
 
+/* Per-request delta parity updates on DEVICE cells: agg_update_parity's
+ * xor_gen(old, new) + ec_encode_data_update(vec_i) of one updated data cell
+ * (ref:src/object/srv_ec_aggregate.c:1086-1102), nreq requests in one call:
+ *   parity_r ^= coef[r][vec_i[i]] * (old ^ new)        r < p
+ * with the codec's Cauchy parity rows.  cells[i*(2+p) + 0] = old cell,
+ * + 1 = new cell, + 2 + r = parity cell r of request i (device addresses,
+ * cell_bytes each, any alignment).  Requests may name the same parity cells
+ * (several cells of one stripe) or overlapping ones: the result is every
+ * request applied, as if one after another.  Requests naming the same parity
+ * cells are folded into one pass over that parity; the rest run in as few
+ * ordered launches as keep every parity byte's read-modify-writes apart.  An
+ * old/new cell must not overlap a parity cell of the call; one request's
+ * parity cells must not overlap one another (-DER_INVAL).  k <= 16, p <= 8.
+ * The table is a host array, staged internally.  Asynchronous on `stream`. */
+int ecg_update_ptrs(ecg_ctx_t *ctx, int k, int p, uint64_t cell_bytes, uint32_t nreq,
+		    void *const *cells, const uint8_t *vec_i, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

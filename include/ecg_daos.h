@@ -72,6 +72,8 @@ struct ecg_obj_ec_recov_codec {
 	int k;
 	int p;
 	int reused_encode;	/* all-parity-lost shortcut (cli_ec.c:2205-2210) */
+	uint32_t er_builds;	/* times ecg_obj_ec_recov_codec_init built the rows into this
+				 * codec (a repeat init with the same erasures builds nothing) */
 };
 
 /* 0, or -ECG_DER_NOMEM. Idempotent. */
@@ -101,7 +103,14 @@ struct ecg_obj_ec_recov_codec *ecg_obj_ec_recov_codec_alloc(void);
 void ecg_obj_ec_recov_codec_free(struct ecg_obj_ec_recov_codec *recov);
 
 /* Build the recovery codec for LOGICAL erased cells err_list[nerrs].
- * 0 / -ECG_DER_DATA_LOSS (nerrs > p) / -ECG_DER_INVAL. */
+ * 0 / -ECG_DER_DATA_LOSS (nerrs > p) / -ECG_DER_INVAL.  As the reference's
+ * obj_ec_recov_codec_init with its per-object codec (efi_recov_codec,
+ * ref:src/object/cli_ec.c:2176-2185, obj_ec_err_match :2141-2150): when
+ * `recov` already holds the rows of this class and the same nerrs and
+ * err_list (same order), it returns 0 at once and rebuilds nothing
+ * (er_builds unchanged).  `recov` must therefore come from
+ * ecg_obj_ec_recov_codec_alloc (zeroed, like the reference's D_ALLOC) or be
+ * zeroed by the caller before its first init. */
 int ecg_obj_ec_recov_codec_init(uint32_t oc_id, const uint32_t *err_list, uint32_t nerrs,
 				struct ecg_obj_ec_recov_codec *recov);
 
@@ -109,7 +118,19 @@ int ecg_obj_ec_recov_codec_init(uint32_t oc_id, const uint32_t *err_list, uint32
  * [nstripes][k+p][cell_sz] (the recovery buffer of ref:src/object/cli_ec.c:
  * 2449-2464), in place, through device ctx's staging pipeline (NULL = the
  * calling thread's default device; in a process without a usable device, or
- * with ECG_FORCE_CPU=1, the product CPU path, stripe by stripe). */
+ * with ECG_FORCE_CPU=1, the product CPU path, stripe by stripe).
+ *
+ * One deliberate byte difference from the reference: when err_list names a
+ * PARITY cell before a data cell (DAOS keeps failures in insertion order,
+ * ref:src/object/cli_ec.c:1388-1391), the reference indexes its inverse with
+ * the first er_data_nerrs entries (:2226-2231) and reads an all-zero row
+ * of its zeroed (k+p) x k buffer (:1963-1984), so it writes that parity cell
+ * as ZEROS.  This codec builds its rows data-first and writes the TRUE parity
+ * there.  Every data cell is byte-identical to the reference's, and a
+ * degraded read never returns a parity cell; only that parity cell differs
+ * (tests/test_gpu_parity.py::test_recover_parity_first_order asserts the true
+ * parity; oracle/ec_ref.c reproduces the reference's zeros,
+ * tests/test_oracle.py::test_reference_quirk_parity_first). */
 int ecg_obj_ec_recov_data(ecg_ctx_t *ctx, const struct ecg_obj_ec_recov_codec *recov,
 			  uint64_t cell_sz, unsigned char *buf_stripes, uint32_t nstripes);
 

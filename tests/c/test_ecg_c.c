@@ -165,6 +165,161 @@ static void host_checks(void)
 	ecg_obj_ec_codec_fini();
 }
 
+/* ---- the queue's CPU executor under many submitters ------------------------
+ * ecg_queue_create(NULL): no device, the same lock-free reservations (CAS on
+ * the slot's generation|open|count word), slot close / reopen and completion
+ * threads as the device queue.  Small slots (max_batch 4) make every slot
+ * close and reopen hundreds of times; threads mix encodes, in-place
+ * recoveries and parity updates of their own stripes, wait for their own
+ * callbacks, and some call ecg_queue_flush while others submit.  Run under
+ * ThreadSanitizer in the host-only half (tests/c/Makefile test_ecg_c_tsan). */
+struct qcpu_job {
+	ecg_queue_t *q;
+	int id, rounds, bad;
+	pthread_mutex_t lock;
+	pthread_cond_t cv;
+	int pending, rcs;
+};
+
+static void qcpu_cb(void *arg, int rc)
+{
+	struct qcpu_job *j = arg;
+
+	pthread_mutex_lock(&j->lock);
+	j->pending--;
+	j->rcs += rc != 0;
+	pthread_cond_signal(&j->cv);
+	pthread_mutex_unlock(&j->lock);
+}
+
+static void *qcpu_thread(void *arg)
+{
+	enum { K = 4, P = 2, NR = 6, CMAX = 1536 };
+	struct qcpu_job *j = arg;
+	unsigned char en[(K + P) * K], tb[K * P * 32], rtb[K * P * 32];
+	static unsigned char bufs[48][NR][(K + P) * CMAX], want[48][NR][(K + P) * CMAX];
+	unsigned char (*b)[(K + P) * CMAX] = bufs[j->id], (*w)[(K + P) * CMAX] = want[j->id];
+	uint64_t st = 0x9E3779B97F4A7C15ull * (uint64_t)(j->id + 3);
+
+	ref_gf_gen_cauchy1_matrix(en, K + P, K);
+	ref_ec_init_tables(K, P, &en[K * K], tb);
+	memcpy(rtb, tb, sizeof(tb));
+	for (int it = 0; it < j->rounds; it++) {
+		/* every other round one cell size for all threads: their requests
+		 * share classes, so submitters race on one slot's reservation word;
+		 * the other rounds spread over many classes (slot opens) */
+		const int C = it % 2 ? 256 + (int)((uint64_t)(j->id * 131 + it * 17) % (CMAX - 256)) : 1024;
+		unsigned char *data[K], *par[P], *wd[K], *wp[P];
+
+		for (int n = 0; n < NR; n++)
+			for (int i = 0; i < (K + P) * C; i++) {
+				st ^= st << 13;
+				st ^= st >> 7;
+				st ^= st << 17;
+				b[n][i] = (unsigned char)st;
+			}
+		/* expected results first (the oracle), then the requests */
+		for (int n = 0; n < NR; n++) {
+			memcpy(w[n], b[n], (size_t)(K + P) * C);
+			for (int c = 0; c < K; c++)
+				wd[c] = w[n] + c * C;
+			for (int r = 0; r < P; r++)
+				wp[r] = w[n] + (K + r) * C;
+			if (n % 3 == 2) {		/* update: cell 1 changes to cell 3's bytes */
+				unsigned char delta[CMAX];
+
+				for (int i = 0; i < C; i++)
+					delta[i] = w[n][1 * C + i] ^ w[n][3 * C + i];
+				ref_ec_encode_data_update(C, K, P, 1, rtb, delta, wp);
+			} else {			/* encode; recovery regenerates the same */
+				ref_ec_encode_data(C, K, P, rtb, wd, wp);
+			}
+		}
+		pthread_mutex_lock(&j->lock);
+		j->pending = NR;
+		pthread_mutex_unlock(&j->lock);
+		for (int n = 0; n < NR; n++) {
+			int rc;
+
+			for (int c = 0; c < K; c++)
+				data[c] = b[n] + c * C;
+			for (int r = 0; r < P; r++)
+				par[r] = b[n] + (K + r) * C;
+			if (n % 3 == 0) {
+				rc = ecg_queue_encode(j->q, K, P, (uint64_t)C, data, par, qcpu_cb, j);
+			} else if (n % 3 == 1) {
+				/* true parity in, then d2 and p1 erased and recovered */
+				static const uint32_t err[2] = {2, 5};
+
+				memcpy(b[n] + K * C, w[n] + K * C, (size_t)P * C);
+				memset(b[n] + 2 * C, 0, (size_t)C);
+				memset(b[n] + 5 * C, 0, (size_t)C);
+				rc = ecg_queue_recover(j->q, K, P, (uint64_t)C, b[n], err, 2, qcpu_cb, j);
+			} else {
+				rc = ecg_queue_update(j->q, K, P, (uint64_t)C, 1, b[n] + 1 * C, b[n] + 3 * C, par,
+						      qcpu_cb, j);
+			}
+			if (rc) {
+				j->bad++;
+				qcpu_cb(j, rc);
+			}
+		}
+		if (j->id % 4 == 0 && it % 5 == 0)
+			j->bad += ecg_queue_flush(j->q) != 0;
+		pthread_mutex_lock(&j->lock);
+		while (j->pending)
+			pthread_cond_wait(&j->cv, &j->lock);
+		pthread_mutex_unlock(&j->lock);
+		for (int n = 0; n < NR; n++) {
+			/* an update leaves the data cells as they were; w has cell 1
+			 * unchanged too (only its delta went into the parity) */
+			j->bad += memcmp(b[n], w[n], (size_t)(K + P) * C) != 0;
+		}
+	}
+	return NULL;
+}
+
+static void queue_cpu_stress(void)
+{
+	static const int nthreads[] = {2, 12, 48};
+	struct qcpu_job jobs[48];
+	pthread_t th[48];
+
+	for (size_t x = 0; x < sizeof(nthreads) / sizeof(nthreads[0]); x++) {
+		const int T = nthreads[x];
+		ecg_queue_attr_t attr = {.max_batch = 4, .max_wait_us = 20, .max_cell_bytes = 2048};
+		ecg_queue_t *q = NULL;
+		uint64_t nreq = 0, nb = 0;
+		int bad = 0, rcs = 0;
+
+		CHECK(ecg_queue_create(NULL, &attr, &q) == 0, "cpu queue_create: %s", ecg_strerror());
+		if (q == NULL)
+			return;
+		for (int t = 0; t < T; t++) {
+			jobs[t] = (struct qcpu_job){.q = q, .id = t, .rounds = T > 12 ? 12 : 30};
+			pthread_mutex_init(&jobs[t].lock, NULL);
+			pthread_cond_init(&jobs[t].cv, NULL);
+			pthread_create(&th[t], NULL, qcpu_thread, &jobs[t]);
+		}
+		for (int t = 0; t < T; t++) {
+			pthread_join(th[t], NULL);
+			bad += jobs[t].bad;
+			rcs += jobs[t].rcs;
+			pthread_mutex_destroy(&jobs[t].lock);
+			pthread_cond_destroy(&jobs[t].cv);
+		}
+		CHECK(ecg_queue_flush(q) == 0, "cpu queue flush");
+		CHECK(ecg_queue_stats(q, &nreq, &nb) == 0, "cpu queue stats");
+		ecg_queue_destroy(q);
+		CHECK(bad == 0 && rcs == 0, "cpu queue, %d threads: %d mismatches, %d failed requests", T, bad, rcs);
+		/* 4-request slots: many closes and reopens */
+		CHECK(nb >= nreq / 4 && nb > 50, "cpu queue, %d threads: %llu requests in %llu batches", T,
+		      (unsigned long long)nreq, (unsigned long long)nb);
+		printf("cpu queue: %d threads, %llu requests, %llu batches\n", T, (unsigned long long)nreq,
+		       (unsigned long long)nb);
+	}
+}
+
 /* ---- device checks -------------------------------------------------------- */
 struct tjob {
 	int k, p, len, iters, id;
@@ -535,6 +690,7 @@ int main(void)
 {
 	host_checks();
 	isal_threads("cpu-path");
+	queue_cpu_stress();
 	if (ecg_device_count() > 0)
 		device_checks();
 	else

@@ -884,19 +884,20 @@ def test_queue_device_cell_alone_launches_at_once(ctx, oracle, ecglib):
 
 
 def test_queue_device_cell_errors(ctx, ecglib):
-    """Device cells: updates are not queued (-DER_NOSYS), a cell running past
-    its allocation and more than 16 data cells are refused (-DER_INVAL) --
-    before anything reaches the GPU."""
+    """Device cells: a request mixing host and device cells (an update whose
+    old cell is host memory), a cell running past its allocation and more than
+    16 data cells are refused (-DER_INVAL) -- before anything reaches the GPU."""
     L = ecglib.lib()
     k, p, C_ = 8, 2, 4096
     dbuf = ctx.alloc((k + p) * C_)
     q = ecglib.Queue(ctx)
     try:
         dp = (ecglib.u8p * p)(*[C.cast(C.c_void_p(dbuf.ptr + (k + r) * C_), ecglib.u8p) for r in range(p)])
-        old = C.cast(C.c_void_p(dbuf.ptr), ecglib.u8p)
+        host_old = np.zeros(C_, dtype=np.uint8)
         new = C.cast(C.c_void_p(dbuf.ptr + C_), ecglib.u8p)
-        rc = L.ecg_queue_update(q.h, k, p, C_, 0, old, new, dp, None, None)
-        assert rc == -ecglib.DER_NOSYS, rc
+        rc = L.ecg_queue_update(q.h, k, p, C_, 0, host_old.ctypes.data_as(ecglib.u8p), new, dp, None, None)
+        assert rc == -ecglib.DER_INVAL, rc
+        assert "host memory" in L.ecg_strerror().decode(), L.ecg_strerror()
         sp = (ecglib.u8p * k)(*[C.cast(C.c_void_p(dbuf.ptr + j * C_ + (C_ // 2 if j == k - 1 else 0)),
                                        ecglib.u8p) for j in range(k)])
         dp_bad = (ecglib.u8p * p)(*[C.cast(C.c_void_p(dbuf.ptr + (k + p) * C_ - C_ // 2 if r == p - 1 else

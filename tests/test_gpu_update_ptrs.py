@@ -1,0 +1,254 @@
+"""Per-request delta parity updates on device cells (include/ecg.h
+ecg_update_ptrs) and the batching queue's device-cell aggregation updates
+(ecg_queue_update on HBM cells), against the oracle.
+
+What the reference does per updated data cell of a stripe
+(agg_update_parity, ref:src/object/srv_ec_aggregate.c:1062-1105):
+xor_gen(old, new -> diff) then ec_encode_data_update(vec_i) into the stripe's
+p parity cells.  XOR commutes, so any set of such requests applied in any
+order gives one parity: the oracle applies them one by one
+(oracle.encode_data_update = ISA-L ec_encode_data_update_base restated), and
+the queue test also checks whole stripes against oracle.agg_update_parity.
+"""
+import ctypes as C
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def rand(shape, seed):
+    return np.random.default_rng(seed).integers(0, 256, shape, dtype=np.uint8)
+
+
+def _expected(oracle, k, p, parity0, reqs, olds, news):
+    """parity0 [S][p][C]; reqs = [(stripe, vec_i)]; old/new cells per request."""
+    en = oracle.cauchy1(k, p)[k:]
+    want = parity0.copy()
+    for i, (s, v) in enumerate(reqs):
+        want[s] = oracle.encode_data_update(en, v, olds[i] ^ news[i], want[s])
+    return want
+
+
+@pytest.mark.parametrize("k,p,C_,align", [
+    (2, 1, 65536, 16), (4, 2, 65536 + 4096 * 3, 16), (8, 2, 131072, 16), (8, 3, 4096 * 5 + 48, 16),
+    (16, 2, 65536, 16), (4, 5, 32768, 16), (8, 8, 8192 + 16, 16),
+    (8, 2, 12288 + 4, 4), (4, 2, 4096 * 3 + 8, 1), (8, 2, 4096 + 3, 1), (2, 1, 999, 1),
+])
+def test_update_ptrs_matches_oracle(ctx, oracle, ecglib, k, p, C_, align):
+    """Random requests over S stripes, several per stripe (some stripes more
+    than ECG_UPD_MU = 8, so a parity set spans ordered launches); cells at
+    offsets of the given alignment; the byte kernel for C % 4 != 0."""
+    S, nreq = 24, 96
+    rng = np.random.default_rng(k * 1000 + p * 10 + C_ + align)
+    stripe_of = np.concatenate([np.zeros(12, dtype=int), rng.integers(0, S, nreq - 12)])   # stripe 0: 12 updates
+    vec = rng.integers(0, k, nreq)
+    par0 = rand((S, p, C_), 7)
+    olds = rand((nreq, C_), 8)
+    news = rand((nreq, C_), 9)
+    slot = (C_ + 64 + 15) & ~15
+    off = 0 if align == 16 else (4 if align == 4 else 3)
+    # one device image: parity cells [S][p], then old and new cells, each at slot*i + off
+    npar = S * p
+    img = np.zeros((npar + 2 * nreq) * slot + 64, dtype=np.uint8)
+
+    def put(i, a):
+        img[i * slot + off: i * slot + off + C_] = a
+
+    for s in range(S):
+        for r in range(p):
+            put(s * p + r, par0[s, r])
+    for i in range(nreq):
+        put(npar + i, olds[i])
+        put(npar + nreq + i, news[i])
+    d = ctx.to_device(img)
+    try:
+        def addr(i):
+            return d.ptr + i * slot + off
+        reqs = [(int(vec[i]), addr(npar + i), addr(npar + nreq + i),
+                 [addr(int(stripe_of[i]) * p + r) for r in range(p)]) for i in range(nreq)]
+        before = ctx.stats()
+        ctx.update_ptrs(k, p, C_, reqs)
+        ctx.sync()
+        kname = ecglib.last_kernel()
+        after = ctx.stats()
+        got = d.download()
+        want = _expected(oracle, k, p, par0, list(zip(stripe_of, vec)), olds, news)
+        for s in range(S):
+            for r in range(p):
+                i = s * p + r
+                assert np.array_equal(got[i * slot + off: i * slot + off + C_], want[s, r]), (s, r, kname)
+        assert after["update_cells"] - before["update_cells"] == nreq
+        # 12 requests on stripe 0 -> 2 items of it -> at least 2 ordered launches
+        assert after["launches"] - before["launches"] >= 2
+        if C_ % 4:
+            assert kname == "ecg_upd_ptr_byte_kernel", kname
+        elif align == 16 and C_ % 16 == 0:
+            assert kname.startswith("ecg_upd_ptr_kernel<") and kname.endswith(",g16>"), kname
+        else:
+            assert kname.endswith(",g4>"), kname
+        # the untouched old/new cells are unchanged
+        for i in range(nreq):
+            assert np.array_equal(got[(npar + i) * slot + off:(npar + i) * slot + off + C_], olds[i])
+    finally:
+        d.free()
+
+
+def test_update_ptrs_overlapping_parity_sets(ctx, oracle, ecglib):
+    """Requests whose parity cells are different pointers into overlapping
+    bytes (a cell at x and another at x + C/2): they may not run in one
+    launch; the result equals applying the requests one by one to the shared
+    buffer."""
+    k, p, C_ = 4, 2, 16384
+    half = C_ // 2
+    nreq = 10
+    rng = np.random.default_rng(77)
+    buf0 = rand(10 * C_, 78)                      # the shared parity buffer
+    olds = rand((nreq, C_), 79)
+    news = rand((nreq, C_), 80)
+    vec = rng.integers(0, k, nreq)
+    # request i's parity cells: rows at (i * half) and (i * half + 3 C) -- request i and i+1 overlap by half a cell
+    pofs = [(i * half, i * half + 3 * C_ + (half if i % 2 else 0)) for i in range(nreq)]
+    assert all(b + C_ <= len(buf0) for _, b in pofs)
+    img = np.concatenate([buf0, olds.reshape(-1), news.reshape(-1)])
+    d = ctx.to_device(img)
+    try:
+        obase = d.ptr + len(buf0)
+        nbase = obase + nreq * C_
+        reqs = [(int(vec[i]), obase + i * C_, nbase + i * C_, [d.ptr + pofs[i][0], d.ptr + pofs[i][1]])
+                for i in range(nreq)]
+        ctx.update_ptrs(k, p, C_, reqs)
+        ctx.sync()
+        got = d.download(len(buf0))
+        en = oracle.cauchy1(k, p)[k:]
+        want = buf0.copy()
+        for i in range(nreq):
+            par = np.stack([want[pofs[i][r]: pofs[i][r] + C_] for r in range(p)])
+            par = oracle.encode_data_update(en, int(vec[i]), olds[i] ^ news[i], par)
+            for r in range(p):
+                want[pofs[i][r]: pofs[i][r] + C_] = par[r]
+        assert np.array_equal(got, want)
+    finally:
+        d.free()
+
+
+def test_update_ptrs_errors(ctx, ecglib):
+    """One request's own parity cells overlapping, vec_i >= k, k > 16 and a
+    NULL cell are refused (-DER_INVAL) before any launch."""
+    L = ecglib.lib()
+    C_ = 4096
+    d = ctx.alloc(8 * C_)
+    try:
+        def call(k, p, vec_i, cells):
+            arr = (C.c_void_p * len(cells))(*cells)
+            v = np.array([vec_i], dtype=np.uint8)
+            return L.ecg_update_ptrs(ctx.h, k, p, C_, 1, arr, v.ctypes.data_as(ecglib.u8p), None)
+
+        assert call(4, 2, 0, [d.ptr, d.ptr + C_, d.ptr + 2 * C_, d.ptr + 2 * C_ + 100]) == -ecglib.DER_INVAL
+        assert "overlap" in L.ecg_strerror().decode()
+        assert call(4, 2, 4, [d.ptr, d.ptr + C_, d.ptr + 2 * C_, d.ptr + 3 * C_]) == -ecglib.DER_INVAL
+        assert call(17, 2, 0, [d.ptr, d.ptr + C_, d.ptr + 2 * C_, d.ptr + 3 * C_]) == -ecglib.DER_INVAL
+        assert call(4, 2, 0, [d.ptr, None, d.ptr + 2 * C_, d.ptr + 3 * C_]) == -ecglib.DER_INVAL
+        assert L.ecg_update_ptrs(ctx.h, 4, 2, C_, 0, None, None, None) == 0     # nothing to do
+    finally:
+        d.free()
+
+
+def test_queue_device_updates_16_threads(ctx, oracle, ecglib):
+    """16 threads post per-cell aggregation
+    updates (agg_update_parity's xor_gen + ec_encode_data_update per updated
+    cell, ref:src/object/srv_ec_aggregate.c:1086-1102) of overlapping stripes
+    on DEVICE cells -- every stripe's updated cells posted by different
+    threads, so one stripe's requests land in one batch, in different
+    batches and in different ordered launches.  Final parity of every stripe
+    equals oracle.agg_update_parity over its updated cells."""
+    k, p, C_ = 8, 2, 65536
+    S, T = 64, 16
+    rng = np.random.default_rng(2606)
+    par0 = rand((S, p, C_), 11)
+    upd = []                                   # (stripe, cell)
+    for s in range(S):
+        ncell = int(rng.integers(1, 5))       # DAOS updates when fewer than half the cells changed
+        for c in rng.choice(k, ncell, replace=False):
+            upd.append((s, int(c)))
+    rng.shuffle(upd)
+    n = len(upd)
+    olds = rand((n, C_), 12)
+    news = rand((n, C_), 13)
+    img = np.concatenate([par0.reshape(-1), olds.reshape(-1), news.reshape(-1)])
+    d = ctx.to_device(img)
+    q = ecglib.Queue(ctx, max_batch=64, max_wait_us=200)
+    h2d0 = ctx.stats()["h2d_bytes"]
+    try:
+        obase = d.ptr + par0.nbytes
+        nbase = obase + olds.nbytes
+
+        def worker(t):
+            for i in range(t, n, T):
+                s, c = upd[i]
+                q.update_ptrs(i, k, p, C_, c, obase + i * C_, nbase + i * C_,
+                              [d.ptr + (s * p + r) * C_ for r in range(p)])
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        q.flush()
+        nr, nb = q.stats()
+        assert nr == n and len(q.done) == n and all(rc == 0 for rc in q.done.values()), q.done
+        got = d.download(par0.nbytes).reshape(S, p, C_)
+        for s in range(S):
+            mine = sorted((c, i) for i, (ss, c) in enumerate(upd) if ss == s)
+            bit_map = bytearray(2)
+            for c, _ in mine:
+                bit_map[c // 8] |= 1 << (c % 8)
+            o = np.stack([olds[i] for _, i in mine])
+            w = np.stack([news[i] for _, i in mine])
+            want = oracle.agg_update_parity(k, p, C_, 1, bytes(bit_map), o, w, [(0, k * C_)], par0[s])
+            assert np.array_equal(got[s], want), s
+        # device cells in place: no request crossed PCIe
+        assert ctx.stats()["h2d_bytes"] == h2d0
+        assert 1 <= nb <= n
+    finally:
+        q.close()
+        d.free()
+
+
+def test_queue_device_updates_same_cell_chain(ctx, oracle, ecglib):
+    """The same data cell of one stripe updated again and again (old -> v1 ->
+    v2 -> ... -> new) from several threads at once: the deltas telescope, so
+    the final parity is the encode of the final data."""
+    k, p, C_ = 4, 2, 32768
+    steps = 24
+    vals = rand((steps + 1, C_), 21)           # successive contents of data cell 2
+    data = rand((k, C_), 22)
+    data[2] = vals[0]
+    en = oracle.cauchy1(k, p)
+    par0 = oracle.encode_data(en[k:], data)
+    img = np.concatenate([par0.reshape(-1), vals.reshape(-1)])
+    d = ctx.to_device(img)
+    q = ecglib.Queue(ctx, max_batch=8, max_wait_us=100)
+    try:
+        vbase = d.ptr + par0.nbytes
+
+        def worker(t):
+            for i in range(t, steps, 4):
+                q.update_ptrs(i, k, p, C_, 2, vbase + i * C_, vbase + (i + 1) * C_,
+                              [d.ptr + r * C_ for r in range(p)])
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        q.flush()
+        assert all(rc == 0 for rc in q.done.values()) and len(q.done) == steps
+        data[2] = vals[steps]
+        got = d.download(par0.nbytes).reshape(p, C_)
+        assert np.array_equal(got, oracle.encode_data(en[k:], data))
+    finally:
+        q.close()
+        d.free()
