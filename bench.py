@@ -532,37 +532,66 @@ def pinned_copy_rates(ctx, n=1 << 30):
     return out
 
 
-def time_kernel(ctx, fn, iters, warm=3):
-    """Median kernel time of `iters` launches issued back to back, as an
-    engine streams batches: an event between consecutive launches, all read
-    after the last one (no host synchronisation -- and no idle GPU gap --
-    between launches)."""
-    return time_interleaved(ctx, [fn], iters, warm)[0]
+def time_kernel(ctx, fn, iters, warm=3, blocks_out=None):
+    """Median kernel time of `iters` timed blocks of launches issued back to
+    back, as an engine streams batches: an event between consecutive blocks,
+    all read after the last one (no host synchronisation -- and no idle GPU
+    gap -- between launches).  A block is one launch, or several for launches
+    shorter than ~1 ms (time_interleaved)."""
+    return time_interleaved(ctx, [fn], iters, warm, blocks_out)[0]
 
 
-def time_interleaved(ctx, fns, iters, warm=3):
-    """Median kernel time of each of `fns`, launched in turn (one launch of
+# Launches per timed block: enough for ~1 ms of work.  An event recorded
+# between two launches costs the stream ~5 us (the next launch waits for the
+# event's completion signal): a 60 us EC_2P1 128 KiB x 1024 launch timed one
+# per event pair read 65.4 us (0.77 of the HBM spec, BENCH_r05) where the kernel
+# trace gives 59.7 us and blocks of back-to-back launches 60.4 us with no fixed
+# per-launch cost in the batch-size fit (0.83-0.84, tools/short_launch.py,
+# profiles/r06/short_launch/).  Launches of >= 0.5 ms keep one per block.
+BLOCK_TARGET_MS = 1.0
+
+
+def time_interleaved(ctx, fns, iters, warm=3, blocks_out=None):
+    """Median kernel time of each of `fns`, launched in turn (one block of
     each per round): the box's clocks drift over a long run, so timing one
     configuration's block of launches after another's biases a ratio.  The
-    launches go back to back with an event at every boundary, read after the
-    last launch (a host wait per launch would leave the GPU idle between
+    launches go back to back with an event at every block boundary, read after
+    the last launch (a host wait per launch would leave the GPU idle between
     launches, which short launches feel: EC_16P2 x 1024 ran 0.43 ms that way
-    against 0.40 ms for the launch tuner's back-to-back arms, round 3)."""
+    against 0.40 ms for the launch tuner's back-to-back arms, round 3).  Each
+    fn's block holds B launches, B = BLOCK_TARGET_MS / its warm-up time per
+    launch (1 for launches of >= 0.5 ms); blocks_out (a list) receives the Bs."""
     for _ in range(warm):           # warm-up rounds interleaved like the timed ones
         for fn in fns:
             fn()
     ctx.sync()
+    # per-fn launch time from 4 back-to-back launches each -> launches per block
+    nb = []
+    e0, e1 = ctx.event(), ctx.event()
+    for fn in fns:
+        ctx.record(e0)
+        for _ in range(4):
+            fn()
+        ctx.record(e1)
+        ctx.sync()
+        est = ctx.elapsed_ms(e0, e1) / 4
+        nb.append(max(1, min(64, int(round(BLOCK_TARGET_MS / est)))) if est < BLOCK_TARGET_MS / 2 else 1)
+    ctx.destroy_event(e0)
+    ctx.destroy_event(e1)
+    if blocks_out is not None:
+        blocks_out[:] = nb
     evs = [ctx.event() for _ in range(iters * len(fns) + 1)]
     ctx.record(evs[0])
     n = 0
     for _ in range(iters):
-        for fn in fns:
-            fn()
+        for fn, b in zip(fns, nb):
+            for _ in range(b):
+                fn()
             n += 1
             ctx.record(evs[n])
     ms = [[] for _ in fns]
     for i in range(n):
-        ms[i % len(fns)].append(ctx.elapsed_ms(evs[i], evs[i + 1]))
+        ms[i % len(fns)].append(ctx.elapsed_ms(evs[i], evs[i + 1]) / nb[i % len(fns)])
     for e in evs:
         ctx.destroy_event(e)
     return [sorted(v)[len(v) // 2] for v in ms]
@@ -803,7 +832,8 @@ def detail_rows(ctx, ceil, iters=11, shapes=DETAIL_SHAPES, csum=True):
         # cap needs no switch; the first ~10-20 launches after a switch to a cap run up to
         # 12 % slow: EC_16P2 cap 2 0.434 ms, then 0.38, tools/state_check3.py,
         # profiles/r03/tuner_check/); the timed launches run its choice in steady state
-        ms = time_kernel(ctx, fn, iters, warm=80)
+        nblk = []
+        ms = time_kernel(ctx, fn, iters, warm=80, blocks_out=nblk)
         tuned = (ctx.tune_state(k, p, C, S, k * C, C) if mode == "enc"
                  else ctx.tune_state(k, 2, C, S, st, st))
         alg = (rd + wr) * C * S
@@ -813,7 +843,7 @@ def detail_rows(ctx, ceil, iters=11, shapes=DETAIL_SHAPES, csum=True):
                       "roofline_frac": round(gbs / HBM_PEAK_GBS, 4),
                       "read_frac": round(k * C * S / ms / 1e6 / HBM_PEAK_GBS, 4),
                       "measured_mix_ceiling_GBps": round(mix, 1), "frac_of_measured_mix": round(gbs / mix, 4),
-                      "kernel": ecg.last_kernel(), "ms": round(ms, 4),
+                      "kernel": ecg.last_kernel(), "ms": round(ms, 4), "launches_per_timed_block": nblk[0],
                       "layout": "client [S][k][C] -> [p][S][C]" if mode == "enc" else "recovery [S][k+p][C]"}
         if tuned is not None:
             rows[name]["launch_tuner"] = {"wg_per_cu": None if tuned[0] == 255 else tuned[0],
@@ -1217,11 +1247,14 @@ def leg_stream(args, ctx, world, rank, steps, numa_info):
     share = conc["node_h2d"] / world
     row.update({"h2d_GBps": round(h2d, 2),
                 "concurrent_pinned_GBps": {"h2d": conc["h2d"], "d2h": conc["d2h"]},
-                "fair_share_h2d_GBps": round(share, 2), "frac_of_h2d": round(h2d / share, 4),
+                "fair_share_h2d_GBps": round(share, 2), "frac_of_fair_share_h2d": round(h2d / share, 4),
                 "frac_of_own_concurrent_h2d": round(h2d / conc["h2d"], 4),
-                "denominator": "1/N of the node's concurrent pinned H2D rate (all ranks copying at once)"})
+                "frac_of_h2d": None,
+                "denominator": "frac_of_h2d: the rank's solo pinned H2D rate (ranks copying in turn; the "
+                               "round-4 meaning); frac_of_fair_share_h2d: 1/N of the node's concurrent pinned "
+                               "H2D rate (all ranks copying at once)"})
     if solo is not None:
-        row.update({"measured_pinned_GBps": solo, "frac_of_solo_h2d": round(h2d / solo["h2d"], 4)})
+        row.update({"measured_pinned_GBps": solo, "frac_of_h2d": round(h2d / solo["h2d"], 4)})
     if wl is not None:
         row.update({"d2h_GBps": round(wl.d2h_bytes_per_step() * steps / mine / 1e9, 2),
                     "verified": all(wl.verify().values())})

@@ -18,10 +18,12 @@
  * Placement is decided from EVERY cell (ecg_cells_place), so a device address
  * never reaches the CPU path; cells of two devices in one call, or a device
  * cell past its allocation, fail with the cell named.
- * The default crossover is the measured one (on the MI355X box
- * one EPYC core with GFNI beats the PCIe round trip of a synchronous call at
- * every size up to the largest measured, so host cells stay on the CPU);
- * ECG_DROPIN_CROSSOVER=<bytes> or ecg_set_dropin_crossover() move it.
+ * The default crossover is the measured one for the CPU path in use
+ * (crossover_for_isa below, DESIGN.md §7: on the MI355X box one EPYC core with
+ * GFNI beats the PCIe round trip of a synchronous call at every size, so with
+ * GFNI host cells stay on the CPU; the nibble-table and scalar paths hand
+ * large calls to the GPU); ECG_DROPIN_CROSSOVER=<bytes> or
+ * ecg_set_dropin_crossover() move it.
  *
  * Contexts: one per device of $ECG_DEVICES ("0,1,2,3" / "all"; default
  * $ECG_DEVICE, else device 0), created on the first call that needs the GPU;
@@ -38,14 +40,31 @@
 
 #define DROPIN_MAXDEV 64
 
-/* Measured crossover in bytes of len * (k + rows): DESIGN.md §7,
- * profiles/r05/dropin/.  UINT64_MAX = host cells never take the GPU. */
-#define DROPIN_CROSSOVER_DEFAULT UINT64_MAX
+/* Measured crossover in bytes of len * (k + rows), by the CPU path the
+ * process runs (ecg_cpu_isa(): the one-thread synchronous call on the CPU vs
+ * the GPU through pinned staging, EC_4P2 / EC_8P2 / EC_16P2 with 4 KiB - 4 MiB
+ * cells on the MI355X box's EPYC 9575F, tools/dropin_bench.c with
+ * $ECG_CPU_ISA forcing each variant; DESIGN.md §7, profiles/r06/dropin_isa/):
+ *   GFNI (avx512 / avx2)  the CPU ahead at every size: never the GPU
+ *   avx2 (nibble tables)  the CPU ahead below 64 MiB (16P2 x 4 MiB = 72 MiB
+ *                         ties: 4.10 vs 4.08 ms)
+ *   scalar                the GPU ahead from 64 KiB (16P2 x 4 KiB = 72 KiB:
+ *                         17.5 vs 27.2 us; 8P2 x 4 KiB = 40 KiB: 17.9 vs 13.9)
+ * $ECG_DROPIN_CROSSOVER or ecg_set_dropin_crossover() replace it. */
+static uint64_t crossover_for_isa(const char *isa)
+{
+	if (strstr(isa, "gfni"))
+		return UINT64_MAX;
+	if (strcmp(isa, "avx2") == 0)
+		return 64ull << 20;
+	return 64ull << 10;
+}
 
 static pthread_once_t g_once = PTHREAD_ONCE_INIT;
 static int g_gpu;		/* a gfx950 device is visible */
 static int g_force_cpu;		/* ECG_FORCE_CPU=1: host cells never take the GPU */
-static uint64_t g_crossover = DROPIN_CROSSOVER_DEFAULT;
+static uint64_t g_crossover;	/* explicit crossover (g_crossover_set) */
+static int g_crossover_set;
 
 static pthread_once_t g_ctx_once = PTHREAD_ONCE_INIT;
 static ecg_ctx_t *g_ctx[DROPIN_MAXDEV];
@@ -61,8 +80,10 @@ static void once_init(void)
 	const char *force = getenv("ECG_FORCE_CPU");
 	const char *x = getenv("ECG_DROPIN_CROSSOVER");
 
-	if (x && *x)
+	if (x && *x) {
 		g_crossover = strtoull(x, NULL, 0);
+		g_crossover_set = 1;
+	}
 	g_force_cpu = force && force[0] == '1';
 	g_gpu = ecg_device_count() > 0;
 }
@@ -107,12 +128,16 @@ int ecg_set_dropin_crossover(uint64_t bytes)
 {
 	pthread_once(&g_once, once_init);
 	__atomic_store_n(&g_crossover, bytes, __ATOMIC_RELAXED);
+	__atomic_store_n(&g_crossover_set, 1, __ATOMIC_RELEASE);
 	return 0;
 }
 
 uint64_t ecg_dropin_crossover(void)
 {
 	pthread_once(&g_once, once_init);
+	/* the default follows the CPU path in use (ecg_cpu_set_isa may narrow it) */
+	if (!__atomic_load_n(&g_crossover_set, __ATOMIC_ACQUIRE))
+		return crossover_for_isa(ecg_cpu_isa());
 	return __atomic_load_n(&g_crossover, __ATOMIC_RELAXED);
 }
 

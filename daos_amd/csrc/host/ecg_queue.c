@@ -73,6 +73,7 @@
 #define NSLOT_MIN 4	/* staging slots for one device; 2 per device beyond */
 #define NSLOT_MAX 32
 #define NFIN 4		/* completion threads: output scatter + callbacks */
+#define NFIN_CPU 16	/* ... of the CPU executor, which also compute the products there */
 #define NDSTLOCK 64	/* striped locks serialising update deltas into one parity cell */
 #define RES_OPEN (1ull << 31)
 #define RES_CNT (RES_OPEN - 1)
@@ -149,7 +150,7 @@ struct ecg_queue {
 	uint64_t submitted, completed, batches, flush_target;
 	int stop, worker_exited;
 	pthread_t worker;
-	pthread_t fin[NFIN];
+	pthread_t fin[NFIN_CPU];
 	int nfin;
 	/* Updates of one stripe submitted back to back (one per updated cell, all
 	 * naming the same parity cells) land in one batch or in batches of
@@ -691,6 +692,18 @@ static void slot_free(struct qslot *s)
 	free(s->uvec);
 }
 
+/* Completion threads of the CPU executor: they compute the products, so one
+ * per CPU the process may run on, NFIN .. NFIN_CPU. */
+static int cpu_workers(void)
+{
+	cpu_set_t set;
+	int n = NFIN;
+
+	if (sched_getaffinity(0, sizeof(set), &set) == 0)
+		n = CPU_COUNT(&set);
+	return n < NFIN ? NFIN : n > NFIN_CPU ? NFIN_CPU : n;
+}
+
 /* Slots round-robin over ctxs[nctx] (one context = one device); nctx = 0:
  * the CPU executor. */
 static int queue_create(ecg_ctx_t *const *ctxs, int nctx, const ecg_queue_attr_t *attr,
@@ -779,7 +792,7 @@ static int queue_create(ecg_ctx_t *const *ctxs, int nctx, const ecg_queue_attr_t
 		if (e == hipSuccess)
 			e = hipEventCreateWithFlags(&q->uev[i], hipEventDisableTiming);
 	}
-	for (i = 0; i < NFIN && e == hipSuccess; i++) {
+	for (i = 0; i < (q->cpu ? cpu_workers() : NFIN) && e == hipSuccess; i++) {
 		if (pthread_create(&q->fin[i], NULL, fin_main, q) != 0)
 			e = hipErrorOutOfMemory;
 		else

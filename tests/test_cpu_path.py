@@ -124,3 +124,26 @@ def test_cpu_random_shapes(ecglib, oracle, isa):
             if acc:
                 want = want ^ before
             assert np.array_equal(np.stack(dst), want), (name, k, rows, n, acc)
+
+
+@pytest.mark.parametrize("isa,want", [("scalar", 64 << 10), ("avx2", 64 << 20), ("auto", None)])
+def test_default_crossover_follows_cpu_path(isa, want):
+    """the drop-in's default crossover is per CPU path, measured on
+    the MI355X box (daos_amd/csrc/host/ecg_dropin.c crossover_for_isa, DESIGN
+    §7): GFNI never hands host cells to the GPU, the nibble-table path from
+    64 MiB of len * (k + rows), the scalar path from 64 KiB.  An explicit
+    crossover ($ECG_DROPIN_CROSSOVER) overrides it whatever the path."""
+    code = ("from daos_amd import ecg; import sys; "
+            f"assert ecg.cpu_set_isa({isa!r}) == 0 or {isa!r} != 'auto'; "
+            "print(ecg.cpu_isa(), ecg.dropin_crossover())")
+    for env_x, expect_set in (({}, False), ({"ECG_DROPIN_CROSSOVER": "12345"}, True)):
+        r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env_x), cwd=ROOT,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        got_isa, got = r.stdout.split()
+        if expect_set:
+            assert int(got) == 12345
+        elif "gfni" in got_isa:
+            assert int(got) == (1 << 64) - 1, (got_isa, got)
+        elif want is not None and got_isa == isa:
+            assert int(got) == want, (got_isa, got)

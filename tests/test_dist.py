@@ -122,7 +122,9 @@ def test_bench_gpus_n_spawns_ranks():
     for r in stream["ranks"]:
         assert set(r["concurrent_pinned_GBps"]) == {"h2d", "d2h"} and r["concurrent_pinned_GBps"]["h2d"] > 0
         assert abs(r["fair_share_h2d_GBps"] - node["h2d_GBps"] / 2) < 0.02
-        assert abs(r["frac_of_h2d"] / (r["h2d_GBps"] / r["fair_share_h2d_GBps"]) - 1) < 1e-2   # 2-decimal rounding
+        assert abs(r["frac_of_fair_share_h2d"] / (r["h2d_GBps"] / r["fair_share_h2d_GBps"]) - 1) < 1e-2   # rounding
+        if r.get("measured_pinned_GBps"):
+            assert abs(r["frac_of_h2d"] / (r["h2d_GBps"] / r["measured_pinned_GBps"]["h2d"]) - 1) < 1e-2
 
 def test_strong_split_ranges():
     """configs[3]'s 8192 stripes cut into contiguous ranges that cover the

@@ -22,7 +22,13 @@
  * into pointer-table launches in place; QB_VERIFY=1: one queue run over a
  * patterned image, every stripe's parity checked against the CPU
  * restatement -- in host mode likewise, parity zeroed first).
- * usage: queue_bench C T [update|device] [stripes per thread, default 64].
+ * With "devupdate" the update calls run on DEVICE cells: the drop-in
+ * (xor_gen + ec_encode_data_update on device cells, one synchronous launch
+ * pair per call) against the queue (ecg_queue_update on device cells, batched
+ * into ecg_update_ptrs launches in place); QB_VERIFY=1 checks every stripe's
+ * parity after one queue run against the CPU restatement.  QB_CPU_QUEUE=1
+ * creates the queue with no context (the CPU executor; host cells).
+ * usage: queue_bench C T [update|device|devupdate] [stripes per thread, default 64].
  * Bench infrastructure.
  */
 #include <pthread.h>
@@ -44,6 +50,8 @@ static ecg_queue_t *g_q;
 static int g_mode;			/* 0 isal, 1 queue, 2 cpu */
 static int g_update;			/* calls are one-cell delta updates */
 static unsigned char *g_new;		/* T * N new cells (update) */
+static unsigned char *g_dnew;		/* the same in device memory ("devupdate") */
+static unsigned char *g_ddiff;		/* T device diff cells (drop-in devupdate) */
 static unsigned char g_col[64][8 * 32];	/* vec_i -> the P tables of column vec_i */
 
 struct cnt {
@@ -74,8 +82,8 @@ static void done_cb(void *arg, int rc)
 
 static void update_one(long t, int i)
 {
-	unsigned char *s = g_cells + ((size_t)t * N + i) * (K + P) * CB;
-	unsigned char *nw = g_new + ((size_t)t * N + i) * CB;
+	unsigned char *s = (g_dcells ? g_dcells : g_cells) + ((size_t)t * N + i) * (K + P) * CB;
+	unsigned char *nw = (g_dnew ? g_dnew : g_new) + ((size_t)t * N + i) * CB;
 	const int vec_i = (int)((t * N + i) % K);
 	unsigned char *old = s + vec_i * CB, *par[8];
 
@@ -85,7 +93,7 @@ static void update_one(long t, int i)
 		ecg_queue_update(g_q, K, P, CB, vec_i, old, nw, par, done_cb, NULL);
 		return;
 	}
-	unsigned char *diff = malloc(CB), *tmp[8];
+	unsigned char *diff = g_ddiff ? g_ddiff + (size_t)t * CB : malloc(CB), *tmp[8];
 
 	if (g_mode == 0) {
 		void *arr[3] = {old, nw, diff};
@@ -116,7 +124,8 @@ static void update_one(long t, int i)
 			free(tmp[r]);
 		}
 	}
-	free(diff);
+	if (!g_ddiff)
+		free(diff);
 }
 
 static void *worker(void *arg)
@@ -179,8 +188,9 @@ int main(int argc, char **argv)
 		CB = strtoull(argv[1], NULL, 0);
 	if (argc > 2)
 		T = atoi(argv[2]);
-	g_update = argc > 3 && strcmp(argv[3], "update") == 0;
-	const int device = argc > 3 && strcmp(argv[3], "device") == 0;
+	const int devupdate = argc > 3 && strcmp(argv[3], "devupdate") == 0;
+	g_update = argc > 3 && (strcmp(argv[3], "update") == 0 || devupdate);
+	const int device = argc > 3 && (strcmp(argv[3], "device") == 0 || devupdate);
 	if (argc > 4)
 		N = atoi(argv[4]);	/* stripes per thread (device cells: HBM holds many) */
 	if (N < 1 || T < 1 || T > 64)
@@ -196,7 +206,7 @@ int main(int argc, char **argv)
 	for (int j = 0; j < K; j++)	/* ISA-L layout: row r, source j at (r * K + j) * 32 */
 		for (int r = 0; r < P; r++)
 			memcpy(&g_col[j][r * 32], &g_tbls[(r * K + j) * 32], 32);
-	if (ecg_ctx_create(0, &ctx) || ecg_queue_create(ctx, &qa, &g_q)) {
+	if (ecg_ctx_create(0, &ctx) || ecg_queue_create(getenv("QB_CPU_QUEUE") ? NULL : ctx, &qa, &g_q)) {
 		fprintf(stderr, "no device: %s\n", ecg_strerror());
 		return 1;
 	}
@@ -210,6 +220,56 @@ int main(int argc, char **argv)
 			return 1;
 		}
 		g_dcells = d;
+		if (devupdate) {
+			void *dn = NULL, *dd = NULL;
+
+			if (ecg_dev_alloc(ctx, (size_t)T * N * CB, &dn) || ecg_dev_alloc(ctx, (size_t)T * CB, &dd) ||
+			    ecg_memset(ctx, dn, 0xA7, (size_t)T * N * CB, NULL) || ecg_stream_sync(ctx, NULL)) {
+				fprintf(stderr, "device new cells: %s\n", ecg_strerror());
+				return 1;
+			}
+			g_dnew = dn;
+			g_ddiff = dd;
+		}
+		if (getenv("QB_VERIFY") && devupdate) {
+			/* patterned image and new cells, one queue run, every stripe's
+			 * parity against parity ^= coef[vec_i] * (old ^ new) on the CPU */
+			const size_t nn = (size_t)T * N * CB;
+			unsigned char *h = malloc(nb), *g = malloc(nb), *hn = malloc(nn), *delta = malloc(CB);
+			long bad = 0;
+
+			for (size_t i = 0; i < nb / 8; i++) {
+				const uint64_t v = (i + 1) * 0x9E3779B97F4A7C15ull;
+
+				memcpy(h + i * 8, &v, 8);
+			}
+			for (size_t i = 0; i < nn / 8; i++) {
+				const uint64_t v = (i + 7) * 0xC2B2AE3D27D4EB4Full;
+
+				memcpy(hn + i * 8, &v, 8);
+			}
+			if (ecg_memcpy(ctx, d, h, nb, 0, NULL) || ecg_memcpy(ctx, g_dnew, hn, nn, 0, NULL) ||
+			    ecg_stream_sync(ctx, NULL))
+				return 1;
+			run(1);
+			if (ecg_memcpy(ctx, g, d, nb, 1, NULL) || ecg_stream_sync(ctx, NULL))
+				return 1;
+			for (size_t st = 0; st < (size_t)T * N; st++) {
+				unsigned char *s = h + st * (K + P) * CB, *par[8];
+				const int vec_i = (int)(st % K);
+
+				for (uint64_t b = 0; b < CB; b++)
+					delta[b] = s[vec_i * CB + b] ^ hn[st * CB + b];
+				for (int r = 0; r < P; r++)
+					par[r] = s + (K + r) * CB;
+				ref_ec_encode_data_update((int)CB, K, P, vec_i, g_tbls, delta, par);
+				bad += memcmp(s, g + st * (K + P) * CB, (size_t)(K + P) * CB) != 0;
+			}
+			printf("{\"op\": \"update\", \"cells\": \"device\", \"verify\": true, \"k\": %d, \"p\": %d, "
+			       "\"cell_bytes\": %llu, \"threads\": %d, \"stripes\": %d, \"bad_stripes\": %ld}\n", K, P,
+			       (unsigned long long)CB, T, T * N, bad);
+			return bad ? 1 : 0;
+		}
 		if (getenv("QB_VERIFY")) {
 			/* every stripe distinct: one queue run over a patterned image,
 			 * then every stripe's parity against the CPU restatement */
@@ -258,12 +318,16 @@ int main(int argc, char **argv)
 					(unsigned long long)(reqs - r0), (unsigned long long)(batches - b0));
 			}
 		}
-		printf("{\"op\": \"encode\", \"cells\": \"device\", \"k\": %d, \"p\": %d, \"cell_bytes\": %llu, "
+		printf("{\"op\": \"%s\", \"cells\": \"device\", \"k\": %d, \"p\": %d, \"cell_bytes\": %llu, "
 		       "\"threads\": %d, \"stripes_per_thread\": %d, \"isal_one_stripe_GiBps\": %.2f, "
-		       "\"queue_GiBps\": %.2f, \"queue_requests\": %llu, \"queue_batches\": %llu}\n", K, P,
-		       (unsigned long long)CB, T, N, isal, queue, (unsigned long long)reqs,
+		       "\"queue_GiBps\": %.2f, \"queue_requests\": %llu, \"queue_batches\": %llu}\n",
+		       g_update ? "update" : "encode", K, P, (unsigned long long)CB, T, N, isal, queue, (unsigned long long)reqs,
 		       (unsigned long long)batches);
 		ecg_dev_free(ctx, d);
+		if (g_dnew) {
+			ecg_dev_free(ctx, g_dnew);
+			ecg_dev_free(ctx, g_ddiff);
+		}
 		ecg_queue_destroy(g_q);
 		ecg_ctx_destroy(ctx);
 		free(g_cells);
@@ -300,11 +364,11 @@ int main(int argc, char **argv)
 	queue = run(1);
 	ecg_queue_stats(g_q, &reqs, &batches);
 	cpu = run(2);
-	printf("{\"op\": \"%s\", \"k\": %d, \"p\": %d, \"cell_bytes\": %llu, \"threads\": %d, \"stripes_per_thread\": %d, "
+	printf("{\"op\": \"%s\", \"queue\": \"%s\", \"k\": %d, \"p\": %d, \"cell_bytes\": %llu, \"threads\": %d, \"stripes_per_thread\": %d, "
 	       "\"isal_one_stripe_GiBps\": %.2f, \"queue_GiBps\": %.2f, \"queue_requests\": %llu, "
 	       "\"queue_batches\": %llu, \"cpu_gfni_same_threads_GiBps\": %.2f}\n",
-	       g_update ? "update" : "encode", K, P, (unsigned long long)CB, T, N, isal, queue,
-	       (unsigned long long)reqs,
+	       g_update ? "update" : "encode", getenv("QB_CPU_QUEUE") ? "cpu-executor" : "gpu", K, P,
+	       (unsigned long long)CB, T, N, isal, queue, (unsigned long long)reqs,
 	       (unsigned long long)batches, cpu);
 	ecg_queue_destroy(g_q);
 	ecg_ctx_destroy(ctx);
