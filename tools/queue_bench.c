@@ -213,17 +213,20 @@ int main(int argc, char **argv)
 	if (device) {
 		void *d = NULL;
 		const size_t nb = (size_t)T * N * (K + P) * CB;
+		/* QB_ONE_ALLOC=1: the new cells share the stripes' allocation (one
+		 * placement lookup per request instead of two) */
+		const int one = devupdate && getenv("QB_ONE_ALLOC") != NULL;
 
-		if (ecg_dev_alloc(ctx, nb, &d) || ecg_memset(ctx, d, 0x5A, nb, NULL) ||
+		if (ecg_dev_alloc(ctx, nb + (one ? (size_t)T * N * CB : 0), &d) || ecg_memset(ctx, d, 0x5A, nb, NULL) ||
 		    ecg_stream_sync(ctx, NULL)) {
 			fprintf(stderr, "device cells: %s\n", ecg_strerror());
 			return 1;
 		}
 		g_dcells = d;
 		if (devupdate) {
-			void *dn = NULL, *dd = NULL;
+			void *dn = one ? (unsigned char *)d + nb : NULL, *dd = NULL;
 
-			if (ecg_dev_alloc(ctx, (size_t)T * N * CB, &dn) || ecg_dev_alloc(ctx, (size_t)T * CB, &dd) ||
+			if ((!one && ecg_dev_alloc(ctx, (size_t)T * N * CB, &dn)) || ecg_dev_alloc(ctx, (size_t)T * CB, &dd) ||
 			    ecg_memset(ctx, dn, 0xA7, (size_t)T * N * CB, NULL) || ecg_stream_sync(ctx, NULL)) {
 				fprintf(stderr, "device new cells: %s\n", ecg_strerror());
 				return 1;
@@ -325,7 +328,8 @@ int main(int argc, char **argv)
 		       (unsigned long long)batches);
 		ecg_dev_free(ctx, d);
 		if (g_dnew) {
-			ecg_dev_free(ctx, g_dnew);
+			if (!one)
+				ecg_dev_free(ctx, g_dnew);
 			ecg_dev_free(ctx, g_ddiff);
 		}
 		ecg_queue_destroy(g_q);
