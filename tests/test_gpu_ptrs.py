@@ -87,6 +87,45 @@ def test_matmul_ptrs(oracle, ecglib, ctx, k, rows, C, S, iskew, oskew):
         buf.free()
 
 
+@pytest.mark.parametrize("rows", [1, 2, 3])
+def test_matmul_ptrs_g2_generic_variant(oracle, ecglib, ctx, rows):
+    """k = 8 with a source off a 16-byte boundary picks the g2
+    lanes, which exist only as k = 8 shapes; with ecg_set_launch variant 1 (the
+    runtime-shaped kernels) no g2 entry matches, and the launch must fall back
+    to the funnel-shifted dword lanes (g1, runtime-shaped) instead of failing
+    with hipErrorInvalidDeviceFunction."""
+    k, C, S = 8, 65536 + 64, 5
+    rng = np.random.default_rng(880 + rows)
+    slot = C + 64
+    buf = ctx.alloc(S * (k + rows) * slot + 64)
+    host = rng.integers(0, 256, S * (k + rows) * slot + 64, dtype=np.uint8)
+    # shuffled slots: not an affine table, so the pointer-table kernel runs
+    order = rng.permutation(S * (k + rows))
+    offs = [int(order[s * (k + rows) + j]) * slot + (1 if j == 0 else 0)
+            for s in range(S) for j in range(k + rows)]        # source 0 of every stripe at +1
+    addrs = [buf.ptr + o for o in offs]
+    coef = rng.integers(0, 256, (rows, k), dtype=np.uint8)
+    try:
+        buf.upload(host)
+        ctx.set_launch(0, 0, 1)
+        try:
+            ctx.matmul_ptrs(k, rows, coef, C, S, addrs)
+            ctx.sync()
+        finally:
+            ctx.set_launch(0, 0, 0)
+        kern = ecglib.last_kernel()
+        assert kern == "ecg_mm_ptr_kernel<0,0,g1>", kern
+        dev = buf.download()
+        for s in range(S):
+            cells = np.stack([host[offs[s * (k + rows) + j]:][:C] for j in range(k)])
+            want = oracle.encode_data(coef, cells)
+            for r in range(rows):
+                o = offs[s * (k + rows) + k + r]
+                assert np.array_equal(dev[o:o + C], want[r]), (s, r)
+    finally:
+        buf.free()
+
+
 def _oc(k, p):
     redun = {(2, 1): 32, (2, 2): 33, (4, 1): 34, (4, 2): 35, (8, 1): 36, (8, 2): 37, (16, 1): 38, (16, 2): 39,
              (4, 3): 40, (8, 3): 41, (16, 3): 42}[(k, p)]

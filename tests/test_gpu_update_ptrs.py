@@ -252,3 +252,56 @@ def test_queue_device_updates_same_cell_chain(ctx, oracle, ecglib):
     finally:
         q.close()
         d.free()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_update_ptrs_random_overlaps(ctx, oracle, ecglib, seed):
+    """Seeded random batches whose parity cells land at random offsets of one
+    small buffer -- identical sets, partial overlaps and disjoint cells mixed,
+    so the fold, the ordered launches and the greedy colouring all run --
+    against the oracle applying the requests one by one."""
+    rng = np.random.default_rng(4242 + seed)
+    k = int(rng.choice([2, 4, 8, 16]))
+    p = int(rng.integers(1, 4))
+    C_ = int(rng.choice([4096, 8192 + 16, 12288 + 4, 3000]))
+    span = C_ * int(rng.integers(3 * p, 6 * p))          # small: overlaps are common
+    nreq = int(rng.integers(5, 60))
+    base_sets = []                                        # a few parity sets reused verbatim
+    for _ in range(int(rng.integers(1, 5))):
+        base_sets.append(sorted(int(x) for x in rng.choice(span // C_ - 1, p, replace=False) * C_))
+    reqs_off = []
+    for _ in range(nreq):
+        if rng.random() < 0.5:
+            offs = list(base_sets[int(rng.integers(0, len(base_sets)))])
+        else:                                             # rows at random byte offsets, disjoint among themselves
+            while True:
+                offs = sorted(int(x) for x in rng.integers(0, span - C_, p))
+                if all(offs[i + 1] - offs[i] >= C_ for i in range(p - 1)):
+                    break
+            if C_ % 4 == 0 and rng.random() < 0.7:
+                offs = [o & ~3 for o in offs]
+                if not all(offs[i + 1] - offs[i] >= C_ for i in range(p - 1)):
+                    offs = list(base_sets[0])
+        reqs_off.append(offs)
+    vec = rng.integers(0, k, nreq)
+    buf0 = rand(span, 5000 + seed)
+    olds = rand((nreq, C_), 5100 + seed)
+    news = rand((nreq, C_), 5200 + seed)
+    img = np.concatenate([buf0, olds.reshape(-1), news.reshape(-1)])
+    d = ctx.to_device(img)
+    try:
+        ob, nb = d.ptr + span, d.ptr + span + nreq * C_
+        ctx.update_ptrs(k, p, C_, [(int(vec[i]), ob + i * C_, nb + i * C_, [d.ptr + o for o in reqs_off[i]])
+                                   for i in range(nreq)])
+        ctx.sync()
+        got = d.download(span)
+        en = oracle.cauchy1(k, p)[k:]
+        want = buf0.copy()
+        for i in range(nreq):
+            par = np.stack([want[o:o + C_] for o in reqs_off[i]])
+            par = oracle.encode_data_update(en, int(vec[i]), olds[i] ^ news[i], par)
+            for r, o in enumerate(reqs_off[i]):
+                want[o:o + C_] = par[r]
+        assert np.array_equal(got, want), (k, p, C_, nreq, ecglib.last_kernel())
+    finally:
+        d.free()
