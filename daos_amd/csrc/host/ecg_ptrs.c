@@ -40,6 +40,22 @@ int ecg_scratch_reserve(ecg_ctx_t *ctx, size_t pin_bytes, size_t dev_bytes,
 			return ecg_hip_fail(e, "scratch wait");
 		sc->pending = 0;
 	}
+	/* grow in whole steps (at least 64 KiB, at least double): a pinned
+	 * re-allocation costs ~250 us (hipHostFree + hipHostMalloc), and the
+	 * batching queue's tables grow batch by batch (gpurun_out/r6f: 7-8
+	 * re-allocations per queue_bench run at 128 KiB cells) */
+	if (pin_bytes > sc->pin_bytes && pin_bytes < (16u << 20)) {
+		size_t want = sc->pin_bytes * 2 > (64u << 10) ? sc->pin_bytes * 2 : (64u << 10);
+
+		pin_bytes = pin_bytes > want ? pin_bytes : want;
+	}
+	/* (device scratch also holds gathered cells, which can be GiBs: doubled
+	 * only while small) */
+	if (dev_bytes > sc->dev_bytes && dev_bytes < (16u << 20)) {
+		size_t want = sc->dev_bytes * 2 > (64u << 10) ? sc->dev_bytes * 2 : (64u << 10);
+
+		dev_bytes = dev_bytes > want ? dev_bytes : want;
+	}
 	if (pin_bytes > sc->pin_bytes) {
 		if (sc->pin)
 			(void)hipHostFree(sc->pin);

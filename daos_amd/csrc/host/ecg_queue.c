@@ -44,8 +44,9 @@
  * ecg_update_ptrs launches: requests naming the same parity cells (one
  * stripe's cells updated one by one) fold into one pass over that parity, and
  * requests whose parity bytes would meet inside one launch go to ordered
- * launches; the update batches of one device are ordered behind each other
- * (q->uev), so two batches never read-modify-write one parity byte at once.
+ * launches; the update batches of one device run in order on its one update
+ * stream (q->ust), so two batches never read-modify-write one parity byte at
+ * once.
  * Such a slot closes as soon as its device has no batch of this queue in
  * flight, so a lone request launches at once and requests arriving while a
  * batch runs form the next one.
@@ -133,10 +134,9 @@ struct ecg_queue {
 	int cpu;			/* CPU executor: no device, host cells only */
 	int nctx;
 	ecg_ctx_t *ctxs[NSLOT_MAX];
-	/* device-cell update batches of device ctxs[i] run in order: each waits
-	 * for uev[i], recorded after the previous one (uev_set[i]) */
-	hipEvent_t uev[NSLOT_MAX];
-	int uev_set[NSLOT_MAX];
+	/* device-cell update batches of device ctxs[i] run in order on its one
+	 * update stream */
+	hipStream_t ust[NSLOT_MAX];
 	ecg_queue_attr_t attr;
 	size_t slot_bytes;
 	pthread_mutex_t lock;
@@ -362,29 +362,19 @@ static void launch_slot(struct ecg_queue *q, struct qslot *s)
 	if (s->devcells) {
 		/* the cells in place: one pointer-table launch (its table upload
 		 * and kernel on the slot's stream), nothing crosses back */
+		/* updates run on the device's one update stream, after the previous
+		 * update batch: one parity cell's read-modify-writes never overlap
+		 * across batches */
+		hipStream_t st = s->op == OP_UPDATE ? q->ust[s->ci] : s->st;
+
 		rc = e == hipSuccess ? 0 : ecg_hip_fail(e, "queue set device");
-		if (rc == 0 && s->op == OP_UPDATE) {
-			/* after the device's previous update batch: one parity cell's
-			 * read-modify-writes never overlap across batches */
-			if (q->uev_set[s->ci]) {
-				e = hipStreamWaitEvent(s->st, q->uev[s->ci], 0);
-				if (e != hipSuccess)
-					rc = ecg_hip_fail(e, "queue update order");
-			}
-			if (rc == 0)
-				rc = ecg_update_ptrs_coef(s->ctx, s->k, s->rows, s->coef, s->C, n, (void *const *)s->tab,
-							  s->uvec, s->st, NULL);
-			if (rc == 0) {
-				e = hipEventRecord(q->uev[s->ci], s->st);
-				if (e != hipSuccess)
-					rc = ecg_hip_fail(e, "queue update event");
-				q->uev_set[s->ci] = rc == 0;
-			}
-		} else if (rc == 0) {
-			rc = ecg_matmul_ptrs(s->ctx, s->k, s->rows, s->coef, s->C, n, (void *const *)s->tab, s->st);
-		}
+		if (rc == 0 && s->op == OP_UPDATE)
+			rc = ecg_update_ptrs_coef(s->ctx, s->k, s->rows, s->coef, s->C, n, (void *const *)s->tab,
+						  s->uvec, st, NULL);
+		else if (rc == 0)
+			rc = ecg_matmul_ptrs(s->ctx, s->k, s->rows, s->coef, s->C, n, (void *const *)s->tab, st);
 		if (rc == 0) {
-			e = hipEventRecord(s->done, s->st);
+			e = hipEventRecord(s->done, st);
 			if (e != hipSuccess)
 				rc = ecg_hip_fail(e, "queue batch event");
 		}
@@ -790,7 +780,7 @@ static int queue_create(ecg_ctx_t *const *ctxs, int nctx, const ecg_queue_attr_t
 	for (i = 0; i < q->nctx && e == hipSuccess; i++) {
 		e = hipSetDevice(q->ctxs[i]->device);
 		if (e == hipSuccess)
-			e = hipEventCreateWithFlags(&q->uev[i], hipEventDisableTiming);
+			e = hipStreamCreateWithFlags(&q->ust[i], hipStreamNonBlocking);
 	}
 	for (i = 0; i < (q->cpu ? cpu_workers() : NFIN) && e == hipSuccess; i++) {
 		if (pthread_create(&q->fin[i], NULL, fin_main, q) != 0)
@@ -814,8 +804,8 @@ static int queue_create(ecg_ctx_t *const *ctxs, int nctx, const ecg_queue_attr_t
 		const int cpu = q->cpu;
 
 		for (i = 0; i < q->nctx; i++)
-			if (q->uev[i])
-				(void)hipEventDestroy(q->uev[i]);
+			if (q->ust[i])
+				(void)hipStreamDestroy(q->ust[i]);
 		free(q);
 		return cpu ? ecg_fail(-ECG_DER_NOMEM, "queue_create: out of memory or threads")
 			   : ecg_hip_fail(e, "queue_create");
@@ -868,7 +858,7 @@ void ecg_queue_destroy(ecg_queue_t *q)
 		slot_free(&q->slot[i]);
 	for (int i = 0; i < q->nctx; i++) {
 		(void)hipSetDevice(q->ctxs[i]->device);
-		(void)hipEventDestroy(q->uev[i]);
+		(void)hipStreamDestroy(q->ust[i]);
 	}
 	pthread_cond_destroy(&q->cv_work);
 	pthread_cond_destroy(&q->cv_slot);
