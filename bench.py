@@ -52,7 +52,7 @@ sys.path.insert(0, ROOT)
 GIB = float(1 << 30)
 PARITY_ROW_PAD = 4096
 HBM_PEAK_GBS = 8000.0          # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
-ROUND = "r05"
+ROUND = "r06"
 
 # name -> (k, p, cell bytes, stripes, ops, strong scaling?)
 WORKLOADS = {
@@ -1054,7 +1054,7 @@ def cpu_baseline(k, p, C, budget_s, ops=("enc", "dec"), per_config=True):
 
 def pmc_traffic():
     path = os.path.join(ROOT, "profiles", ROUND, "pmc_traffic.json")
-    for older in ("r04", "r03", "r02", "r01"):    # the newest committed pass
+    for older in ("r05", "r04", "r03", "r02", "r01"):    # the newest committed pass
         if not os.path.exists(path):
             path = os.path.join(ROOT, "profiles", older, "pmc_traffic.json")
     if os.path.exists(path):
