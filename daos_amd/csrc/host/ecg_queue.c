@@ -91,7 +91,8 @@ struct qreq {
 
 struct qslot {
 	ecg_ctx_t *ctx;			/* device this slot's staging and launches live on (NULL: CPU) */
-	int ci;				/* index of ctx in the queue's ctxs[] */
+	int ui;				/* update stream of ctx's DEVICE: the first ctxs[] entry on
+					 * that device (a multi-device queue may list a device twice) */
 	enum slot_state state;
 	/* class */
 	int op, k, p, nerrs, rows;
@@ -365,7 +366,7 @@ static void launch_slot(struct ecg_queue *q, struct qslot *s)
 		/* updates run on the device's one update stream, after the previous
 		 * update batch: one parity cell's read-modify-writes never overlap
 		 * across batches */
-		hipStream_t st = s->op == OP_UPDATE ? q->ust[s->ci] : s->st;
+		hipStream_t st = s->op == OP_UPDATE ? q->ust[s->ui] : s->st;
 
 		rc = e == hipSuccess ? 0 : ecg_hip_fail(e, "queue set device");
 		if (rc == 0 && s->op == OP_UPDATE)
@@ -755,8 +756,9 @@ static int queue_create(ecg_ctx_t *const *ctxs, int nctx, const ecg_queue_attr_t
 				e = hipErrorOutOfMemory;
 			continue;
 		}
-		s->ci = i % nctx;
-		s->ctx = ctxs[s->ci];
+		s->ctx = ctxs[i % nctx];
+		for (s->ui = 0; ctxs[s->ui]->device != s->ctx->device; s->ui++)
+			;
 		e = hipSetDevice(s->ctx->device);
 		if (e == hipSuccess) {
 			/* the slot's pinned staging on its device's NUMA node: the
@@ -778,6 +780,7 @@ static int queue_create(ecg_ctx_t *const *ctxs, int nctx, const ecg_queue_attr_t
 			e = hipEventCreateWithFlags(&s->done, hipEventDisableTiming);
 	}
 	for (i = 0; i < q->nctx && e == hipSuccess; i++) {
+		/* one per device (ust[i] of the first entry naming it; ui above) */
 		e = hipSetDevice(q->ctxs[i]->device);
 		if (e == hipSuccess)
 			e = hipStreamCreateWithFlags(&q->ust[i], hipStreamNonBlocking);

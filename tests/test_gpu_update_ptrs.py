@@ -305,3 +305,51 @@ def test_update_ptrs_random_overlaps(ctx, oracle, ecglib, seed):
         assert np.array_equal(got, want), (k, p, C_, nreq, ecglib.last_kernel())
     finally:
         d.free()
+
+
+def test_queue_device_updates_multi_context_same_device(ctx, oracle, ecglib):
+    """A queue over an ecg_multi_t that lists one device twice: its slots
+    alternate between two contexts of the same GPU, so update batches of one
+    stripe land on both.  They must still run one after another (one update
+    stream per DEVICE, not per context) -- 8 threads updating the same 6
+    stripes over and over, every stripe's final parity the oracle's."""
+    k, p, C_ = 4, 2, 65536
+    S, per_stripe, T = 6, 24, 8
+    m = ecglib.Multi([0, 0])
+    rng = np.random.default_rng(77)
+    par0 = rand((S, p, C_), 31)
+    n = S * per_stripe
+    upd = [(i % S, int(rng.integers(0, k))) for i in range(n)]
+    olds = rand((n, C_), 32)
+    news = rand((n, C_), 33)
+    img = np.concatenate([par0.reshape(-1), olds.reshape(-1), news.reshape(-1)])
+    d = m.ctxs[0].to_device(img)
+    q = ecglib.Queue(m, max_batch=16, max_wait_us=50)
+    try:
+        ob = d.ptr + par0.nbytes
+        nb = ob + olds.nbytes
+
+        def worker(t):
+            for i in range(t, n, T):
+                s, c = upd[i]
+                q.update_ptrs(i, k, p, C_, c, ob + i * C_, nb + i * C_, [d.ptr + (s * p + r) * C_ for r in range(p)])
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        q.flush()
+        assert len(q.done) == n and all(rc == 0 for rc in q.done.values())
+        got = d.download(par0.nbytes).reshape(S, p, C_)
+        en = oracle.cauchy1(k, p)[k:]
+        for s in range(S):
+            want = par0[s]
+            for i, (ss, c) in enumerate(upd):
+                if ss == s:
+                    want = oracle.encode_data_update(en, c, olds[i] ^ news[i], want)
+            assert np.array_equal(got[s], want), s
+    finally:
+        q.close()
+        d.free()
+        m.close()
