@@ -60,6 +60,7 @@
  * only.
  */
 #define _GNU_SOURCE
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/prctl.h>
@@ -128,6 +129,9 @@ struct qslot {
 	hipStream_t st;
 	hipEvent_t done;
 	int rc;
+#ifdef ECG_QUEUE_TIMING
+	uint64_t tm[4];			/* closed, launch start, launch end, completion seen */
+#endif
 };
 
 struct ecg_queue {
@@ -160,7 +164,20 @@ struct ecg_queue {
 	 * interleave.  A lock striped on the destination address serialises
 	 * exactly those (XOR commutes, so their order does not matter). */
 	pthread_mutex_t dst_lock[NDSTLOCK];
+#ifdef ECG_QUEUE_TIMING
+	uint64_t tm_sum[5], tm_n;	/* per-batch phase times (ns), requests */
+#endif
 };
+
+/* Diagnostic build only (make EXP_CFLAGS=-DECG_QUEUE_TIMING): where a batch's
+ * time goes -- closed -> launch start (inputs landing, worker wake-up),
+ * launch (host side), in flight (GPU + completion poll), completion (callbacks,
+ * slot freed) -- printed when the queue is destroyed. */
+#ifdef ECG_QUEUE_TIMING
+#define QT(x) x
+#else
+#define QT(x)
+#endif
 
 static uint64_t now_ns(void)
 {
@@ -169,6 +186,20 @@ static uint64_t now_ns(void)
 	clock_gettime(CLOCK_MONOTONIC, &ts);
 	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
 }
+
+#ifdef ECG_QUEUE_TIMING
+static void queue_timing_add(struct ecg_queue *q, const struct qslot *s)
+{
+	const uint64_t t = now_ns();
+
+	q->tm_sum[0] += s->tm[1] - s->tm[0];
+	q->tm_sum[1] += s->tm[2] - s->tm[1];
+	q->tm_sum[2] += s->tm[3] - s->tm[2];
+	q->tm_sum[3] += t - s->tm[3];
+	q->tm_sum[4] += s->reserved;
+	q->tm_n++;
+}
+#endif
 
 static void abs_deadline(struct timespec *ts, uint64_t wait_ns)
 {
@@ -236,6 +267,7 @@ static void slot_close(struct qslot *s)
 
 	s->reserved = (uint32_t)(w & RES_CNT);
 	s->state = S_READY;
+	QT(s->tm[0] = now_ns());
 }
 
 /* Assign a FREE slot to a class: decode rows for recovery, capacity from the
@@ -354,6 +386,7 @@ static void launch_slot(struct ecg_queue *q, struct qslot *s)
 		s->fin_next = 0;
 		s->fin_done = 0;
 		s->state = S_DONE;
+		QT(s->tm[3] = now_ns());
 		q->batches++;
 		pthread_cond_broadcast(&q->cv_fin);
 		return;
@@ -575,6 +608,7 @@ static void *fin_main(void *argp)
 		pthread_mutex_lock(&q->lock);
 		if ((s->fin_done += n) == s->reserved) {
 			q->completed += s->reserved;
+			QT(queue_timing_add(q, s));
 			s->state = S_FREE;
 			pthread_cond_broadcast(&q->cv_slot);
 			pthread_cond_broadcast(&q->cv_done);
@@ -602,7 +636,9 @@ static void *worker_main(void *argp)
 			struct qslot *s = &q->slot[i];
 
 			if (s->state == S_READY && __atomic_load_n(&s->filled, __ATOMIC_SEQ_CST) == s->reserved) {
+				QT(s->tm[1] = now_ns());
 				launch_slot(q, s);
+				QT(s->tm[2] = now_ns());
 				idle = 0;
 			}
 		}
@@ -621,6 +657,7 @@ static void *worker_main(void *argp)
 				s->fin_next = 0;
 				s->fin_done = 0;
 				s->state = S_DONE;
+				QT(s->tm[3] = now_ns());
 				pthread_cond_broadcast(&q->cv_fin);
 				idle = 0;
 			} else if (s->state == S_FILLING && res_count(s) > 0) {
@@ -857,6 +894,13 @@ void ecg_queue_destroy(ecg_queue_t *q)
 	pthread_join(q->worker, NULL);
 	for (int i = 0; i < q->nfin; i++)
 		pthread_join(q->fin[i], NULL);
+#ifdef ECG_QUEUE_TIMING
+	if (q->tm_n)
+		fprintf(stderr, "ecg queue timing: %llu batches, %.1f requests each; us per batch: closed->launch %.1f, "
+			"launch %.1f, in flight %.1f, completion %.1f\n", (unsigned long long)q->tm_n,
+			(double)q->tm_sum[4] / q->tm_n, q->tm_sum[0] / 1e3 / q->tm_n, q->tm_sum[1] / 1e3 / q->tm_n,
+			q->tm_sum[2] / 1e3 / q->tm_n, q->tm_sum[3] / 1e3 / q->tm_n);
+#endif
 	for (int i = 0; i < q->nslot; i++)
 		slot_free(&q->slot[i]);
 	for (int i = 0; i < q->nctx; i++) {
