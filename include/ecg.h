@@ -219,10 +219,12 @@ int ecg_recover_host(ecg_ctx_t *ctx, int k, int p, uint64_t cell_bytes, uint32_t
  * Host buffers must stay valid until the callback runs.  Callbacks run on the
  * queue's completion threads and must not block on the queue.
  * Cells may be host memory (staged through the queue's pinned slots, PCIe
- * both ways) or, for encode and recover, device memory of one of the queue's
- * devices (k <= 16): such requests batch into one pointer-table launch on the
- * cells in place, and a batch launches as soon as the device has none of the
- * queue's in flight -- a lone request does not wait max_wait_us. */
+ * both ways) or device memory of one of the queue's devices (k <= 16): such
+ * requests batch into one pointer-table launch on the cells in place
+ * (updates: one ecg_update_ptrs call), and a batch launches as soon as the
+ * device has fewer than 2 of the queue's batches in flight -- a lone request
+ * does not wait max_wait_us.  A request's cells are all host memory or all
+ * memory of one device (-ECG_DER_INVAL naming the odd cell otherwise). */
 typedef struct ecg_queue ecg_queue_t;
 typedef void (*ecg_done_cb_t)(void *arg, int rc);
 
@@ -232,7 +234,10 @@ typedef struct ecg_queue_attr {
 	uint64_t max_cell_bytes; /* staging sized for this cell size (default 1 MiB) */
 } ecg_queue_attr_t;
 
-/* attr may be NULL for defaults. */
+/* attr may be NULL for defaults.  ctx NULL (or $ECG_FORCE_CPU=1): the CPU
+ * executor -- the same requests, batching and callbacks with no device, the
+ * products computed on the queue's completion threads by the CPU path (host
+ * cells only; a GPU-less process can use the facade). */
 int ecg_queue_create(ecg_ctx_t *ctx, const ecg_queue_attr_t *attr, ecg_queue_t **q);
 /* Drains outstanding requests (their callbacks run) then frees the queue. */
 void ecg_queue_destroy(ecg_queue_t *q);
@@ -249,10 +254,12 @@ int ecg_queue_recover(ecg_queue_t *q, int k, int p, uint64_t cell_bytes, unsigne
 /* Aggregation delta update of one stripe's parity (agg_update_parity:
  * xor_gen(old, new -> diff) then ec_encode_data_update(vec_i), ref:src/object/
  * srv_ec_aggregate.c:1086-1102):  parity[r] ^= coef[r][vec_i] * (old ^ new)
- * for the p parity cells (host memory, updated in place when the callback
- * runs).  Requests of one (k, p, cell size) batch together whatever their
- * vec_i.  k <= 16; host cells only (-DER_NOSYS for device cells: ecg_update
- * / ecg_agg_update_parity run them on the device). */
+ * for the p parity cells (updated in place when the callback runs).  Requests
+ * of one (k, p, cell size) batch together whatever their vec_i.  k <= 16.
+ * Host cells: old ^ new staged, the deltas XORed into the parity on the host.
+ * Device cells: ecg_update_ptrs batches in place -- requests naming the same
+ * parity cells fold into one pass, and the update batches of one device run
+ * in order, so concurrent updates of one stripe never lose a delta. */
 int ecg_queue_update(ecg_queue_t *q, int k, int p, uint64_t cell_bytes, int vec_i,
 		     const unsigned char *old_cell, const unsigned char *new_cell,
 		     unsigned char *const *parity, ecg_done_cb_t cb, void *arg);
