@@ -179,6 +179,14 @@ struct ecg_queue {
 #define QT(x)
 #endif
 
+/* Cell addresses per request in s->tab (device-cell slots and the CPU
+ * executor): k + rows (encode, recovery), or old, new and the rows parity
+ * cells (updates). */
+static uint32_t qtab_width(const struct qslot *s)
+{
+	return s->op == OP_UPDATE ? 2u + (uint32_t)s->rows : (uint32_t)(s->k + s->rows);
+}
+
 static uint64_t now_ns(void)
 {
 	struct timespec ts;
@@ -309,7 +317,7 @@ static int slot_open(struct ecg_queue *q, struct qslot *s, int op, int k, int p,
 	per = s->pitch * (uint64_t)(s->nin + s->rows) + (op == OP_UPDATE ? 1 : 0);
 	/* device cells stage nothing: only the pointer table bounds a batch */
 	{
-		uint32_t cap = dev >= 0 ? q->attr.max_batch : (uint32_t)((q->slot_bytes - 64) / per);
+		uint32_t cap = dev >= 0 || q->cpu ? q->attr.max_batch : (uint32_t)((q->slot_bytes - 64) / per);
 
 		ST(s->cap, cap > q->attr.max_batch ? q->attr.max_batch : cap);
 	}
@@ -528,50 +536,83 @@ static void xor_into_locked(struct ecg_queue *q, unsigned char *dst, const unsig
 	}
 }
 
-/* CPU executor: request i's product from its staged inputs -- encode and
- * recovery straight into the request's cells, an update's parity deltas into
- * the slot's output staging (XORed in below like the device's) */
-static int cpu_product(struct qslot *s, uint32_t i)
+/* A completion thread's scratch: the CPU executor's update deltas. */
+struct fin_scratch {
+	unsigned char *p;
+	size_t n;
+};
+
+/* Columns per CPU-executor product: an update's deltas (rows x this) stay in
+ * the thread's cache until XORed into the parity, and any cell size fits the
+ * kernels' int length. */
+#define CPU_CHUNK (256u << 10)
+
+/* CPU executor: request i's product straight from the caller's cells (the
+ * request holds only their addresses, s->tab, as the device-cell path does:
+ * the callers keep them valid until the callback) -- encode and recovery into
+ * the request's output cells, an update's p deltas coef[r][vec_i] * (old ^
+ * new) into the thread's scratch, then XORed into the parity under the region
+ * locks like the staged path's.  Returns 0 or a negative DER code. */
+static int cpu_product(struct ecg_queue *q, struct qslot *s, uint32_t i, struct fin_scratch *fs)
 {
-	const uint64_t in_stride = s->pitch * (uint64_t)s->nin, out_stride = s->pitch * (uint64_t)s->rows;
-	unsigned char *in = s->host + (size_t)i * in_stride;
+	const uint64_t *t = s->tab + (size_t)i * (uint64_t)qtab_width(s);
+	const int upd = s->op == OP_UPDATE, nin = upd ? 2 : s->k;
 	unsigned char *src[ECG_MAX_K], *dst[ECG_MAX_P];
-	unsigned char col[ECG_MAX_P];
+	unsigned char col[2 * ECG_MAX_P];
+	const unsigned char *coef = s->coef;
+	int rc = 0;
 
-	for (int j = 0; j < s->nin; j++)
-		src[j] = in + (uint64_t)j * s->pitch;
-	if (s->op == OP_UPDATE) {
-		const unsigned vec = s->host[(size_t)s->pitch * s->nin * s->cap + i];
+	if (upd) {
+		const size_t need = (size_t)CPU_CHUNK * s->rows;
 
-		for (int r = 0; r < s->rows; r++) {
-			dst[r] = s->host + s->out_off + i * out_stride + (uint64_t)r * s->pitch;
-			col[r] = s->coef[(size_t)r * s->k + vec];
+		if (fs->n < need) {
+			unsigned char *np = realloc(fs->p, need);
+
+			if (np == NULL)
+				return ecg_fail(-ECG_DER_NOMEM, "queue: update scratch");
+			fs->p = np;
+			fs->n = need;
 		}
-		return ecg_cpu_matmul((int)s->C, 1, s->rows, col, src, dst, 0);
+		/* parity delta r = c * old ^ c * new, c = coef[r][vec_i]: one
+		 * product of the two cells, no diff buffer */
+		for (int r = 0; r < s->rows; r++)
+			col[2 * r] = col[2 * r + 1] = s->coef[(size_t)r * s->k + s->uvec[i]];
+		coef = col;
 	}
-	return ecg_cpu_matmul((int)s->C, s->k, s->rows, s->coef, src, s->reqs[i].dst, 0);
+	for (uint64_t off = 0; off < s->C && rc == 0; off += CPU_CHUNK) {
+		const uint64_t n = s->C - off < CPU_CHUNK ? s->C - off : CPU_CHUNK;
+
+		for (int j = 0; j < nin; j++)
+			src[j] = (unsigned char *)(uintptr_t)t[j] + off;
+		for (int r = 0; r < s->rows; r++)
+			dst[r] = upd ? fs->p + (size_t)r * CPU_CHUNK : (unsigned char *)(uintptr_t)t[s->k + r] + off;
+		rc = ecg_cpu_matmul((int)n, nin, s->rows, coef, src, dst, 0);
+		for (int r = 0; upd && rc == 0 && r < s->rows; r++)
+			xor_into_locked(q, (unsigned char *)(uintptr_t)t[2 + r] + off, dst[r], n);
+	}
+	return rc;
 }
 
-static void finish_req(struct ecg_queue *q, struct qslot *s, uint32_t i)
+static void finish_req(struct ecg_queue *q, struct qslot *s, uint32_t i, struct fin_scratch *fs)
 {
-	const uint64_t out_stride = s->pitch * (uint64_t)s->rows;
-	const unsigned char *out = s->host + s->out_off + i * out_stride;
 	struct qreq *r = &s->reqs[i];
 	int rc = s->rc;
 
 	ecg_trace_push("ecg:queue_complete");
 	if (q->cpu) {
-		rc = cpu_product(s, i);
-		for (int j = 0; rc == 0 && s->op == OP_UPDATE && j < s->rows; j++)
-			xor_into_locked(q, r->dst[j], out + j * s->pitch, s->C);
-	} else if (s->devcells)
+		rc = cpu_product(q, s, i, fs);
+	} else if (s->devcells) {
 		;				/* written in place by the launch */
-	else if (s->rc == 0 && s->op == OP_UPDATE)	/* parity ^= coef[r][vec_i] * diff */
-		for (int j = 0; j < s->rows; j++)
-			xor_into_locked(q, r->dst[j], out + j * s->pitch, s->C);
-	else if (s->rc == 0)
-		for (int j = 0; j < s->rows; j++)
-			memcpy(r->dst[j], out + j * s->pitch, s->C);
+	} else if (s->rc == 0) {		/* the staged outputs of request i */
+		const unsigned char *out = s->host + s->out_off + i * s->pitch * (uint64_t)s->rows;
+
+		for (int j = 0; j < s->rows; j++) {
+			if (s->op == OP_UPDATE)	/* parity ^= coef[r][vec_i] * diff */
+				xor_into_locked(q, r->dst[j], out + j * s->pitch, s->C);
+			else
+				memcpy(r->dst[j], out + j * s->pitch, s->C);
+		}
+	}
 	ecg_trace_pop();
 	if (r->cb)
 		r->cb(r->arg, rc);
@@ -584,6 +625,7 @@ static void finish_req(struct ecg_queue *q, struct qslot *s, uint32_t i)
 static void *fin_main(void *argp)
 {
 	struct ecg_queue *q = argp;
+	struct fin_scratch fs = {NULL, 0};
 
 	pthread_mutex_lock(&q->lock);
 	for (;;) {
@@ -604,7 +646,7 @@ static void *fin_main(void *argp)
 		s->fin_next += n;
 		pthread_mutex_unlock(&q->lock);
 		for (uint32_t x = 0; x < n; x++)
-			finish_req(q, s, i + x);
+			finish_req(q, s, i + x, &fs);
 		pthread_mutex_lock(&q->lock);
 		if ((s->fin_done += n) == s->reserved) {
 			q->completed += s->reserved;
@@ -616,6 +658,7 @@ static void *fin_main(void *argp)
 		}
 	}
 	pthread_mutex_unlock(&q->lock);
+	free(fs.p);
 	return NULL;
 }
 
@@ -780,19 +823,18 @@ static int queue_create(ecg_ctx_t *const *ctxs, int nctx, const ecg_queue_attr_t
 		struct qslot *s = &q->slot[i];
 
 		s->reqs = calloc(q->attr.max_batch, sizeof(*s->reqs));
-		s->tab = calloc((size_t)q->attr.max_batch * (ECG_KMAX_K + ECG_KMAX_R), sizeof(*s->tab));
+		/* cell addresses: device cells k <= ECG_KMAX_K (one launch); the CPU
+		 * executor any k */
+		s->tab = calloc((size_t)q->attr.max_batch * (q->cpu ? ECG_MAX_K + ECG_MAX_P : ECG_KMAX_K + ECG_KMAX_R),
+				sizeof(*s->tab));
 		s->uvec = calloc(q->attr.max_batch, 1);
 		if (s->reqs == NULL || s->tab == NULL || s->uvec == NULL) {
 			e = hipErrorOutOfMemory;
 			break;
 		}
 		s->bytes = q->slot_bytes;
-		if (q->cpu) {
-			s->host = aligned_alloc(64, (s->bytes + 63) & ~(size_t)63);
-			if (s->host == NULL)
-				e = hipErrorOutOfMemory;
+		if (q->cpu)		/* nothing staged: the completion threads read the cells */
 			continue;
-		}
 		s->ctx = ctxs[i % nctx];
 		for (s->ui = 0; ctxs[s->ui]->device != s->ctx->device; s->ui++)
 			;
@@ -1027,7 +1069,8 @@ static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const u
 
 	{
 		struct qreq *r = &s->reqs[idx];
-		unsigned char *in = s->host + (size_t)idx * s->pitch * (uint64_t)s->nin;
+		const int addr = s->devcells || q->cpu;	/* the request holds addresses */
+		unsigned char *in = addr ? NULL : s->host + (size_t)idx * s->pitch * (uint64_t)s->nin;
 
 		r->op = op;
 		r->k = k;
@@ -1036,7 +1079,7 @@ static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const u
 		r->nerrs = nerrs;
 		r->cb = cb;
 		r->arg = arg;
-		if (s->devcells && op == OP_UPDATE) {	/* old, new, parity: ecg_update_ptrs' row */
+		if (addr && op == OP_UPDATE) {	/* old, new, parity: ecg_update_ptrs' row */
 			uint64_t *t = s->tab + (size_t)idx * (uint64_t)(2 + s->rows);
 
 			t[0] = (uint64_t)(uintptr_t)src[0];
@@ -1044,7 +1087,7 @@ static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const u
 			for (i = 0; i < s->rows; i++)
 				t[2 + i] = (uint64_t)(uintptr_t)dst[i];
 			s->uvec[idx] = (uint8_t)vec_i;
-		} else if (s->devcells) {	/* the stripe's ISA-L pointers, nothing copied */
+		} else if (addr) {	/* the stripe's ISA-L pointers, nothing copied */
 			uint64_t *t = s->tab + (size_t)idx * (uint64_t)(k + s->rows);
 
 			for (i = 0; i < k; i++)
@@ -1057,7 +1100,7 @@ static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const u
 			xor_into(in, src[0], src[1], C);
 			s->host[(size_t)s->pitch * s->nin * s->cap + idx] = (unsigned char)vec_i;
 		}
-		for (i = 0; !s->devcells && op != OP_UPDATE && i < k; i++) {
+		for (i = 0; !addr && op != OP_UPDATE && i < k; i++) {
 			const unsigned char *from = op == OP_ENCODE ? src[i]
 					: stripe + (uint64_t)s->dec_idx[i] * C;
 

@@ -236,8 +236,9 @@ typedef struct ecg_queue_attr {
 
 /* attr may be NULL for defaults.  ctx NULL (or $ECG_FORCE_CPU=1): the CPU
  * executor -- the same requests, batching and callbacks with no device, the
- * products computed on the queue's completion threads by the CPU path (host
- * cells only; a GPU-less process can use the facade). */
+ * products computed on the queue's completion threads by the CPU path
+ * straight from the callers' cells, nothing staged (host cells only; a
+ * GPU-less process can use the facade). */
 int ecg_queue_create(ecg_ctx_t *ctx, const ecg_queue_attr_t *attr, ecg_queue_t **q);
 /* Drains outstanding requests (their callbacks run) then frees the queue. */
 void ecg_queue_destroy(ecg_queue_t *q);

@@ -88,6 +88,37 @@ def test_cpu_queue_updates_many_threads(cpuq, oracle):
         assert np.array_equal(par[s], want), s
 
 
+def test_cpu_queue_cells_in_place_large(cpuq, oracle):
+    """Nothing is staged: cells bigger than the queue's max_cell_bytes (64 KiB
+    here) and than one 256 KiB product chunk, ragged tails, k > 16 -- encode,
+    recovery and updates straight from the callers' cells."""
+    k, p, C_ = 20, 3, (256 << 10) * 2 + 77
+    en = oracle.cauchy1(k, p)
+    data = rand((3, k, C_), 77)
+    par = [[np.zeros(C_, dtype=np.uint8) for _ in range(p)] for _ in range(3)]
+    for s in range(3):
+        cpuq.encode(s, k, p, list(data[s]), par[s])
+    cpuq.flush()
+    for s in range(3):
+        assert np.array_equal(np.stack(par[s]), oracle.encode_data(en[k:], data[s])), s
+    full = np.concatenate([data[0], np.stack(par[0])])
+    work = full.copy()
+    work[[3, 17, 21]] = 0
+    cpuq.recover(100, k, p, work, [3, 17, 21])
+    cpuq.flush()
+    assert np.array_equal(work, full)
+    k, p = 8, 2
+    par0 = rand((p, C_), 78)
+    old, new = rand((2, C_), 79)
+    got = par0.copy()
+    cpuq.update(200, k, p, 5, old, new, [got[0], got[1]])
+    cpuq.flush()
+    bm = bytes([1 << 5, 0])
+    want = oracle.agg_update_parity(k, p, C_, 1, bm, old[None], new[None], [(0, k * C_)], par0)
+    assert np.array_equal(got, want)
+    assert all(rc == 0 for rc in cpuq.done.values())
+
+
 def test_cpu_queue_batches_and_drain(ecglib, oracle):
     """Requests coalesce into slots (batches < requests) and destroy drains:
     every callback runs before ecg_queue_destroy returns."""
