@@ -328,13 +328,16 @@ struct upd_item {
 
 /* Any two items of different parity sets whose parity bytes overlap?  A
  * request whose own parity cells overlap one another is refused (its rows
- * would race inside one work item). */
+ * would race inside one work item), and so is an old or new cell that
+ * overlaps any parity cell of the call (a launch would read bytes another
+ * work item is rewriting). */
 static int upd_sets_overlap(const struct upd_req *rq, const struct upd_item *it, uint32_t nit, int rows,
-			    uint64_t C, int *overlap)
+			    uint64_t C, void *const *cells, uint32_t nreq, int *overlap)
 {
 	struct upd_ival *v;
 	uint64_t hi = 0;
 	size_t n = 0;
+	int rc = 0;
 
 	*overlap = 0;
 	for (uint32_t i = 0; i < nit; i++) {
@@ -363,9 +366,29 @@ static int upd_sets_overlap(const struct upd_req *rq, const struct upd_item *it,
 			*overlap = 1;
 		if (v[i].hi > hi)
 			hi = v[i].hi;
+		v[i].hi = hi;		/* from here on: the running maximum of the ends */
 	}
+	/* an input [a, a + C) meets a parity interval iff, among the intervals
+	 * starting below a + C, the highest end exceeds a */
+	for (uint32_t i = 0; i < nreq && rc == 0; i++)
+		for (uint32_t j = 0; j < 2 && rc == 0; j++) {
+			const uint64_t a = (uint64_t)(uintptr_t)cells[(size_t)i * (rows + 2) + j];
+			size_t lo = 0, up = n;	/* first interval with lo >= a + C */
+
+			while (lo < up) {
+				const size_t mid = (lo + up) / 2;
+
+				if (v[mid].lo < a + C)
+					lo = mid + 1;
+				else
+					up = mid;
+			}
+			if (lo > 0 && v[lo - 1].hi > a)
+				rc = ecg_fail(-ECG_DER_INVAL, "update_ptrs: request %u: the %s cell overlaps a parity cell "
+					      "of the call", i, j ? "new" : "old");
+		}
 	free(v);
-	return 0;
+	return rc;
 }
 
 static int upd_items_conflict(const struct upd_req *rq, const struct upd_item *a, const struct upd_item *b,
@@ -446,7 +469,7 @@ int ecg_update_ptrs_coef(ecg_ctx_t *ctx, int k, int rows, const unsigned char *c
 		nset++;
 		i = e;
 	}
-	rc = upd_sets_overlap(rq, it, nit, rows, C, &overlap);
+	rc = upd_sets_overlap(rq, it, nit, rows, C, cells, nreq, &overlap);
 	if (rc)
 		goto out;
 	if (overlap) {

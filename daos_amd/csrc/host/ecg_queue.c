@@ -88,6 +88,7 @@ struct qreq {
 	unsigned char *dst[ECG_MAX_P];	/* where each output row goes (XORed in for updates) */
 	ecg_done_cb_t cb;
 	void *arg;
+	int rc;				/* this request's own result (a batch split up) */
 };
 
 struct qslot {
@@ -410,10 +411,20 @@ static void launch_slot(struct ecg_queue *q, struct qslot *s)
 		hipStream_t st = s->op == OP_UPDATE ? q->ust[s->ui] : s->st;
 
 		rc = e == hipSuccess ? 0 : ecg_hip_fail(e, "queue set device");
-		if (rc == 0 && s->op == OP_UPDATE)
+		if (rc == 0 && s->op == OP_UPDATE) {
 			rc = ecg_update_ptrs_coef(s->ctx, s->k, s->rows, s->coef, s->C, n, (void *const *)s->tab,
 						  s->uvec, st, NULL);
-		else if (rc == 0)
+			/* refused as a batch (some request's old / new cell overlaps a
+			 * parity cell of the batch): the requests one after another on
+			 * the update stream, each with its own result -- the order
+			 * they would have run in one by one */
+			for (uint32_t i = 0; rc == -ECG_DER_INVAL && n > 1 && i < n; i++)
+				s->reqs[i].rc = ecg_update_ptrs_coef(s->ctx, s->k, s->rows, s->coef, s->C, 1,
+								     (void *const *)s->tab + (size_t)i * (2 + s->rows),
+								     &s->uvec[i], st, NULL);
+			if (rc == -ECG_DER_INVAL && n > 1)
+				rc = 0;
+		} else if (rc == 0)
 			rc = ecg_matmul_ptrs(s->ctx, s->k, s->rows, s->coef, s->C, n, (void *const *)s->tab, st);
 		if (rc == 0) {
 			e = hipEventRecord(s->done, st);
@@ -602,7 +613,8 @@ static void finish_req(struct ecg_queue *q, struct qslot *s, uint32_t i, struct 
 	if (q->cpu) {
 		rc = cpu_product(q, s, i, fs);
 	} else if (s->devcells) {
-		;				/* written in place by the launch */
+		if (rc == 0)			/* written in place by the launch */
+			rc = r->rc;
 	} else if (s->rc == 0) {		/* the staged outputs of request i */
 		const unsigned char *out = s->host + s->out_off + i * s->pitch * (uint64_t)s->rows;
 
@@ -1079,6 +1091,7 @@ static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const u
 		r->nerrs = nerrs;
 		r->cb = cb;
 		r->arg = arg;
+		r->rc = 0;
 		if (addr && op == OP_UPDATE) {	/* old, new, parity: ecg_update_ptrs' row */
 			uint64_t *t = s->tab + (size_t)idx * (uint64_t)(2 + s->rows);
 

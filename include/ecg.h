@@ -260,7 +260,11 @@ int ecg_queue_recover(ecg_queue_t *q, int k, int p, uint64_t cell_bytes, unsigne
  * Host cells: old ^ new staged, the deltas XORed into the parity on the host.
  * Device cells: ecg_update_ptrs batches in place -- requests naming the same
  * parity cells fold into one pass, and the update batches of one device run
- * in order, so concurrent updates of one stripe never lose a delta. */
+ * in order, so concurrent updates of one stripe never lose a delta; a batch
+ * ecg_update_ptrs refuses (an old / new cell overlapping a parity cell of
+ * the batch) runs its requests one by one, each with its own result.  An
+ * old / new cell that is another pending request's parity is read before or
+ * after that request's delta, whichever ran first. */
 int ecg_queue_update(ecg_queue_t *q, int k, int p, uint64_t cell_bytes, int vec_i,
 		     const unsigned char *old_cell, const unsigned char *new_cell,
 		     unsigned char *const *parity, ecg_done_cb_t cb, void *arg);

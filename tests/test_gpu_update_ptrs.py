@@ -135,8 +135,9 @@ def test_update_ptrs_overlapping_parity_sets(ctx, oracle, ecglib):
 
 
 def test_update_ptrs_errors(ctx, ecglib):
-    """One request's own parity cells overlapping, vec_i >= k, k > 16 and a
-    NULL cell are refused (-DER_INVAL) before any launch."""
+    """One request's own parity cells overlapping, vec_i >= k, k > 16, a
+    NULL cell and an old / new cell overlapping any parity cell of the call
+    are refused (-DER_INVAL) before any launch."""
     L = ecglib.lib()
     C_ = 4096
     d = ctx.alloc(8 * C_)
@@ -152,7 +153,53 @@ def test_update_ptrs_errors(ctx, ecglib):
         assert call(17, 2, 0, [d.ptr, d.ptr + C_, d.ptr + 2 * C_, d.ptr + 3 * C_]) == -ecglib.DER_INVAL
         assert call(4, 2, 0, [d.ptr, None, d.ptr + 2 * C_, d.ptr + 3 * C_]) == -ecglib.DER_INVAL
         assert L.ecg_update_ptrs(ctx.h, 4, 2, C_, 0, None, None, None) == 0     # nothing to do
+        # an old / new cell overlapping a parity cell of the call: its own, or another request's
+        assert call(4, 2, 0, [d.ptr + 2 * C_ + 8, d.ptr + C_, d.ptr + 2 * C_, d.ptr + 4 * C_]) == -ecglib.DER_INVAL
+        assert "old cell overlaps a parity cell" in L.ecg_strerror().decode()
+        cells = [d.ptr, d.ptr + C_, d.ptr + 2 * C_, d.ptr + 3 * C_,
+                 d.ptr + 4 * C_, d.ptr + 3 * C_ + C_ - 1, d.ptr + 6 * C_, d.ptr + 7 * C_]
+        arr = (C.c_void_p * 8)(*cells)
+        v = np.zeros(2, dtype=np.uint8)
+        assert L.ecg_update_ptrs(ctx.h, 4, 2, C_, 2, arr, v.ctypes.data_as(ecglib.u8p), None) == -ecglib.DER_INVAL
+        assert "request 1: the new cell overlaps" in L.ecg_strerror().decode()
+        cells[5] = d.ptr + 4 * C_ + C_                  # adjacent, not overlapping
+        arr = (C.c_void_p * 8)(*cells)
+        assert L.ecg_update_ptrs(ctx.h, 4, 2, C_, 2, arr, v.ctypes.data_as(ecglib.u8p), None) == 0
+        ctx.sync()
     finally:
+        d.free()
+
+
+def test_queue_device_updates_input_is_parity(ctx, oracle, ecglib):
+    """A queued batch the direct call refuses (request 1 reads, as its old
+    cell, the parity request 0 rewrites; request 3 names its own parity as
+    its new cell): the queue runs the batch's requests one by one in order,
+    each with its own result -- request 3 fails alone (-DER_INVAL), the
+    others give what applying them one after another gives."""
+    k, p, C_ = 4, 2, 8192
+    img0 = rand(16 * C_, 31)
+    d = ctx.to_device(img0)
+    q = ecglib.Queue(ctx, max_batch=8, max_wait_us=200000)     # the 4 requests wait for one batch
+    cell = lambda i: d.ptr + i * C_                             # noqa: E731
+    reqs = [(1, 8, 9, [0, 1]),          # (vec_i, old, new, parity) as cell indices
+            (2, 0, 10, [2, 3]),         # old = request 0's parity 0
+            (0, 11, 12, [4, 5]),
+            (3, 13, 6, [6, 7])]         # new = its own parity 0: refused
+    try:
+        for i, (v, o, n, par) in enumerate(reqs):
+            q.update_ptrs(i, k, p, C_, v, cell(o), cell(n), [cell(r) for r in par])
+        q.flush()
+        assert q.done[3] == -ecglib.DER_INVAL and all(q.done[i] == 0 for i in range(3)), q.done
+        got = d.download().reshape(16, C_)
+        en = oracle.cauchy1(k, p)[k:]
+        want = img0.reshape(16, C_).copy()
+        for v, o, n, par in reqs[:3]:
+            upd = oracle.encode_data_update(en, v, want[o] ^ want[n], np.stack([want[r] for r in par]))
+            for j, r in enumerate(par):
+                want[r] = upd[j]
+        assert np.array_equal(got, want)
+    finally:
+        q.close()
         d.free()
 
 
