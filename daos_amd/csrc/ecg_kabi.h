@@ -262,6 +262,12 @@ extern "C" {
 int ecg_k_unaligned_check(void *stream, int *ok);
 /* Tiles one segment occupies (0 when len == 0). */
 uint64_t ecg_k_copy_tiles(uint64_t dst, uint64_t len);
+/* A launch's table (pointer table, update records, copy segments) from the
+ * pinned host buffer it was written into to device memory: a kernel reading
+ * the host words over PCIe at system scope, queued on `stream` like any
+ * launch -- where a small hipMemcpyAsync behind running work keeps the
+ * calling thread busy in the runtime until that work drains. */
+int ecg_k_launch_fetch(const uint64_t *host_src, uint64_t *dst, uint32_t nwords, void *stream);
 /* One launch of ntiles workgroups over nseg segments (segs_dev in device memory). */
 int ecg_k_launch_copy_segs(const ecg_copy_seg_t *segs_dev, uint32_t nseg, uint64_t ntiles,
 			   void *stream, uint32_t *kernel_id);

@@ -1025,6 +1025,7 @@ int ecg_dev_free(ecg_ctx_t *ctx, void *ptr)
 
 	if (rc)
 		return rc;
+	ecg_place_forget();
 	HIPCHK(hipFree(ptr));
 	return 0;
 }

@@ -36,7 +36,9 @@ struct ecg_stage {
 /* Pointer tables and gathered cells (ecg_ptrs.c): two slots used in turn,
  * each guarded by ctx->lock and the `done` event of the last launch that read
  * it, so a call only waits for the launch before last. */
+#ifndef ECG_NSCRATCH
 #define ECG_NSCRATCH 2
+#endif
 struct ecg_scratch_slot {
 	void *pin;
 	size_t pin_bytes;
@@ -120,6 +122,9 @@ int ecg_update_ptrs_coef(ecg_ctx_t *ctx, int k, int rows, const unsigned char *c
 /* next scratch slot with at least these sizes, free of readers (ctx->lock held) */
 int ecg_scratch_reserve(ecg_ctx_t *ctx, size_t pin_bytes, size_t dev_bytes,
 			struct ecg_scratch_slot **out);
+/* The first `bytes` of sc->pin to sc->dev, queued on st (a fetch kernel:
+ * ecg_k_launch_fetch); `what` names the table in the error. */
+int ecg_table_upload(struct ecg_scratch_slot *sc, size_t bytes, hipStream_t st, const char *what);
 
 /* batched segment copies (ecg_sgl.c).  A fixed list (cap preset, fixed = 1)
  * writes into caller memory and fails instead of growing. */
@@ -195,6 +200,9 @@ int ecg_tune_launch_fn(ecg_ctx_t *ctx, const ecg_mm_params_t *p, uint32_t g, uin
  * placement of the k + rows cells (NULL: all host memory) (ecg_stage.c) */
 int ecg_matmul_host_mem(ecg_ctx_t *ctx, int len, int k, int rows, const unsigned char *coef,
 			unsigned char *const *src, unsigned char *const *dst, unsigned flags, const signed char *place);
+/* Forget every thread's remembered device ranges (ecg_cells_place): called
+ * when the library frees device memory. */
+void ecg_place_forget(void);
 /* placement of every cell of a one-stripe call: place[i] = device or -1
  * (host); returns the device cells' count (*dev their device) or a negative
  * DER code (cells on two devices, a device cell past its allocation) */
@@ -215,6 +223,9 @@ ecg_ctx_t *ecg_dropin_ctx(void);
 
 /* context helpers (ecg_core.c) */
 int ecg_ctx_enter(ecg_ctx_t *ctx);
+#ifdef ECG_QUEUE_TIMING
+void ecg_ptrs_timing_print(void);	/* diagnostic build: update_ptrs call phases */
+#endif
 
 /* NUMA placement (ecg_numa.c); the cpu_set_t helpers need _GNU_SOURCE in the
  * including file */

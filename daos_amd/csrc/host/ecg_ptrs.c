@@ -80,6 +80,25 @@ int ecg_scratch_reserve(ecg_ctx_t *ctx, size_t pin_bytes, size_t dev_bytes,
 	return 0;
 }
 
+int ecg_table_upload(struct ecg_scratch_slot *sc, size_t bytes, hipStream_t st, const char *what)
+{
+	const size_t words = (bytes + 7) / 8;
+	hipError_t e;
+
+	if (words > UINT32_MAX)
+		return ecg_fail(-ECG_DER_INVAL, "%s: %zu bytes", what, bytes);
+	/* A fetch kernel, not hipMemcpyAsync: a small pinned H2D copy queued
+	 * behind running work keeps the calling thread inside the runtime until
+	 * that work drains (47-185 us per queue batch measured,
+	 * profiles/r06/queue_dev_update/), while a launch returns at once. */
+#ifdef ECG_TABLE_MEMCPY		/* diagnostic A/B build only */
+	e = hipMemcpyAsync(sc->dev, sc->pin, bytes, hipMemcpyHostToDevice, st);
+#else
+	e = (hipError_t)ecg_k_launch_fetch((const uint64_t *)sc->pin, (uint64_t *)sc->dev, (uint32_t)words, st);
+#endif
+	return e == hipSuccess ? 0 : ecg_hip_fail(e, what);
+}
+
 void ecg_scratch_free(ecg_ctx_t *ctx)
 {
 	for (int i = 0; i < ECG_NSCRATCH; i++) {
@@ -200,9 +219,9 @@ static int launch_table(ecg_ctx_t *ctx, struct ecg_scratch_slot *sc, int k, int 
 	}
 	if (gather && gather->n)
 		tbytes = seg_off + gather->n * sizeof(ecg_copy_seg_t);
-	e = hipMemcpyAsync(sc->dev, sc->pin, tbytes, hipMemcpyHostToDevice, st);
-	if (e != hipSuccess)
-		return ecg_hip_fail(e, "pointer table H2D");
+	r = ecg_table_upload(sc, tbytes, st, "pointer table");
+	if (r)
+		return r;
 	if (gather && gather->n) {
 		r = ecg_segs_launch(gather, (unsigned char *)sc->dev + seg_off, st);
 		if (r)
@@ -278,6 +297,36 @@ int ecg_matmul_ptrs(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, 
 }
 
 /* ---- per-request delta updates on device cells -------------------------- */
+
+/* Diagnostic build only (-DECG_QUEUE_TIMING): where an update_ptrs call's
+ * host time goes -- set device, host planning, ctx lock, scratch, H2D
+ * enqueue, kernel launches, event -- wall ns summed over calls. */
+#ifdef ECG_QUEUE_TIMING
+#include <stdio.h>
+#include <time.h>
+static uint64_t g_upt[8], g_upn;
+static uint64_t upt_now(void)
+{
+	struct timespec ts;
+
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+#define UPT(i) (tp[i] = upt_now())
+void ecg_ptrs_timing_print(void)
+{
+	static const char *nm[7] = {"set device", "plan", "lock", "scratch", "h2d", "kernels", "event"};
+
+	if (g_upn == 0)
+		return;
+	fprintf(stderr, "update_ptrs timing: %llu calls; us per call:", (unsigned long long)g_upn);
+	for (int i = 0; i < 7; i++)
+		fprintf(stderr, " %s %.1f", nm[i], g_upt[i] / 1e3 / g_upn);
+	fprintf(stderr, "\n");
+}
+#else
+#define UPT(i) ((void)0)
+#endif
 
 /*
  * agg_update_parity runs, per updated data cell of a stripe, xor_gen(old, new)
@@ -437,9 +486,14 @@ int ecg_update_ptrs_coef(ecg_ctx_t *ctx, int k, int rows, const unsigned char *c
 			bits |= (uint64_t)(uintptr_t)cells[(size_t)i * per + j];
 		}
 	}
+#ifdef ECG_QUEUE_TIMING
+	uint64_t tp[8];
+#endif
+	UPT(0);
 	rc = ecg_ctx_enter(ctx);
 	if (rc)
 		return rc;
+	UPT(1);
 	rq = calloc(nreq, sizeof(*rq));
 	it = calloc(nreq, sizeof(*it));
 	prm = calloc(1, sizeof(*prm));
@@ -511,9 +565,12 @@ int ecg_update_ptrs_coef(ecg_ctx_t *ctx, int k, int rows, const unsigned char *c
 		for (int j = 0; j < k; j++)
 			ecg_build_ptbl(coef[(size_t)r * k + j], &prm->tbl[r][j]);
 	st = ecg_pick_stream(ctx, stream);
+	UPT(2);
 	pthread_mutex_lock(&ctx->lock);
+	UPT(3);
 	rc = ecg_scratch_reserve(ctx, (size_t)nit * rec * sizeof(uint64_t), (size_t)nit * rec * sizeof(uint64_t),
 				 &sc);
+	UPT(4);
 	if (rc == 0) {
 		uint64_t *t = sc->pin;
 		uint32_t at = 0, w, i;
@@ -541,9 +598,8 @@ int ecg_update_ptrs_coef(ecg_ctx_t *ctx, int k, int rows, const unsigned char *c
 				at++;
 			}
 		}
-		e = hipMemcpyAsync(sc->dev, sc->pin, (size_t)nit * rec * sizeof(uint64_t), hipMemcpyHostToDevice, st);
-		if (e != hipSuccess)
-			rc = ecg_hip_fail(e, "update table H2D");
+		rc = ecg_table_upload(sc, (size_t)nit * rec * sizeof(uint64_t), st, "update table");
+		UPT(5);
 		for (w = 0, at = 0; w < nwave && rc == 0; w++) {
 			uint32_t cnt = 0;
 			int ke;
@@ -557,12 +613,19 @@ int ecg_update_ptrs_coef(ecg_ctx_t *ctx, int k, int rows, const unsigned char *c
 				rc = ecg_hip_fail((hipError_t)ke, "update_ptrs kernel launch");
 			at += cnt;
 		}
+		UPT(6);
 		if (rc == 0) {
 			e = hipEventRecord(sc->done, st);
 			if (e != hipSuccess)
 				rc = ecg_hip_fail(e, "scratch event record");
 			sc->pending = rc == 0;
 		}
+		UPT(7);
+#ifdef ECG_QUEUE_TIMING
+		for (int i = 0; i < 7; i++)
+			__atomic_add_fetch(&g_upt[i], tp[i + 1] - tp[i], __ATOMIC_RELAXED);
+		__atomic_add_fetch(&g_upn, 1, __ATOMIC_RELAXED);
+#endif
 	}
 	pthread_mutex_unlock(&ctx->lock);
 	if (rc == 0) {

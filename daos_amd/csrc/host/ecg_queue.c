@@ -167,6 +167,7 @@ struct ecg_queue {
 	pthread_mutex_t dst_lock[NDSTLOCK];
 #ifdef ECG_QUEUE_TIMING
 	uint64_t tm_sum[5], tm_n;	/* per-batch phase times (ns), requests */
+	uint64_t tm_cpu;		/* the worker's thread CPU time inside launches */
 #endif
 };
 
@@ -197,6 +198,14 @@ static uint64_t now_ns(void)
 }
 
 #ifdef ECG_QUEUE_TIMING
+static uint64_t cpu_ns(void)
+{
+	struct timespec ts;
+
+	clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
 static void queue_timing_add(struct ecg_queue *q, const struct qslot *s)
 {
 	const uint64_t t = now_ns();
@@ -333,8 +342,12 @@ static int slot_open(struct ecg_queue *q, struct qslot *s, int op, int k, int p,
 	s->rc = 0;
 	s->t_open_ns = now_ns();
 	s->state = S_FILLING;
-	/* the class above is published with the open bit */
-	__atomic_store_n(&s->res, ((s->res >> 32) + 1) << 32 | RES_OPEN, __ATOMIC_RELEASE);
+	/* the class above is published with the open bit.  `res` is read
+	 * atomically: a submitter that loaded the last generation's word may
+	 * still be running its (failing) compare-exchange on it -- the C driver's
+	 * ThreadSanitizer run flagged the plain read here */
+	__atomic_store_n(&s->res, ((__atomic_load_n(&s->res, __ATOMIC_RELAXED) >> 32) + 1) << 32 | RES_OPEN,
+			 __ATOMIC_RELEASE);
 	return 0;
 }
 
@@ -692,7 +705,9 @@ static void *worker_main(void *argp)
 
 			if (s->state == S_READY && __atomic_load_n(&s->filled, __ATOMIC_SEQ_CST) == s->reserved) {
 				QT(s->tm[1] = now_ns());
+				QT(q->tm_cpu -= cpu_ns());
 				launch_slot(q, s);
+				QT(q->tm_cpu += cpu_ns());
 				QT(s->tm[2] = now_ns());
 				idle = 0;
 			}
@@ -954,6 +969,9 @@ void ecg_queue_destroy(ecg_queue_t *q)
 			"launch %.1f, in flight %.1f, completion %.1f\n", (unsigned long long)q->tm_n,
 			(double)q->tm_sum[4] / q->tm_n, q->tm_sum[0] / 1e3 / q->tm_n, q->tm_sum[1] / 1e3 / q->tm_n,
 			q->tm_sum[2] / 1e3 / q->tm_n, q->tm_sum[3] / 1e3 / q->tm_n);
+	if (q->tm_n)
+		fprintf(stderr, "ecg queue timing: launch thread CPU %.1f us per batch\n", q->tm_cpu / 1e3 / q->tm_n);
+	ecg_ptrs_timing_print();
 #endif
 	for (int i = 0; i < q->nslot; i++)
 		slot_free(&q->slot[i]);

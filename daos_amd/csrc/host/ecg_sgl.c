@@ -74,7 +74,6 @@ static int segs_submit(ecg_ctx_t *ctx, const struct ecg_segs *v, hipStream_t st)
 {
 	const size_t b = v->n * sizeof(ecg_copy_seg_t);
 	struct ecg_scratch_slot *sc = NULL;
-	hipError_t e;
 	int rc;
 
 	if (v->n == 0)
@@ -83,10 +82,9 @@ static int segs_submit(ecg_ctx_t *ctx, const struct ecg_segs *v, hipStream_t st)
 	if (rc)
 		return rc;
 	memcpy(sc->pin, v->seg, b);
-	e = hipMemcpyAsync(sc->dev, sc->pin, b, hipMemcpyHostToDevice, st);
-	if (e != hipSuccess)
-		return ecg_hip_fail(e, "segment table H2D");
-	rc = ecg_segs_launch(v, sc->dev, st);
+	rc = ecg_table_upload(sc, b, st, "segment table");
+	if (rc == 0)
+		rc = ecg_segs_launch(v, sc->dev, st);
 	if (hipEventRecord(sc->done, st) == hipSuccess)	/* the H2D may still read pin */
 		sc->pending = 1;
 	return rc;

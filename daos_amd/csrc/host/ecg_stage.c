@@ -11,6 +11,7 @@
  */
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "ecg_internal.h"
 
@@ -222,23 +223,75 @@ int ecg_cells_on_device(ecg_ctx_t *ctx, unsigned char *const *v, int n, uint64_t
 	return 0;
 }
 
+/* The device allocations a thread's recent calls found their cells in, each
+ * with its range and device: a cell inside one costs no query.  The pointer
+ * and range queries serialise on a runtime lock that launches need too -- 16
+ * threads posting device-cell requests to a queue kept its worker's launches
+ * waiting on it (profiles/r06/queue_dev_update/).  A device range is
+ * remembered for 1 ms (ECG_PLACE_CACHE_US; 0 = within one call only, the
+ * round-5 behaviour); runtime-known host ranges (pinned, registered, managed)
+ * only within the call.  ecg_dev_free clears every thread's ranges.  What the
+ * window does not see: an allocation freed by the caller's own hipFree and
+ * its addresses reallocated within it -- as pinned host memory the kernel
+ * still reaches the cells (they are GPU-mapped), as another device's memory
+ * it would not. */
+#define PLACE_N 4
+static __thread struct {
+	uintptr_t lo, hi;
+	uint64_t until;
+	int dev;
+} t_place[PLACE_N];
+static __thread unsigned t_place_next;
+static __thread uint64_t t_place_gen;
+static int64_t g_place_ttl_ns = -1;
+static uint64_t g_place_gen;	/* bumped by every device free through the library */
+
+void ecg_place_forget(void)
+{
+	__atomic_add_fetch(&g_place_gen, 1, __ATOMIC_RELEASE);
+}
+
+static uint64_t place_ttl_ns(void)
+{
+	int64_t t = __atomic_load_n(&g_place_ttl_ns, __ATOMIC_RELAXED);
+
+	if (t < 0) {
+		const char *env = getenv("ECG_PLACE_CACHE_US");
+
+		t = env && *env ? (int64_t)strtoll(env, NULL, 10) * 1000 : 1000000;
+		if (t < 0)
+			t = 0;
+		__atomic_store_n(&g_place_ttl_ns, t, __ATOMIC_RELAXED);
+	}
+	return (uint64_t)t;
+}
+
 /* Placement of every cell of a one-stripe call (src[0..k) then dst[0..rows)):
  * place[i] = the device whose allocation holds cell i whole, or -1 for host
  * memory (plain malloc / mmap, pinned, registered, managed: the CPU can
  * address it).  `query` is the placement lookup (ecg_ptr_device, or the
- * drop-in's cached one).  Cells inside a range already seen in this call
- * (one allocation: the usual stripe) cost no query.  Returns the number of
- * device cells (*dev = their device), or -DER_INVAL naming the cell for cells
- * on two devices or a device cell running past its allocation. */
+ * drop-in's cached one).  Cells inside a runtime-known range seen by this
+ * thread within the cache window (one allocation: the usual stripe, a
+ * buffer pool) cost no query.  Returns the number of device cells (*dev =
+ * their device), or -DER_INVAL naming the cell for cells on two devices or a
+ * device cell running past its allocation. */
 int ecg_cells_place(unsigned char *const *src, int k, unsigned char *const *dst, int rows, uint64_t len,
 		    int (*query)(const void *), signed char *place, int *dev)
 {
-	struct {
-		uintptr_t lo, hi;
-		int dev;
-	} seen[4];
-	int nseen = 0, ndev = 0, i, x;
+	struct timespec ts;
+	uint64_t now;
+	int ndev = 0, i, x;
 
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	now = (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+	{
+		const uint64_t gen = __atomic_load_n(&g_place_gen, __ATOMIC_ACQUIRE);
+
+		if (gen != t_place_gen) {	/* a device free since: start over */
+			memset(t_place, 0, sizeof(t_place));
+			t_place_gen = gen;
+		}
+	}
 	*dev = -1;
 	for (i = 0; i < k + rows; i++) {
 		const unsigned char *c = i < k ? src[i] : dst[i - k];
@@ -251,11 +304,11 @@ int ecg_cells_place(unsigned char *const *src, int k, unsigned char *const *dst,
 
 		if (c == NULL)
 			return ecg_fail(-ECG_DER_INVAL, "%s %d is NULL", what, idx);
-		for (x = 0; x < nseen; x++)
-			if (a >= seen[x].lo && e <= seen[x].hi)
+		for (x = 0; x < PLACE_N; x++)
+			if (now <= t_place[x].until && a >= t_place[x].lo && e <= t_place[x].hi)
 				break;
-		if (x < nseen) {
-			d = seen[x].dev;
+		if (x < PLACE_N) {
+			d = t_place[x].dev;
 		} else {
 			d = query(c);
 			if (d != ECG_PTR_UNKNOWN) {
@@ -265,10 +318,14 @@ int ecg_cells_place(unsigned char *const *src, int k, unsigned char *const *dst,
 					if (d >= 0 && e > (uintptr_t)base + size)
 						return ecg_fail(-ECG_DER_INVAL, "%s %d: %llu bytes run past the end of its "
 								"device allocation", what, idx, (unsigned long long)len);
-					x = nseen < 4 ? nseen++ : i % 4;
-					seen[x].lo = (uintptr_t)base;
-					seen[x].hi = (uintptr_t)base + size;
-					seen[x].dev = d >= 0 ? d : -1;
+					x = (int)(t_place_next++ % PLACE_N);
+					t_place[x].lo = (uintptr_t)base;
+					t_place[x].hi = (uintptr_t)base + size;
+					t_place[x].dev = d >= 0 ? d : -1;
+					/* host ranges only for this call: a device
+					 * allocation reusing their addresses must never
+					 * reach the CPU path */
+					t_place[x].until = now + (d >= 0 ? place_ttl_ns() : 0);
 				} else {
 					(void)hipGetLastError();
 					if (d >= 0)

@@ -146,6 +146,31 @@ ecg_copy_segs_kernel(const ecg_copy_seg_t *__restrict__ segs, uint32_t nseg)
 	}
 }
 
+// Table fetch: one 64-bit word per lane, read from pinned host memory at
+// system scope (the CPU wrote it just before the launch; nothing stale may
+// come from a cache) and stored to device memory for the launches behind it.
+#define FETCH_BLOCK 256
+
+__global__ void __launch_bounds__(FETCH_BLOCK) ecg_fetch_kernel(const uint64_t *__restrict__ src,
+								  uint64_t *__restrict__ dst, uint32_t n)
+{
+	const uint32_t i = blockIdx.x * FETCH_BLOCK + threadIdx.x;
+
+	if (i < n)
+		dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+extern "C" int ecg_k_launch_fetch(const uint64_t *host_src, uint64_t *dst, uint32_t nwords, void *stream)
+{
+	if (nwords == 0)
+		return (int)hipSuccess;
+	if (host_src == nullptr || dst == nullptr)
+		return (int)hipErrorInvalidValue;
+	hipLaunchKernelGGL(ecg_fetch_kernel, dim3((nwords + FETCH_BLOCK - 1) / FETCH_BLOCK), dim3(FETCH_BLOCK), 0,
+			   (hipStream_t)stream, host_src, dst, nwords);
+	return (int)hipGetLastError();
+}
+
 extern "C" uint64_t ecg_k_copy_tiles(uint64_t dst, uint64_t len)
 {
 	uint64_t head = (16u - (dst & 15u)) & 15u;
