@@ -80,7 +80,9 @@
 #define RES_OPEN (1ull << 31)
 #define RES_CNT (RES_OPEN - 1)
 
-enum slot_state { S_FREE, S_FILLING, S_READY, S_INFLIGHT, S_DONE };
+/* S_LAUNCHING: the worker is enqueuing the batch's work with the queue lock
+ * released (only the worker moves a slot out of it). */
+enum slot_state { S_FREE, S_FILLING, S_READY, S_LAUNCHING, S_INFLIGHT, S_DONE };
 
 struct qreq {
 	int op, k, p, nerrs;
@@ -367,7 +369,8 @@ static int device_busy(const struct ecg_queue *q, const ecg_ctx_t *ctx)
 	for (int i = 0; i < q->nslot; i++) {
 		const struct qslot *s = &q->slot[i];
 
-		if (s->ctx == ctx && s->devcells && (s->state == S_INFLIGHT || s->state == S_READY))
+		if (s->ctx == ctx && s->devcells &&
+		    (s->state == S_INFLIGHT || s->state == S_READY || s->state == S_LAUNCHING))
 			n++;
 	}
 	return n >= ECG_QUEUE_DEV_DEPTH;
@@ -388,8 +391,11 @@ static void close_due_slots(struct ecg_queue *q, uint64_t t, int force)
 	}
 }
 
-/* READY and fully copied in: launch H2D -> product -> D2H (lock held; only
- * enqueues asynchronous work). */
+/* READY and fully copied in: launch H2D -> product -> D2H.  The CPU
+ * executor's slots go straight to DONE (lock held); a device slot is
+ * S_LAUNCHING and the lock is NOT held -- the HIP calls enqueuing its work
+ * take tens of microseconds, which submitters and completion threads need
+ * not wait out -- and the worker marks it INFLIGHT afterwards. */
 static void launch_slot(struct ecg_queue *q, struct qslot *s)
 {
 	const uint32_t n = s->reserved;
@@ -454,8 +460,6 @@ static void launch_slot(struct ecg_queue *q, struct qslot *s)
 			ECG_STAT_ADD(s->ctx, recover_bytes, (uint64_t)s->rows * s->C * n);
 		}
 		s->rc = rc;
-		s->state = S_INFLIGHT;
-		q->batches++;
 		ecg_trace_pop();
 		return;
 	}
@@ -498,8 +502,6 @@ static void launch_slot(struct ecg_queue *q, struct qslot *s)
 		}
 	}
 	s->rc = rc;
-	s->state = S_INFLIGHT;
-	q->batches++;
 	ecg_trace_pop();
 }
 
@@ -706,7 +708,16 @@ static void *worker_main(void *argp)
 			if (s->state == S_READY && __atomic_load_n(&s->filled, __ATOMIC_SEQ_CST) == s->reserved) {
 				QT(s->tm[1] = now_ns());
 				QT(q->tm_cpu -= cpu_ns());
-				launch_slot(q, s);
+				if (q->cpu) {
+					launch_slot(q, s);
+				} else {
+					s->state = S_LAUNCHING;
+					pthread_mutex_unlock(&q->lock);
+					launch_slot(q, s);
+					pthread_mutex_lock(&q->lock);
+					s->state = S_INFLIGHT;
+					q->batches++;
+				}
 				QT(q->tm_cpu += cpu_ns());
 				QT(s->tm[2] = now_ns());
 				idle = 0;

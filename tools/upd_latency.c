@@ -3,7 +3,9 @@
  * launch: ecg_update_ptrs (n one-cell EC_8P2 updates on distinct device
  * stripes) against ecg_matmul_ptrs (n EC_8P2 stripe encodes), n = 1 .. 256.
  * Per call: the time inside the call (host work + enqueue) and the time to
- * completion (call + stream sync), median of 200 calls.  One JSON line per n.
+ * completion (call + stream sync), median of 200 calls; and the time inside
+ * the call when calls are issued back to back behind running work ("busy").
+ * One JSON line per n.
  * usage: upd_latency [cell bytes, default 131072].  Bench infrastructure.
  */
 #include <stdint.h>
@@ -45,7 +47,7 @@ int main(int argc, char **argv)
 	void *d = NULL, *st = NULL;
 	static void *ucells[NMAX * (2 + P)], *ecells[NMAX * (K + P)];
 	static uint8_t vec[NMAX];
-	static double call_u[REPS], done_u[REPS], call_e[REPS], done_e[REPS];
+	static double call_u[REPS], done_u[REPS], call_e[REPS], done_e[REPS], async_u[REPS], async_e[REPS];
 
 	if (ecg_ctx_create(0, &ctx) || ecg_stream_create(ctx, &st) ||
 	    ecg_dev_alloc(ctx, (size_t)NMAX * (K + P + 1) * C, &d)) {
@@ -100,9 +102,33 @@ int main(int argc, char **argv)
 			call_e[i] = t1 - t0;
 			done_e[i] = t2 - t0;
 		}
+		/* back to back, the stream kept busy (synchronised every 8 calls):
+		 * what a queue's worker sees, launching behind its last batch */
+		for (int i = 0; i < REPS; i++) {
+			double t0 = now_us();
+
+			if (ecg_update_ptrs(ctx, K, P, C, (uint32_t)n, ucells, vec, st))
+				return fprintf(stderr, "update_ptrs: %s\n", ecg_strerror()), 1;
+			async_u[i] = now_us() - t0;
+			if (i % 8 == 7)
+				ecg_stream_sync(ctx, st);
+		}
+		ecg_stream_sync(ctx, st);
+		for (int i = 0; i < REPS; i++) {
+			double t0 = now_us();
+
+			if (ecg_matmul_ptrs(ctx, K, P, &en[K * K], C, (uint32_t)n, ecells, st))
+				return fprintf(stderr, "matmul_ptrs: %s\n", ecg_strerror()), 1;
+			async_e[i] = now_us() - t0;
+			if (i % 8 == 7)
+				ecg_stream_sync(ctx, st);
+		}
+		ecg_stream_sync(ctx, st);
 		printf("{\"n\": %d, \"cell_bytes\": %llu, \"update_ptrs_call_us\": %.1f, \"update_ptrs_done_us\": %.1f, "
-		       "\"matmul_ptrs_call_us\": %.1f, \"matmul_ptrs_done_us\": %.1f}\n", n, (unsigned long long)C,
-		       median(call_u, REPS), median(done_u, REPS), median(call_e, REPS), median(done_e, REPS));
+		       "\"matmul_ptrs_call_us\": %.1f, \"matmul_ptrs_done_us\": %.1f, \"update_ptrs_busy_call_us\": %.1f, "
+		       "\"matmul_ptrs_busy_call_us\": %.1f}\n", n, (unsigned long long)C,
+		       median(call_u, REPS), median(done_u, REPS), median(call_e, REPS), median(done_e, REPS),
+		       median(async_u, REPS), median(async_e, REPS));
 		fflush(stdout);
 	}
 	ecg_dev_free(ctx, d);
