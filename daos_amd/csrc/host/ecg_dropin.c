@@ -132,6 +132,12 @@ int ecg_set_dropin_crossover(uint64_t bytes)
 	return 0;
 }
 
+int ecg_dropin_host_on_cpu(uint64_t bytes)
+{
+	(void)ecg_dropin_gpu();		/* reads the environment once */
+	return g_force_cpu || bytes < ecg_dropin_crossover();
+}
+
 uint64_t ecg_dropin_crossover(void)
 {
 	pthread_once(&g_once, once_init);

@@ -218,6 +218,9 @@ int ecg_dropin_product(const char *fn, ecg_ctx_t *ctx, int len, int k, int rows,
 		       unsigned char *const *src, unsigned char *const *dst, unsigned flags);
 /* 1 when the drop-in may use a GPU in this process */
 int ecg_dropin_gpu(void);
+/* Host cells of `bytes` (len x (k + rows)) compute on the CPU path: below the
+ * drop-in crossover, or $ECG_FORCE_CPU=1 (ecg_dropin.c). */
+int ecg_dropin_host_on_cpu(uint64_t bytes);
 /* the calling thread's default context; NULL without a usable device */
 ecg_ctx_t *ecg_dropin_ctx(void);
 

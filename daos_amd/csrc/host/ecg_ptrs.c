@@ -61,7 +61,9 @@ int ecg_scratch_reserve(ecg_ctx_t *ctx, size_t pin_bytes, size_t dev_bytes,
 			(void)hipHostFree(sc->pin);
 		sc->pin = NULL;
 		sc->pin_bytes = 0;
-		e = hipHostMalloc(&sc->pin, pin_bytes, hipHostMallocDefault);
+		/* read by the fetch kernel of whichever device the context
+		 * drives: mapped for every device */
+		e = hipHostMalloc(&sc->pin, pin_bytes, hipHostMallocPortable);
 		if (e != hipSuccess)
 			return ecg_hip_fail(e, "scratch pinned alloc");
 		sc->pin_bytes = pin_bytes;

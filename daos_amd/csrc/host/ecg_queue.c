@@ -101,6 +101,9 @@ struct qslot {
 	/* class */
 	int op, k, p, nerrs, rows;
 	int devcells;			/* cells in device memory of ctx's device: tab, no staging */
+	int cpuexec;			/* host cells computed on the completion threads (the CPU
+					 * executor, or a device queue's host cells below the
+					 * drop-in crossover): tab, no staging */
 	uint64_t C, pitch;
 	uint32_t err[ECG_MAX_P];
 	unsigned char coef[ECG_MAX_P * ECG_MAX_K];
@@ -244,10 +247,10 @@ static uint64_t pitch_of(uint64_t C)
 #define ST(x, v) __atomic_store_n(&(x), (v), __ATOMIC_RELAXED)
 
 static int class_matches(const struct qslot *s, int op, int k, int p, uint64_t C,
-			 const uint32_t *err, int nerrs, int dev)
+			 const uint32_t *err, int nerrs, int dev, int cpuexec)
 {
 	if (LD(s->op) != op || LD(s->k) != k || LD(s->p) != p || LD(s->C) != C || LD(s->nerrs) != nerrs ||
-	    LD(s->devcells) != (dev >= 0) || (dev >= 0 && s->ctx->device != dev))
+	    LD(s->devcells) != (dev >= 0) || LD(s->cpuexec) != cpuexec || (dev >= 0 && s->ctx->device != dev))
 		return 0;
 	for (int i = 0; op == OP_RECOVER && i < nerrs; i++)
 		if (LD(s->err[i]) != err[i])
@@ -258,12 +261,12 @@ static int class_matches(const struct qslot *s, int op, int k, int p, uint64_t C
 /* Reserve a request index in an open slot of this class; 0 if it is not
  * open, not this class or full. */
 static int slot_try_reserve(struct qslot *s, int op, int k, int p, uint64_t C, const uint32_t *err,
-			    int nerrs, int dev, uint32_t *idx)
+			    int nerrs, int dev, int cpuexec, uint32_t *idx)
 {
 	uint64_t w = __atomic_load_n(&s->res, __ATOMIC_ACQUIRE);
 	const uint64_t gen = w >> 32;
 
-	if (!(w & RES_OPEN) || !class_matches(s, op, k, p, C, err, nerrs, dev))
+	if (!(w & RES_OPEN) || !class_matches(s, op, k, p, C, err, nerrs, dev, cpuexec))
 		return 0;
 	/* the class was checked for this opening (generation) only */
 	while ((w >> 32) == gen && (w & RES_OPEN) && (uint32_t)(w & RES_CNT) < LD(s->cap)) {
@@ -293,7 +296,7 @@ static void slot_close(struct qslot *s)
 /* Assign a FREE slot to a class: decode rows for recovery, capacity from the
  * slot's staging bytes. */
 static int slot_open(struct ecg_queue *q, struct qslot *s, int op, int k, int p, uint64_t C,
-		     const uint32_t *err, int nerrs, int dev)
+		     const uint32_t *err, int nerrs, int dev, int cpuexec)
 {
 	unsigned char en[(ECG_MAX_K + ECG_MAX_P) * ECG_MAX_K];
 	uint64_t per;
@@ -325,11 +328,12 @@ static int slot_open(struct ecg_queue *q, struct qslot *s, int op, int k, int p,
 	}
 	s->nin = op == OP_UPDATE ? 1 : k;	/* staged input cells per request */
 	ST(s->devcells, dev >= 0);
+	ST(s->cpuexec, cpuexec);
 	/* an update request also stages its vec_i byte (+64 B of alignment slack) */
 	per = s->pitch * (uint64_t)(s->nin + s->rows) + (op == OP_UPDATE ? 1 : 0);
 	/* device cells stage nothing: only the pointer table bounds a batch */
 	{
-		uint32_t cap = dev >= 0 || q->cpu ? q->attr.max_batch : (uint32_t)((q->slot_bytes - 64) / per);
+		uint32_t cap = dev >= 0 || cpuexec ? q->attr.max_batch : (uint32_t)((q->slot_bytes - 64) / per);
 
 		ST(s->cap, cap > q->attr.max_batch ? q->attr.max_batch : cap);
 	}
@@ -407,9 +411,9 @@ static void launch_slot(struct ecg_queue *q, struct qslot *s)
 	hipError_t e;
 	int j, rc;
 
-	if (q->cpu) {
-		/* no device: the completion threads compute each request from
-		 * its staged inputs (finish_req) */
+	if (s->cpuexec) {
+		/* the completion threads compute each request from its cells
+		 * (finish_req) */
 		s->rc = 0;
 		s->fin_next = 0;
 		s->fin_done = 0;
@@ -625,7 +629,7 @@ static void finish_req(struct ecg_queue *q, struct qslot *s, uint32_t i, struct 
 	int rc = s->rc;
 
 	ecg_trace_push("ecg:queue_complete");
-	if (q->cpu) {
+	if (s->cpuexec) {
 		rc = cpu_product(q, s, i, fs);
 	} else if (s->devcells) {
 		if (rc == 0)			/* written in place by the launch */
@@ -708,7 +712,7 @@ static void *worker_main(void *argp)
 			if (s->state == S_READY && __atomic_load_n(&s->filled, __ATOMIC_SEQ_CST) == s->reserved) {
 				QT(s->tm[1] = now_ns());
 				QT(q->tm_cpu -= cpu_ns());
-				if (q->cpu) {
+				if (s->cpuexec) {
 					launch_slot(q, s);
 				} else {
 					s->state = S_LAUNCHING;
@@ -863,8 +867,7 @@ static int queue_create(ecg_ctx_t *const *ctxs, int nctx, const ecg_queue_attr_t
 		s->reqs = calloc(q->attr.max_batch, sizeof(*s->reqs));
 		/* cell addresses: device cells k <= ECG_KMAX_K (one launch); the CPU
 		 * executor any k */
-		s->tab = calloc((size_t)q->attr.max_batch * (q->cpu ? ECG_MAX_K + ECG_MAX_P : ECG_KMAX_K + ECG_KMAX_R),
-				sizeof(*s->tab));
+		s->tab = calloc((size_t)q->attr.max_batch * (ECG_MAX_K + ECG_MAX_P), sizeof(*s->tab));
 		s->uvec = calloc(q->attr.max_batch, 1);
 		if (s->reqs == NULL || s->tab == NULL || s->uvec == NULL) {
 			e = hipErrorOutOfMemory;
@@ -902,7 +905,7 @@ static int queue_create(ecg_ctx_t *const *ctxs, int nctx, const ecg_queue_attr_t
 		if (e == hipSuccess)
 			e = hipStreamCreateWithFlags(&q->ust[i], hipStreamNonBlocking);
 	}
-	for (i = 0; i < (q->cpu ? cpu_workers() : NFIN) && e == hipSuccess; i++) {
+	for (i = 0; i < cpu_workers() && e == hipSuccess; i++) {
 		if (pthread_create(&q->fin[i], NULL, fin_main, q) != 0)
 			e = hipErrorOutOfMemory;
 		else
@@ -1063,13 +1066,20 @@ static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const u
 	struct qslot *s = NULL;
 	uint32_t idx;
 	int i, rc = 0;
-	const int dev = request_device(q, op, k, p, C, op == OP_RECOVER ? nerrs : p, src, stripe, dst, &rc);
+	const int rows = op == OP_RECOVER ? nerrs : p;
+	const int dev = request_device(q, op, k, p, C, rows, src, stripe, dst, &rc);
+	/* host cells where the drop-in would compute them: on the CPU path below
+	 * its crossover (with a GFNI CPU always -- one core outruns a PCIe round
+	 * trip at every size), so the queue's completion threads
+	 * compute them in place instead of staging them over PCIe */
+	const int cpuexec = q->cpu ||
+			    (dev < 0 && ecg_dropin_host_on_cpu(C * (uint64_t)((op == OP_UPDATE ? 2 : k) + rows)));
 
 	if (rc)
 		return rc;
 	/* fast path, no lock: an open slot of this class with room */
 	for (i = 0; i < q->nslot && s == NULL; i++)
-		if (slot_try_reserve(&q->slot[i], op, k, p, C, err, nerrs, dev, &idx))
+		if (slot_try_reserve(&q->slot[i], op, k, p, C, err, nerrs, dev, cpuexec, &idx))
 			s = &q->slot[i];
 	if (s == NULL) {
 		pthread_mutex_lock(&q->lock);
@@ -1080,7 +1090,7 @@ static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const u
 			}
 			for (i = 0; i < q->nslot && s == NULL; i++)
 				if (q->slot[i].state == S_FILLING &&
-				    slot_try_reserve(&q->slot[i], op, k, p, C, err, nerrs, dev, &idx))
+				    slot_try_reserve(&q->slot[i], op, k, p, C, err, nerrs, dev, cpuexec, &idx))
 					s = &q->slot[i];
 			/* open FREE slots from a rotating start: batches spread over
 			 * the devices of a multi-device queue */
@@ -1088,14 +1098,14 @@ static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const u
 				struct qslot *f = &q->slot[(q->open_next + (uint32_t)i) % (uint32_t)q->nslot];
 
 				if (f->state == S_FREE && (dev < 0 || f->ctx->device == dev)) {
-					rc = slot_open(q, f, op, k, p, C, err, nerrs, dev);
+					rc = slot_open(q, f, op, k, p, C, err, nerrs, dev, cpuexec);
 					if (rc) {
 						f->state = S_FREE;
 						pthread_mutex_unlock(&q->lock);
 						return rc;
 					}
 					q->open_next = (uint32_t)(f - q->slot) + 1;
-					if (slot_try_reserve(f, op, k, p, C, err, nerrs, dev, &idx))
+					if (slot_try_reserve(f, op, k, p, C, err, nerrs, dev, cpuexec, &idx))
 						s = f;
 				}
 			}
@@ -1110,7 +1120,7 @@ static int submit(struct ecg_queue *q, int op, int k, int p, uint64_t C, const u
 
 	{
 		struct qreq *r = &s->reqs[idx];
-		const int addr = s->devcells || q->cpu;	/* the request holds addresses */
+		const int addr = s->devcells || s->cpuexec;	/* the request holds addresses */
 		unsigned char *in = addr ? NULL : s->host + (size_t)idx * s->pitch * (uint64_t)s->nin;
 
 		r->op = op;

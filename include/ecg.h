@@ -218,8 +218,12 @@ int ecg_recover_host(ecg_ctx_t *ctx, int k, int p, uint64_t cell_bytes, uint32_t
  * callback -- the place DAOS sets its ABT_eventual (srv_ec_aggregate.c:696).
  * Host buffers must stay valid until the callback runs.  Callbacks run on the
  * queue's completion threads and must not block on the queue.
- * Cells may be host memory (staged through the queue's pinned slots, PCIe
- * both ways) or device memory of one of the queue's devices (k <= 16): such
+ * Cells may be host memory or device memory of one of the queue's devices.
+ * Host cells go where the ISA-L drop-in would send them: below its crossover
+ * (ecg_set_dropin_crossover; with a GFNI CPU, every size) the queue's
+ * completion threads compute them in place on the CPU path, else they are
+ * staged through the queue's pinned slots (PCIe both ways).  Device cells
+ * (k <= 16): such
  * requests batch into one pointer-table launch on the cells in place
  * (updates: one ecg_update_ptrs call), and a batch launches as soon as the
  * device has fewer than 2 of the queue's batches in flight -- a lone request
@@ -257,7 +261,9 @@ int ecg_queue_recover(ecg_queue_t *q, int k, int p, uint64_t cell_bytes, unsigne
  * srv_ec_aggregate.c:1086-1102):  parity[r] ^= coef[r][vec_i] * (old ^ new)
  * for the p parity cells (updated in place when the callback runs).  Requests
  * of one (k, p, cell size) batch together whatever their vec_i.  k <= 16.
- * Host cells: old ^ new staged, the deltas XORed into the parity on the host.
+ * Host cells: on the CPU path the deltas are computed and XORed into the
+ * parity on the completion threads; staged, old ^ new crosses PCIe and the
+ * deltas are XORed in on the host.
  * Device cells: ecg_update_ptrs batches in place -- requests naming the same
  * parity cells fold into one pass, and the update batches of one device run
  * in order, so concurrent updates of one stripe never lose a delta; a batch

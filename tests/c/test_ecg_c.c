@@ -578,15 +578,19 @@ static void device_checks(void)
 		free(h);
 		free(g);
 	}
-	/* batching queue from several threads' worth of submissions */
-	{
+	/* batching queue from several threads' worth of submissions, host cells
+	 * on both routes: computed on the completion threads (below the
+	 * drop-in crossover) and staged through the device (crossover 0) */
+	for (int route = 0; route < 2; route++) {
 		ecg_queue_t *q = NULL;
 		struct qdone qd = {PTHREAD_MUTEX_INITIALIZER, 0, 0};
 		enum { N = 64 };
 		const int k = 4, p = 2, C = 4096 + 8;
 		unsigned char *cells = malloc((size_t)N * (k + p) * C);
 		unsigned char en[6 * 4], tb[4 * 2 * 32];
+		const uint64_t cross = ecg_dropin_crossover();
 
+		ecg_set_dropin_crossover(route == 0 ? UINT64_MAX : 0);
 		fill(cells, (size_t)N * (k + p) * C);
 		CHECK(ecg_queue_create(ctx, NULL, &q) == 0, "queue_create");
 		for (int i = 0; i < N; i++) {
@@ -611,10 +615,11 @@ static void device_checks(void)
 			dst[1] = w1;
 			ref_ec_encode_data(C, k, p, tb, src, dst);
 			CHECK(memcmp(w0, cells + ((size_t)i * (k + p) + k) * C, C) == 0 &&
-			      memcmp(w1, cells + ((size_t)i * (k + p) + k + 1) * C, C) == 0, "queue stripe %d",
-			      i);
+			      memcmp(w1, cells + ((size_t)i * (k + p) + k + 1) * C, C) == 0, "queue stripe %d (%s)",
+			      i, route == 0 ? "cpu" : "staged");
 		}
 		ecg_queue_destroy(q);
+		ecg_set_dropin_crossover(cross);
 		free(cells);
 	}
 	/* the same queue API on device cells, from NQT pthreads */

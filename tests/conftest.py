@@ -39,3 +39,14 @@ def ctx(ecglib):
     c = ecglib.Context(0)
     yield c
     c.close()
+
+
+@pytest.fixture(params=["cpu", "gpu"])
+def route(request, ecglib):
+    """Host-cell drop-in calls and host-cell queue requests on the product CPU
+    path (the default: below the measured crossover) or forced onto the GPU
+    staging path (crossover 0); device cells always take the GPU."""
+    old = ecglib.dropin_crossover()
+    ecglib.set_dropin_crossover((1 << 64) - 1 if request.param == "cpu" else 0)
+    yield request.param
+    ecglib.set_dropin_crossover(old)

@@ -326,7 +326,7 @@ def test_random_dropin_calls(ctx, oracle, ecglib):
 
 
 @pytest.mark.gpu
-def test_random_queue_requests(ctx, oracle, ecglib):
+def test_random_queue_requests(ctx, oracle, ecglib, route):
     """Seeded random one-stripe requests posted to one ecg_queue from 6
     threads at once: encodes and recoveries on host or device cells (device
     stripes at random byte offsets in one shared allocation, so the queue's

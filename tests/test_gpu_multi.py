@@ -107,7 +107,7 @@ def test_multi_errors(ecglib, multi4):
         ecglib.Multi([0, 99])
 
 
-def test_queue_multi_updates_concurrent(ecglib, oracle):
+def test_queue_multi_updates_concurrent(ecglib, oracle, route):
     """8 threads x 24 one-cell aggregation updates (agg_update_parity's
     xor_gen + ec_encode_data_update, ref:src/object/srv_ec_aggregate.c:
     1086-1102) through a queue whose slots span 2 shards; every vec_i mixes in
@@ -146,7 +146,7 @@ def test_queue_multi_updates_concurrent(ecglib, oracle):
     m.close()
 
 
-def test_queue_update_same_stripe_accumulates(ecglib, ctx, oracle):
+def test_queue_update_same_stripe_accumulates(ecglib, ctx, oracle, route):
     """Two updates of different cells of the same stripe, submitted back to
     back (the reference calls ec_encode_data_update once per updated cell on
     the same parity buffers): both deltas land."""
@@ -166,7 +166,7 @@ def test_queue_update_same_stripe_accumulates(ecglib, ctx, oracle):
     q.close()
 
 
-def test_queue_updates_of_one_stripe_no_flush(ecglib, ctx, oracle):
+def test_queue_updates_of_one_stripe_no_flush(ecglib, ctx, oracle, route):
     """agg_update_parity's calling pattern (ref:src/object/srv_ec_aggregate.c:
     1086-1102): one ecg_queue_update per updated cell of a stripe, all naming
     the same parity cells, submitted back to back with no flush in between --
@@ -197,7 +197,7 @@ def test_queue_updates_of_one_stripe_no_flush(ecglib, ctx, oracle):
     m.close()
 
 
-def test_queue_updates_overlapping_parity_ranges(ecglib, ctx, oracle):
+def test_queue_updates_overlapping_parity_ranges(ecglib, ctx, oracle, route):
     """Updates whose parity cells overlap through DIFFERENT pointers into one
     buffer (views at offsets of half a cell): the queue's locks
     are striped over address regions, not keyed on the cell pointer, so every

@@ -42,17 +42,6 @@ def oracle_parity(oracle, k, p, data):
     return np.stack([oracle.encode_data(en[k:], data[s]) for s in range(data.shape[0])], axis=1)
 
 
-@pytest.fixture(params=["cpu", "gpu"])
-def route(request, ecglib):
-    """Host-cell drop-in calls on the product CPU path (the default: below
-    the measured crossover) or forced onto the GPU staging path (crossover
-    0); device cells always take the GPU."""
-    old = ecglib.dropin_crossover()
-    ecglib.set_dropin_crossover((1 << 64) - 1 if request.param == "cpu" else 0)
-    yield request.param
-    ecglib.set_dropin_crossover(old)
-
-
 def check_route(ecglib, route):
     k = ecglib.last_kernel()
     assert k.startswith("cpu:") if route == "cpu" else k.startswith("ecg_mm"), (route, k)
@@ -719,12 +708,16 @@ def test_recover_host_erasure_runs(ctx, oracle, errs):
 
 
 # --------------------------------------------------------------- batching facade
-def test_queue_batches_concurrent_one_stripe_calls(ctx, oracle, ecglib):
+def test_queue_batches_concurrent_one_stripe_calls(ctx, oracle, ecglib, route):
     """8 threads x 40 one-stripe EC_8P2 encodes (the reference's calling
-    pattern) complete bit-exact and are coalesced into far fewer launches."""
+    pattern) complete bit-exact and are coalesced into far fewer batches --
+    host cells computed on the completion threads (below the drop-in
+    crossover, route "cpu": nothing crosses PCIe) or staged through the
+    device (crossover 0, route "gpu")."""
     import threading
 
     k, p, C_ = 8, 2, 32768
+    h2d0 = ctx.stats()["h2d_bytes"]
     q = ecglib.Queue(ctx, max_batch=64, max_wait_us=2000)
     en = oracle.cauchy1(k, p)
     jobs = {}
@@ -752,11 +745,14 @@ def test_queue_batches_concurrent_one_stripe_calls(ctx, oracle, ecglib):
         want = oracle.encode_data(en[k:], np.stack(data))
         assert np.array_equal(np.stack(par), want), rid
     q.close()
+    h2d = ctx.stats()["h2d_bytes"] - h2d0
+    assert (h2d == 0) if route == "cpu" else (h2d == 320 * k * C_), (route, h2d)
 
 
-def test_queue_mixed_classes_and_recovery(ctx, oracle, ecglib):
+def test_queue_mixed_classes_and_recovery(ctx, oracle, ecglib, route):
     """Interleaved encode 4P2 / encode 8P3 (odd cell size) / recover with two
-    different erasure sets: each class batched separately, all bit-exact."""
+    different erasure sets: each class batched separately, all bit-exact, on
+    either host-cell route."""
     q = ecglib.Queue(ctx, max_batch=16, max_wait_us=100)
     checks = []
     rid = 0
@@ -919,7 +915,7 @@ def test_queue_device_cell_errors(ctx, ecglib):
         dbuf.free()
 
 
-def test_queue_destroy_drains(ctx, oracle, ecglib):
+def test_queue_destroy_drains(ctx, oracle, ecglib, route):
     k, p, C_ = 2, 1, 4096
     q = ecglib.Queue(ctx, max_batch=1000, max_wait_us=1000000)   # would wait 1 s for company
     data = [rand(C_, 1), rand(C_, 2)]
