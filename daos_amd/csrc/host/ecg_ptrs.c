@@ -442,19 +442,83 @@ static int upd_sets_overlap(const struct upd_req *rq, const struct upd_item *it,
 	return rc;
 }
 
-static int upd_items_conflict(const struct upd_req *rq, const struct upd_item *a, const struct upd_item *b,
-			      int rows, uint64_t C)
+/* Launch (wave) of every item when parity sets share bytes: greedy colouring
+ * in item order over the conflict graph -- two items conflict when any of
+ * their parity intervals meet (items of one set always do) -- built by one
+ * sweep over every item's intervals sorted by start, so the cost is
+ * O(n log n + conflicting pairs), not a pairwise scan. */
+static int upd_color(const struct upd_req *rq, struct upd_item *it, uint32_t nit, int rows, uint64_t C,
+		     uint32_t *nwave)
 {
-	if (a->set == b->set)
-		return 1;
-	for (int r = 0; r < rows; r++)
-		for (int q = 0; q < rows; q++) {
-			const uint64_t x = rq[a->first].par[r], y = rq[b->first].par[q];
+	const size_t n = (size_t)nit * (size_t)rows;
+	struct upd_ival *v = malloc(sizeof(*v) * n);
+	uint32_t *deg = calloc((size_t)nit + 1, sizeof(*deg)), *adj = NULL, *used = NULL;
+	size_t ne = 0, x, y;
+	int rc = 0;
 
-			if (x < y + C && y < x + C)
-				return 1;
+	if (v == NULL || deg == NULL) {
+		rc = ecg_fail(-ECG_DER_NOMEM, "update_ptrs: malloc");
+		goto out;
+	}
+	for (uint32_t i = 0; i < nit; i++)
+		for (int r = 0; r < rows; r++)
+			v[(size_t)i * rows + r] = (struct upd_ival){rq[it[i].first].par[r], rq[it[i].first].par[r] + C, i};
+	qsort(v, n, sizeof(*v), upd_ival_cmp);
+	/* each meeting pair once, listed under its later item (CSR: count, then fill) */
+	for (int pass = 0; pass < 2; pass++) {
+		if (pass == 1) {
+			for (uint32_t i = 0; i < nit; i++)
+				deg[i + 1] += deg[i];	/* deg[i] = start of item i's list */
+			adj = malloc(sizeof(*adj) * (ne ? ne : 1));
+			if (adj == NULL) {
+				rc = ecg_fail(-ECG_DER_NOMEM, "update_ptrs: malloc");
+				goto out;
+			}
 		}
-	return 0;
+		for (x = 0; x < n; x++)
+			for (y = x + 1; y < n && v[y].lo < v[x].hi; y++) {
+				const uint32_t a = v[x].item < v[y].item ? v[x].item : v[y].item;
+				const uint32_t b = v[x].item ^ v[y].item ^ a;
+
+				if (a == b)
+					continue;
+				if (pass == 0) {
+					deg[b + 1]++;
+					ne++;
+				} else {
+					adj[deg[b]++] = a;
+				}
+			}
+		if (pass == 1)		/* fill advanced each start to the next item's */
+			for (uint32_t i = nit; i > 0; i--)
+				deg[i] = deg[i - 1];
+	}
+	deg[0] = 0;
+	used = calloc((size_t)nit + 1, sizeof(*used));
+	if (used == NULL) {
+		rc = ecg_fail(-ECG_DER_NOMEM, "update_ptrs: malloc");
+		goto out;
+	}
+	*nwave = 0;
+	for (uint32_t i = 0; i < nit; i++) {
+		uint32_t w = 0;
+
+		/* used[w] == i + 1: wave w holds an earlier item meeting item i */
+		for (uint32_t e = deg[i]; e < deg[i + 1]; e++)
+			if (it[adj[e]].wave <= nit)
+				used[it[adj[e]].wave] = i + 1;
+		while (used[w] == i + 1)
+			w++;
+		it[i].wave = w;
+		if (w + 1 > *nwave)
+			*nwave = w + 1;
+	}
+out:
+	free(v);
+	free(deg);
+	free(adj);
+	free(used);
+	return rc;
 }
 
 int ecg_update_ptrs_coef(ecg_ctx_t *ctx, int k, int rows, const unsigned char *coef, uint64_t C, uint32_t nreq,
@@ -529,26 +593,11 @@ int ecg_update_ptrs_coef(ecg_ctx_t *ctx, int k, int rows, const unsigned char *c
 	if (rc)
 		goto out;
 	if (overlap) {
-		/* parity sets that share bytes: greedy, each item in the first
-		 * launch none of its conflicting items is in */
-		nwave = 0;
-		for (uint32_t i = 0; i < nit; i++) {
-			uint32_t w = 0;
-
-			for (;;) {
-				uint32_t j;
-
-				for (j = 0; j < i; j++)
-					if (it[j].wave == w && upd_items_conflict(rq, &it[i], &it[j], rows, C))
-						break;
-				if (j == i)
-					break;
-				w++;
-			}
-			it[i].wave = w;
-			if (w + 1 > nwave)
-				nwave = w + 1;
-		}
+		/* parity sets that share bytes: each item in the first launch
+		 * none of its conflicting items is in */
+		rc = upd_color(rq, it, nit, rows, C, &nwave);
+		if (rc)
+			goto out;
 	}
 	/* lane access: 16-byte lanes when everything is 16-byte aligned; dword
 	 * lanes when C % 4 == 0 and the addresses are dword-aligned or the device

@@ -400,3 +400,45 @@ def test_queue_device_updates_multi_context_same_device(ctx, oracle, ecglib):
         q.close()
         d.free()
         m.close()
+
+
+def test_update_ptrs_large_overlapping_batch(ctx, oracle, ecglib):
+    """1500 requests whose parity cells sit at random byte offsets of a
+    buffer 40 cells long: nearly every item meets several others, so the
+    launches come from the conflict-graph colouring (one sweep over the
+    sorted parity intervals) -- every parity byte's read-modify-writes in
+    separate launches, the result the requests applied one by one."""
+    rng = np.random.default_rng(1500)
+    k, p, C_, nreq = 8, 2, 512, 1500
+    span = C_ * 40
+    offs = []
+    for _ in range(nreq):
+        while True:
+            o = sorted(int(x) for x in rng.integers(0, span - C_, p))
+            if o[1] - o[0] >= C_:
+                break
+        offs.append(o)
+    vec = rng.integers(0, k, nreq)
+    buf0 = rand(span, 77)
+    olds = rand((nreq, C_), 78)
+    news = rand((nreq, C_), 79)
+    d = ctx.to_device(np.concatenate([buf0, olds.reshape(-1), news.reshape(-1)]))
+    try:
+        ob, nb = d.ptr + span, d.ptr + span + nreq * C_
+        before = ctx.stats()["launches"]
+        ctx.update_ptrs(k, p, C_, [(int(vec[i]), ob + i * C_, nb + i * C_, [d.ptr + o for o in offs[i]])
+                                   for i in range(nreq)])
+        ctx.sync()
+        launches = ctx.stats()["launches"] - before
+        got = d.download(span)
+        en = oracle.cauchy1(k, p)[k:]
+        want = buf0.copy()
+        for i in range(nreq):
+            par = oracle.encode_data_update(en, int(vec[i]), olds[i] ^ news[i],
+                                            np.stack([want[o:o + C_] for o in offs[i]]))
+            for r, o in enumerate(offs[i]):
+                want[o:o + C_] = par[r]
+        assert np.array_equal(got, want)
+        assert 2 <= launches < nreq, launches
+    finally:
+        d.free()
