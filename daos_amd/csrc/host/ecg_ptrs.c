@@ -92,12 +92,9 @@ int ecg_table_upload(struct ecg_scratch_slot *sc, size_t bytes, hipStream_t st, 
 	/* A fetch kernel, not hipMemcpyAsync: a small pinned H2D copy queued
 	 * behind running work keeps the calling thread inside the runtime until
 	 * that work drains (47-185 us per queue batch measured,
-	 * profiles/r06/queue_dev_update/), while a launch returns at once. */
-#ifdef ECG_TABLE_MEMCPY		/* diagnostic A/B build only */
-	e = hipMemcpyAsync(sc->dev, sc->pin, bytes, hipMemcpyHostToDevice, st);
-#else
+	 * profiles/r06/queue_unlocked/qt_fetch_vs_memcpy.log), while a launch
+	 * returns at once. */
 	e = (hipError_t)ecg_k_launch_fetch((const uint64_t *)sc->pin, (uint64_t *)sc->dev, (uint32_t)words, st);
-#endif
 	return e == hipSuccess ? 0 : ecg_hip_fail(e, what);
 }
 
