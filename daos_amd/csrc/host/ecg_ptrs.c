@@ -90,10 +90,11 @@ int ecg_table_upload(struct ecg_scratch_slot *sc, size_t bytes, hipStream_t st, 
 	if (words > UINT32_MAX)
 		return ecg_fail(-ECG_DER_INVAL, "%s: %zu bytes", what, bytes);
 	/* A fetch kernel, not hipMemcpyAsync: a small pinned H2D copy queued
-	 * behind running work keeps the calling thread inside the runtime until
-	 * that work drains (47-185 us per queue batch measured,
-	 * profiles/r06/queue_unlocked/qt_fetch_vs_memcpy.log), while a launch
-	 * returns at once. */
+	 * behind running work held the queue's worker 47-185 us per batch
+	 * (profiles/r06/queue_unlocked/qt_subphases_before.log), while a launch
+	 * returns in ~5 us; one-thread device-update batches ran 111-204 GiB/s
+	 * against 39-58 with the copy (qt_fetch_vs_memcpy.log), large encode
+	 * batches the same either way. */
 	e = (hipError_t)ecg_k_launch_fetch((const uint64_t *)sc->pin, (uint64_t *)sc->dev, (uint32_t)words, st);
 	return e == hipSuccess ? 0 : ecg_hip_fail(e, what);
 }
