@@ -163,6 +163,7 @@ struct ecg_queue {
 	pthread_t worker;
 	pthread_t fin[NFIN_CPU];
 	int nfin;
+	int fin_busy;			/* requests the completion threads hold (lock) */
 	/* Updates of one stripe submitted back to back (one per updated cell, all
 	 * naming the same parity cells) land in one batch or in batches of
 	 * different devices, and their completions run on different threads:
@@ -380,17 +381,36 @@ static int device_busy(const struct ecg_queue *q, const ecg_ctx_t *ctx)
 	return n >= ECG_QUEUE_DEV_DEPTH;
 }
 
+/* A completion thread has nothing to do: no request of a DONE slot waits
+ * to be claimed and fewer requests are held than there are threads (lock
+ * held).  A CPU-route batch then closes at once -- batching buys the CPU
+ * nothing while a thread idles, and a lone request does not wait
+ * max_wait_us -- and under load, threads busy, requests coalesce as before. */
+static int fin_idle(const struct ecg_queue *q)
+{
+	if (q->fin_busy >= q->nfin)
+		return 0;
+	for (int i = 0; i < q->nslot; i++)
+		if (q->slot[i].state == S_DONE && q->slot[i].fin_next < q->slot[i].reserved)
+			return 0;
+	return 1;
+}
+
 static void close_due_slots(struct ecg_queue *q, uint64_t t, int force)
 {
+	int idle = -1;
+
 	for (int i = 0; i < q->nslot; i++) {
 		struct qslot *s = &q->slot[i];
 
 		uint32_t n;
 
-		if (s->state == S_FILLING && (n = res_count(s)) > 0 &&
-		    (force || n >= s->cap ||
-		     t >= s->t_open_ns + (uint64_t)q->attr.max_wait_us * 1000ull ||
-		     (s->devcells && !device_busy(q, s->ctx))))
+		if (s->state != S_FILLING || (n = res_count(s)) == 0)
+			continue;
+		if (s->cpuexec && idle < 0)
+			idle = fin_idle(q);
+		if (force || n >= s->cap || t >= s->t_open_ns + (uint64_t)q->attr.max_wait_us * 1000ull ||
+		    (s->devcells && !device_busy(q, s->ctx)) || (s->cpuexec && idle))
 			slot_close(s);
 	}
 }
@@ -675,10 +695,14 @@ static void *fin_main(void *argp)
 		i = s->fin_next;
 		n = s->devcells ? s->reserved - i : 1;
 		s->fin_next += n;
+		q->fin_busy += (int)n;
 		pthread_mutex_unlock(&q->lock);
 		for (uint32_t x = 0; x < n; x++)
 			finish_req(q, s, i + x, &fs);
 		pthread_mutex_lock(&q->lock);
+		q->fin_busy -= (int)n;
+		if (s->cpuexec && q->fin_busy < q->nfin)
+			pthread_cond_signal(&q->cv_work);	/* an idle thread: close a waiting CPU batch */
 		if ((s->fin_done += n) == s->reserved) {
 			q->completed += s->reserved;
 			QT(queue_timing_add(q, s));

@@ -28,6 +28,8 @@
  * into ecg_update_ptrs launches in place); QB_VERIFY=1 checks every stripe's
  * parity after one queue run against the CPU restatement.  QB_CPU_QUEUE=1
  * creates the queue with no context (the CPU executor; host cells).
+ * QB_LATENCY=1: one request at a time, each waited for (queue latency), and
+ * the same call through the synchronous drop-in.
  * usage: queue_bench C T [update|device|devupdate] [stripes per thread, default 64].
  * Bench infrastructure.
  */
@@ -128,30 +130,80 @@ static void update_one(long t, int i)
 		free(diff);
 }
 
+/* thread t's i-th call in the current mode */
+static void request(long t, int i)
+{
+	if (g_update) {
+		update_one(t, i);
+		return;
+	}
+	unsigned char *s = (g_dcells ? g_dcells : g_cells) + ((size_t)t * N + i) * (K + P) * CB;
+	unsigned char *data[64], *par[8];
+
+	for (int c = 0; c < K; c++)
+		data[c] = s + c * CB;
+	for (int r = 0; r < P; r++)
+		par[r] = s + (K + r) * CB;
+	if (g_mode == 0)
+		ec_encode_data((int)CB, K, P, g_tbls, data, par);
+	else if (g_mode == 1)
+		ecg_queue_encode(g_q, K, P, CB, data, par, done_cb, NULL);
+	else
+		ref_simd_encode_data((int)CB, K, P, g_tbls, data, par);
+}
+
 static void *worker(void *arg)
 {
 	long t = (long)arg;
 
-	for (int i = 0; i < N; i++) {
-		if (g_update) {
-			update_one(t, i);
-			continue;
-		}
-		unsigned char *s = (g_dcells ? g_dcells : g_cells) + ((size_t)t * N + i) * (K + P) * CB;
-		unsigned char *data[64], *par[8];
-
-		for (int c = 0; c < K; c++)
-			data[c] = s + c * CB;
-		for (int r = 0; r < P; r++)
-			par[r] = s + (K + r) * CB;
-		if (g_mode == 0)
-			ec_encode_data((int)CB, K, P, g_tbls, data, par);
-		else if (g_mode == 1)
-			ecg_queue_encode(g_q, K, P, CB, data, par, done_cb, NULL);
-		else
-			ref_simd_encode_data((int)CB, K, P, g_tbls, data, par);
-	}
+	for (int i = 0; i < N; i++)
+		request(t, i);
 	return NULL;
+}
+
+static int cmp_d(const void *a, const void *b)
+{
+	const double x = *(const double *)a, y = *(const double *)b;
+
+	return x < y ? -1 : x > y;
+}
+
+/* QB_LATENCY=1: one request at a time from one thread, each waited for
+ * (submit -> callback), median and 90th percentile in us; the synchronous
+ * drop-in call of the same request beside it. */
+static void latency(const char *cells)
+{
+	enum { R = 200, WARM = 20 };
+	static double q_us[R], d_us[R];
+
+	for (int i = 0; i < R + WARM; i++) {
+		long before;
+		double t0;
+
+		g_mode = 1;
+		pthread_mutex_lock(&g_cnt.lock);
+		before = g_cnt.done;
+		pthread_mutex_unlock(&g_cnt.lock);
+		t0 = now();
+		request(0, i % N);
+		pthread_mutex_lock(&g_cnt.lock);
+		while (g_cnt.done == before)
+			pthread_cond_wait(&g_cnt.cv, &g_cnt.lock);
+		pthread_mutex_unlock(&g_cnt.lock);
+		if (i >= WARM)
+			q_us[i - WARM] = (now() - t0) * 1e6;
+		g_mode = 0;
+		t0 = now();
+		request(0, i % N);
+		if (i >= WARM)
+			d_us[i - WARM] = (now() - t0) * 1e6;
+	}
+	qsort(q_us, R, sizeof(double), cmp_d);
+	qsort(d_us, R, sizeof(double), cmp_d);
+	printf("{\"op\": \"%s\", \"cells\": \"%s\", \"k\": %d, \"p\": %d, \"cell_bytes\": %llu, "
+	       "\"queue_latency_us\": {\"p50\": %.1f, \"p90\": %.1f}, \"dropin_call_us\": {\"p50\": %.1f, \"p90\": %.1f}}\n",
+	       g_update ? "update" : "encode", cells, K, P, (unsigned long long)CB, q_us[R / 2], q_us[R * 9 / 10],
+	       d_us[R / 2], d_us[R * 9 / 10]);
 }
 
 static double run(int mode)
@@ -309,6 +361,10 @@ int main(int argc, char **argv)
 			free(want);
 			return bad ? 1 : 0;
 		}
+		if (getenv("QB_LATENCY")) {
+			latency("device");
+			return 0;
+		}
 		run(0);
 		isal = run(0);
 		run(1);
@@ -339,6 +395,10 @@ int main(int argc, char **argv)
 		ecg_ctx_destroy(ctx);
 		free(g_cells);
 		free(g_new);
+		return 0;
+	}
+	if (getenv("QB_LATENCY")) {
+		latency(getenv("QB_CPU_QUEUE") ? "host, CPU executor" : "host");
 		return 0;
 	}
 	if (getenv("QB_VERIFY") && !g_update) {
