@@ -381,25 +381,29 @@ static int device_busy(const struct ecg_queue *q, const ecg_ctx_t *ctx)
 	return n >= ECG_QUEUE_DEV_DEPTH;
 }
 
-/* A completion thread has nothing to do: no request of a DONE slot waits
- * to be claimed and fewer requests are held than there are threads (lock
- * held).  A CPU-route batch then closes at once -- batching buys the CPU
- * nothing while a thread idles, and a lone request does not wait
- * max_wait_us -- and under load, threads busy, requests coalesce as before. */
-static int fin_idle(const struct ecg_queue *q)
+/* Close a CPU-route batch now?  Only while a completion thread is free (no
+ * request of a DONE slot waits to be claimed and fewer are held than there
+ * are threads), and then when the batch is the queue's only work -- a lone
+ * request does not wait max_wait_us for company -- or holds at least one
+ * request per free thread.  Closing every request alone instead would tie up
+ * the few slots with one request each (lock held). */
+static int cpu_close_now(const struct ecg_queue *q, const struct qslot *self, uint32_t n)
 {
-	if (q->fin_busy >= q->nfin)
-		return 0;
-	for (int i = 0; i < q->nslot; i++)
-		if (q->slot[i].state == S_DONE && q->slot[i].fin_next < q->slot[i].reserved)
-			return 0;
-	return 1;
+	int free = q->nfin - q->fin_busy, alone = 1;
+
+	for (int i = 0; i < q->nslot; i++) {
+		const struct qslot *o = &q->slot[i];
+
+		if (o->state == S_DONE)
+			free -= (int)(o->reserved - o->fin_next);
+		if (o != self && o->state != S_FREE && !(o->state == S_FILLING && res_count(o) == 0))
+			alone = 0;
+	}
+	return free > 0 && (alone || n >= (uint32_t)free);
 }
 
 static void close_due_slots(struct ecg_queue *q, uint64_t t, int force)
 {
-	int idle = -1;
-
 	for (int i = 0; i < q->nslot; i++) {
 		struct qslot *s = &q->slot[i];
 
@@ -407,10 +411,8 @@ static void close_due_slots(struct ecg_queue *q, uint64_t t, int force)
 
 		if (s->state != S_FILLING || (n = res_count(s)) == 0)
 			continue;
-		if (s->cpuexec && idle < 0)
-			idle = fin_idle(q);
 		if (force || n >= s->cap || t >= s->t_open_ns + (uint64_t)q->attr.max_wait_us * 1000ull ||
-		    (s->devcells && !device_busy(q, s->ctx)) || (s->cpuexec && idle))
+		    (s->devcells && !device_busy(q, s->ctx)) || (s->cpuexec && cpu_close_now(q, s, n)))
 			slot_close(s);
 	}
 }
@@ -701,8 +703,12 @@ static void *fin_main(void *argp)
 			finish_req(q, s, i + x, &fs);
 		pthread_mutex_lock(&q->lock);
 		q->fin_busy -= (int)n;
-		if (s->cpuexec && q->fin_busy < q->nfin)
-			pthread_cond_signal(&q->cv_work);	/* an idle thread: close a waiting CPU batch */
+		for (int j = 0; s->cpuexec && j < q->nslot; j++)	/* a free thread: a waiting */
+			if (q->slot[j].state == S_FILLING && q->slot[j].cpuexec &&	/* CPU batch may close */
+			    res_count(&q->slot[j]) > 0) {
+				pthread_cond_signal(&q->cv_work);
+				break;
+			}
 		if ((s->fin_done += n) == s->reserved) {
 			q->completed += s->reserved;
 			QT(queue_timing_add(q, s));
