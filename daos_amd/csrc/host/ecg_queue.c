@@ -361,6 +361,11 @@ static int slot_open(struct ecg_queue *q, struct qslot *s, int op, int k, int p,
 /* Device-cell batches of this queue queued or running on one device at once:
  * a second one hides the first's completion poll and the next launch
  * (profiles/r05/queue_dev/). */
+/* How often the worker polls batches in flight on a device (ns). */
+#ifndef ECG_QUEUE_POLL_NS
+#define ECG_QUEUE_POLL_NS 20000ull
+#endif
+
 #ifndef ECG_QUEUE_DEV_DEPTH
 #define ECG_QUEUE_DEV_DEPTH 2
 #endif
@@ -796,7 +801,7 @@ static void *worker_main(void *argp)
 		}
 		{
 			struct timespec ts;
-			uint64_t wait = busy ? 20000ull : 100000000ull;	/* poll in-flight work */
+			uint64_t wait = busy ? ECG_QUEUE_POLL_NS : 100000000ull;	/* poll in-flight work */
 
 			if (next != UINT64_MAX)
 				wait = next > t ? (next - t < wait ? next - t : wait) : 0;
