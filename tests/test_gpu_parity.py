@@ -882,6 +882,36 @@ def test_queue_device_cell_alone_launches_at_once(ctx, oracle, ecglib):
         dbuf.free()
 
 
+def test_queue_host_cell_alone_closes_at_once(ctx, oracle, ecglib):
+    """A lone host-cell request on the CPU route (default crossover) does not
+    wait max_wait_us either: its batch closes while a completion thread is
+    free and it is the queue's only work.  On the staged route (crossover 0)
+    the same request waits for company, up to max_wait_us."""
+    import time
+
+    k, p, C_ = 4, 2, 65536
+    data = rand((k, C_), 8300)
+    old = ecglib.dropin_crossover()
+    try:
+        for cross, wait_ok in (((1 << 64) - 1, lambda dt: dt < 1.0), (0, lambda dt: dt >= 0.2)):
+            ecglib.set_dropin_crossover(cross)
+            q = ecglib.Queue(ctx, max_batch=256, max_wait_us=300000)      # 0.3 s for company
+            par = [np.zeros(C_, np.uint8) for _ in range(p)]
+            try:
+                t0 = time.perf_counter()
+                q.encode(1, k, p, list(data), par)
+                while 1 not in q.done and time.perf_counter() - t0 < 3.0:
+                    time.sleep(0.0005)
+                dt = time.perf_counter() - t0
+                assert q.done.get(1) == 0, ("not completed", cross)
+                assert wait_ok(dt), (cross, dt)
+                assert np.array_equal(np.stack(par), oracle.encode_data(oracle.cauchy1(k, p)[k:], data))
+            finally:
+                q.close()
+    finally:
+        ecglib.set_dropin_crossover(old)
+
+
 def test_queue_device_cell_errors(ctx, ecglib):
     """Device cells: a request mixing host and device cells (an update whose
     old cell is host memory), a cell running past its allocation and more than

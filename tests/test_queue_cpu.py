@@ -120,10 +120,10 @@ def test_cpu_queue_cells_in_place_large(cpuq, oracle):
 
 
 def test_cpu_queue_batches_and_drain(ecglib, oracle):
-    """Requests coalesce into slots (batches < requests) and destroy drains:
-    every callback runs before ecg_queue_destroy returns."""
+    """Destroy drains: every callback runs before ecg_queue_destroy
+    returns, the outputs complete."""
     k, p, C_ = 4, 2, 4096
-    q = ecglib.Queue(None, max_batch=64, max_wait_us=1000000)      # would wait 1 s for company
+    q = ecglib.Queue(None, max_batch=64, max_wait_us=1000000)
     data = rand((10, k, C_), 5)
     par = [[np.zeros(C_, dtype=np.uint8) for _ in range(p)] for _ in range(10)]
     for s in range(10):
@@ -134,6 +134,26 @@ def test_cpu_queue_batches_and_drain(ecglib, oracle):
     en = oracle.cauchy1(k, p)
     for s in range(10):
         assert np.array_equal(np.stack(par[s]), oracle.encode_data(en[k:], data[s]))
+
+
+def test_cpu_queue_lone_request_closes_at_once(ecglib, oracle):
+    """A lone request does not wait max_wait_us (here 5 s) for company: with
+    a completion thread free and no other work its batch closes at once."""
+    import time
+
+    k, p, C_ = 4, 2, 4096
+    q = ecglib.Queue(None, max_batch=64, max_wait_us=5000000)
+    try:
+        data = rand((k, C_), 9)
+        par = [np.zeros(C_, dtype=np.uint8) for _ in range(p)]
+        t0 = time.perf_counter()
+        q.encode(1, k, p, list(data), par)
+        while 1 not in q.done and time.perf_counter() - t0 < 6.0:
+            time.sleep(0.0005)
+        assert q.done.get(1) == 0 and time.perf_counter() - t0 < 1.0
+        assert np.array_equal(np.stack(par), oracle.encode_data(oracle.cauchy1(k, p)[k:], data))
+    finally:
+        q.close()
 
 
 def test_cpu_queue_bad_arguments(cpuq, ecglib):
