@@ -51,13 +51,20 @@
  * flight, so a lone request launches at once and requests arriving while a
  * batch runs form the next one.
  *
- * CPU executor (ecg_queue_create(NULL, ...), or $ECG_FORCE_CPU=1): the same
- * slots, reservations and state machine with no device -- the engine's
- * DSS_XS_OFFLOAD ULT + ABT_eventual pattern this facade replaces
+ * The worker enqueues a device batch's HIP work with the queue lock released
+ * (S_LAUNCHING), so submitters and completion threads never wait out a launch.
+ *
+ * CPU route (cpuexec slots): host-cell requests go where the ISA-L drop-in
+ * would send the same cells -- below its crossover (with a GFNI CPU, every
+ * size) the slot, like a device-cell one, holds only the cell addresses, a
+ * closed slot goes straight to DONE and the completion threads (one per CPU,
+ * 4..16) compute each request in place with ecg_cpu_matmul; above it the
+ * staged path above.  Such a slot closes early while a completion thread is
+ * free if it is the queue's only work or holds a request per free thread.
+ * The CPU executor (ecg_queue_create(NULL, ...), or $ECG_FORCE_CPU=1) is the
+ * same with no device at all -- the engine's DSS_XS_OFFLOAD ULT +
+ * ABT_eventual pattern this facade replaces
  * (ref:src/object/srv_ec_aggregate.c:701-734, ref:src/engine/ult.c:394-470).
- * A closed slot goes straight to DONE and the completion threads compute each
- * request's product from its staged inputs with ecg_cpu_matmul.  Host cells
- * only.
  */
 #define _GNU_SOURCE
 #include <stdio.h>
@@ -74,8 +81,8 @@
 #define OP_UPDATE 2
 #define NSLOT_MIN 4	/* staging slots for one device; 2 per device beyond */
 #define NSLOT_MAX 32
-#define NFIN 4		/* completion threads: output scatter + callbacks */
-#define NFIN_CPU 16	/* ... of the CPU executor, which also compute the products there */
+#define NFIN 4		/* completion threads at least: output scatter, callbacks, */
+#define NFIN_CPU 16	/* ... and CPU-route products: one per CPU, at most this many */
 #define NDSTLOCK 64	/* striped locks serialising update deltas into one parity cell */
 #define RES_OPEN (1ull << 31)
 #define RES_CNT (RES_OPEN - 1)
