@@ -221,20 +221,21 @@ int ecg_recover_host(ecg_ctx_t *ctx, int k, int p, uint64_t cell_bytes, uint32_t
  * Cells may be host memory or device memory of one of the queue's devices.
  * Host cells go where the ISA-L drop-in would send them: below its crossover
  * (ecg_set_dropin_crossover; with a GFNI CPU, every size) the queue's
- * completion threads compute them in place on the CPU path, else they are
- * staged through the queue's pinned slots (PCIe both ways).  Device cells
- * (k <= 16): such
- * requests batch into one pointer-table launch on the cells in place
- * (updates: one ecg_update_ptrs call), and a batch launches as soon as the
- * device has fewer than 2 of the queue's batches in flight -- a lone request
- * does not wait max_wait_us.  A request's cells are all host memory or all
+ * completion threads compute them in place on the CPU path -- such a batch
+ * closes while a completion thread is free if it is the queue's only work or
+ * holds a request per free thread, so a lone request does not wait
+ * max_wait_us -- else they are staged through the queue's pinned slots (PCIe
+ * both ways).  Device cells (k <= 16): such requests batch into one
+ * pointer-table launch on the cells in place (updates: one ecg_update_ptrs
+ * call), and a batch launches as soon as the device has fewer than 2 of the
+ * queue's batches in flight -- a lone request does not wait either.  A request's cells are all host memory or all
  * memory of one device (-ECG_DER_INVAL naming the odd cell otherwise). */
 typedef struct ecg_queue ecg_queue_t;
 typedef void (*ecg_done_cb_t)(void *arg, int rc);
 
 typedef struct ecg_queue_attr {
 	uint32_t max_batch;	/* stripes per device batch (default 256) */
-	uint32_t max_wait_us;	/* how long a lone request may wait for company (default 50) */
+	uint32_t max_wait_us;	/* longest a request waits for company (default 50) */
 	uint64_t max_cell_bytes; /* staging sized for this cell size (default 1 MiB) */
 } ecg_queue_attr_t;
 
